@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Headline benchmark: learner env-frames/s, IMPALA deep ResNet + LSTM-256.
+
+Config (BASELINE.json): B=32 per learner, unroll T=100 (T+1=101 frames per
+sequence), 4 action repeats -> 12 800 env frames per learner step, synthetic
+72x96x3 uint8 frames, 9 actions, random-init weights, bf16 convs/GEMMs with
+fp32 V-trace/loss/optimizer state.  One process per GPU; N>1 is weak scaling
+(each learner consumes its own B=32 batch, gradients summed with one RCCL
+all-reduce).
+
+Every timed step does the full learner work of experiment.py:346-427: H2D of
+the next batch from pinned host memory (StagingArea equivalent, overlapped on
+a copy stream), T+1-step re-unroll, V-trace, loss, backward, gradient
+all-reduce, RMSProp with on-device LR decay, frame-counter increment.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+(multi-GPU: launched by torch.distributed.run, one rank per GPU).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from scalable_agent_amd import flags as flags_lib  # noqa: E402
+from scalable_agent_amd.envs.synthetic import make_synthetic_batch  # noqa
+from scalable_agent_amd.learner import Learner, _copy_into, _map_tensors  # noqa
+from scalable_agent_amd.models import Agent  # noqa: E402
+from scalable_agent_amd import parallel  # noqa: E402
+
+METRIC = ('learner env-frames/sec, IMPALA deep-ResNet+LSTM, batch=32 '
+          'unroll=100, 1/2/4/8 GPU')
+BASELINE_FPS = 250000.0  # BASELINE.md §B best published single-learner figure
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=20)
+  ap.add_argument('--warmup', type=int, default=5)
+  ap.add_argument('--batch_size', type=int, default=32)
+  ap.add_argument('--unroll_length', type=int, default=100)
+  ap.add_argument('--torso', default='deep')
+  ap.add_argument('--height', type=int, default=72)
+  ap.add_argument('--width', type=int, default=96)
+  ap.add_argument('--backend', default='auto', choices=['auto', 'torch', 'hip'])
+  ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+  ap.add_argument('--graph', type=int, default=1)
+  ap.add_argument('--device', default='auto')
+  ap.add_argument('--profile_steps', type=int, default=0)
+  args = ap.parse_args()
+
+  rank, world, local = parallel.init_distributed()
+  if args.device == 'auto':
+    device = torch.device('cuda', local) if torch.cuda.is_available() else \
+        torch.device('cpu')
+  else:
+    device = torch.device(args.device)
+  if device.type == 'cuda':
+    torch.cuda.set_device(device)
+
+  backend = args.backend
+  if backend == 'auto':
+    backend = 'torch'
+    if device.type == 'cuda':
+      from scalable_agent_amd import ops
+      backend = 'hip' if ops.available() else 'torch'
+
+  flags = flags_lib.default_flags(
+      batch_size=args.batch_size, unroll_length=args.unroll_length,
+      torso=args.torso, dtype=args.dtype, height=args.height, width=args.width)
+  num_actions = 9
+  frame_shape = (args.height, args.width, 3)
+  cdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+  agent = Agent(num_actions, torso=args.torso, frame_shape=frame_shape,
+                seed=flags.seed, backend=backend, compute_dtype=cdt)
+  learner = Learner(agent, flags, device, world_size=world)
+  if world > 1:
+    parallel.broadcast_params(learner.flat.params)
+
+  pin = device.type == 'cuda'
+  host_batches = [
+      make_synthetic_batch(args.batch_size, args.unroll_length, frame_shape,
+                           num_actions, seed=1000 * rank + i, pin_memory=pin)
+      for i in range(2)]
+
+  use_graph = bool(args.graph) and device.type == 'cuda'
+  if device.type == 'cuda':
+    copy_stream = torch.cuda.Stream(device)
+    slots = [_map_tensors(hb, lambda t: t.to(device)) for hb in host_batches]
+    if use_graph:
+      # one captured graph per staging slot (static input addresses)
+      learners_graph = []
+      learner.capture(slots[0])
+      g0 = (learner._graph, learner._static_in, learner._static_loss)
+      learner.capture(slots[1])
+      g1 = (learner._graph, learner._static_in, learner._static_loss)
+      graphs = [g0, g1]
+      slots = [g0[1], g1[1]]
+    slot_free = [torch.cuda.Event(), torch.cuda.Event()]
+    slot_ready = [torch.cuda.Event(), torch.cuda.Event()]
+    for e in slot_ready:
+      e.record()
+    for e in slot_free:
+      e.record()
+  comp = torch.cuda.current_stream(device) if device.type == 'cuda' else None
+
+  def run_step(k):
+    i = k % 2
+    if device.type != 'cuda':
+      return learner.step(host_batches[i])
+    # prefetch batch k+1 into the other slot while computing on slot i
+    j = (k + 1) % 2
+    comp.wait_event(slot_ready[i])
+    if use_graph:
+      learner._graph, learner._static_in, learner._static_loss = graphs[i]
+      loss = learner.graph_step()
+    else:
+      loss = learner.step(slots[i])
+    slot_free[i].record(comp)
+    with torch.cuda.stream(copy_stream):
+      copy_stream.wait_event(slot_free[j])
+      _copy_into(slots[j], host_batches[(k + 1) % len(host_batches)], True)
+      slot_ready[j].record(copy_stream)
+    return loss
+
+  def sync():
+    if device.type == 'cuda':
+      torch.cuda.synchronize(device)
+    if world > 1:
+      torch.distributed.barrier()
+    if device.type == 'cuda':
+      torch.cuda.synchronize(device)
+
+  for k in range(args.warmup):
+    run_step(k)
+  sync()
+  t0 = time.perf_counter()
+  for k in range(args.warmup, args.warmup + args.steps):
+    loss = run_step(k)
+  sync()
+  dt = time.perf_counter() - t0
+  if world > 1:
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+  frames = learner.frames_per_step * args.steps
+  value = frames / dt
+  ok = bool(torch.isfinite(loss).item())
+  if rank == 0:
+    rec = {
+        'metric': METRIC, 'value': round(value, 1), 'unit': 'env-frames/s',
+        'n_gpus': world if device.type == 'cuda' else 0,
+        'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(1000 * dt / args.steps, 3),
+        'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': round(value / BASELINE_FPS, 3),
+        'dtype': args.dtype, 'data': 'synthetic (random uint8 frames, '
+                                     'random-init weights)',
+        'config': {'model': 'IMPALA %s-ResNet+LSTM-256' % args.torso
+                            if args.torso == 'deep' else 'IMPALA shallow+LSTM',
+                   'global_batch': args.batch_size * world,
+                   'seq_len': args.unroll_length,
+                   'frame': '%dx%dx3' % (args.height, args.width),
+                   'parallelism': 'dp%d' % world, 'backend': backend,
+                   'hip_graph': use_graph, 'loss_finite': ok,
+                   'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
+                                   'frames/s (BASELINE.md B)'},
+    }
+    print(json.dumps(rec), flush=True)
+  parallel.cleanup()
+
+
+if __name__ == '__main__':
+  main()

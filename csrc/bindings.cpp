@@ -1,0 +1,148 @@
+// PyTorch bindings for the gfx950 kernels (module scalable_agent_amd._C).
+// Validates shapes/dtypes on the host, allocates outputs through the caching
+// allocator and launches on the current HIP stream, so every op can be
+// captured into a hipGraph (torch.cuda.CUDAGraph).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/launchers.h"
+#include "kernels/conv_launchers.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define SA_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define SA_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define SA_CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define SA_CHECK(t) SA_CHECK_CUDA(t); SA_CHECK_CONTIG(t)
+
+const uint8_t* u8ptr(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBool || t.scalar_type() == at::kByte,
+              "mask must be bool/uint8");
+  return reinterpret_cast<const uint8_t*>(t.data_ptr());
+}
+
+void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
+             at::Tensor frames, double lr0, double total_frames, double decay,
+             double momentum, double eps) {
+  SA_CHECK(w); SA_CHECK(g); SA_CHECK(ms); SA_CHECK(mom); SA_CHECK_CUDA(frames);
+  SA_CHECK_F32(w); SA_CHECK_F32(g); SA_CHECK_F32(ms); SA_CHECK_F32(mom);
+  TORCH_CHECK(frames.scalar_type() == at::kLong, "frames must be int64");
+  TORCH_CHECK(w.numel() % 4 == 0, "flat buffer must be a multiple of 4");
+  TORCH_CHECK(g.numel() == w.numel() && ms.numel() == w.numel() &&
+              mom.numel() == w.numel(), "size mismatch");
+  const c10::DeviceGuard guard(w.device());
+  sa::rmsprop_launch(w.data_ptr<float>(), g.data_ptr<float>(),
+                     ms.data_ptr<float>(), mom.data_ptr<float>(),
+                     frames.data_ptr<int64_t>(), w.numel(), (float)lr0,
+                     total_frames, (float)decay, (float)momentum, (float)eps,
+                     cur_stream());
+}
+
+std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
+                                    at::Tensor actions, at::Tensor rewards,
+                                    at::Tensor done, at::Tensor values,
+                                    at::Tensor bootstrap, double discounting,
+                                    int64_t clip_mode, double clip_rho,
+                                    double clip_pg_rho, double baseline_cost,
+                                    double entropy_cost, bool want_targets) {
+  SA_CHECK(behaviour); SA_CHECK(target); SA_CHECK(actions); SA_CHECK(rewards);
+  SA_CHECK(done); SA_CHECK(values); SA_CHECK(bootstrap);
+  SA_CHECK_F32(behaviour); SA_CHECK_F32(target); SA_CHECK_F32(rewards);
+  SA_CHECK_F32(values); SA_CHECK_F32(bootstrap);
+  TORCH_CHECK(actions.scalar_type() == at::kLong, "actions must be int64");
+  TORCH_CHECK(target.dim() == 3, "logits must be [T,B,A]");
+  const int T = target.size(0), B = target.size(1), A = target.size(2);
+  TORCH_CHECK(behaviour.sizes() == target.sizes(), "logit shape mismatch");
+  TORCH_CHECK(actions.numel() == T * B && rewards.numel() == T * B &&
+              done.numel() == T * B && values.numel() == T * B &&
+              bootstrap.numel() == B, "[T,B] shape mismatch");
+  const c10::DeviceGuard guard(target.device());
+  auto f32 = target.options();
+  auto loss = at::empty({4}, f32);
+  auto dlogits = at::empty_like(target);
+  auto dvalues = at::empty({T, B}, f32);
+  auto work = at::empty({4 * T * B}, f32);
+  at::Tensor vs, pg;
+  if (want_targets) {
+    vs = at::empty({T, B}, f32);
+    pg = at::empty({T, B}, f32);
+  }
+  sa::vtrace_loss_launch(
+      behaviour.data_ptr<float>(), target.data_ptr<float>(),
+      actions.data_ptr<int64_t>(), rewards.data_ptr<float>(), u8ptr(done),
+      values.data_ptr<float>(), bootstrap.data_ptr<float>(), T, B, A,
+      (float)discounting, (int)clip_mode, (float)clip_rho, (float)clip_pg_rho,
+      (float)baseline_cost, (float)entropy_cost, loss.data_ptr<float>(),
+      dlogits.data_ptr<float>(), dvalues.data_ptr<float>(),
+      want_targets ? vs.data_ptr<float>() : nullptr,
+      want_targets ? pg.data_ptr<float>() : nullptr, work.data_ptr<float>(),
+      cur_stream());
+  if (want_targets) return {loss, dlogits, dvalues, vs, pg};
+  return {loss, dlogits, dvalues};
+}
+
+std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
+                                 at::Tensor h0, at::Tensor w_h) {
+  SA_CHECK(xw); SA_CHECK(done); SA_CHECK(c0); SA_CHECK(h0); SA_CHECK(w_h);
+  SA_CHECK_F32(xw); SA_CHECK_F32(c0); SA_CHECK_F32(h0); SA_CHECK_F32(w_h);
+  const int T = xw.size(0), B = xw.size(1), H4 = xw.size(2), H = H4 / 4;
+  TORCH_CHECK(H == 256 || H == 64, "hidden size must be 256 or 64");
+  TORCH_CHECK(w_h.size(0) == H && w_h.size(1) == H4, "W_h must be [H,4H]");
+  TORCH_CHECK(c0.numel() == B * H && h0.numel() == B * H, "state shape");
+  TORCH_CHECK(done.numel() == T * B, "done shape");
+  const c10::DeviceGuard guard(xw.device());
+  auto hs = at::empty({T, B, H}, xw.options());
+  auto cs = at::empty({T, B, H}, xw.options());
+  auto acts = at::empty({T, B, H4}, xw.options());
+  auto s = cur_stream();
+  const uint8_t* dn = u8ptr(done);
+  for (int t = 0; t < T; ++t) {
+    const float* hp = t == 0 ? h0.data_ptr<float>() : hs[t - 1].data_ptr<float>();
+    const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
+    sa::lstm_fwd_step_launch(xw[t].data_ptr<float>(), hp, cp, dn + t * B,
+                             w_h.data_ptr<float>(), hs[t].data_ptr<float>(),
+                             cs[t].data_ptr<float>(), acts[t].data_ptr<float>(),
+                             B, H, s);
+  }
+  return {hs, cs, acts};
+}
+
+at::Tensor lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor w_h,
+                    at::Tensor acts, at::Tensor cs, at::Tensor c0) {
+  SA_CHECK(dh_out); SA_CHECK(done); SA_CHECK(w_h); SA_CHECK(acts);
+  SA_CHECK(cs); SA_CHECK(c0);
+  const int T = acts.size(0), B = acts.size(1), H4 = acts.size(2), H = H4 / 4;
+  const c10::DeviceGuard guard(acts.device());
+  auto dg = at::empty({T, B, H4}, acts.options());
+  auto carry = at::zeros({2, B, H}, acts.options());
+  auto s = cur_stream();
+  const uint8_t* dn = u8ptr(done);
+  for (int t = T - 1; t >= 0; --t) {
+    const float* dgn = t == T - 1 ? nullptr : dg[t + 1].data_ptr<float>();
+    const uint8_t* dnext = t == T - 1 ? nullptr : dn + (t + 1) * B;
+    const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
+    const float* cin = t == T - 1 ? nullptr : carry[(t + 1) & 1].data_ptr<float>();
+    sa::lstm_bwd_step_launch(dh_out[t].data_ptr<float>(), dgn, dnext, dn + t * B,
+                             w_h.data_ptr<float>(), acts[t].data_ptr<float>(),
+                             cs[t].data_ptr<float>(), cp, cin,
+                             carry[t & 1].data_ptr<float>(),
+                             dg[t].data_ptr<float>(), B, H, s);
+  }
+  return dg;
+}
+
+}  // namespace
+
+void register_conv_ops(pybind11::module& m);  // conv_bindings.cpp
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "scalable_agent_amd gfx950 HIP kernels";
+  m.def("rmsprop", &rmsprop);
+  m.def("vtrace_loss", &vtrace_loss);
+  m.def("lstm_fwd", &lstm_fwd);
+  m.def("lstm_bwd", &lstm_bwd);
+  register_conv_ops(m);
+}

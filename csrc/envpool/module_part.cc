@@ -1,0 +1,54 @@
+// pybind11 registration of the shared-memory ring (part of module _native).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <vector>
+
+#include "envpool/shm_ring.h"
+
+namespace py = pybind11;
+
+namespace sa {
+
+void register_envpool(py::module& m) {
+  py::class_<ShmRing>(m, "ShmRing", py::buffer_protocol())
+      .def(py::init<const std::string&, int64_t, int64_t, bool>(),
+           py::arg("name"), py::arg("num_slots") = 0, py::arg("slot_bytes") = 0,
+           py::arg("create") = false)
+      .def("acquire_write", [](ShmRing& r, int64_t t) {
+             py::gil_scoped_release nogil;
+             return r.AcquireWrite(t);
+           }, py::arg("timeout_ms") = -1)
+      .def("commit", &ShmRing::Commit)
+      .def("acquire_read", [](ShmRing& r, int64_t t) {
+             py::gil_scoped_release nogil;
+             return r.AcquireRead(t);
+           }, py::arg("timeout_ms") = -1)
+      .def("acquire_read_many", [](ShmRing& r, int64_t n, int64_t t) {
+             std::vector<int64_t> out(static_cast<size_t>(n));
+             int64_t got;
+             {
+               py::gil_scoped_release nogil;
+               got = r.AcquireReadMany(n, out.data(), t);
+             }
+             if (got < 0) return py::object(py::int_(got));
+             out.resize(static_cast<size_t>(got));
+             return py::object(py::cast(out));
+           }, py::arg("n"), py::arg("timeout_ms") = -1)
+      .def("release", &ShmRing::Release)
+      .def("close", &ShmRing::Close)
+      .def_property_readonly("closed", &ShmRing::closed)
+      .def_property_readonly("num_slots", &ShmRing::num_slots)
+      .def_property_readonly("slot_bytes", &ShmRing::slot_bytes)
+      .def_property_readonly("num_ready", &ShmRing::num_ready)
+      .def_property_readonly("name", &ShmRing::name)
+      .def("slot_address", [](ShmRing& r, int64_t s) {
+             return reinterpret_cast<uintptr_t>(r.slot_data(s));
+           })
+      .def("slot_view", [](ShmRing& r, int64_t s) {
+             return py::memoryview::from_memory(r.slot_data(s), r.slot_bytes(), false);
+           }, py::keep_alive<0, 1>())
+      .def_static("unlink", &ShmRing::Unlink);
+}
+
+}  // namespace sa

@@ -1,0 +1,92 @@
+"""Synthetic environment and synthetic trajectory batches.
+
+The image has neither DeepMind Lab nor ViZDoom, so a synthetic env is the
+first-class fake backend and the benchmark data source:
+random uint8 frames of a configurable shape, random rewards, geometric episode
+lengths, an optional instruction string.  Interface = the reference env
+protocol (`initial()`, `step(action)`, `close()`, environments.py:66-140).
+"""
+
+import numpy as np
+import torch
+
+from ..structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
+
+
+class SyntheticEnv(object):
+  """Random-frame env with the PyProcessDmLab interface."""
+
+  def __init__(self, level='synthetic', config=None, num_action_repeats=4,
+               seed=1, frame_shape=(72, 96, 3), episode_length=200,
+               instruction='', num_actions=9, frame_pool=16):
+    config = config or {}
+    self._rng = np.random.RandomState(seed)
+    self._repeats = num_action_repeats
+    self._shape = tuple(frame_shape)
+    self._p_done = 1.0 / max(1, episode_length)
+    self._instruction = instruction
+    self.num_actions = num_actions
+    self.benchmark_mode = bool(config.get('benchmark_mode', 0))
+    # a pool of pre-generated frames keeps the env cheap (throughput tests)
+    self._frames = self._rng.randint(
+        0, 256, size=(frame_pool,) + self._shape, dtype=np.uint8)
+    self._t = 0
+    self.closed = False
+
+  def _obs(self):
+    self._t += 1
+    return [self._frames[self._t % len(self._frames)], self._instruction]
+
+  def initial(self):
+    return self._obs()
+
+  def step(self, action):
+    reward = np.float32(self._rng.randint(-1, 2) * (self._rng.rand() < 0.1))
+    done = np.array(self._rng.rand() < self._p_done)
+    return reward, done, self._obs()
+
+  def close(self):
+    self.closed = True
+
+  @staticmethod
+  def _tensor_specs(method_name, unused_kwargs, constructor_kwargs):
+    shape = tuple(constructor_kwargs.get('frame_shape', (72, 96, 3)))
+    obs = [(shape, np.uint8), ((), object)]
+    if method_name == 'initial':
+      return obs
+    elif method_name == 'step':
+      return (((), np.float32), ((), np.bool_), obs)
+
+
+def make_synthetic_batch(batch_size, unroll_length, frame_shape, num_actions,
+                         seed=0, pin_memory=False, device='cpu',
+                         done_prob=0.005, core_size=256):
+  """A time-major ActorOutput with T+1 steps of synthetic data."""
+  g = torch.Generator().manual_seed(seed)
+  T1, B = unroll_length + 1, batch_size
+  frame = torch.randint(0, 256, (T1, B) + tuple(frame_shape), generator=g,
+                        dtype=torch.uint8)
+  reward = (torch.randint(-1, 2, (T1, B), generator=g).float() *
+            (torch.rand(T1, B, generator=g) < 0.1).float())
+  done = torch.rand(T1, B, generator=g) < done_prob
+  done[0] = True
+  ep_ret = torch.randn(T1, B, generator=g)
+  ep_step = torch.randint(0, 1000, (T1, B), generator=g, dtype=torch.int32)
+  action = torch.randint(0, num_actions, (T1, B), generator=g,
+                         dtype=torch.int64)
+  logits = torch.randn(T1, B, num_actions, generator=g)
+  baseline = torch.randn(T1, B, generator=g)
+  c = torch.randn(B, core_size, generator=g) * 0.1
+  h = torch.randn(B, core_size, generator=g) * 0.1
+  out = ActorOutput(
+      level_name='synthetic', agent_state=(c, h),
+      env_outputs=StepOutput(reward, StepOutputInfo(ep_ret, ep_step), done,
+                             (frame, None)),
+      agent_outputs=AgentOutput(action, logits, baseline))
+  if pin_memory or device != 'cpu':
+    from ..learner import _map_tensors
+    if pin_memory:
+      out = _map_tensors(out, lambda t: t.pin_memory())
+    if device != 'cpu':
+      out = _map_tensors(out, lambda t: t.to(device))
+  return out

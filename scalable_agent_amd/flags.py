@@ -1,0 +1,131 @@
+"""Command-line flags of the IMPALA engine.
+
+Reproduces the flag surface of the reference `experiment.py:46-95` (same names,
+same defaults, `--flag=value` syntax) and adds the MI355X-native knobs listed in
+SURVEY.md §5.6 (torso choice, synthetic env, data-parallel learners, dtype,
+inference batching, PopArt, fault injection).
+
+absl is not installed in this image, so the parser is argparse; argparse accepts
+both `--flag=value` and `--flag value`.
+"""
+
+import argparse
+import dataclasses
+from typing import List, Optional
+
+
+def _str2bool(v):
+  if isinstance(v, bool):
+    return v
+  v = str(v).lower()
+  if v in ('1', 'true', 't', 'yes', 'y'):
+    return True
+  if v in ('0', 'false', 'f', 'no', 'n'):
+    return False
+  raise argparse.ArgumentTypeError('boolean expected, got %r' % v)
+
+
+def build_parser() -> argparse.ArgumentParser:
+  p = argparse.ArgumentParser(
+      description='MI355X-native IMPALA (scalable_agent capabilities).')
+  # --- reference flags (experiment.py:49-95) ---
+  p.add_argument('--logdir', default='/tmp/agent', help='Log/checkpoint dir.')
+  p.add_argument('--mode', default='train', choices=['train', 'test'])
+  p.add_argument('--test_num_episodes', type=int, default=10,
+                 help='Number of episodes per level.')
+  p.add_argument('--task', type=int, default=-1,
+                 help='Task id. Use -1 for local training.')
+  p.add_argument('--job_name', default='learner', choices=['learner', 'actor'],
+                 help='Job name. Ignored when task is set to -1.')
+  p.add_argument('--total_environment_frames', type=int, default=int(1e9))
+  p.add_argument('--num_actors', type=int, default=4)
+  p.add_argument('--batch_size', type=int, default=2)
+  p.add_argument('--unroll_length', type=int, default=100)
+  p.add_argument('--num_action_repeats', type=int, default=4)
+  p.add_argument('--seed', type=int, default=1)
+  p.add_argument('--entropy_cost', type=float, default=0.00025)
+  p.add_argument('--baseline_cost', type=float, default=.5)
+  p.add_argument('--discounting', type=float, default=.99)
+  p.add_argument('--reward_clipping', default='abs_one',
+                 choices=['abs_one', 'soft_asymmetric'])
+  p.add_argument('--dataset_path', default='')
+  p.add_argument('--level_name', default='explore_goal_locations_small')
+  p.add_argument('--width', type=int, default=96)
+  p.add_argument('--height', type=int, default=72)
+  p.add_argument('--renderer', default='software')
+  p.add_argument('--benchmark_mode', type=int, default=0)
+  p.add_argument('--learning_rate', type=float, default=0.00048)
+  p.add_argument('--decay', type=float, default=.99)
+  p.add_argument('--momentum', type=float, default=0.)
+  p.add_argument('--epsilon', type=float, default=.1)
+  # --- MI355X-native additions ---
+  p.add_argument('--torso', default='shallow', choices=['shallow', 'deep'],
+                 help='shallow = experiment.py:178-183 (active in reference); '
+                      'deep = IMPALA ResNet experiment.py:156-176.')
+  p.add_argument('--env', default='auto',
+                 choices=['auto', 'synthetic', 'dmlab', 'doom'],
+                 help='auto: doom_* -> doom, synthetic* -> synthetic, else dmlab.')
+  p.add_argument('--obs_shape', default='',
+                 help='Synthetic env frame shape HxWxC (default height x width x 3).')
+  p.add_argument('--synthetic_episode_length', type=int, default=200,
+                 help='Mean (geometric) episode length of the synthetic env.')
+  p.add_argument('--num_learners', type=int, default=1,
+                 help='Data-parallel learners (one per GPU, RCCL all-reduce).')
+  p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
+                 help='sum: N learners x B == one learner with N*B (reference '
+                      'losses are sums).')
+  p.add_argument('--dtype', default='bf16', choices=['fp32', 'bf16'],
+                 help='Compute dtype of convs/GEMMs (V-trace/loss/optimizer '
+                      'state always fp32).')
+  p.add_argument('--device', default='auto',
+                 help='auto | cpu | cuda | cuda:N')
+  p.add_argument('--inference_min_batch', type=int, default=1)
+  p.add_argument('--inference_max_batch', type=int, default=1024)
+  p.add_argument('--inference_timeout_ms', type=int, default=100)
+  p.add_argument('--inference_device', default='auto',
+                 help='Device for actor inference (auto = learner device).')
+  p.add_argument('--actor_processes', type=int, default=0,
+                 help='0: envs run in py_process workers driven by actor '
+                      'threads (reference single-machine mode).')
+  p.add_argument('--popart', type=_str2bool, default=False,
+                 help='PopArt value normalisation (north-star config #4).')
+  p.add_argument('--popart_beta', type=float, default=3e-4)
+  p.add_argument('--save_checkpoint_secs', type=float, default=600)
+  p.add_argument('--save_summaries_secs', type=float, default=30)
+  p.add_argument('--keep_checkpoints', type=int, default=5)
+  p.add_argument('--log_every_frames', type=int, default=50000,
+                 help='Throughput log period (reference log_step_count_steps).')
+  p.add_argument('--use_hip_graph', type=_str2bool, default=True)
+  p.add_argument('--fault_inject', default='',
+                 help='e.g. env_crash:0.01,actor_stall:50 (tests only).')
+  p.add_argument('--deterministic', type=_str2bool, default=False)
+  p.add_argument('--max_learner_steps', type=int, default=0,
+                 help='Stop after N learner steps (0 = frames limit only).')
+  p.add_argument('--queue_timeout_secs', type=float, default=600.,
+                 help='Learner starvation timeout (diagnostic failure).')
+  return p
+
+
+def parse_flags(argv: Optional[List[str]] = None):
+  """Parses argv (without program name) and returns an argparse Namespace."""
+  parser = build_parser()
+  flags, unknown = parser.parse_known_args(argv)
+  if unknown:
+    raise SystemExit('Unknown flags: %s' % ' '.join(unknown))
+  return flags
+
+
+def default_flags(**overrides):
+  """Default flags with keyword overrides (library/test convenience)."""
+  flags = parse_flags([])
+  for k, v in overrides.items():
+    if not hasattr(flags, k):
+      raise AttributeError('unknown flag %s' % k)
+    setattr(flags, k, v)
+  return flags
+
+
+def frames_per_step(flags, world_size=1):
+  """Env frames consumed per learner step (experiment.py:419-420)."""
+  return (flags.batch_size * flags.unroll_length * flags.num_action_repeats *
+          world_size)

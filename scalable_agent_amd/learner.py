@@ -1,0 +1,187 @@
+"""IMPALA learner: re-unroll, V-trace, losses, TF-RMSProp, frame counter.
+
+Semantics follow `build_learner` (experiment.py:346-427):
+  1. unroll the agent over all T+1 steps from the unroll-start LSTM state;
+  2. bootstrap from baseline[T]; shift agent/env outputs by one step;
+  3. clip rewards (abs_one | soft_asymmetric); discounts = (~done) * gamma;
+  4. V-trace from logits (rho_bar = c_bar = rho_bar_pg = 1);
+  5. loss = PG + baseline_cost * 0.5 sum(adv^2) + entropy_cost * (-sum H);
+  6. RMSProp with LR linearly decayed by the env-frame counter;
+  7. frames += B * T * repeats * world_size.
+
+MI355X execution: everything runs on the GPU (the reference pins V-trace to
+the CPU, experiment.py:386-397).  With the HIP backend the V-trace + loss +
+their gradients are one fused kernel, the optimizer is one fused kernel over a
+flat parameter buffer, and the whole fwd+bwd+optimizer step is captured into a
+HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) replayed per step from
+static staging slots; the data-parallel gradient sum is one RCCL all-reduce on
+the flat gradient buffer.
+"""
+
+import time
+
+import torch
+
+from . import losses as losses_lib
+from . import vtrace as vtrace_lib
+from .optim import FlatParams, RMSProp
+from .structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
+
+
+def compute_loss(agent, data, flags, use_fused=False):
+  """Total loss for one time-major batch (ActorOutput of tensors)."""
+  env_outputs = data.env_outputs
+  agent_outputs = data.agent_outputs
+  learner_outputs, _ = agent.unroll(agent_outputs.action, env_outputs,
+                                    data.agent_state, sample=False)
+  bootstrap_value = learner_outputs.baseline[-1]
+
+  behaviour_logits = agent_outputs.policy_logits[1:]
+  actions = agent_outputs.action[1:]
+  rewards = env_outputs.reward[1:]
+  done = env_outputs.done[1:]
+  target_logits = learner_outputs.policy_logits[:-1]
+  values = learner_outputs.baseline[:-1]
+
+  if use_fused:
+    from . import ops
+    return ops.vtrace_loss(
+        behaviour_logits, target_logits, actions, rewards, done, values,
+        bootstrap_value, discounting=flags.discounting,
+        reward_clipping=flags.reward_clipping,
+        baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost)
+
+  clipped_rewards = losses_lib.clip_rewards(rewards, flags.reward_clipping)
+  discounts = (~done.to(torch.bool)).to(torch.float32) * flags.discounting
+  vt = vtrace_lib.from_logits(
+      behaviour_policy_logits=behaviour_logits,
+      target_policy_logits=target_logits, actions=actions,
+      discounts=discounts, rewards=clipped_rewards, values=values,
+      bootstrap_value=bootstrap_value)
+  total = losses_lib.compute_policy_gradient_loss(target_logits, actions,
+                                                  vt.pg_advantages)
+  total = total + flags.baseline_cost * losses_lib.compute_baseline_loss(
+      vt.vs - values)
+  total = total + flags.entropy_cost * losses_lib.compute_entropy_loss(
+      target_logits)
+  return total
+
+
+def batch_to_device(data, device, non_blocking=True):
+  """Moves a nested ActorOutput of tensors (or None/strings) to `device`."""
+  def mv(x):
+    if torch.is_tensor(x):
+      return x.to(device, non_blocking=non_blocking)
+    if isinstance(x, tuple):
+      return type(x)(*[mv(e) for e in x]) if hasattr(x, '_fields') else tuple(
+          mv(e) for e in x)
+    return x
+  return mv(data)
+
+
+class Learner:
+  """Owns the agent's flat parameters, optimizer state and frame counter."""
+
+  def __init__(self, agent, flags, device, process_group=None, world_size=1):
+    self.flags = flags
+    self.device = torch.device(device)
+    self.agent = agent.to(self.device)
+    self.flat = FlatParams(self.agent)
+    use_hip = getattr(agent, 'backend', 'torch') == 'hip'
+    self.use_fused = use_hip
+    self.opt = RMSProp(self.flat, flags.learning_rate, flags.decay,
+                       flags.momentum, flags.epsilon,
+                       flags.total_environment_frames, use_hip=use_hip)
+    self.frames = torch.zeros((), dtype=torch.int64, device=self.device)
+    self.world_size = world_size
+    self.pg = process_group
+    self.frames_per_step = (flags.batch_size * flags.unroll_length *
+                            flags.num_action_repeats * world_size)
+    self.last_loss = None
+    self._graph = None
+    self._static_in = None
+    self._static_loss = None
+    self.grad_sync = None
+    if world_size > 1:
+      from .parallel import GradientSynchronizer
+      self.grad_sync = GradientSynchronizer(self.flat, process_group,
+                                            reduce=flags.grad_reduce)
+
+  # ------------------------------------------------------------ eager step
+  def _fwd_bwd(self, data):
+    self.flat.zero_grad()
+    loss = compute_loss(self.agent, data, self.flags, self.use_fused)
+    loss.backward()
+    return loss
+
+  def _apply(self):
+    if self.grad_sync is not None:
+      self.grad_sync.all_reduce()
+    self.opt.step(self.frames)
+    self.frames.add_(self.frames_per_step)
+
+  def step(self, data):
+    """One learner update from a device-resident time-major batch."""
+    loss = self._fwd_bwd(data)
+    self.flat.rebind_grads()
+    self._apply()
+    self.last_loss = loss.detach()
+    return self.last_loss
+
+  # ------------------------------------------------------------ graph step
+  def capture(self, example, warmup=2):
+    """Captures fwd+bwd into a HIP graph on static input slots."""
+    assert self.device.type == 'cuda'
+    self._static_in = batch_to_device(example, self.device)
+    # clone so the static slot owns its memory
+    self._static_in = _map_tensors(self._static_in, lambda t: t.clone())
+    s = torch.cuda.Stream(self.device)
+    s.wait_stream(torch.cuda.current_stream(self.device))
+    saved_p = self.flat.params.clone()
+    with torch.cuda.stream(s):
+      for _ in range(warmup):
+        self._fwd_bwd(self._static_in)
+    torch.cuda.current_stream(self.device).wait_stream(s)
+    self.flat.rebind_grads()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+      self._static_loss = self._fwd_bwd(self._static_in)
+    self.flat.params.copy_(saved_p)
+    self._graph = g
+
+  def load_static(self, data, non_blocking=True):
+    _copy_into(self._static_in, data, non_blocking)
+
+  def graph_step(self):
+    self._graph.replay()
+    self._apply()
+    self.last_loss = self._static_loss
+    return self._static_loss
+
+  # ------------------------------------------------------------ state
+  def state_dict(self):
+    return {'params': self.flat.state_dict(), 'opt': self.opt.state_dict(),
+            'frames': int(self.frames.item())}
+
+  def load_state_dict(self, sd):
+    self.flat.load_state_dict(sd['params'])
+    self.opt.load_state_dict(sd['opt'])
+    self.frames.fill_(int(sd['frames']))
+
+
+def _map_tensors(x, fn):
+  if torch.is_tensor(x):
+    return fn(x)
+  if isinstance(x, tuple):
+    vals = [_map_tensors(e, fn) for e in x]
+    return type(x)(*vals) if hasattr(x, '_fields') else tuple(vals)
+  return x
+
+
+def _copy_into(dst, src, non_blocking):
+  if torch.is_tensor(dst):
+    dst.copy_(src, non_blocking=non_blocking)
+    return
+  if isinstance(dst, tuple):
+    for d, s in zip(dst, src):
+      _copy_into(d, s, non_blocking)

@@ -1,0 +1,297 @@
+"""IMPALA agent: conv torso -> LSTM-256 core -> policy/baseline heads.
+
+Behaviour parity with the reference `Agent` (experiment.py:109-237):
+  * torso (experiment.py:148-198): uint8 frame / 255, conv stack, ReLU,
+    flatten, Linear(256), ReLU, concat [torso, clip(reward,-1,1),
+    one_hot(last_action), instruction_encoding];
+      - 'shallow' (active in the reference, :178-183): 32x8x8/4, 64x4x4/2,
+        128x3x3/2, all TF-SAME;
+      - 'deep' (IMPALA ResNet, commented out at :156-176, required by the north
+        star): 3 stages of conv3x3 -> maxpool3x3/2 SAME -> 2 x residual block;
+  * instruction encoder (:123-146): hashed words -> Embed(1000,20) ->
+    LSTM(64) -> last valid output (zeros for an empty instruction);
+  * core (:118, :228-235): LSTMBlockCell(256), state reset to zero *before*
+    the step whenever done[t] is set;
+  * heads (:200-210): Linear(A) logits, Linear(1) baseline, multinomial sample.
+
+The module is backend-switchable: `backend='torch'` is the pure-PyTorch oracle
+(CPU or GPU), `backend='hip'` routes every hot op through the hand-written
+CDNA4 kernels in `scalable_agent_amd.ops` (fails loudly if they are missing).
+Parameters are fp32 master weights in TF layouts (see models/layers.py).
+"""
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..structs import AgentOutput
+from . import layers
+
+CORE_SIZE = 256
+INSTR_BUCKETS = 1000
+INSTR_EMBED = 20
+INSTR_LSTM = 64
+
+
+def _hip_torso_ready():
+  from ..ops import conv
+  return conv.TORSO_READY
+
+
+def hip_ops_in_use(agent):
+  """Names of the ops this agent runs on hand-written HIP kernels."""
+  if agent.backend != 'hip':
+    return []
+  ops = ['lstm_recurrence', 'vtrace_loss', 'rmsprop']
+  if _hip_torso_ready():
+    ops += ['conv_torso', 'linear']
+  return ops
+
+
+def torso_spec(torso, frame_shape):
+  """Returns (conv layer specs, flattened feature size).
+
+  Each spec: dict(kind='conv'|'pool'|'res', ...). Used by both backends.
+  """
+  h, w, c = frame_shape
+  specs = []
+  if torso == 'shallow':
+    for i, (ch, k, s) in enumerate([(32, 8, 4), (64, 4, 2), (128, 3, 2)]):
+      name = 'conv_2d' if i == 0 else 'conv_2d_%d' % i
+      specs.append(dict(kind='conv', name=name, cin=c, cout=ch, k=k, s=s,
+                        relu_out=True))
+      h, w, c = layers.same_out(h, s), layers.same_out(w, s), ch
+  elif torso == 'deep':
+    n_conv = 0
+    for i, (ch, nblocks) in enumerate([(16, 2), (32, 2), (32, 2)]):
+      name = 'conv_2d' if n_conv == 0 else 'conv_2d_%d' % n_conv
+      n_conv += 1
+      specs.append(dict(kind='conv', name=name, cin=c, cout=ch, k=3, s=1,
+                        relu_out=False))
+      specs.append(dict(kind='pool'))
+      h, w, c = layers.same_out(h, 2), layers.same_out(w, 2), ch
+      for j in range(nblocks):
+        specs.append(dict(kind='res', name='residual_%d_%d' % (i, j), ch=ch))
+  else:
+    raise ValueError('unknown torso %r' % torso)
+  return specs, h * w * c, (h, w, c)
+
+
+class Agent(nn.Module):
+  """IMPALA agent (see module docstring)."""
+
+  def __init__(self, num_actions, torso='shallow', frame_shape=(72, 96, 3),
+               seed=None, backend='torch', compute_dtype=torch.float32):
+    super().__init__()
+    self.num_actions = num_actions
+    self.torso_kind = torso
+    self.frame_shape = tuple(frame_shape)
+    self.backend = backend
+    self.compute_dtype = compute_dtype
+    gen = None
+    if seed is not None:
+      gen = torch.Generator().manual_seed(int(seed))
+
+    self.specs, flat, self.conv_out_shape = torso_spec(torso, self.frame_shape)
+    self.flat_size = flat
+    self.convnet = nn.ParameterDict()
+    for sp in self.specs:
+      if sp['kind'] == 'conv':
+        w = nn.Parameter(torch.empty(sp['k'], sp['k'], sp['cin'], sp['cout']))
+        layers.sonnet_linear_init_(w.data, gen)
+        self.convnet[sp['name'] + '__w'] = w
+        self.convnet[sp['name'] + '__b'] = nn.Parameter(torch.zeros(sp['cout']))
+      elif sp['kind'] == 'res':
+        for sub in ('conv_2d', 'conv_2d_1'):
+          w = nn.Parameter(torch.empty(3, 3, sp['ch'], sp['ch']))
+          layers.sonnet_linear_init_(w.data, gen)
+          self.convnet[sp['name'] + '__' + sub + '__w'] = w
+          self.convnet[sp['name'] + '__' + sub + '__b'] = nn.Parameter(
+              torch.zeros(sp['ch']))
+
+    self.linear_w = nn.Parameter(
+        layers.sonnet_linear_init_(torch.empty(flat, CORE_SIZE), gen))
+    self.linear_b = nn.Parameter(torch.zeros(CORE_SIZE))
+
+    self.embed = nn.Parameter(
+        layers.truncated_normal_(torch.empty(INSTR_BUCKETS, INSTR_EMBED),
+                                 1.0, gen))
+    self.language_lstm_kernel = nn.Parameter(layers.glorot_uniform_(
+        torch.empty(INSTR_EMBED + INSTR_LSTM, 4 * INSTR_LSTM), gen))
+    self.language_lstm_bias = nn.Parameter(torch.zeros(4 * INSTR_LSTM))
+
+    self.core_input_size = CORE_SIZE + 1 + num_actions + INSTR_LSTM
+    self.lstm_kernel = nn.Parameter(layers.glorot_uniform_(
+        torch.empty(self.core_input_size + CORE_SIZE, 4 * CORE_SIZE), gen))
+    self.lstm_bias = nn.Parameter(torch.zeros(4 * CORE_SIZE))
+
+    self.policy_w = nn.Parameter(
+        layers.sonnet_linear_init_(torch.empty(CORE_SIZE, num_actions), gen))
+    self.policy_b = nn.Parameter(torch.zeros(num_actions))
+    self.baseline_w = nn.Parameter(
+        layers.sonnet_linear_init_(torch.empty(CORE_SIZE, 1), gen))
+    self.baseline_b = nn.Parameter(torch.zeros(1))
+
+  # ------------------------------------------------------------------ naming
+  def tf_variable_names(self):
+    """Maps parameter names to reference-style TF variable names (§7.4)."""
+    out = {}
+    for name, _ in self.named_parameters():
+      if name.startswith('convnet.'):
+        tf = 'agent/convnet/' + name[len('convnet.'):].replace('__', '/')
+      else:
+        tf = {
+            'linear_w': 'agent/linear/w', 'linear_b': 'agent/linear/b',
+            'embed': 'agent/embed/embeddings',
+            'language_lstm_kernel': 'agent/language_lstm/kernel',
+            'language_lstm_bias': 'agent/language_lstm/bias',
+            'lstm_kernel': 'agent/lstm_cell/kernel',
+            'lstm_bias': 'agent/lstm_cell/bias',
+            'policy_w': 'agent/policy_logits/w',
+            'policy_b': 'agent/policy_logits/b',
+            'baseline_w': 'agent/baseline/w',
+            'baseline_b': 'agent/baseline/b'}[name]
+      out[name] = tf
+    return out
+
+  def initial_state(self, batch_size, device=None):
+    device = device or self.lstm_bias.device
+    z = torch.zeros(batch_size, CORE_SIZE, device=device)
+    return (z, z.clone())
+
+  # ------------------------------------------------------------------ torso
+  def _conv_params(self, name):
+    return self.convnet[name + '__w'], self.convnet[name + '__b']
+
+  def conv_features(self, frames):
+    """frames uint8 [N,H,W,C] -> flattened conv features [N, flat]."""
+    if self.backend == 'hip' and _hip_torso_ready():
+      from .. import ops
+      return ops.torso_forward(self, frames)
+    x = frames.to(torch.float32) / 255.0
+    cdt = self.compute_dtype
+    if cdt != torch.float32:
+      x = x.to(cdt)
+    for sp in self.specs:
+      if sp['kind'] == 'conv':
+        w, b = self._conv_params(sp['name'])
+        x = layers.conv2d_same_nhwc(x, w.to(x.dtype), b.to(x.dtype), sp['s'])
+        if sp['relu_out']:
+          x = F.relu(x)
+      elif sp['kind'] == 'pool':
+        x = layers.maxpool_same_nhwc(x, 3, 2)
+      else:
+        block_in = x
+        for sub in ('conv_2d', 'conv_2d_1'):
+          w, b = self._conv_params(sp['name'] + '__' + sub)
+          x = F.relu(x)
+          x = layers.conv2d_same_nhwc(x, w.to(x.dtype), b.to(x.dtype), 1)
+        x = x + block_in
+    x = F.relu(x)
+    return x.reshape(x.shape[0], -1)
+
+  def torso_fc(self, feats):
+    if self.backend == 'hip' and _hip_torso_ready():
+      from .. import ops
+      return ops.linear_relu(feats, self.linear_w, self.linear_b)
+    w = self.linear_w.to(feats.dtype)
+    b = self.linear_b.to(feats.dtype)
+    return F.relu(feats @ w + b).to(torch.float32)
+
+  def instruction_encoding(self, instr, n, device):
+    """instr: None or (ids [N,L] int64, lengths [N] int64) -> [N, 64]."""
+    if instr is None:
+      return torch.zeros(n, INSTR_LSTM, device=device)
+    ids, lengths = instr
+    ids = ids.reshape(n, -1).to(device)
+    lengths = lengths.reshape(n).to(device)
+    if lengths.numel() == 0 or int(lengths.max()) == 0:
+      return torch.zeros(n, INSTR_LSTM, device=device)
+    emb = F.embedding(ids, self.embed)  # [N, L, 20]
+    c = torch.zeros(n, INSTR_LSTM, device=device)
+    h = torch.zeros_like(c)
+    out = torch.zeros_like(c)
+    for t in range(ids.shape[1]):
+      h, c = layers.lstm_block_cell(emb[:, t], c, h, self.language_lstm_kernel,
+                                    self.language_lstm_bias)
+      out = torch.where((lengths - 1 == t).unsqueeze(-1), h, out)
+    return out
+
+  def core_inputs(self, frames, rewards, last_actions, instr):
+    """Builds the LSTM core input [N, 256+1+A+64] (experiment.py:185-198)."""
+    n = frames.shape[0]
+    feats = self.conv_features(frames)
+    torso_out = self.torso_fc(feats)
+    clipped_reward = torch.clamp(rewards.reshape(n, 1).to(torch.float32), -1, 1)
+    one_hot = F.one_hot(last_actions.reshape(n).long(),
+                        self.num_actions).to(torch.float32)
+    instr_out = self.instruction_encoding(instr, n, frames.device)
+    return torch.cat([torso_out, clipped_reward, one_hot, instr_out], dim=1)
+
+  # ------------------------------------------------------------------ core
+  def core_unroll(self, x, done, state):
+    """x [T,B,F], done [T,B] bool, state (c,h) -> (h_all [T,B,256], state)."""
+    if self.backend == 'hip':
+      from .. import ops
+      return ops.lstm_unroll(x, done, state, self.lstm_kernel, self.lstm_bias)
+    c, h = state
+    T = x.shape[0]
+    kx = self.lstm_kernel[:self.core_input_size]
+    kh = self.lstm_kernel[self.core_input_size:]
+    xw = torch.matmul(x, kx) + self.lstm_bias  # one GEMM for all steps
+    outs = []
+    for t in range(T):
+      keep = (~done[t]).to(torch.float32).unsqueeze(-1)
+      c = c * keep
+      h = h * keep
+      gates = xw[t] + h @ kh
+      i, ci, f, o = gates.chunk(4, dim=-1)
+      c = torch.tanh(ci) * torch.sigmoid(i) + c * torch.sigmoid(f + 1.0)
+      h = torch.tanh(c) * torch.sigmoid(o)
+      outs.append(h)
+    return torch.stack(outs), (c, h)
+
+  def heads(self, core_out):
+    logits = core_out @ self.policy_w + self.policy_b
+    baseline = (core_out @ self.baseline_w + self.baseline_b).squeeze(-1)
+    return logits, baseline
+
+  # ------------------------------------------------------------------ API
+  def unroll(self, actions, env_outputs, core_state, sample=True,
+             generator=None):
+    """Unrolls over T steps (experiment.py:219-237).
+
+    actions: [T,B] last actions; env_outputs: StepOutput with [T,B,...]
+    fields whose observation is (frame uint8 [T,B,H,W,C], instr or None).
+    """
+    reward, _, done, (frame, instr) = env_outputs
+    T, B = actions.shape[0], actions.shape[1]
+    frames = frame.reshape((T * B,) + tuple(frame.shape[2:]))
+    if instr is not None:
+      instr = (instr[0].reshape(T * B, -1), instr[1].reshape(T * B))
+    x = self.core_inputs(frames, reward.reshape(T * B),
+                         actions.reshape(T * B), instr)
+    x = x.view(T, B, -1)
+    done = done.to(torch.bool).view(T, B)
+    core_out, core_state = self.core_unroll(x, done, core_state)
+    logits, baseline = self.heads(core_out)
+    if sample:
+      probs = torch.softmax(logits.reshape(T * B, -1).float(), -1)
+      action = torch.multinomial(probs, 1, generator=generator).view(T, B)
+    else:
+      action = None
+    return AgentOutput(action, logits, baseline), core_state
+
+  def step(self, last_action, env_output, core_state, generator=None):
+    """Single batched step for actors: inputs [B,...] -> outputs [B,...]."""
+    exp = lambda t: None if t is None else t.unsqueeze(0)
+    reward, info, done, (frame, instr) = env_output
+    if instr is not None:
+      instr = (instr[0].unsqueeze(0), instr[1].unsqueeze(0))
+    eo = (exp(reward), info, exp(done), (exp(frame), instr))
+    out, state = self.unroll(exp(last_action), eo, core_state,
+                             generator=generator)
+    return AgentOutput(out.action[0], out.policy_logits[0],
+                       out.baseline[0]), state

@@ -1,0 +1,14 @@
+"""Hand-written CDNA4 (gfx950) HIP kernels for the learner/actor hot path.
+
+Every op here is backed by the in-tree extension `scalable_agent_amd/_C*.so`
+built from `csrc/kernels/*.hip` by `csrc/build.py` (hipcc --offload-arch=gfx950,
+no hipify, no CUDA shims).  On a GPU the ops FAIL LOUDLY if the extension is
+missing; the pure-PyTorch oracles they are tested against live next to the
+callers (models/layers.py, vtrace.py, losses.py, optim.py).
+"""
+
+from ._ext import available, load, ext  # noqa: F401
+from .rmsprop import rmsprop_step  # noqa: F401
+from .vtrace_loss import vtrace_loss, vtrace_fused_forward  # noqa: F401
+from .lstm import lstm_unroll  # noqa: F401
+from .conv import torso_forward, linear_relu  # noqa: F401

@@ -1,0 +1,152 @@
+"""V-trace off-policy actor-critic targets (Espeholt et al., IMPALA).
+
+Public API parity with the reference `vtrace.py`:
+  * `log_probs_from_logits_and_actions`   vtrace.py:45-68
+  * `from_logits`                         vtrace.py:71-161
+  * `from_importance_weights`             vtrace.py:164-280
+
+This module is the *semantic reference* (pure PyTorch, any device, any extra
+trailing dims).  The learner hot path uses the fused HIP kernel in
+`scalable_agent_amd.ops.vtrace_loss`, which is parity-tested against this file.
+
+The reverse recursion `acc_t = delta_t + discount_t * c_t * acc_{t+1}` is a
+serial scan over T in the reference (`tf.scan(..., parallel_iterations=1)`,
+vtrace.py:250-262).  Here it is evaluated as an associative affine scan
+(a, b) o (a', b') = (a a', b + a b') in O(log T) depth with torch ops, which is
+exact up to fp32 reassociation.
+"""
+
+import torch
+
+from .structs import VTraceFromLogitsReturns, VTraceReturns
+
+
+def _as_f32(x, device=None):
+  t = torch.as_tensor(x, device=device)
+  return t.to(torch.float32)
+
+
+def _check_rank(t, rank, name):
+  if t.dim() != rank:
+    raise ValueError('Shape of %s must have rank %d, but has rank %d (shape %s)'
+                     % (name, rank, t.dim(), tuple(t.shape)))
+
+
+def log_probs_from_logits_and_actions(policy_logits, actions):
+  """log pi(a_t | x_t) for a softmax policy.
+
+  Args:
+    policy_logits: float [T, B, NUM_ACTIONS].
+    actions: int [T, B].
+  Returns:
+    float32 [T, B].
+  """
+  policy_logits = _as_f32(policy_logits)
+  actions = torch.as_tensor(actions, device=policy_logits.device).long()
+  _check_rank(policy_logits, 3, 'policy_logits')
+  _check_rank(actions, 2, 'actions')
+  log_p = torch.log_softmax(policy_logits, dim=-1)
+  return log_p.gather(-1, actions.unsqueeze(-1)).squeeze(-1)
+
+
+def _reverse_affine_scan(a, b):
+  """acc_t = b_t + a_t * acc_{t+1}, acc_T = 0, computed for t = T-1..0.
+
+  Hillis-Steele doubling over the time axis (dim 0): O(log T) passes.
+  """
+  a = a.clone()
+  b = b.clone()
+  T = a.shape[0]
+  shift = 1
+  while shift < T:
+    # Combine element t with element t+shift (which summarises t+shift..).
+    b_next = torch.zeros_like(b)
+    a_next = torch.zeros_like(a)
+    b_next[:T - shift] = b[shift:]
+    a_next[:T - shift] = a[shift:]
+    # positions beyond the end act as identity (a=0 contribution of zero acc)
+    b = b + a * b_next
+    a = a * a_next
+    shift *= 2
+  return b
+
+
+def from_importance_weights(log_rhos, discounts, rewards, values,
+                            bootstrap_value, clip_rho_threshold=1.0,
+                            clip_pg_rho_threshold=1.0):
+  """V-trace from log importance weights (vtrace.py:164-280).
+
+  All tensors share the leading [T, B] dims and any number of extra trailing
+  dims; `bootstrap_value` has rank one less.  Outputs carry no gradient.
+  """
+  log_rhos = _as_f32(log_rhos)
+  dev = log_rhos.device
+  discounts = _as_f32(discounts, dev)
+  rewards = _as_f32(rewards, dev)
+  values = _as_f32(values, dev)
+  bootstrap_value = _as_f32(bootstrap_value, dev)
+
+  rho_rank = log_rhos.dim()
+  _check_rank(values, rho_rank, 'values')
+  _check_rank(bootstrap_value, rho_rank - 1, 'bootstrap_value')
+  _check_rank(discounts, rho_rank, 'discounts')
+  _check_rank(rewards, rho_rank, 'rewards')
+  if clip_rho_threshold is not None:
+    _check_rank(torch.as_tensor(clip_rho_threshold), 0, 'clip_rho_threshold')
+  if clip_pg_rho_threshold is not None:
+    _check_rank(torch.as_tensor(clip_pg_rho_threshold), 0,
+                'clip_pg_rho_threshold')
+
+  with torch.no_grad():
+    log_rhos = log_rhos.detach()
+    values = values.detach()
+    bootstrap_value = bootstrap_value.detach()
+    rhos = torch.exp(log_rhos)
+    if clip_rho_threshold is not None:
+      clipped_rhos = torch.clamp(rhos, max=float(clip_rho_threshold))
+    else:
+      clipped_rhos = rhos
+    cs = torch.clamp(rhos, max=1.0)
+    values_t_plus_1 = torch.cat([values[1:], bootstrap_value.unsqueeze(0)], 0)
+    deltas = clipped_rhos * (rewards + discounts * values_t_plus_1 - values)
+
+    a = discounts * cs
+    a, deltas = torch.broadcast_tensors(a, deltas)
+    vs_minus_v_xs = _reverse_affine_scan(a, deltas)
+    vs = vs_minus_v_xs + values
+
+    vs_t_plus_1 = torch.cat([vs[1:], bootstrap_value.unsqueeze(0)], 0)
+    if clip_pg_rho_threshold is not None:
+      clipped_pg_rhos = torch.clamp(rhos, max=float(clip_pg_rho_threshold))
+    else:
+      clipped_pg_rhos = rhos
+    pg_advantages = clipped_pg_rhos * (rewards + discounts * vs_t_plus_1 -
+                                       values)
+  return VTraceReturns(vs=vs, pg_advantages=pg_advantages)
+
+
+def from_logits(behaviour_policy_logits, target_policy_logits, actions,
+                discounts, rewards, values, bootstrap_value,
+                clip_rho_threshold=1.0, clip_pg_rho_threshold=1.0):
+  """V-trace for softmax policies (vtrace.py:71-161)."""
+  behaviour_policy_logits = _as_f32(behaviour_policy_logits)
+  dev = behaviour_policy_logits.device
+  target_policy_logits = _as_f32(target_policy_logits, dev)
+  actions = torch.as_tensor(actions, device=dev)
+  _check_rank(behaviour_policy_logits, 3, 'behaviour_policy_logits')
+  _check_rank(target_policy_logits, 3, 'target_policy_logits')
+  _check_rank(actions, 2, 'actions')
+
+  target_action_log_probs = log_probs_from_logits_and_actions(
+      target_policy_logits, actions)
+  behaviour_action_log_probs = log_probs_from_logits_and_actions(
+      behaviour_policy_logits, actions)
+  log_rhos = target_action_log_probs - behaviour_action_log_probs
+  ret = from_importance_weights(
+      log_rhos=log_rhos, discounts=discounts, rewards=rewards, values=values,
+      bootstrap_value=bootstrap_value, clip_rho_threshold=clip_rho_threshold,
+      clip_pg_rho_threshold=clip_pg_rho_threshold)
+  return VTraceFromLogitsReturns(
+      vs=ret.vs, pg_advantages=ret.pg_advantages, log_rhos=log_rhos,
+      behaviour_action_log_probs=behaviour_action_log_probs,
+      target_action_log_probs=target_action_log_probs)
