@@ -1,6 +1,35 @@
-// Launchers for the NHWC implicit-GEMM conv / pool kernels (conv*.hip).
+// Launchers for the NHWC bf16 conv torso kernels (conv_torso.hip).
+// Activations are NHWC bf16 (void* = raw bf16 bits), weights fp32 TF HWIO
+// [3][3][CIN][COUT], weight/bias gradients fp32 and ACCUMULATED (zero first).
+// pb_h/pb_w: TF-SAME pad_before of the 3x3/2 max-pool.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-namespace sa {}  // namespace sa
+namespace sa {
+namespace conv {
+
+int res_conv_rows(int H, int W);
+
+void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
+                           void* pooled, uint8_t* argmax, int N, int H, int W,
+                           int pb_h, int pb_w, hipStream_t s);
+void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
+                          void* pooled, uint8_t* argmax, int N, int H, int W,
+                          int CIN, int COUT, int pb_h, int pb_w, hipStream_t s);
+void res_conv_fwd_launch(const void* x, const float* w, const float* b,
+                         const void* resid, void* y, int N, int H, int W,
+                         int C, bool post_relu, hipStream_t s);
+void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
+                         const float* w, void* dx, float* dw, float* db, int N,
+                         int H, int W, int C, hipStream_t s);
+void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
+                          const float* w, void* dx, float* dw, float* db, int N,
+                          int H, int W, int CIN, int COUT, int pb_h, int pb_w,
+                          hipStream_t s);
+void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
+                           const uint8_t* x, float* dw, float* db, int N,
+                           int H, int W, int pb_h, int pb_w, hipStream_t s);
+
+}  // namespace conv
+}  // namespace sa

@@ -35,9 +35,9 @@ INSTR_EMBED = 20
 INSTR_LSTM = 64
 
 
-def _hip_torso_ready():
+def _hip_torso_ready(agent):
   from ..ops import conv
-  return conv.TORSO_READY
+  return conv.TORSO_READY and conv.supports(agent)
 
 
 def hip_ops_in_use(agent):
@@ -45,8 +45,8 @@ def hip_ops_in_use(agent):
   if agent.backend != 'hip':
     return []
   ops = ['lstm_recurrence', 'vtrace_loss', 'rmsprop']
-  if _hip_torso_ready():
-    ops += ['conv_torso', 'linear']
+  if _hip_torso_ready(agent):
+    ops += ['conv_torso']
   return ops
 
 
@@ -167,7 +167,7 @@ class Agent(nn.Module):
 
   def conv_features(self, frames):
     """frames uint8 [N,H,W,C] -> flattened conv features [N, flat]."""
-    if self.backend == 'hip' and _hip_torso_ready():
+    if self.backend == 'hip' and _hip_torso_ready(self):
       from .. import ops
       return ops.torso_forward(self, frames)
     x = frames.to(torch.float32) / 255.0
@@ -193,7 +193,7 @@ class Agent(nn.Module):
     return x.reshape(x.shape[0], -1)
 
   def torso_fc(self, feats):
-    if self.backend == 'hip' and _hip_torso_ready():
+    if self.backend == 'hip' and _hip_torso_ready(self):
       from .. import ops
       return ops.linear_relu(feats, self.linear_w, self.linear_b)
     w = self.linear_w.to(feats.dtype)

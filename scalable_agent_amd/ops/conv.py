@@ -1,11 +1,144 @@
-"""Conv torso on hand-written gfx950 implicit-GEMM kernels (WIP)."""
+"""Deep-ResNet conv torso on the fused gfx950 kernels (csrc/kernels/conv_torso.hip).
 
-TORSO_READY = False
+Forward per stage s (reference experiment.py:156-176):
+  conv_pool_fwd      conv3x3 + bias + maxpool3x3/2 SAME (stage 1 straight from
+                     the uint8 frame, x/255 folded into the weights)
+  2 x [res_conv_fwd  t = conv(relu(x)) + b
+       res_conv_fwd  y = conv(relu(t)) + b + x   (+ final ReLU on the last)]
+Backward per residual block: two fused dgrad+wgrad+bias passes; per stage head
+one pass that gathers the pooled gradient through the saved argmax in LDS.
+All activations NHWC bf16; weights/biases fp32 master copies (TF HWIO); their
+gradients accumulate in fp32 directly inside the kernels.
+"""
+
+import torch
+
+from ._ext import ext
+from ..models import layers
+
+TORSO_READY = True
+
+
+def supports(agent):
+  return agent.torso_kind == 'deep'
+
+
+def _pool_pads(h, w):
+  return layers.same_pads(h, 3, 2)[0], layers.same_pads(w, 3, 2)[0]
+
+
+def deep_param_list(agent):
+  """[w, b, (w1, b1, w2, b2) x 2] per stage, in spec order."""
+  out = []
+  for sp in agent.specs:
+    if sp['kind'] == 'conv':
+      out += list(agent._conv_params(sp['name']))
+    elif sp['kind'] == 'res':
+      for sub in ('conv_2d', 'conv_2d_1'):
+        out += list(agent._conv_params(sp['name'] + '__' + sub))
+  return out
+
+
+class _DeepTorso(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, frames, *params):
+    C = ext()
+    frames = frames.contiguous()
+    x = frames
+    saved = [frames]
+    shapes = []
+    p = 0
+    for s in range(3):
+      w, b = params[p], params[p + 1]
+      p += 2
+      H, W = x.shape[1], x.shape[2]
+      pb_h, pb_w = _pool_pads(H, W)
+      if s == 0:
+        pooled, arg = C.conv1_pool_fwd(x, w, b, pb_h, pb_w)
+      else:
+        pooled, arg = C.conv_pool_fwd(x, w, b, pb_h, pb_w)
+      shapes.append((H, W, pb_h, pb_w))
+      saved += [arg]
+      xa = pooled
+      for blk in range(2):
+        w1, b1, w2, b2 = params[p:p + 4]
+        p += 4
+        t = C.res_conv_fwd(xa, w1, b1)
+        last = (s == 2 and blk == 1)
+        y = C.res_conv_fwd(t, w2, b2, xa, last)
+        saved += [xa, t]
+        xa = y
+      if s < 2:
+        saved += [xa]  # input of the next stage's conv
+      x = xa
+    ctx.save_for_backward(*saved, x, *params)
+    ctx.shapes = shapes
+    ctx.nparams = len(params)
+    return x.reshape(x.shape[0], -1)
+
+  @staticmethod
+  def backward(ctx, grad_out):
+    C = ext()
+    t = ctx.saved_tensors
+    params = t[-ctx.nparams:]
+    out = t[-ctx.nparams - 1]
+    saved = list(t[:-ctx.nparams - 1])
+    frames = saved[0]
+    # unpack per stage: arg, (xa, t) x2, [stage_out]
+    stages = []
+    k = 1
+    for s in range(3):
+      arg = saved[k]
+      k += 1
+      blocks = []
+      for _ in range(2):
+        blocks.append((saved[k], saved[k + 1]))
+        k += 2
+      stage_out = None
+      if s < 2:
+        stage_out = saved[k]
+        k += 1
+      stages.append((arg, blocks, stage_out))
+    grads = torch.zeros(sum(q.numel() for q in params), dtype=torch.float32,
+                        device=out.device)
+    gviews = []
+    o = 0
+    for q in params:
+      gviews.append(grads[o:o + q.numel()].view_as(q))
+      o += q.numel()
+    dy = grad_out.reshape(out.shape).to(torch.bfloat16)
+    dy = (dy * (out > 0)).contiguous()
+    p_base = [0, 10, 20]
+    for s in reversed(range(3)):
+      arg, blocks, _ = stages[s]
+      pb = p_base[s]
+      for blk in reversed(range(2)):
+        xa, tt = blocks[blk]
+        i1 = pb + 2 + 4 * blk
+        w1, w2 = params[i1], params[i1 + 2]
+        dt = C.res_conv_bwd(dy, tt, None, w2, gviews[i1 + 2], gviews[i1 + 3])
+        dy = C.res_conv_bwd(dt, xa, dy, w1, gviews[i1], gviews[i1 + 1])
+      H, W, pb_h, pb_w = ctx.shapes[s]
+      if s == 0:
+        C.conv1_pool_bwd(dy, arg, frames, gviews[pb], gviews[pb + 1], pb_h,
+                         pb_w)
+      else:
+        x_in = stages[s - 1][2]
+        dy = C.pool_conv_bwd(dy, arg, x_in, params[pb], gviews[pb],
+                             gviews[pb + 1], True, pb_h, pb_w)
+    return (None,) + tuple(gviews)
 
 
 def torso_forward(agent, frames):
-  raise NotImplementedError('HIP conv torso not built yet')
+  """uint8 frames [N,H,W,3] -> relu'd conv features [N, flat] (bf16)."""
+  if not supports(agent):
+    raise NotImplementedError('HIP torso implements the deep ResNet only')
+  return _DeepTorso.apply(frames, *deep_param_list(agent))
 
 
 def linear_relu(x, w, b):
-  raise NotImplementedError('HIP linear not built yet')
+  """Torso FC: relu(x W + b) as a bf16 hipBLASLt GEMM (plain library GEMM)."""
+  y = torch.addmm(b.to(torch.bfloat16), x.to(torch.bfloat16),
+                  w.to(torch.bfloat16))
+  return torch.relu(y).to(torch.float32)
