@@ -84,6 +84,18 @@ std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
   return {loss, dlogits, dvalues};
 }
 
+// Operand packing shared by the fwd/bwd step kernels (see lstm.hip):
+// fwd A:  [RT][8 waves][2 mt][NS=H/32][64 lanes] of h (rows padded to 32)
+// bwd A:  [RT][16 waves][2 mt][NS=H/16][64 lanes] of dG
+at::Tensor pack_rows(const at::Tensor& x, int64_t nwaves) {
+  // x [B, K] -> packed [RT][nwaves][2][NS][4 q][16 rr]
+  const int64_t B = x.size(0), K = x.size(1), RT = (B + 31) / 32;
+  const int64_t NS = K / nwaves / 4;
+  auto xp = at::zeros({RT * 32, K}, x.options());
+  xp.narrow(0, 0, B).copy_(x);
+  return xp.view({RT, 2, 16, nwaves, NS, 4}).permute({0, 3, 1, 4, 5, 2}).contiguous();
+}
+
 std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
                                  at::Tensor h0, at::Tensor w_h) {
   SA_CHECK(xw); SA_CHECK(done); SA_CHECK(c0); SA_CHECK(h0); SA_CHECK(w_h);
@@ -97,13 +109,18 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   auto hs = at::empty({T, B, H}, xw.options());
   auto cs = at::empty({T, B, H}, xw.options());
   auto acts = at::empty({T, B, H4}, xw.options());
+  // weight slices packed per workgroup: [H/4][H][4 units][4 gates]
+  auto w4 = w_h.view({H, 4, H / 4, 4}).permute({2, 0, 3, 1}).contiguous();
+  const int64_t RT = (B + 31) / 32;
+  auto hpk = at::zeros({2, RT * 32 * H}, xw.options());
+  hpk[0].copy_(pack_rows(h0.reshape({B, H}), 8).reshape(-1));
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
   for (int t = 0; t < T; ++t) {
-    const float* hp = t == 0 ? h0.data_ptr<float>() : hs[t - 1].data_ptr<float>();
     const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
-    sa::lstm_fwd_step_launch(xw[t].data_ptr<float>(), hp, cp, dn + t * B,
-                             w_h.data_ptr<float>(), hs[t].data_ptr<float>(),
+    sa::lstm_fwd_step_launch(xw[t].data_ptr<float>(), hpk[t & 1].data_ptr<float>(),
+                             cp, dn + t * B, w4.data_ptr<float>(),
+                             hs[t].data_ptr<float>(), hpk[(t + 1) & 1].data_ptr<float>(),
                              cs[t].data_ptr<float>(), acts[t].data_ptr<float>(),
                              B, H, s);
   }
@@ -118,20 +135,28 @@ at::Tensor lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor w_h,
   const c10::DeviceGuard guard(acts.device());
   auto dg = at::empty({T, B, H4}, acts.options());
   auto carry = at::zeros({2, B, H}, acts.options());
+  const int64_t RT = (B + 31) / 32;
+  auto dgpk = at::zeros({2, RT * 32 * H4}, acts.options());
+  // W_h^T packed: [H/16 blk][16 waves][NS][4 q][16 rr] = W_h[16 blk + rr][64 w + 4 s + q]
+  auto wt = w_h.view({H / 16, 16, 16, H4 / 64, 4}).permute({0, 2, 3, 4, 1}).contiguous();
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
   for (int t = T - 1; t >= 0; --t) {
-    const float* dgn = t == T - 1 ? nullptr : dg[t + 1].data_ptr<float>();
+    const float* dgn = t == T - 1 ? nullptr : dgpk[(t + 1) & 1].data_ptr<float>();
     const uint8_t* dnext = t == T - 1 ? nullptr : dn + (t + 1) * B;
     const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
     const float* cin = t == T - 1 ? nullptr : carry[(t + 1) & 1].data_ptr<float>();
     sa::lstm_bwd_step_launch(dh_out[t].data_ptr<float>(), dgn, dnext, dn + t * B,
-                             w_h.data_ptr<float>(), acts[t].data_ptr<float>(),
+                             wt.data_ptr<float>(), acts[t].data_ptr<float>(),
                              cs[t].data_ptr<float>(), cp, cin,
-                             carry[t & 1].data_ptr<float>(),
-                             dg[t].data_ptr<float>(), B, H, s);
+                             carry[t & 1].data_ptr<float>(), dg[t].data_ptr<float>(),
+                             dgpk[t & 1].data_ptr<float>(), B, H, s);
   }
   return dg;
+}
+
+void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
+  sa::noop_launch(blocks, threads, counter.data_ptr<int>(), cur_stream());
 }
 
 }  // namespace
@@ -144,5 +169,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);
+  m.def("noop", &noop);
   register_conv_ops(m);
 }

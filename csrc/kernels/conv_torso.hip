@@ -121,40 +121,6 @@ __device__ __forceinline__ void load4(const bf16_t* src, float v[4]) {
   v[3] = __uint_as_float(o.y & 0xFFFF0000u);
 }
 
-template <int C, bool RESID, bool POST_RELU>
-__global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
-    const bf16_t* __restrict__ x, const float* __restrict__ w,
-    const float* __restrict__ bias, const bf16_t* __restrict__ resid,
-    bf16_t* __restrict__ y, int H, int W, int R) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* x_s = w_s + 9 * C * C;
-  const int tiles_per_img = (H + R - 1) / R;
-  const int n = blockIdx.x / tiles_per_img;
-  const int r0 = (blockIdx.x - n * tiles_per_img) * R;
-  const int Rv = min(R, H - r0);
-  load_weights<C, C, true>(w, 1.f, w_s);
-  load_halo_tile<C, true>(x, n, H, W, r0 - 1, Rv + 2, x_s);
-  __syncthreads();
-  const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
-  conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4]) {
-    const int64_t off = (img0 + q) * C + co0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
-    if (RESID) {
-      float r[4];
-      load4(resid + off, r);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] += r[i];
-    }
-    if (POST_RELU) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
-    }
-    store4(y + off, v);
-  });
-}
-
 // Max-pool 3x3/2 (TF SAME: pad_before pb, -inf padding) over a conv tile held
 // in LDS y_s [Rc][W][COUT] whose row 0 is conv row cr0; writes pooled rows
 // [i0, i0+Rpv).  8 channels per thread-iteration.
@@ -213,97 +179,6 @@ __device__ __forceinline__ void pool_tile(const bf16_t* y_s, int cr0, int H,
     av.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (static_cast<uint32_t>(arg[7]) << 24);
     *reinterpret_cast<uint2*>(argmax + o) = av;
   }
-}
-
-template <int CIN, int COUT>
-__global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
-    const bf16_t* __restrict__ x, const float* __restrict__ w,
-    const float* __restrict__ bias, bf16_t* __restrict__ pooled,
-    uint8_t* __restrict__ argmax, int H, int W, int Rp, int pb_h, int pb_w) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int tiles_per_img = (Hp + Rp - 1) / Rp;
-  const int n = blockIdx.x / tiles_per_img;
-  const int i0 = (blockIdx.x - n * tiles_per_img) * Rp;
-  const int Rpv = min(Rp, Hp - i0);
-  const int cr0 = 2 * i0 - pb_h;
-  const int Rc = 2 * Rpv + 1;
-  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* x_s = w_s + 9 * CIN * COUT;
-  bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN;
-  load_weights<CIN, COUT, true>(w, 1.f, w_s);
-  load_halo_tile<CIN, false>(x, n, H, W, cr0 - 1, Rc + 2, x_s);
-  __syncthreads();
-  conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
-    store4(y_s + q * COUT + co0, v);
-  });
-  __syncthreads();
-  pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled, argmax);
-}
-
-// First layer: uint8 RGB frame, K = 27 (tap*3+ci) padded to 32, one
-// 16x16x32 MFMA per 16 pixels.  1/255 is folded into the bf16 weights; the
-// raw byte values are exact in bf16.
-__global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
-    const uint8_t* __restrict__ x, const float* __restrict__ w,
-    const float* __restrict__ bias, bf16_t* __restrict__ pooled,
-    uint8_t* __restrict__ argmax, int H, int W, int Rp, int pb_h, int pb_w) {
-  constexpr int COUT = 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int tiles_per_img = (Hp + Rp - 1) / Rp;
-  const int n = blockIdx.x / tiles_per_img;
-  const int i0 = (blockIdx.x - n * tiles_per_img) * Rp;
-  const int Rpv = min(Rp, Hp - i0);
-  const int cr0 = 2 * i0 - pb_h;
-  const int Rc = 2 * Rpv + 1;
-  const int Wp = W + 2;
-  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);          // [16][32]
-  bf16_t* y_s = w_s + COUT * 32;                           // [Rc][W][16]
-  uint8_t* x_s = reinterpret_cast<uint8_t*>(y_s + (2 * Rp + 1) * W * COUT);
-  for (int e = threadIdx.x; e < COUT * 32; e += blockDim.x) {
-    const int co = e / 32, k = e % 32;
-    w_s[e] = k < 27 ? f2bf(w[k * COUT + co] * (1.0f / 255.0f)) : 0;
-  }
-  load_halo_tile_u8(x, n, H, W, cr0 - 1, Rc + 2, x_s);
-  __syncthreads();
-  const int lane = lane_id();
-  const int wave = wave_id();
-  // per-lane k -> LDS byte offsets (relative to the output pixel's origin)
-  int koff[8];
-  bool kval[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * (lane >> 4) + j;
-    kval[j] = k < 27;
-    const int tap = k / 3, ci = k % 3;
-    koff[j] = kval[j] ? ((tap / 3) * Wp + (tap % 3)) * 3 + ci : 0;
-  }
-  const bf8 a = *reinterpret_cast<const bf8*>(w_s + (lane & 15) * 32 + 8 * (lane >> 4));
-  const int npix = Rc * W;
-  const int ngroups = (npix + 15) / 16;
-  for (int g = wave; g < ngroups; g += kWaves) {
-    int q = g * 16 + (lane & 15);
-    const bool valid = q < npix;
-    if (!valid) q = 0;
-    const int qr = q / W, qc = q - (q / W) * W;
-    const uint8_t* px = x_s + (qr * Wp + qc) * 3;
-    bf8 b;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      b[j] = kval[j] ? (__bf16)static_cast<float>(px[koff[j]]) : (__bf16)0.0f;
-    f4 acc = mfma32(a, b, f4{0.f, 0.f, 0.f, 0.f});
-    if (valid) {
-      const int co0 = 4 * (lane >> 4);
-      float v[4] = {acc[0] + bias[co0], acc[1] + bias[co0 + 1],
-                    acc[2] + bias[co0 + 2], acc[3] + bias[co0 + 3]};
-      store4(y_s + q * COUT + co0, v);
-    }
-  }
-  __syncthreads();
-  pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled, argmax);
 }
 
 // ----------------------------------------------------------------- backward
@@ -480,6 +355,365 @@ __device__ __forceinline__ void flush_wgrad(const WgradAcc<CIN, COUT>& acc,
   }
 }
 
+// ----------------------------------------------------------------- staging
+// Register-staged loads: issue() puts a tile's global loads in flight (16-B
+// per lane), commit() writes them into LDS after the previous tile's compute
+// finished.  A persistent workgroup thus overlaps the HBM reads of tile k+1
+// with the MFMA work and stores of tile k (cdna_hip_programming.md T14).
+
+// Full-width NHWC rows [r_begin, r_begin+rows) of image n (rows outside
+// [0,H) read as zero) -> LDS [rows][W(+2)][C]; HALO adds zeroed halo columns.
+template <int C, int NREG>
+struct RowStager {
+  uint4 v[NREG];
+  int total;
+  __device__ __forceinline__ void issue(const bf16_t* __restrict__ src, int n,
+                                        int H, int W, int r_begin, int rows) {
+    constexpr int CH = C / 8;
+    const int rc = W * CH;
+    total = rows * rc;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (e < total) {
+        const int rr = e / rc;
+        const int r = r_begin + rr;
+        if (r >= 0 && r < H)
+          v[k] = *reinterpret_cast<const uint4*>(
+              src + (static_cast<int64_t>(n) * H + r) * W * C + (e - rr * rc) * 8);
+      }
+    }
+  }
+  template <bool RELU, bool HALO>
+  __device__ __forceinline__ void commit(bf16_t* lds, int W) const {
+    constexpr int CH = C / 8;
+    const int rc = W * CH;
+    const int Wl = HALO ? W + 2 : W;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < total) {
+        const int rr = e / rc;
+        const int rem = e - rr * rc;
+        const int px = rem / CH;
+        const int part = rem - px * CH;
+        uint4 x = v[k];
+        if (RELU) x = relu8(x);
+        *reinterpret_cast<uint4*>(lds + (rr * Wl + px + (HALO ? 1 : 0)) * C +
+                                  part * 8) = x;
+      }
+    }
+    if (HALO) {
+      const int rows = total / rc;
+      for (int e = threadIdx.x; e < rows * 2 * CH; e += kThreads) {
+        const int rr = e / (2 * CH);
+        const int side = (e / CH) & 1;
+        const int part = e % CH;
+        *reinterpret_cast<uint4*>(lds + (rr * Wl + (side ? W + 1 : 0)) * C +
+                                  part * 8) = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+};
+
+// Contiguous byte span [off, off+bytes) of `src` (16-B aligned) -> LDS.
+template <int NREG>
+struct SpanStager {
+  uint4 v[NREG];
+  int total;
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ src,
+                                        int64_t off, int bytes) {
+    total = bytes / 16;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      v[k] = make_uint4(0, 0, 0, 0);
+      if (e < total) v[k] = *reinterpret_cast<const uint4*>(src + off + e * 16);
+    }
+  }
+  __device__ __forceinline__ void commit(uint8_t* lds) const {
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < total) *reinterpret_cast<uint4*>(lds + e * 16) = v[k];
+    }
+  }
+};
+
+// uint8 RGB frame rows -> LDS rows of stride U8_STRIDE(W) bytes: byte
+// 4 + 3c + ci holds pixel c (c = -1..W, halo zero), channel ci.
+__host__ __device__ __forceinline__ int u8_stride(int W) { return (3 * W + 8 + 3) & ~3; }
+
+template <int NREG>
+struct U8Stager {
+  uint32_t v[NREG];
+  int total;  // dword chunks over the row span
+  int span;   // bytes in the (clipped) row span
+  int row0;   // first staged row (tile coordinates)
+  __device__ __forceinline__ void issue(const uint8_t* __restrict__ src, int n,
+                                        int H, int W, int r_begin, int rows) {
+    const int rlo = max(r_begin, 0), rhi = min(r_begin + rows, H);
+    row0 = rlo - r_begin;
+    span = rhi > rlo ? (rhi - rlo) * W * 3 : 0;
+    total = (span + 3) / 4;
+    const uint8_t* base = src + (static_cast<int64_t>(n) * H + rlo) * W * 3;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      uint32_t x = 0;
+      if (e < total) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (4 * e + b < span) x |= static_cast<uint32_t>(base[4 * e + b]) << (8 * b);
+      }
+      v[k] = x;
+    }
+  }
+  __device__ __forceinline__ void commit(uint8_t* lds, int W, int rows) const {
+    const int S = u8_stride(W);
+    // zero the whole tile first (halo pixels, rows outside the image)
+    for (int e = threadIdx.x; e < rows * S / 4; e += kThreads)
+      reinterpret_cast<uint32_t*>(lds)[e] = 0;
+    __syncthreads();
+    const int rb = 3 * W;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < total) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = 4 * e + b;
+          if (i < span) {
+            const int rr = i / rb;
+            lds[(row0 + rr) * S + 4 + (i - rr * rb)] = (v[k] >> (8 * b)) & 0xFF;
+          }
+        }
+      }
+    }
+  }
+};
+
+// uint8 rows -> bf16x4 halo tile [rows][W+2][4] (channel 3 and halo zero);
+// `pad` extra zero pixels follow the tile (MFMA reads may run 3 pixels past
+// the last row into weights-zero columns).
+template <int NREG>
+__device__ __forceinline__ void commit_x4(const U8Stager<NREG>& st, bf16_t* x4,
+                                          int W, int rows, int pad) {
+  const int Wp = W + 2;
+  const int nq = (rows * Wp + pad) * 4 / 8;  // uint4 = 8 bf16
+  for (int e = threadIdx.x; e < nq; e += kThreads)
+    reinterpret_cast<uint4*>(x4)[e] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const int rb = 3 * W;
+#pragma unroll
+  for (int k = 0; k < NREG; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    if (e < st.total) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int i = 4 * e + b;
+        if (i < st.span) {
+          const int rr = i / rb;
+          const int rem = i - rr * rb;
+          const int px = rem / 3;
+          const int ci = rem - px * 3;
+          x4[((st.row0 + rr) * Wp + px + 1) * 4 + ci] =
+              f2bf(static_cast<float>((st.v[k] >> (8 * b)) & 0xFF));
+        }
+      }
+    }
+  }
+}
+
+// Fast fp32 [3][3][CIN][COUT] -> LDS bf16 weight load (float4 over co).
+template <int CIN, int COUT, bool FWD>
+__device__ __forceinline__ void load_weights4(const float* __restrict__ w,
+                                              bf16_t* lds) {
+  const int total = 9 * CIN * COUT / 4;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(w)[e];
+    const int co = (e * 4) % COUT;
+    const int ci = ((e * 4) / COUT) % CIN;
+    const int tap = (e * 4) / (COUT * CIN);
+    const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (FWD)
+        lds[(tap * COUT + co + i) * CIN + ci] = f2bf(f[i]);
+      else
+        lds[(tap * CIN + ci) * COUT + co + i] = f2bf(f[i]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- kernels
+constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
+
+template <int C, bool RESID, bool POST_RELU>
+__global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ w,
+    const float* __restrict__ bias, const bf16_t* __restrict__ resid,
+    bf16_t* __restrict__ y, int N, int H, int W, int R) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* x_s = w_s + 9 * C * C;
+  bf16_t* r_s = x_s + (R + 2) * (W + 2) * C;
+  load_weights4<C, C, true>(w, w_s);
+  const int tpi = (H + R - 1) / R;
+  const int ntiles = N * tpi;
+  RowStager<C, NREG> sx, sr;
+  int tile = blockIdx.x;
+  if (tile < ntiles) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    sx.issue(x, n, H, W, r0 - 1, Rv + 2);
+    if (RESID) sr.issue(resid, n, H, W, r0, Rv);
+  }
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    __syncthreads();
+    sx.template commit<true, true>(x_s, W);
+    if (RESID) sr.template commit<false, false>(r_s, W);
+    __syncthreads();
+    const int nt = tile + gridDim.x;
+    if (nt < ntiles) {
+      const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
+      sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
+      if (RESID) sr.issue(resid, n2, H, W, r2, Rv2);
+    }
+    const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
+      if (RESID) {
+        float r[4];
+        load4(r_s + q * C + co0, r);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += r[i];
+      }
+      if (POST_RELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
+      }
+      store4(y + (img0 + q) * C + co0, v);
+    });
+  }
+}
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ w,
+    const float* __restrict__ bias, bf16_t* __restrict__ pooled,
+    uint8_t* __restrict__ argmax, int N, int H, int W, int Rp, int pb_h,
+    int pb_w) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
+  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* x_s = w_s + 9 * CIN * COUT;
+  bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN;
+  load_weights4<CIN, COUT, true>(w, w_s);
+  const int tpi = (Hp + Rp - 1) / Rp;
+  const int ntiles = N * tpi;
+  RowStager<CIN, NREG> sx;
+  int tile = blockIdx.x;
+  auto issue = [&](int t) {
+    const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
+    sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
+  };
+  if (tile < ntiles) issue(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, i0 = (tile - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
+    const int cr0 = 2 * i0 - pb_h;
+    const int Rc = 2 * Rpv + 1;
+    __syncthreads();
+    sx.template commit<false, true>(x_s, W);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
+      store4(y_s + q * COUT + co0, v);
+    });
+    __syncthreads();
+    pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
+                    argmax);
+  }
+}
+
+// First layer: the uint8 frame tile is staged as bf16x4 pixels (raw byte
+// values are exact in bf16; 1/255 is folded into the weights).  With 4 values
+// per pixel, one 16x16x16 MFMA covers a whole kernel row (kx = 0..2 plus a
+// zero-weight kx = 3, ci = 0..3): 3 MFMAs and 3 ds_read_b64 per 16 pixels.
+__global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
+    const uint8_t* __restrict__ x, const float* __restrict__ w,
+    const float* __restrict__ bias, bf16_t* __restrict__ pooled,
+    uint8_t* __restrict__ argmax, int N, int H, int W, int Rp, int pb_h,
+    int pb_w) {
+  constexpr int COUT = 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int Wp = W + 2;
+  bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);        // [3 ky][16 co][16 k]
+  bf16_t* y_s = w_s + 3 * 16 * 16;                        // [(2Rp+1)*W][16]
+  bf16_t* x4 = y_s + (2 * Rp + 1) * W * COUT;             // [(2Rp+3)][W+2][4] + pad
+  for (int e = threadIdx.x; e < 3 * 16 * 16; e += blockDim.x) {
+    const int ky = e / 256, co = (e / 16) % 16, k = e % 16;
+    const int kx = k / 4, ci = k % 4;
+    w_s[e] = (kx < 3 && ci < 3)
+                 ? f2bf(w[((ky * 3 + kx) * 3 + ci) * COUT + co] * (1.0f / 255.0f))
+                 : 0;
+  }
+  const int lane = lane_id();
+  const int wave = wave_id();
+  const int tpi = (Hp + Rp - 1) / Rp;
+  const int ntiles = N * tpi;
+  U8Stager<NREG> sx;
+  auto issue = [&](int t) {
+    const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
+    sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue(tile);
+  const float b0 = bias[4 * (lane >> 4)], b1 = bias[4 * (lane >> 4) + 1],
+              b2 = bias[4 * (lane >> 4) + 2], b3 = bias[4 * (lane >> 4) + 3];
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, i0 = (tile - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
+    const int cr0 = 2 * i0 - pb_h;
+    const int Rc = 2 * Rpv + 1;
+    const int npix = Rc * W;
+    __syncthreads();
+    commit_x4(sx, x4, W, Rc + 2, 4);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    s4 a[3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+      a[ky] = *reinterpret_cast<const s4*>(w_s + (ky * 16 + (lane & 15)) * 16 +
+                                           4 * (lane >> 4));
+    const int ngroups = (npix + 15) / 16;
+    for (int g = wave; g < ngroups; g += kWaves) {
+      int q = g * 16 + (lane & 15);
+      const bool valid = q < npix;
+      if (!valid) q = 0;
+      const int qr = q / W, qc = q - (q / W) * W;
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const s4 bv = *reinterpret_cast<const s4*>(
+            x4 + ((qr + ky) * Wp + qc + (lane >> 4)) * 4);
+        acc = mfma16(a[ky], bv, acc);
+      }
+      if (valid) {
+        const float v[4] = {acc[0] + b0, acc[1] + b1, acc[2] + b2, acc[3] + b3};
+        store4(y_s + q * COUT + 4 * (lane >> 4), v);
+      }
+    }
+    __syncthreads();
+    pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
+                    argmax);
+  }
+}
+
 template <int C, bool ADD_SKIP>
 __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ act,
@@ -492,48 +726,57 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* d_s = w_s + 9 * C * C;
   bf16_t* a_s = d_s + tile_elems + C;  // + one zero pixel each
-  load_weights<C, C, false>(w, 1.f, w_s);
+  bf16_t* s_s = a_s + tile_elems + C;  // skip interior [R][W][C]
+  load_weights4<C, C, false>(w, w_s);
   for (int e = threadIdx.x; e < C; e += blockDim.x) {
     d_s[tile_elems + e] = 0;
     a_s[tile_elems + e] = 0;
   }
   WgradAcc<C, C> acc;
   acc.zero();
-  const int tiles_per_img = (H + R - 1) / R;
-  const int ntiles = N * tiles_per_img;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int n = tile / tiles_per_img;
-    const int r0 = (tile - n * tiles_per_img) * R;
-    const int Rv = min(R, H - r0);
+  const int tpi = (H + R - 1) / R;
+  const int ntiles = N * tpi;
+  RowStager<C, NREG> sd, sa, ss;
+  auto issue = [&](int t) {
+    const int n = t / tpi, r0 = (t - n * tpi) * R, Rv = min(R, H - r0);
+    sd.issue(dy, n, H, W, r0 - 1, Rv + 2);
+    sa.issue(act, n, H, W, r0 - 1, Rv + 2);
+    if (ADD_SKIP) ss.issue(skip, n, H, W, r0, Rv);
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();  // previous tile's LDS reads done
-    load_halo_tile<C, false>(dy, n, H, W, r0 - 1, Rv + 2, d_s);
-    load_halo_tile<C, true>(act, n, H, W, r0 - 1, Rv + 2, a_s);
+    sd.template commit<false, true>(d_s, W);
+    sa.template commit<true, true>(a_s, W);
+    if (ADD_SKIP) ss.template commit<false, false>(s_s, W);
     __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
     const int npix = Rv * W;
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
       const int qr = q / W, qc = q - (q / W) * W;
       float m[4];
       load4(a_s + ((qr + 1) * Wp + qc + 1) * C + ci0, m);
-      const int64_t off = (img0 + q) * C + ci0;
       float s[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ADD_SKIP) load4(skip + off, s);
+      if (ADD_SKIP) load4(s_s + q * C + ci0, s);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = s[i] + (m[i] > 0.f ? v[i] : 0.f);
-      store4(dx + off, v);
+      store4(dx + (img0 + q) * C + ci0, v);
     });
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
   }
   flush_wgrad<C, C>(acc, 1.f, dw, db);
 }
 
-// Gathers dY of the conv that feeds a max-pool, for the halo tile rows
-// [cr0-1, cr0-1+rows) x cols [-1, W], from pooled grads dP and the argmax.
+// dY of the conv feeding a max-pool, for the halo tile rows [r_begin,
+// r_begin+rows) x cols [-1, W], gathered from LDS copies of the pooled grads
+// p_s and argmax g_s holding pooled rows [i_lo, ...).
 template <int COUT>
-__device__ __forceinline__ void gather_pool_grad(
-    const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax, int n,
-    int H, int W, int Hp, int Wo, int pb_h, int pb_w, int r_begin, int rows,
-    bf16_t* d_s) {
+__device__ __forceinline__ void gather_pool_grad_lds(
+    const bf16_t* p_s, const uint8_t* g_s, int i_lo, int H, int W, int Hp,
+    int Wo, int pb_h, int pb_w, int r_begin, int rows, bf16_t* d_s) {
   constexpr int CH = COUT / 8;
   const int Wp = W + 2;
   const int total = rows * Wp * CH;
@@ -545,18 +788,17 @@ __device__ __forceinline__ void gather_pool_grad(
     const int r = r_begin + rr, c = cc - 1;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (r >= 0 && r < H && c >= 0 && c < W) {
-      // windows i with 2i-pb <= r <= 2i-pb+2
-      const int ilo = max(0, (r + pb_h - 1) / 2);  // ceil((r+pb-2)/2)
+      const int ilo = max(0, (r + pb_h - 1) / 2);
       const int ihi = min(Hp - 1, (r + pb_h) / 2);
       const int jlo = max(0, (c + pb_w - 1) / 2);
       const int jhi = min(Wo - 1, (c + pb_w) / 2);
       for (int i = ilo; i <= ihi; ++i) {
-        const int dy = r - (2 * i - pb_h);
+        const int dyy = r - (2 * i - pb_h);
         for (int j = jlo; j <= jhi; ++j) {
-          const int code = dy * 3 + (c - (2 * j - pb_w));
-          const int64_t o = ((static_cast<int64_t>(n) * Hp + i) * Wo + j) * COUT + part * 8;
-          const uint2 a = *reinterpret_cast<const uint2*>(argmax + o);
-          const uint4 d = *reinterpret_cast<const uint4*>(dP + o);
+          const int code = dyy * 3 + (c - (2 * j - pb_w));
+          const int o = ((i - i_lo) * Wo + j) * COUT + part * 8;
+          const uint2 a = *reinterpret_cast<const uint2*>(g_s + o);
+          const uint4 d = *reinterpret_cast<const uint4*>(p_s + o);
           const uint32_t du[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -577,6 +819,15 @@ __device__ __forceinline__ void gather_pool_grad(
   }
 }
 
+__host__ __device__ __forceinline__ void pooled_rows(int r_begin, int rows,
+                                                     int pb_h, int Hp, int* lo,
+                                                     int* hi) {
+  const int a = r_begin + pb_h - 1;
+  *lo = a < 0 ? 0 : a / 2;
+  int h = (r_begin + rows - 1 + pb_h) / 2;
+  *hi = h > Hp - 1 ? Hp - 1 : h;
+}
+
 template <int CIN, int COUT, bool NEED_DX>
 __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
@@ -588,24 +839,46 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int d_elems = (R + 2) * Wp * COUT;
   const int x_elems = (R + 2) * Wp * CIN;
+  const int prow_max = (R + 2) / 2 + 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* d_s = w_s + 9 * CIN * COUT;
   bf16_t* x_s = d_s + d_elems + COUT;
-  load_weights<CIN, COUT, false>(w, 1.f, w_s);
+  bf16_t* p_s = x_s + x_elems + CIN;
+  uint8_t* g_s = reinterpret_cast<uint8_t*>(p_s + prow_max * Wo * COUT);
+  load_weights4<CIN, COUT, false>(w, w_s);
   for (int e = threadIdx.x; e < COUT; e += blockDim.x) d_s[d_elems + e] = 0;
   for (int e = threadIdx.x; e < CIN; e += blockDim.x) x_s[x_elems + e] = 0;
   WgradAcc<CIN, COUT> acc;
   acc.zero();
-  const int tiles_per_img = (H + R - 1) / R;
-  const int ntiles = N * tiles_per_img;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int n = tile / tiles_per_img;
-    const int r0 = (tile - n * tiles_per_img) * R;
-    const int Rv = min(R, H - r0);
+  const int tpi = (H + R - 1) / R;
+  const int ntiles = N * tpi;
+  RowStager<CIN, NREG> sx;
+  SpanStager<NREG> sp, sg;
+  const int prow_bytes = Wo * COUT;
+  auto issue = [&](int t) {
+    const int n = t / tpi, r0 = (t - n * tpi) * R, Rv = min(R, H - r0);
+    sx.issue(x, n, H, W, r0 - 1, Rv + 2);
+    int lo, hi;
+    pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
+    const int64_t prow0 = static_cast<int64_t>(n) * Hp + lo;
+    sp.issue(reinterpret_cast<const uint8_t*>(dP), prow0 * prow_bytes * 2,
+             (hi - lo + 1) * prow_bytes * 2);
+    sg.issue(argmax, prow0 * prow_bytes, (hi - lo + 1) * prow_bytes);
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    int lo, hi;
+    pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
-    gather_pool_grad<COUT>(dP, argmax, n, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
-                           Rv + 2, d_s);
-    load_halo_tile<CIN, false>(x, n, H, W, r0 - 1, Rv + 2, x_s);
+    sx.template commit<false, true>(x_s, W);
+    sp.commit(reinterpret_cast<uint8_t*>(p_s));
+    sg.commit(g_s);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
+                               Rv + 2, d_s);
     __syncthreads();
     const int npix = Rv * W;
     if (NEED_DX) {
@@ -619,9 +892,10 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
   flush_wgrad<CIN, COUT>(acc, 1.f, dw, db);
 }
 
-// First-layer weight gradient: dW[k=(tap,ci)][co] = sum_p x[p+off(tap)][ci]/255
-// * dY[p][co]; K=27 rows as two 16-row MFMA m-tiles; A gathered from the u8
-// halo tile, B = dY via transposed LDS reads.
+// First-layer weight gradient on the bf16x4 frame tile: for each kernel row
+// ky, D[m = 4 kx + ci][co] += X4[p + (ky-1, kx-1)][ci] dY[p][co]; the A tile
+// (4 pixels x 16 contiguous values = kx 0..3 x ci 0..3) and dY both come from
+// transposed LDS reads.  Scaled by 1/255 at the flush.
 __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const uint8_t* __restrict__ x, float* __restrict__ dw,
@@ -631,77 +905,82 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
   const int Wp = W + 2;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int d_elems = (R + 2) * Wp * COUT;
+  const int prow_max = (R + 2) / 2 + 2;
   bf16_t* d_s = reinterpret_cast<bf16_t*>(smem);
-  uint8_t* x_s = reinterpret_cast<uint8_t*>(d_s + d_elems + COUT);
+  bf16_t* x4 = d_s + d_elems + COUT;                     // [(R+2)][W+2][4] + pad
+  bf16_t* p_s = x4 + (((R + 2) * Wp + 4 + 1) & ~1) * 4;  // keep 16-B alignment
+  uint8_t* g_s = reinterpret_cast<uint8_t*>(p_s + prow_max * Wo * COUT);
   for (int e = threadIdx.x; e < COUT; e += blockDim.x) d_s[d_elems + e] = 0;
   const int lane = lane_id();
   const int wave = wave_id();
   const int sub = lane & 15;
-  // A row k (two m-tiles): offset of (tap, ci) relative to the pixel origin
-  int koff[2];
-  bool kval[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int k = sub + 16 * mt;
-    kval[mt] = k < 27;
-    const int tap = k / 3, ci = k % 3;
-    koff[mt] = kval[mt] ? (((tap / 3) - 1) * Wp + ((tap % 3) - 1)) * 3 + ci : 0;
-  }
-  f4 accw[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  f4 accw[3] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f},
+                f4{0.f, 0.f, 0.f, 0.f}};
   f4 accb = f4{0.f, 0.f, 0.f, 0.f};
   s4 ones;
   ones[0] = ones[1] = ones[2] = ones[3] = 0x3F80;
-  const int tiles_per_img = (H + R - 1) / R;
-  const int ntiles = N * tiles_per_img;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int n = tile / tiles_per_img;
-    const int r0 = (tile - n * tiles_per_img) * R;
-    const int Rv = min(R, H - r0);
+  const int tpi = (H + R - 1) / R;
+  const int ntiles = N * tpi;
+  U8Stager<NREG> sx;
+  SpanStager<NREG> sp, sg;
+  const int prow_bytes = Wo * COUT;
+  auto issue = [&](int t) {
+    const int n = t / tpi, r0 = (t - n * tpi) * R, Rv = min(R, H - r0);
+    sx.issue(x, n, H, W, r0 - 1, Rv + 2);
+    int lo, hi;
+    pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
+    const int64_t prow0 = static_cast<int64_t>(n) * Hp + lo;
+    sp.issue(reinterpret_cast<const uint8_t*>(dP), prow0 * prow_bytes * 2,
+             (hi - lo + 1) * prow_bytes * 2);
+    sg.issue(argmax, prow0 * prow_bytes, (hi - lo + 1) * prow_bytes);
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    int lo, hi;
+    pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
-    gather_pool_grad<COUT>(dP, argmax, n, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
-                           Rv + 2, d_s);
-    load_halo_tile_u8(x, n, H, W, r0 - 1, Rv + 2, x_s);
+    commit_x4(sx, x4, W, Rv + 2, 4);  // (contains a barrier)
+    sp.commit(reinterpret_cast<uint8_t*>(p_s));
+    sg.commit(g_s);
     __syncthreads();
+    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
     const int npix = Rv * W;
+    gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
+                               Rv + 2, d_s);
+    __syncthreads();
     const int ngroups = (npix + 15) / 16;
     for (int g = wave; g < ngroups; g += kWaves) {
-      // B: dY rows (pixels 4(l>>4)+qrow of the group), channel columns
       const int qb = g * 16 + 4 * (lane >> 4) + (sub >> 2);
       const bool vb = qb < npix;
       const int qbr = vb ? qb / W : 0, qbc = vb ? qb - qbr * W : 0;
       const s4 bd = lds_tr4(d_s + (vb ? ((qbr + 1) * Wp + qbc + 1) * COUT : d_elems) +
                             (sub & 3) * 4);
-      // A: rows k, columns = the 4 pixels 4(l>>4)+j of the group
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        s4 aa;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int q = g * 16 + 4 * (lane >> 4) + j;
-          float v = 0.f;
-          if (q < npix && kval[mt]) {
-            const int qr = q / W, qc = q - (q / W) * W;
-            v = static_cast<float>(x_s[((qr + 1) * Wp + qc + 1) * 3 + koff[mt]]);
-          }
-          aa[j] = static_cast<short>(f2bf(v));
-        }
-        accw[mt] = mfma16(aa, bd, accw[mt]);
+      for (int ky = 0; ky < 3; ++ky) {
+        // row = pixel qb (invalid pixels read halo zeros of row 0), columns =
+        // 16 contiguous values starting at x4 pixel (qbr+ky, qbc) -> (kx, ci)
+        const int prow = vb ? (qbr + ky) * Wp + qbc : 0;
+        const s4 aa = lds_tr4(x4 + (prow + (sub & 3)) * 4);
+        accw[ky] = mfma16(aa, bd, accw[ky]);
       }
       accb = mfma16(ones, bd, accb);
     }
   }
-  // flush: D[m=k][n=co] ; dw layout [k][co] (k = tap*3+ci, TF HWIO)
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int k = 16 * mt + 4 * (lane >> 4) + i;
-      if (k < 27) atomicAdd(dw + k * COUT + sub, accw[mt][i] * (1.0f / 255.0f));
+      const int kx = lane >> 4, ci = i;
+      if (kx < 3 && ci < 3)
+        atomicAdd(dw + ((ky * 3 + kx) * 3 + ci) * COUT + sub,
+                  accw[ky][i] * (1.0f / 255.0f));
     }
   if ((lane >> 4) == 0) atomicAdd(db + sub, accb[0]);
 }
 
-int persistent_grid(int ntiles) {
+int num_cus() {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -709,7 +988,16 @@ int persistent_grid(int ntiles) {
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  return ntiles < 2 * cus ? ntiles : 2 * cus;
+  return cus;
+}
+
+// Persistent grid: enough workgroups for `per_cu` resident per CU.
+int grid_for(int ntiles, size_t smem, int per_cu_cap) {
+  int per_cu = static_cast<int>((160 * 1024) / (smem + 1024));
+  if (per_cu > per_cu_cap) per_cu = per_cu_cap;
+  if (per_cu < 1) per_cu = 1;
+  const int g = num_cus() * per_cu;
+  return ntiles < g ? ntiles : g;
 }
 
 template <typename K>
@@ -720,21 +1008,27 @@ void set_smem(K kernel, size_t bytes) {
                         static_cast<int>(bytes));
 }
 
+// rows per tile such that the staged halo fits NREG*256 16-B chunks per
+// stream and the tile holds ~target pixels
+int rows_for(int H, int W, int C, int target) {
+  int R = target / W;
+  if (R < 1) R = 1;
+  while (R > 1 && (R + 2) * W * C / 8 > NREG * kThreads) --R;
+  return R < H ? R : H;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- launchers
-int res_conv_rows(int H, int W) {
-  int R = 192 / W;
-  if (R < 1) R = 1;
-  return R < H ? R : H;
-}
+int res_conv_rows(int H, int W) { return rows_for(H, W, 32, 192); }
 
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
                          int C, bool post_relu, hipStream_t s) {
-  const int R = res_conv_rows(H, W);
-  const int grid = N * ((H + R - 1) / R);
-  const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C) * sizeof(bf16_t);
+  const int R = rows_for(H, W, C, 192);
+  const int ntiles = N * ((H + R - 1) / R);
+  const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C + R * W * C) * sizeof(bf16_t);
+  const int grid = grid_for(ntiles, smem, 4);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
   auto Y = static_cast<bf16_t*>(y);
@@ -743,7 +1037,7 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
     auto k = res_conv_fwd_kernel<CC, RE, PR>;                                 \
     set_smem(k, smem);                                                        \
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, X, w, b, RS,   \
-                       Y, H, W, R);                                           \
+                       Y, N, H, W, R);                                        \
   }
   const bool re = resid != nullptr;
   if (C == 16) {
@@ -758,27 +1052,19 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
 #undef SA_RF
 }
 
-int pool_rows(int W, int CIN, int COUT, int Hp) {
-  // ~480 conv pixels per tile, LDS <= 64 KB
-  int Rp = (480 / W - 1) / 2;
-  if (Rp < 1) Rp = 1;
-  while (Rp > 1) {
-    const size_t lds = (9 * CIN * COUT + (2 * Rp + 3) * (W + 2) * CIN +
-                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
-    if (lds <= 64 * 1024) break;
-    --Rp;
-  }
-  return Rp < Hp ? Rp : Hp;
-}
-
 void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           void* pooled, uint8_t* argmax, int N, int H, int W,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
-  const int Rp = pool_rows(W, CIN, COUT, Hp);
-  const int grid = N * ((Hp + Rp - 1) / Rp);
+  // ~400 conv pixels per tile; staged halo (2Rp+3 rows) within NREG*256 chunks
+  int Rp = (400 / W - 1) / 2;
+  if (Rp < 1) Rp = 1;
+  while (Rp > 1 && (2 * Rp + 3) * W * CIN / 8 > NREG * kThreads) --Rp;
+  if (Rp > Hp) Rp = Hp;
+  const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (9 * CIN * COUT + (2 * Rp + 3) * (W + 2) * CIN +
                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
+  const int grid = grid_for(ntiles, smem, 4);
   auto X = static_cast<const bf16_t*>(x);
   auto P = static_cast<bf16_t*>(pooled);
 #define SA_CP(CI, CO)                                                          \
@@ -786,12 +1072,11 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
     auto k = conv_pool_fwd_kernel<CI, CO>;                                     \
     set_smem(k, smem);                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, X, w, b, P,     \
-                       argmax, H, W, Rp, pb_h, pb_w);                          \
+                       argmax, N, H, W, Rp, pb_h, pb_w);                       \
   }
   if (CIN == 16 && COUT == 32) SA_CP(16, 32)
   else if (CIN == 32 && COUT == 32) SA_CP(32, 32)
   else if (CIN == 16 && COUT == 16) SA_CP(16, 16)
-  else if (CIN == 32 && COUT == 16) SA_CP(32, 16)
 #undef SA_CP
 }
 
@@ -801,23 +1086,26 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
   const int Hp = (H + 1) / 2;
   int Rp = (480 / W - 1) / 2;
   if (Rp < 1) Rp = 1;
+  while (Rp > 1 && ((2 * Rp + 3) * W * 3 + 3) / 4 > NREG * kThreads) --Rp;
   if (Rp > Hp) Rp = Hp;
-  const int grid = N * ((Hp + Rp - 1) / Rp);
-  const size_t smem = (16 * 32 + (2 * Rp + 1) * W * 16) * sizeof(bf16_t) +
-                      (2 * Rp + 3) * (W + 2) * 3;
+  const int ntiles = N * ((Hp + Rp - 1) / Rp);
+  const size_t smem = (3 * 16 * 16 + (2 * Rp + 1) * W * 16 +
+                       ((2 * Rp + 3) * (W + 2) + 4) * 4) * sizeof(bf16_t);
+  const int grid = grid_for(ntiles, smem, 4);
   set_smem(conv1_pool_fwd_kernel, smem);
   hipLaunchKernelGGL(conv1_pool_fwd_kernel, dim3(grid), dim3(kThreads), smem,
-                     s, x, w, b, static_cast<bf16_t*>(pooled), argmax, H, W,
+                     s, x, w, b, static_cast<bf16_t*>(pooled), argmax, N, H, W,
                      Rp, pb_h, pb_w);
 }
 
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
                          int H, int W, int C, hipStream_t s) {
-  const int R = res_conv_rows(H, W);
+  const int R = rows_for(H, W, C, 192);
   const int ntiles = N * ((H + R - 1) / R);
-  const int grid = persistent_grid(ntiles);
-  const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
+  const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C) + R * W * C) *
+                      sizeof(bf16_t);
+  const int grid = grid_for(ntiles, smem, 2);
   auto DY = static_cast<const bf16_t*>(dy);
   auto A = static_cast<const bf16_t*>(act);
   auto SK = static_cast<const bf16_t*>(skip);
@@ -841,18 +1129,16 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           const float* w, void* dx, float* dw, float* db, int N,
                           int H, int W, int CIN, int COUT, int pb_h, int pb_w,
                           hipStream_t s) {
-  // up to ~384 conv pixels per tile, LDS <= 60 KB
-  int R = 384 / W;
-  if (R < 1) R = 1;
-  if (R > H) R = H;
-  auto smem_of = [&](int r) {
-    return (9 * CIN * COUT + (r + 2) * (W + 2) * (CIN + COUT) + CIN + COUT) *
-           sizeof(bf16_t);
-  };
-  while (R > 1 && smem_of(R) > 60 * 1024) --R;
+  const int Wo = (W + 1) / 2;
+  int R = rows_for(H, W, CIN, 256);
+  // pooled rows staged: ((R+2)/2+2) * Wo * COUT * 2 bytes within NREG*256*16
+  while (R > 1 && ((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16) --R;
+  const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
-  const int grid = persistent_grid(ntiles);
-  const size_t smem = smem_of(R);
+  const size_t smem = (9 * CIN * COUT + (R + 2) * (W + 2) * (CIN + COUT) +
+                       CIN + COUT + prow_max * Wo * COUT) * sizeof(bf16_t) +
+                      prow_max * Wo * COUT;
+  const int grid = grid_for(ntiles, smem, 2);
   auto DP = static_cast<const bf16_t*>(dP);
   auto X = static_cast<const bf16_t*>(x);
   auto DX = static_cast<bf16_t*>(dx);
@@ -877,13 +1163,19 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
 void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
                            int H, int W, int pb_h, int pb_w, hipStream_t s) {
+  const int Wo = (W + 1) / 2;
   int R = 384 / W;
   if (R < 1) R = 1;
+  while (R > 1 && (((R + 2) / 2 + 2) * Wo * 16 * 2 > NREG * kThreads * 16 ||
+                   ((R + 2) * W * 3 + 3) / 4 > NREG * kThreads))
+    --R;
   if (R > H) R = H;
+  const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
-  const int grid = persistent_grid(ntiles);
-  const size_t smem = ((R + 2) * (W + 2) * 16 + 16) * sizeof(bf16_t) +
-                      (R + 2) * (W + 2) * 3;
+  const size_t smem = ((R + 2) * (W + 2) * 16 + 16 + (((R + 2) * (W + 2) + 5) & ~1) * 4 +
+                       prow_max * Wo * 16) * sizeof(bf16_t) +
+                      prow_max * Wo * 16;
+  const int grid = grid_for(ntiles, smem, 2);
   set_smem(conv1_pool_bwd_kernel, smem);
   hipLaunchKernelGGL(conv1_pool_bwd_kernel, dim3(grid), dim3(kThreads), smem,
                      s, static_cast<const bf16_t*>(dP), argmax, x, dw, db, N,

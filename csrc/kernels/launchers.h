@@ -35,17 +35,25 @@ void vtrace_loss_launch(const float* behaviour, const float* target,
 
 // ---- lstm.hip --------------------------------------------------------------
 // One LSTMBlockCell step over all B rows with done-reset (gate order i,c,f,o,
-// forget bias +1).  xw_t [B,4H] = x_t W_x + b precomputed; W_h [H,4H].
-void lstm_fwd_step_launch(const float* xw_t, const float* h_prev,
+// forget bias +1).  xw_t [B,4H] = x_t W_x + b precomputed; w4 = W_h [H,4H]
+// packed as [H/4 blocks][H k][4 units][4 gates]; h_pk = h_{t-1} in the fwd
+// MFMA-operand order (see lstm.hip), written for the next step as h_pk_out.
+void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           const float* c_prev, const uint8_t* done_t,
-                          const float* w_h, float* h_t, float* c_t,
-                          float* acts_t, int B, int H, hipStream_t stream);
-// Reverse step t: consumes dG_{t+1} (null at t=T-1), writes dG_t.
-void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_next,
+                          const float* w4, float* h_t, float* h_pk_out,
+                          float* c_t, float* acts_t, int B, int H,
+                          hipStream_t stream);
+// Reverse step t: consumes dG_{t+1} (packed, null at t=T-1), writes dG_t
+// (plain [B,4H] and packed).  wt = W_h^T packed [H/16][16][4H/64][64].
+void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const uint8_t* done_next, const uint8_t* done_t,
-                          const float* w_h, const float* acts_t,
+                          const float* wt, const float* acts_t,
                           const float* c_t, const float* c_prev,
                           const float* dcarry_in, float* dcarry_out,
-                          float* dg_t, int B, int H, hipStream_t stream);
+                          float* dg_t, float* dg_pk_out, int B, int H,
+                          hipStream_t stream);
+
+// ---- calibration ----------------------------------------------------------
+void noop_launch(int blocks, int threads, int* p, hipStream_t s);
 
 }  // namespace sa

@@ -12,82 +12,117 @@
 //                dcarry' = dc_t f_t keep_t
 // dW_h = sum_t (keep_t h_{t-1})^T dG_t and dX are plain GEMMs on the caller.
 //
-// Mapping (gfx950, wave64): a workgroup owns UB=4 hidden units (16 gate
-// columns) for up to 32 batch rows; thread = (row, unit, k-split) with the
-// 8-way k-split on the lowest lane bits so the partial dot products reduce
-// with three __shfl_xor.  The W_h slice and the (masked) h_{t-1} tile are
-// staged through LDS once per step and reused by all rows / all units.
+// Latency design: the 101 dependent steps per direction are replayed from a
+// hipGraph (~1.6 us per dependent launch on MI355X, measured by
+// tools/launch_bench.py), so each step kernel must finish in ~1-2 us.  The
+// recurrent product runs on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, a
+// k-ordered fmaf chain) with BOTH operands loaded straight from global into
+// registers (no LDS staging, no bank conflicts); the K dimension is split
+// across the waves of the workgroup and reduced once through LDS.
 #include "launchers.h"
 
 namespace sa {
 namespace {
 
-constexpr int UB = 4;      // hidden units per workgroup
-constexpr int KS = 8;      // k-split lanes
-constexpr int RB = 32;     // batch rows per workgroup
-constexpr int kThreads = RB * UB * KS;  // 1024
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ f4v mfma_f32(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
+// ---------------------------------------------------------------- forward
+// Workgroup = 16 gate columns (4 units x 4 gates, packed n = 4u + g) x 32 rows.
+// 8 waves; wave w owns k in [H/8 w, H/8 (w+1)).  w4: [H/4][H][16].
+// h_pk_in / h_pk_out: h in MFMA-operand order, [row tile][wave][mt][s][lane]
+// with lane l <-> (row 16 mt + (l&15), k = KW w + 4 s + (l>>4)): every operand
+// load is one contiguous 256-B wave access.
 template <int H>
-__global__ __launch_bounds__(kThreads) void lstm_fwd_step_kernel(
-    const float* __restrict__ xw_t, const float* __restrict__ h_prev,
+__global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
+    const float* __restrict__ xw_t, const float* __restrict__ h_pk_in,
     const float* __restrict__ c_prev, const uint8_t* __restrict__ done_t,
-    const float* __restrict__ w_h, float* __restrict__ h_t,
-    float* __restrict__ c_t, float* __restrict__ acts_t, int B) {
-  __shared__ float4 w_s[H * UB];     // [k][unit] -> (i, c, f, o)
-  __shared__ float h_s[RB * H];      // [row][k], masked by keep
+    const float* __restrict__ w4, float* __restrict__ h_t,
+    float* __restrict__ h_pk_out, float* __restrict__ c_t,
+    float* __restrict__ acts_t, int B) {
+  constexpr int NW = 8;
+  constexpr int KW = H / NW;     // k per wave
+  constexpr int NS = KW / 4;     // mfma k-steps per wave
+  __shared__ f4v red[NW][2][64];  // per wave, per row tile, per lane
+  __shared__ float g_s[32][17];
   const int tid = threadIdx.x;
-  const int u0 = blockIdx.x * UB;
-  const int r0 = blockIdx.y * RB;
-  for (int e = tid; e < H * UB; e += kThreads) {
-    const int k = e / UB, u = e - k * UB;
-    const float* row = w_h + static_cast<int64_t>(k) * 4 * H + u0 + u;
-    w_s[e] = make_float4(row[0], row[H], row[2 * H], row[3 * H]);
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int blk = blockIdx.x;
+  const int r0 = blockIdx.y * 32;
+  // epilogue operands (thread = (row r, unit u) for tid < 128)
+  const int er = tid >> 2, eu = tid & 3;
+  const int egr = r0 + er;
+  const int ej = blk * 4 + eu;
+  float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, ekeep = 0.f;
+  if (tid < 128 && egr < B) {
+    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+    xi = xw_t[g0];
+    xc = xw_t[g0 + H];
+    xf = xw_t[g0 + 2 * H];
+    xo = xw_t[g0 + 3 * H];
+    cp = c_prev[static_cast<int64_t>(egr) * H + ej];
+    ekeep = done_t[egr] ? 0.f : 1.f;
   }
-  for (int e = tid; e < RB * H; e += kThreads) {
-    const int r = e / H;
-    const int gr = r0 + r;
-    float v = 0.f;
-    if (gr < B && !done_t[gr]) v = h_prev[static_cast<int64_t>(gr) * H + (e - r * H)];
-    h_s[e] = v;
+  // B operand: W[k = kw0 + 4s + (l>>4)][n = l&15]
+  const int kw0 = wave * KW;
+  float wb[NS];
+  const float* wsrc = w4 + (static_cast<int64_t>(blk) * H + kw0 + (lane >> 4)) * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 4 * 16];
+  // A operand: h[row = r0 + 16 mt + (l&15)][k = kw0 + 4s + (l>>4)] * keep
+  float ha[2][NS];
+  const float* pk = h_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * H +
+                    wave * 2 * NS * 64 + lane;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int row = r0 + 16 * mt + (lane & 15);
+    const float kf = (row < B && !done_t[row < B ? row : 0]) ? 1.f : 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ha[mt][s] = pk[(mt * NS + s) * 64] * kf;
+  }
+  f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    acc[0] = mfma_f32(ha[0][s], wb[s], acc[0]);
+    acc[1] = mfma_f32(ha[1][s], wb[s], acc[1]);
+  }
+  red[wave][0][lane] = acc[0];
+  red[wave][1][lane] = acc[1];
+  __syncthreads();
+  // reduce: output (row m in 0..31, col n in 0..15); D[m=4(l>>4)+i][n=l&15]
+  {
+    const int m = tid >> 4, n = tid & 15;  // 512 threads == 32 x 16 outputs
+    const int mt = m >> 4, mm = m & 15;
+    const int src_lane = ((mm >> 2) << 4) | n;
+    const int i = mm & 3;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += red[w][mt][src_lane][i];
+    g_s[m][n] = sum;
   }
   __syncthreads();
-  const int ks = tid & (KS - 1);
-  const int u = (tid / KS) & (UB - 1);
-  const int r = tid / (KS * UB);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 8
-  for (int kk = 0; kk < H / KS; ++kk) {
-    const int k = kk * KS + ks;
-    const float hv = h_s[r * H + k];
-    const float4 w = w_s[k * UB + u];
-    acc.x += hv * w.x;
-    acc.y += hv * w.y;
-    acc.z += hv * w.z;
-    acc.w += hv * w.w;
-  }
-#pragma unroll
-  for (int off = 1; off < KS; off <<= 1) {
-    acc.x += __shfl_xor(acc.x, off, 64);
-    acc.y += __shfl_xor(acc.y, off, 64);
-    acc.z += __shfl_xor(acc.z, off, 64);
-    acc.w += __shfl_xor(acc.w, off, 64);
-  }
-  const int gr = r0 + r;
-  if (ks == 0 && gr < B) {
-    const int j = u0 + u;
-    const int64_t g0 = static_cast<int64_t>(gr) * 4 * H + j;
-    const float ai = acc.x + xw_t[g0];
-    const float ac = acc.y + xw_t[g0 + H];
-    const float af = acc.z + xw_t[g0 + 2 * H];
-    const float ao = acc.w + xw_t[g0 + 3 * H];
-    const float i = sigm(ai), g = tanhf(ac), f = sigm(af + 1.0f), o = sigm(ao);
-    const float keep = done_t[gr] ? 0.f : 1.f;
-    const float c = f * keep * c_prev[static_cast<int64_t>(gr) * H + j] + i * g;
+  if (tid < 128 && egr < B) {
+    const float i = sigm(g_s[er][eu * 4 + 0] + xi);
+    const float g = tanhf(g_s[er][eu * 4 + 1] + xc);
+    const float f = sigm(g_s[er][eu * 4 + 2] + xf + 1.0f);
+    const float o = sigm(g_s[er][eu * 4 + 3] + xo);
+    const float c = f * ekeep * cp + i * g;
     const float h = o * tanhf(c);
-    c_t[static_cast<int64_t>(gr) * H + j] = c;
-    h_t[static_cast<int64_t>(gr) * H + j] = h;
+    const int64_t hj = static_cast<int64_t>(egr) * H + ej;
+    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+    c_t[hj] = c;
+    h_t[hj] = h;
+    {  // packed copy for the next step's A operand
+      const int k = ej, rr = egr - r0;
+      const int w = k / KW, s2 = (k % KW) >> 2, q = k & 3;
+      h_pk_out[static_cast<int64_t>(blockIdx.y) * 32 * H +
+               ((w * 2 + (rr >> 4)) * NS + s2) * 64 + (q << 4) + (rr & 15)] = h;
+    }
     acts_t[g0] = i;
     acts_t[g0 + H] = g;
     acts_t[g0 + 2 * H] = f;
@@ -95,95 +130,143 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_step_kernel(
   }
 }
 
+// ---------------------------------------------------------------- backward
+// Workgroup = 16 hidden units x 32 rows; 16 waves, wave w owns n (gate
+// columns of dG) in [4H/16 w, 4H/16 (w+1)).  dh_rec = dG_{t+1} W_h^T.
+// dg_pk_in/out: dG in MFMA-operand order [row tile][wave][mt][s][lane];
+// wt: W_h^T packed [H/16][wave][s][lane] (lane <-> unit l&15, n = 4s+(l>>4)).
 template <int H>
-__global__ __launch_bounds__(kThreads) void lstm_bwd_step_kernel(
-    const float* __restrict__ dh_out_t, const float* __restrict__ dg_next,
+__global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
+    const float* __restrict__ dh_out_t, const float* __restrict__ dg_pk_in,
     const uint8_t* __restrict__ done_next, const uint8_t* __restrict__ done_t,
-    const float* __restrict__ w_h, const float* __restrict__ acts_t,
+    const float* __restrict__ wt, const float* __restrict__ acts_t,
     const float* __restrict__ c_t, const float* __restrict__ c_prev,
     const float* __restrict__ dcarry_in, float* __restrict__ dcarry_out,
-    float* __restrict__ dg_t, int B) {
-  __shared__ float w_s[UB * 4 * H];  // W_h rows u0..u0+3, all 4H columns
+    float* __restrict__ dg_t, float* __restrict__ dg_pk_out, int B) {
+  const float* dg_next = dg_pk_in;
+  constexpr int NW = 16;
+  constexpr int NWID = 4 * H / NW;  // n per wave
+  constexpr int NS = NWID / 4;
+  __shared__ f4v red[NW][2][64];
+  __shared__ float r_s[32][17];
   const int tid = threadIdx.x;
-  const int u0 = blockIdx.x * UB;
-  const int r0 = blockIdx.y * RB;
-  const int ks = tid & (KS - 1);
-  const int u = (tid / KS) & (UB - 1);
-  const int r = tid / (KS * UB);
-  const int gr = r0 + r;
-  float acc = 0.f;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int u0 = blockIdx.x * 16;
+  const int r0 = blockIdx.y * 32;
+  // epilogue operands: thread = (row er, unit eu) for tid < 512
+  const int er = tid >> 4, eu = tid & 15;
+  const int egr = r0 + er;
+  const int ej = u0 + eu;
+  const bool eok = tid < 512 && egr < B;
+  float dho = 0.f, ai = 0.f, ag = 0.f, af = 0.f, ao = 0.f, cc = 0.f, cpv = 0.f,
+        dci = 0.f, kf = 0.f, knext = 1.f;
+  if (eok) {
+    const int64_t hj = static_cast<int64_t>(egr) * H + ej;
+    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+    dho = dh_out_t[hj];
+    ai = acts_t[g0];
+    ag = acts_t[g0 + H];
+    af = acts_t[g0 + 2 * H];
+    ao = acts_t[g0 + 3 * H];
+    cc = c_t[hj];
+    cpv = c_prev[hj];
+    if (dcarry_in) dci = dcarry_in[hj];
+    kf = done_t[egr] ? 0.f : 1.f;
+    if (done_next) knext = done_next[egr] ? 0.f : 1.f;
+  }
   if (dg_next != nullptr) {
-    for (int e = tid; e < UB * 4 * H; e += kThreads) {
-      const int uu = e / (4 * H);
-      w_s[e] = w_h[static_cast<int64_t>(u0 + uu) * 4 * H + (e - uu * 4 * H)];
+    // B[k = n][col = unit]: W_h[u0 + (l&15)][n0 + 4s + (l>>4)] (packed)
+    float wb[NS];
+    const float* wsrc = wt + (static_cast<int64_t>(blockIdx.x) * NW + wave) * NS * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 64];
+    float da[2][NS];
+    const float* pk = dg_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * 4 * H +
+                      wave * 2 * NS * 64 + lane;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) da[mt][s] = pk[(mt * NS + s) * 64];
+    f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      acc[0] = mfma_f32(da[0][s], wb[s], acc[0]);
+      acc[1] = mfma_f32(da[1][s], wb[s], acc[1]);
+    }
+    red[wave][0][lane] = acc[0];
+    red[wave][1][lane] = acc[1];
+    __syncthreads();
+    if (tid < 512) {
+      const int m = tid >> 4, n = tid & 15;
+      const int mt = m >> 4, mm = m & 15;
+      const int src_lane = ((mm >> 2) << 4) | n;
+      const int i = mm & 3;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w][mt][src_lane][i];
+      r_s[m][n] = sum;
     }
     __syncthreads();
-    if (gr < B) {
-      const float* dg = dg_next + static_cast<int64_t>(gr) * 4 * H;
-      const float* w = w_s + u * 4 * H;
-#pragma unroll 8
-      for (int kk = 0; kk < 4 * H / KS; ++kk) {
-        const int n = kk * KS + ks;
-        acc += dg[n] * w[n];
-      }
-    }
   }
+  if (eok) {
+    const float rec = dg_next != nullptr ? r_s[er][eu] : 0.f;
+    const int64_t hj = static_cast<int64_t>(egr) * H + ej;
+    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+    const float dh = dho + knext * rec;
+    const float tc = tanhf(cc);
+    const float dc = dci + dh * ao * (1.f - tc * tc);
+    const float dgv[4] = {dc * ag * ai * (1.f - ai), dc * ai * (1.f - ag * ag),
+                          dc * kf * cpv * af * (1.f - af),
+                          dh * tc * ao * (1.f - ao)};
+    const int rr = egr - r0;
+    float* pko = dg_pk_out + static_cast<int64_t>(blockIdx.y) * 32 * 4 * H;
 #pragma unroll
-  for (int off = 1; off < KS; off <<= 1) acc += __shfl_xor(acc, off, 64);
-  if (ks == 0 && gr < B) {
-    const int j = u0 + u;
-    const int64_t hj = static_cast<int64_t>(gr) * H + j;
-    const int64_t g0 = static_cast<int64_t>(gr) * 4 * H + j;
-    const float keep_next = (done_next != nullptr && done_next[gr]) ? 0.f : 1.f;
-    const float keep = done_t[gr] ? 0.f : 1.f;
-    const float dh = dh_out_t[hj] + keep_next * acc;
-    const float i = acts_t[g0], g = acts_t[g0 + H], f = acts_t[g0 + 2 * H],
-                o = acts_t[g0 + 3 * H];
-    const float c = c_t[hj];
-    const float tc = tanhf(c);
-    const float dc = (dcarry_in ? dcarry_in[hj] : 0.f) + dh * o * (1.f - tc * tc);
-    const float cp = keep * c_prev[hj];
-    dg_t[g0] = dc * g * i * (1.f - i);
-    dg_t[g0 + H] = dc * i * (1.f - g * g);
-    dg_t[g0 + 2 * H] = dc * cp * f * (1.f - f);
-    dg_t[g0 + 3 * H] = dh * tc * o * (1.f - o);
-    dcarry_out[hj] = dc * f * keep;
+    for (int g = 0; g < 4; ++g) {
+      dg_t[g0 + g * H] = dgv[g];
+      const int n = g * H + ej;
+      const int w = n / NWID, s2 = (n % NWID) >> 2, q = n & 3;
+      pko[((w * 2 + (rr >> 4)) * NS + s2) * 64 + (q << 4) + (rr & 15)] = dgv[g];
+    }
+    dcarry_out[hj] = dc * af * kf;
   }
 }
 
 }  // namespace
 
-void lstm_fwd_step_launch(const float* xw_t, const float* h_prev,
+void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           const float* c_prev, const uint8_t* done_t,
-                          const float* w_h, float* h_t, float* c_t,
-                          float* acts_t, int B, int H, hipStream_t stream) {
-  dim3 grid(H / UB, (B + RB - 1) / RB);
+                          const float* w4, float* h_t, float* h_pk_out,
+                          float* c_t, float* acts_t, int B, int H,
+                          hipStream_t stream) {
+  dim3 grid(H / 4, (B + 31) / 32);
   if (H == 256) {
-    hipLaunchKernelGGL(lstm_fwd_step_kernel<256>, grid, dim3(kThreads), 0,
-                       stream, xw_t, h_prev, c_prev, done_t, w_h, h_t, c_t,
+    hipLaunchKernelGGL(lstm_fwd_step_kernel<256>, grid, dim3(512), 0, stream,
+                       xw_t, h_pk_in, c_prev, done_t, w4, h_t, h_pk_out, c_t,
                        acts_t, B);
   } else if (H == 64) {
-    hipLaunchKernelGGL(lstm_fwd_step_kernel<64>, grid, dim3(kThreads), 0,
-                       stream, xw_t, h_prev, c_prev, done_t, w_h, h_t, c_t,
+    hipLaunchKernelGGL(lstm_fwd_step_kernel<64>, grid, dim3(512), 0, stream,
+                       xw_t, h_pk_in, c_prev, done_t, w4, h_t, h_pk_out, c_t,
                        acts_t, B);
   }
 }
 
-void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_next,
+void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const uint8_t* done_next, const uint8_t* done_t,
-                          const float* w_h, const float* acts_t,
+                          const float* wt, const float* acts_t,
                           const float* c_t, const float* c_prev,
                           const float* dcarry_in, float* dcarry_out,
-                          float* dg_t, int B, int H, hipStream_t stream) {
-  dim3 grid(H / UB, (B + RB - 1) / RB);
+                          float* dg_t, float* dg_pk_out, int B, int H,
+                          hipStream_t stream) {
+  dim3 grid(H / 16, (B + 31) / 32);
   if (H == 256) {
-    hipLaunchKernelGGL(lstm_bwd_step_kernel<256>, grid, dim3(kThreads), 0,
-                       stream, dh_out_t, dg_next, done_next, done_t, w_h,
-                       acts_t, c_t, c_prev, dcarry_in, dcarry_out, dg_t, B);
+    hipLaunchKernelGGL(lstm_bwd_step_kernel<256>, grid, dim3(1024), 0, stream,
+                       dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, B);
   } else if (H == 64) {
-    hipLaunchKernelGGL(lstm_bwd_step_kernel<64>, grid, dim3(kThreads), 0,
-                       stream, dh_out_t, dg_next, done_next, done_t, w_h,
-                       acts_t, c_t, c_prev, dcarry_in, dcarry_out, dg_t, B);
+    hipLaunchKernelGGL(lstm_bwd_step_kernel<64>, grid, dim3(1024), 0, stream,
+                       dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, B);
   }
 }
 

@@ -60,3 +60,16 @@ void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
 }
 
 }  // namespace sa
+
+// ---- calibration kernel (tools/launch_bench.py): measures the fixed cost of
+// a dependent launch at a given geometry (no memory traffic).
+namespace sa {
+namespace {
+__global__ void noop_kernel(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
+}
+}  // namespace
+void noop_launch(int blocks, int threads, int* p, hipStream_t s) {
+  hipLaunchKernelGGL(noop_kernel, dim3(blocks), dim3(threads), 0, s, p);
+}
+}  // namespace sa
