@@ -1,0 +1,132 @@
+"""Checkpoint / resume (reference: MonitoredTrainingSession, experiment.py:608-612).
+
+Layout in `logdir` (TF-Saver-like):
+  checkpoint                         text file naming the latest checkpoint
+  checkpoint_<num_env_frames>.pt     {params (by TF variable name), RMSProp
+                                      ms/mom, num_environment_frames, flags,
+                                      rng state, format version}
+Saved atomically (write to a temp file, fsync, rename), every
+`save_checkpoint_secs` (600 by default), keeping the newest `keep` (5, the TF
+Saver default).  Restore happens automatically on start; `--mode=test` reads
+the same files.  Files are loaded with `torch.load(weights_only=True)`.
+"""
+
+import glob
+import os
+import re
+import time
+
+import torch
+
+FORMAT_VERSION = 1
+_RE = re.compile(r'checkpoint_(\d+)\.pt$')
+
+
+def _list(logdir):
+  out = []
+  for p in glob.glob(os.path.join(logdir, 'checkpoint_*.pt')):
+    m = _RE.search(p)
+    if m:
+      out.append((int(m.group(1)), p))
+  return sorted(out)
+
+
+def latest_checkpoint(logdir):
+  """Path of the latest checkpoint in logdir, or None."""
+  idx = os.path.join(logdir, 'checkpoint')
+  if os.path.exists(idx):
+    name = open(idx).read().strip()
+    p = os.path.join(logdir, name)
+    if os.path.exists(p):
+      return p
+  ckpts = _list(logdir)
+  return ckpts[-1][1] if ckpts else None
+
+
+def _to_cpu(x):
+  if torch.is_tensor(x):
+    return x.detach().to('cpu')
+  if isinstance(x, dict):
+    return {k: _to_cpu(v) for k, v in x.items()}
+  return x
+
+
+def save(logdir, learner, flags=None, keep=5, extra=None):
+  """Writes checkpoint_<frames>.pt atomically and prunes old ones."""
+  os.makedirs(logdir, exist_ok=True)
+  frames = int(learner.frames.item())
+  names = learner.agent.tf_variable_names()
+  state = {
+      'format_version': FORMAT_VERSION,
+      'num_environment_frames': frames,
+      'params': {names[n]: p.detach().cpu() for n, p in learner.flat.named},
+      'rmsprop': {'ms': learner.opt.ms.detach().cpu(),
+                  'mom': learner.opt.mom.detach().cpu()},
+      'flags': {k: v for k, v in vars(flags).items()
+                if isinstance(v, (int, float, str, bool))} if flags else {},
+      'torch_rng': torch.get_rng_state(),
+      'time': time.time(),
+  }
+  if extra:
+    state['extra'] = _to_cpu(extra)
+  name = 'checkpoint_%d.pt' % frames
+  path = os.path.join(logdir, name)
+  tmp = path + '.tmp'
+  with open(tmp, 'wb') as f:
+    torch.save(state, f)
+    f.flush()
+    os.fsync(f.fileno())
+  os.replace(tmp, path)
+  idx_tmp = os.path.join(logdir, 'checkpoint.tmp')
+  with open(idx_tmp, 'w') as f:
+    f.write(name + '\n')
+  os.replace(idx_tmp, os.path.join(logdir, 'checkpoint'))
+  for _, old in _list(logdir)[:-keep]:
+    try:
+      os.remove(old)
+    except OSError:
+      pass
+  return path
+
+
+def load_state(path):
+  return torch.load(path, map_location='cpu', weights_only=True)
+
+
+def restore_agent(agent, state):
+  """Loads parameters (by TF variable name) into an Agent."""
+  names = agent.tf_variable_names()
+  params = state['params']
+  with torch.no_grad():
+    for n, p in agent.named_parameters():
+      p.copy_(params[names[n]].to(p.device))
+
+
+def restore(logdir, learner):
+  """Restores the latest checkpoint into a Learner; returns frames or None."""
+  path = latest_checkpoint(logdir)
+  if path is None:
+    return None
+  state = load_state(path)
+  restore_agent(learner.agent, state)
+  learner.opt.ms.copy_(state['rmsprop']['ms'].to(learner.opt.ms.device))
+  learner.opt.mom.copy_(state['rmsprop']['mom'].to(learner.opt.mom.device))
+  learner.frames.fill_(int(state['num_environment_frames']))
+  if 'torch_rng' in state:
+    torch.set_rng_state(state['torch_rng'])
+  return int(state['num_environment_frames'])
+
+
+class PeriodicSaver(object):
+  """Saves every `secs` seconds (save_checkpoint_secs)."""
+
+  def __init__(self, logdir, learner, flags, secs=600, keep=5):
+    self.logdir, self.learner, self.flags = logdir, learner, flags
+    self.secs, self.keep = secs, keep
+    self._last = time.time()
+
+  def maybe_save(self, force=False):
+    if force or time.time() - self._last >= self.secs:
+      self._last = time.time()
+      return save(self.logdir, self.learner, self.flags, self.keep)
+    return None

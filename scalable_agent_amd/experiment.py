@@ -1,0 +1,417 @@
+"""Importance Weighted Actor-Learner Architectures: train / test drivers.
+
+Same CLI and run modes as the reference experiment.py:
+  * `--mode=train`, single machine (`--task=-1`, :479-672): env processes,
+    `num_actors` actor threads whose per-step inference is dynamically batched
+    onto the GPU, a bounded unroll queue, the learner loop (V-trace, RMSProp,
+    frame counter), per-episode logging + summaries, DMLab-30 scores,
+    checkpoints every `save_checkpoint_secs`, auto-restore on start;
+  * distributed (`--job_name=learner|actor --task=i`, :497-512, README :55-71):
+    actor processes run the agent on their own CPU with weights pulled from the
+    learner and ship unrolls to it - here through a shared-memory slot ring
+    and a shared-memory weight snapshot on one node (runtime/shm_transport.py)
+    instead of TF gRPC;
+  * `--mode=test` (:675-708): restores the latest checkpoint, runs each level
+    until `test_num_episodes` episodes, prints the mean return and DMLab-30
+    scores;
+  * data-parallel learners (new): launch with torch.distributed.run, one rank
+    per GPU; gradients are summed with RCCL (see parallel/).
+
+Log lines kept verbatim: 'Level: %s Episode return: %f', 'Mean episode
+return: %f', 'No cap.: %f Cap 100: %f'.
+"""
+
+import collections
+import logging
+import os
+import queue
+import sys
+import threading
+import time
+
+import numpy as np
+
+from . import dmlab30
+from . import environments
+from . import flags as flags_lib
+from . import py_process
+
+log = logging.getLogger('scalable_agent_amd')
+
+
+# --------------------------------------------------------------- env factory
+def env_kind(flags, level_name):
+  if flags.env != 'auto':
+    return flags.env
+  if level_name.startswith('doom_'):
+    return 'doom'
+  if level_name.startswith('synthetic'):
+    return 'synthetic'
+  return 'dmlab'
+
+
+def frame_shape_for(flags, level_name):
+  kind = env_kind(flags, level_name)
+  if kind == 'doom':
+    from .envs.doom import DOOM_H, DOOM_W
+    return (DOOM_H, DOOM_W, 3)
+  if flags.obs_shape:
+    return tuple(int(x) for x in flags.obs_shape.lower().split('x'))
+  return (flags.height, flags.width, 3)
+
+
+def action_set_for(flags, level_name):
+  if env_kind(flags, level_name) == 'doom':
+    from .envs.doom import DOOM_ACTION_SET
+    return DOOM_ACTION_SET
+  return environments.DEFAULT_ACTION_SET
+
+
+def create_environment(flags, level_name, seed, is_test=False):
+  """Returns an unstarted EnvProcess (reference create_environment :430-459)."""
+  kind = env_kind(flags, level_name)
+  shape = frame_shape_for(flags, level_name)
+  if kind == 'doom':
+    from .envs.doom import PyProcessDoom
+    return py_process.EnvProcess(PyProcessDoom, shape, level_name, None,
+                                 flags.num_action_repeats, seed)
+  if kind == 'synthetic':
+    from .envs.synthetic import SyntheticEnv
+    cfg = {'benchmark_mode': flags.benchmark_mode}
+    return py_process.EnvProcess(
+        SyntheticEnv, shape, level_name, cfg, flags.num_action_repeats, seed,
+        frame_shape=shape, episode_length=flags.synthetic_episode_length)
+  if level_name in dmlab30.ALL_LEVELS:
+    level_name = 'contributed/dmlab30/' + level_name
+  config = {
+      'width': shape[1], 'height': shape[0],
+      'datasetPath': flags.dataset_path, 'logLevel': 'WARN',
+      'gpuDeviceIndex': '0', 'renderer': flags.renderer,
+      'benchmark_mode': flags.benchmark_mode,
+  }
+  if is_test:
+    config['allowHoldOutLevels'] = 'true'
+    config['mixerSeed'] = 0x600D5EED
+  return py_process.EnvProcess(environments.PyProcessDmLab, shape, level_name,
+                               config, flags.num_action_repeats, seed)
+
+
+def level_names_for(flags):
+  if flags.level_name == 'dmlab30':
+    src = (dmlab30.LEVEL_MAPPING.keys() if flags.mode == 'train'
+           else dmlab30.LEVEL_MAPPING.values())
+    return list(src)
+  return [flags.level_name]
+
+
+def uses_instruction(flags, level_names):
+  return all(env_kind(flags, l) == 'dmlab' for l in level_names)
+
+
+# --------------------------------------------------------------- helpers
+def _device(flags, local_rank=0):
+  import torch
+  if flags.device == 'auto':
+    return (torch.device('cuda', local_rank) if torch.cuda.is_available()
+            else torch.device('cpu'))
+  return torch.device(flags.device)
+
+
+def _make_agent(flags, num_actions, frame_shape, device, seed):
+  import torch
+  from .models import Agent
+  backend = 'torch'
+  if device.type == 'cuda':
+    from . import ops
+    ops.load()  # fail loudly on a GPU box without the kernels
+    backend = 'hip'
+  cdt = torch.bfloat16 if flags.dtype == 'bf16' else torch.float32
+  return Agent(num_actions, torso=flags.torso, frame_shape=frame_shape,
+               seed=seed, backend=backend, compute_dtype=cdt)
+
+
+class EpisodeLogger(object):
+  """Per-episode logs, summaries and DMLab-30 scores (experiment.py:629-667)."""
+
+  def __init__(self, flags, level_names, writer):
+    self.flags = flags
+    self.writer = writer
+    self.level_names = level_names
+    self.level_returns = {l: [] for l in level_names}
+    self.episodes = 0
+    self.recent_returns = collections.deque(maxlen=100)
+
+  def log_batch(self, level_name_per_b, done, episode_return, episode_step,
+                frames):
+    """done/returns/steps: numpy [T, B] (already shifted to env_outputs[1:])."""
+    ts, bs = np.nonzero(done)
+    for t, b in zip(ts, bs):
+      level = level_name_per_b[b]
+      ret = float(episode_return[t, b])
+      ep_frames = int(episode_step[t, b]) * self.flags.num_action_repeats
+      log.info('Level: %s Episode return: %f', level, ret)
+      self.episodes += 1
+      self.recent_returns.append(ret)
+      if self.writer is not None:
+        self.writer.add_scalars({'%s/episode_return' % level: ret,
+                                 '%s/episode_frames' % level: ep_frames},
+                                frames)
+      if self.flags.level_name == 'dmlab30':
+        self.level_returns[level].append(ret)
+    if (self.flags.level_name == 'dmlab30' and
+        min(map(len, self.level_returns.values())) >= 1):
+      no_cap = dmlab30.compute_human_normalized_score(self.level_returns,
+                                                      per_level_cap=None)
+      cap_100 = dmlab30.compute_human_normalized_score(self.level_returns,
+                                                       per_level_cap=100)
+      if self.writer is not None:
+        self.writer.add_scalars({'dmlab30/training_no_cap': no_cap,
+                                 'dmlab30/training_cap_100': cap_100}, frames)
+      self.level_returns = {l: [] for l in self.level_names}
+
+
+# --------------------------------------------------------------- train
+def train(flags):
+  """Single-machine or data-parallel learner(s) with local actors."""
+  import torch
+  from . import checkpoint as ckpt_lib
+  from . import inference as inference_lib
+  from . import parallel
+  from .actor import Actor, stack_unrolls
+  from .learner import Learner, batch_to_device
+  from .summary import SummaryWriter
+  from .utils.timing import StepTimer
+
+  level_names = level_names_for(flags)
+  action_set = action_set_for(flags, level_names[0])
+  num_actions = len(action_set)
+  frame_shape = frame_shape_for(flags, level_names[0])
+  use_instr = uses_instruction(flags, level_names)
+
+  if flags.task >= 0 and flags.job_name == 'actor':
+    from .runtime import shm_transport
+    return shm_transport.run_actor_process(flags, level_names, action_set,
+                                           frame_shape, use_instr)
+
+  rank, world, local_rank = parallel.world_info()
+  # Env processes are forked BEFORE the GPU is initialised.
+  distributed_actors = flags.task >= 0 and flags.job_name == 'learner'
+  envs, actors_levels = [], []
+  if not distributed_actors:
+    for i in range(flags.num_actors):
+      level = level_names[i % len(level_names)]
+      seed = flags.seed * 1000003 * (rank + 1) + i + 1
+      envs.append(create_environment(flags, level, seed))
+      actors_levels.append(level)
+    py_process.start_all(envs)
+
+  rank, world, local_rank = parallel.init_distributed()
+  device = _device(flags, local_rank)
+  if device.type == 'cuda':
+    torch.cuda.set_device(device)
+  torch.manual_seed(flags.seed + rank)
+  logdir = flags.logdir if rank == 0 else os.path.join(flags.logdir,
+                                                       'rank%d' % rank)
+  os.makedirs(logdir, exist_ok=True)
+  writer = SummaryWriter(logdir) if rank == 0 else None
+
+  agent = _make_agent(flags, num_actions, frame_shape, device, flags.seed)
+  learner = Learner(agent, flags, device, world_size=world)
+  restored = ckpt_lib.restore(flags.logdir, learner)
+  if restored is not None:
+    log.info('Restored checkpoint at %d frames', restored)
+  if world > 1:
+    parallel.broadcast_params(learner.flat.params)
+  saver = ckpt_lib.PeriodicSaver(flags.logdir, learner, flags,
+                                 flags.save_checkpoint_secs,
+                                 flags.keep_checkpoints) if rank == 0 else None
+
+  unroll_queue = queue.Queue(maxsize=max(2 * flags.batch_size,
+                                         flags.num_actors))
+  stop = threading.Event()
+  threads = []
+  transport = None
+  infer = None
+  if distributed_actors:
+    from .runtime import shm_transport
+    transport = shm_transport.LearnerTransport(flags, frame_shape,
+                                               num_actions, learner)
+    threading.Thread(target=transport.pump, args=(unroll_queue, stop),
+                     daemon=True).start()
+  else:
+    inf_agent = _make_agent(flags, num_actions, frame_shape, device,
+                            flags.seed)
+    model = inference_lib.InferenceModel(inf_agent, device, use_instr,
+                                         seed=flags.seed + 17 * rank)
+    model.publish(learner.flat.params)
+    infer = inference_lib.make_batched_infer(
+        model, flags.inference_min_batch, flags.inference_max_batch,
+        flags.inference_timeout_ms)
+    actor_errors = []
+
+    def actor_loop(actor):
+      try:
+        while not stop.is_set():
+          out = actor.unroll()
+          while not stop.is_set():
+            try:
+              unroll_queue.put(out, timeout=0.5)
+              break
+            except queue.Full:
+              pass
+      except Exception as e:  # pylint: disable=broad-except
+        if not stop.is_set():
+          actor_errors.append(e)
+          log.exception('actor failed')
+
+    for i, env in enumerate(envs):
+      actor = Actor(environments.FlowEnvironment(env), infer,
+                    actors_levels[i], action_set, flags.unroll_length,
+                    num_actions, use_instruction=use_instr)
+      t = threading.Thread(target=actor_loop, args=(actor,), daemon=True,
+                           name='actor-%d' % i)
+      t.start()
+      threads.append(t)
+
+  episode_logger = EpisodeLogger(flags, level_names, writer)
+  timer = StepTimer(learner.frames_per_step)
+  last_summary = time.time()
+  last_log_frames = int(learner.frames.item())
+  steps = 0
+  use_graph = flags.use_hip_graph and device.type == 'cuda'
+  try:
+    frames = int(learner.frames.item())
+    while frames < flags.total_environment_frames:
+      if flags.max_learner_steps and steps >= flags.max_learner_steps:
+        break
+      t_wait = time.time()
+      unrolls = []
+      while len(unrolls) < flags.batch_size:
+        try:
+          unrolls.append(unroll_queue.get(timeout=flags.queue_timeout_secs))
+        except queue.Empty:
+          raise RuntimeError(
+              'learner starved: no unroll for %.0fs (actors alive: %s)' %
+              (flags.queue_timeout_secs,
+               [t.is_alive() for t in threads] or 'remote'))
+      timer.add_wait(time.time() - t_wait)
+      host = stack_unrolls(unrolls, use_instruction=use_instr,
+                           pin=device.type == 'cuda')
+      data = batch_to_device(host, device)
+      if use_graph:
+        if learner._graph is None:
+          learner.capture(data)
+        learner.load_static(data)
+        loss = learner.graph_step()
+      else:
+        loss = learner.step(data)
+      steps += 1
+      if infer is not None:
+        model.publish(learner.flat.params)
+      elif transport is not None:
+        transport.publish_weights()
+      frames = int(learner.frames.item())
+      timer.step()
+      # episode logging on env_outputs[1:] (experiment.py:372-375, 632-647)
+      eo = host.env_outputs
+      episode_logger.log_batch(host.level_name, eo.done[1:].numpy(),
+                               eo.info.episode_return[1:].numpy(),
+                               eo.info.episode_step[1:].numpy(), frames)
+      if writer is not None and (time.time() - last_summary >=
+                                 flags.save_summaries_secs):
+        last_summary = time.time()
+        lr = learner.opt.current_lr(frames - learner.frames_per_step)
+        writer.add_scalars({'learning_rate': lr,
+                            'total_loss': float(loss),
+                            'frames_per_sec': timer.frames_per_sec(),
+                            'learner_steps_per_sec': timer.steps_per_sec(),
+                            'queue_wait_frac': timer.wait_fraction()},
+                           frames)
+        writer.add_histogram('action',
+                             host.agent_outputs.action[1:].numpy(), frames)
+        writer.flush()
+      if frames - last_log_frames >= flags.log_every_frames:
+        last_log_frames = frames
+        log.info('frames %d  %.0f frames/s  %.2f steps/s  loss %.3f  '
+                 'queue-wait %.0f%%', frames, timer.frames_per_sec(),
+                 timer.steps_per_sec(), float(loss),
+                 100 * timer.wait_fraction())
+      if saver is not None:
+        saver.maybe_save()
+  finally:
+    stop.set()
+    if infer is not None:
+      infer.close()
+    for t in threads:
+      t.join(timeout=5)
+    py_process.close_all(envs)
+    if transport is not None:
+      transport.close()
+    if saver is not None:
+      saver.maybe_save(force=True)
+    if writer is not None:
+      writer.close()
+    parallel.cleanup()
+  return learner
+
+
+# --------------------------------------------------------------- test
+def test(flags):
+  """Evaluates the latest checkpoint (experiment.py:675-708)."""
+  import torch
+  from . import checkpoint as ckpt_lib
+  from . import inference as inference_lib
+  from .actor import Actor
+
+  level_names = level_names_for(flags)
+  action_set = action_set_for(flags, level_names[0])
+  frame_shape = frame_shape_for(flags, level_names[0])
+  use_instr = uses_instruction(flags, level_names)
+  envs = [create_environment(flags, l, seed=1, is_test=True)
+          for l in level_names]
+  py_process.start_all(envs)
+  device = _device(flags)
+  agent = _make_agent(flags, len(action_set), frame_shape, device, flags.seed)
+  path = ckpt_lib.latest_checkpoint(flags.logdir)
+  if path is None:
+    raise FileNotFoundError('no checkpoint in %s' % flags.logdir)
+  model = inference_lib.InferenceModel(agent, device, use_instr)
+  ckpt_lib.restore_agent(model.agent, ckpt_lib.load_state(path))
+  level_returns = {l: [] for l in level_names}
+  try:
+    for env, level in zip(envs, level_names):
+      log.info('Testing level: %s', level)
+      actor = Actor(environments.FlowEnvironment(env), model.infer, level,
+                    action_set, flags.unroll_length, len(action_set),
+                    use_instruction=use_instr)
+      returns = level_returns[level]
+      while True:
+        out = actor.unroll()
+        d = out.env_outputs.done[1:]
+        returns.extend(out.env_outputs.info.episode_return[1:][d].tolist())
+        if len(returns) >= flags.test_num_episodes:
+          log.info('Mean episode return: %f', np.mean(returns))
+          break
+  finally:
+    py_process.close_all(envs)
+  if flags.level_name == 'dmlab30':
+    no_cap = dmlab30.compute_human_normalized_score(level_returns,
+                                                    per_level_cap=None)
+    cap_100 = dmlab30.compute_human_normalized_score(level_returns,
+                                                     per_level_cap=100)
+    log.info('No cap.: %f Cap 100: %f', no_cap, cap_100)
+  return level_returns
+
+
+def main(argv=None):
+  logging.basicConfig(level=logging.INFO,
+                      format='[%(asctime)s %(levelname)s] %(message)s')
+  flags = flags_lib.parse_flags(argv if argv is not None else sys.argv[1:])
+  if flags.mode == 'train':
+    train(flags)
+  else:
+    test(flags)
+
+
+if __name__ == '__main__':
+  main()

@@ -1,0 +1,82 @@
+"""Data-parallel learners without a cluster: gloo
+process group, world size 2, CPU.  N learners x batch B with grad_reduce=sum
+must equal one learner with batch N*B under the reference's sum losses."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from scalable_agent_amd import flags as flags_lib
+from scalable_agent_amd.envs.synthetic import make_synthetic_batch
+from scalable_agent_amd.learner import Learner, _map_tensors
+from scalable_agent_amd.models import Agent
+
+T, B, SHAPE = 5, 4, (16, 24, 3)
+
+
+def _free_port():
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  p = s.getsockname()[1]
+  s.close()
+  return p
+
+
+def _slice_batch(batch, lo, hi):
+  out = _map_tensors(batch, lambda t: t)
+  def sl_time(t):
+    return t[:, lo:hi]
+  env = out.env_outputs
+  return out._replace(
+      agent_state=(out.agent_state[0][lo:hi], out.agent_state[1][lo:hi]),
+      env_outputs=env._replace(
+          reward=sl_time(env.reward), done=sl_time(env.done),
+          info=env.info._replace(episode_return=sl_time(env.info.episode_return),
+                                 episode_step=sl_time(env.info.episode_step)),
+          observation=(sl_time(env.observation[0]), None)),
+      agent_outputs=out.agent_outputs._replace(
+          action=sl_time(out.agent_outputs.action),
+          policy_logits=sl_time(out.agent_outputs.policy_logits),
+          baseline=sl_time(out.agent_outputs.baseline)))
+
+
+def _worker(rank, world, port, result_path):
+  os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                    MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  from scalable_agent_amd import parallel
+  parallel.init_distributed(backend='gloo')
+  torch.manual_seed(0)
+  f = flags_lib.default_flags(batch_size=B // world, unroll_length=T,
+                              torso='shallow', grad_reduce='sum')
+  agent = Agent(9, torso='shallow', frame_shape=SHAPE, seed=rank + 10)
+  learner = Learner(agent, f, 'cpu', world_size=world)
+  parallel.broadcast_params(learner.flat.params)   # rank 0's init wins
+  full = make_synthetic_batch(B, T, SHAPE, 9, seed=7)
+  per = B // world
+  learner.step(_slice_batch(full, rank * per, (rank + 1) * per))
+  learner.step(_slice_batch(full, rank * per, (rank + 1) * per))
+  assert parallel.param_checksum_consistent(learner.flat.params)
+  if rank == 0:
+    torch.save({'params': learner.flat.params.clone(),
+                'frames': int(learner.frames)}, result_path)
+  parallel.cleanup()
+
+
+def test_dp_sum_equals_single_learner_with_full_batch(tmp_path):
+  path = str(tmp_path / 'dp.pt')
+  mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+  dp = torch.load(path, weights_only=True)
+  # single learner, full batch, same init as rank 0
+  torch.manual_seed(0)
+  f = flags_lib.default_flags(batch_size=B, unroll_length=T, torso='shallow')
+  agent = Agent(9, torso='shallow', frame_shape=SHAPE, seed=10)
+  learner = Learner(agent, f, 'cpu')
+  full = make_synthetic_batch(B, T, SHAPE, 9, seed=7)
+  learner.step(full)
+  learner.step(full)
+  assert dp['frames'] == int(learner.frames)
+  torch.testing.assert_close(dp['params'], learner.flat.params, rtol=1e-4,
+                             atol=1e-6)

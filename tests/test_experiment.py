@@ -1,0 +1,64 @@
+"""End-to-end CPU runs of the experiment driver with the synthetic env (the
+reference's Dockerfile smoke: short train + `--mode=test`), plus the
+multi-process distributed mode (learner + actor processes on one node)."""
+
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ['--level_name=synthetic', '--unroll_length=5', '--device=cpu',
+          '--dtype=fp32', '--torso=shallow', '--synthetic_episode_length=6',
+          '--height=24', '--width=32']
+
+
+def _run(args, timeout=240):
+  env = dict(os.environ, PYTHONPATH=ROOT)
+  return subprocess.run([sys.executable, os.path.join(ROOT, 'experiment.py')]
+                        + COMMON + args, capture_output=True, text=True,
+                        timeout=timeout, env=env)
+
+
+def test_train_then_test(tmp_path):
+  logdir = str(tmp_path / 'run')
+  r = _run(['--logdir=' + logdir, '--num_actors=3', '--batch_size=2',
+            '--total_environment_frames=480', '--save_summaries_secs=0'])
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Episode return' in r.stderr
+  assert os.path.exists(os.path.join(logdir, 'checkpoint'))
+  assert glob.glob(os.path.join(logdir, 'events.out.tfevents*'))
+  # resume continues from the checkpoint's frame counter
+  r = _run(['--logdir=' + logdir, '--num_actors=2', '--batch_size=2',
+            '--total_environment_frames=560'])
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Restored checkpoint at 480 frames' in r.stderr
+  r = _run(['--logdir=' + logdir, '--mode=test', '--test_num_episodes=2'])
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Mean episode return' in r.stderr
+
+
+def test_distributed_actor_processes(tmp_path):
+  logdir = str(tmp_path / 'dist')
+  env = dict(os.environ, PYTHONPATH=ROOT)
+  base = [sys.executable, os.path.join(ROOT, 'experiment.py')] + COMMON + [
+      '--logdir=' + logdir, '--num_actors=2', '--batch_size=2']
+  learner = subprocess.Popen(base + ['--job_name=learner', '--task=0',
+                                     '--max_learner_steps=3'],
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True, env=env)
+  actors = [subprocess.Popen(base + ['--job_name=actor', '--task=%d' % i],
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True, env=env) for i in range(2)]
+  try:
+    out, err = learner.communicate(timeout=240)
+    assert learner.returncode == 0, err[-3000:]
+    for a in actors:
+      a.wait(timeout=60)
+  finally:
+    for p in [learner] + actors:
+      if p.poll() is None:
+        p.kill()
+  assert os.path.exists(os.path.join(logdir, 'checkpoint'))
