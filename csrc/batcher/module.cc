@@ -13,6 +13,7 @@ namespace py = pybind11;
 namespace sa {
 
 void register_envpool(py::module& m);  // csrc/envpool/module_part.cc
+void register_image_ops(py::module& m);  // csrc/envpool/image_ops.cc
 
 namespace {
 
@@ -194,4 +195,5 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("maximum_batch_size", &PyBatcher::max_b)
       .def_property_readonly("timeout_ms", &PyBatcher::timeout);
   sa::register_envpool(m);
+  sa::register_image_ops(m);
 }

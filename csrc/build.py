@@ -141,8 +141,12 @@ def build_native(workers=8, force=False, sanitize=None):
       if os.path.exists(o):
         os.remove(o)
   _compile_all(jobs, workers)
-  suffix = '' if not sanitize else '_' + sanitize
-  out = os.path.join(PKG, 'runtime', '_native%s.so' % suffix)
+  # Sanitizer builds keep the module name `_native` (PyInit__native) and live
+  # in their own directory; runtime/native.py loads them by path.
+  outdir = os.path.join(PKG, 'runtime') if not sanitize else \
+      os.path.join(BUILD, 'san_' + sanitize)
+  os.makedirs(outdir, exist_ok=True)
+  out = os.path.join(outdir, '_native.so')
   objs = [o for _, o, _ in jobs]
   if (force or not os.path.exists(out) or
       max(os.path.getmtime(o) for o in objs) > os.path.getmtime(out)):

@@ -1,7 +1,9 @@
 """VizDoom support (reference environments_doom.py + envs/doom/).
 
-ViZDoom is not installed in this image; everything here imports it lazily
-and raises a clear ImportError when an env is actually constructed.
+Real ViZDoom is used when importable.  This image does not ship it, so
+`SA_DOOM_BACKEND=sim` (or cfg.doom_backend='sim') selects the in-tree
+`SimDoomGame` test double; without either, constructing a Doom env raises a
+clear ImportError.
 """
 
 from .impala_adapter import DOOM_W, DOOM_H, DOOM_ACTION_SET, PyProcessDoom  # noqa

@@ -217,12 +217,21 @@ def test_invalid_computation_id():
 def test_op_shape():
   batcher = db.Batcher(minimum_batch_size=1, maximum_batch_size=1,
                        timeout_ms=None)
-  t = threading.Thread(target=lambda: batcher.compute([np.array([1])]))
+  errors = []
+
+  def call():
+    try:
+      batcher.compute([np.array([1])])
+    except db.CancelledError as e:  # close() cancels the pending call
+      errors.append(e)
+
+  t = threading.Thread(target=call)
   t.start()
   _, computation_id = batcher.get_inputs()
   assert isinstance(computation_id, int) and np.ndim(computation_id) == 0
   batcher.close()
   t.join()
+  assert len(errors) == 1
 
 
 # ---- beyond the reference -------------------------------------------------

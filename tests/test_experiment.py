@@ -62,3 +62,18 @@ def test_distributed_actor_processes(tmp_path):
       if p.poll() is None:
         p.kill()
   assert os.path.exists(os.path.join(logdir, 'checkpoint'))
+
+
+def test_train_doom_benchmark_sim(tmp_path):
+  """`--level_name=doom_benchmark` through the IMPALA Doom adaptor (128x72
+  frames, 9 actions) on the in-tree ViZDoom simulator backend."""
+  env = dict(os.environ, PYTHONPATH=ROOT, SA_DOOM_BACKEND='sim')
+  r = subprocess.run(
+      [sys.executable, os.path.join(ROOT, 'experiment.py'),
+       '--level_name=doom_benchmark', '--unroll_length=5', '--device=cpu',
+       '--dtype=fp32', '--torso=shallow', '--num_actors=2', '--batch_size=2',
+       '--total_environment_frames=400', '--logdir=' + str(tmp_path / 'd')],
+      capture_output=True, text=True, timeout=240, env=env)
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Level: doom_benchmark Episode return' in r.stderr or \
+      os.path.exists(str(tmp_path / 'd' / 'checkpoint'))
