@@ -164,4 +164,7 @@ void register_conv_ops(pybind11::module& m) {
   m.def("res_conv_bwd", &res_conv_bwd);
   m.def("pool_conv_bwd", &pool_conv_bwd);
   m.def("conv1_pool_bwd", &conv1_pool_bwd);
+  m.def("conv_tune", [](const std::string& key, int64_t value) {
+          return sa::conv::conv_tune_set(key.c_str(), static_cast<int>(value));
+        }, pybind11::arg("key"), pybind11::arg("value") = -1);
 }

@@ -10,6 +10,9 @@ namespace sa {
 namespace conv {
 
 int res_conv_rows(int H, int W);
+// Sets a launch knob (value < 0: query only); returns the previous value or
+// -1 for an unknown key.
+int conv_tune_set(const char* key, int value);
 
 void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                            void* pooled, uint8_t* argmax, int N, int H, int W,

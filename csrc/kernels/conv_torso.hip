@@ -23,6 +23,9 @@
 #include "conv_common.h"
 #include "conv_launchers.h"
 
+#include <cstring>
+#include <type_traits>
+
 namespace sa {
 namespace conv {
 namespace {
@@ -30,6 +33,32 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int GPW = 4;  // 16-pixel groups per wave per chunk
+
+// Persistent tile schedule.  xcd == 0: tile = blockIdx.x + k * gridDim.x.
+// xcd == 1: XCD-aware - workgroups are dispatched round-robin over the 8 XCDs
+// (b % 8), so each XCD gets one CONTIGUOUS range of tiles (proportional to
+// its workgroup count) and its workgroups sweep that range together; the
+// halo rows neighbouring tiles share then hit the XCD's own L2.
+struct TileIter {
+  int first, stride, end;
+  __device__ __forceinline__ TileIter(int ntiles, int xcd) {
+    if (!xcd) {
+      first = blockIdx.x;
+      stride = gridDim.x;
+      end = ntiles;
+      return;
+    }
+    const int G = gridDim.x, x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int gx = G / 8 + (x < G % 8 ? 1 : 0);
+    const int before = x * (G / 8) + min(x, G % 8);
+    const int lo = static_cast<int>(static_cast<int64_t>(ntiles) * before / G);
+    end = static_cast<int>(static_cast<int64_t>(ntiles) * (before + gx) / G);
+    first = lo + j;
+    stride = gx;
+  }
+  __device__ __forceinline__ bool valid(int t) const { return t < end; }
+  __device__ __forceinline__ int next(int t) const { return t + stride; }
+};
 
 // ----------------------------------------------------------------- forward
 // Per-wave implicit GEMM over a chunk of up to GPW groups. x_s: halo tile
@@ -550,12 +579,13 @@ __device__ __forceinline__ void load_weights4(const float* __restrict__ w,
 // ----------------------------------------------------------------- kernels
 constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
 
-template <int C, bool RESID, bool POST_RELU>
+template <int C, bool RESID, bool POST_RELU, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, const bf16_t* __restrict__ resid,
-    bf16_t* __restrict__ y, int N, int H, int W, int R) {
+    bf16_t* __restrict__ y, int N, int H_, int W_, int R_, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* x_s = w_s + 9 * C * C;
   bf16_t* r_s = x_s + (R + 2) * (W + 2) * C;
@@ -563,20 +593,21 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
   RowStager<C, NREG> sx, sr;
-  int tile = blockIdx.x;
-  if (tile < ntiles) {
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     sx.issue(x, n, H, W, r0 - 1, Rv + 2);
     if (RESID) sr.issue(resid, n, H, W, r0, Rv);
   }
-  for (; tile < ntiles; tile += gridDim.x) {
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();
     sx.template commit<true, true>(x_s, W);
     if (RESID) sr.template commit<false, false>(r_s, W);
     __syncthreads();
-    const int nt = tile + gridDim.x;
-    if (nt < ntiles) {
+    const int nt = it.next(tile);
+    if (it.valid(nt)) {
       const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
       sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
       if (RESID) sr.issue(resid, n2, H, W, r2, Rv2);
@@ -600,13 +631,14 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
   }
 }
 
-template <int CIN, int COUT>
+template <int CIN, int COUT, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, bf16_t* __restrict__ pooled,
-    uint8_t* __restrict__ argmax, int N, int H, int W, int Rp, int pb_h,
-    int pb_w) {
+    uint8_t* __restrict__ argmax, int N, int H_, int W_, int Rp_, int pb_h,
+    int pb_w, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, Rp = RC ? RC : Rp_;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* x_s = w_s + 9 * CIN * COUT;
@@ -615,20 +647,21 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
   const int tpi = (Hp + Rp - 1) / Rp;
   const int ntiles = N * tpi;
   RowStager<CIN, NREG> sx;
-  int tile = blockIdx.x;
   auto issue = [&](int t) {
     const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
   };
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) issue(tile);
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, i0 = (tile - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     const int cr0 = 2 * i0 - pb_h;
     const int Rc = 2 * Rpv + 1;
     __syncthreads();
     sx.template commit<false, true>(x_s, W);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
     conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
@@ -644,13 +677,15 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
 // values are exact in bf16; 1/255 is folded into the weights).  With 4 values
 // per pixel, one 16x16x16 MFMA covers a whole kernel row (kx = 0..2 plus a
 // zero-weight kx = 3, ci = 0..3): 3 MFMAs and 3 ds_read_b64 per 16 pixels.
+template <int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     const uint8_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, bf16_t* __restrict__ pooled,
-    uint8_t* __restrict__ argmax, int N, int H, int W, int Rp, int pb_h,
-    int pb_w) {
+    uint8_t* __restrict__ argmax, int N, int H_, int W_, int Rp_, int pb_h,
+    int pb_w, int xcd) {
   constexpr int COUT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, Rp = RC ? RC : Rp_;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int Wp = W + 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);        // [3 ky][16 co][16 k]
@@ -672,11 +707,12 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
   };
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue(tile);
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) issue(tile);
   const float b0 = bias[4 * (lane >> 4)], b1 = bias[4 * (lane >> 4) + 1],
               b2 = bias[4 * (lane >> 4) + 2], b3 = bias[4 * (lane >> 4) + 3];
-  for (; tile < ntiles; tile += gridDim.x) {
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, i0 = (tile - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     const int cr0 = 2 * i0 - pb_h;
     const int Rc = 2 * Rpv + 1;
@@ -684,7 +720,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     __syncthreads();
     commit_x4(sx, x4, W, Rc + 2, 4);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
     s4 a[3];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
@@ -714,13 +750,14 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   }
 }
 
-template <int C, bool ADD_SKIP>
+template <int C, bool ADD_SKIP, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ act,
     const bf16_t* __restrict__ skip, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    int N, int H, int W, int R) {
+    int N, int H_, int W_, int R_, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   const int Wp = W + 2;
   const int tile_elems = (R + 2) * Wp * C;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
@@ -743,16 +780,17 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
     sa.issue(act, n, H, W, r0 - 1, Rv + 2);
     if (ADD_SKIP) ss.issue(skip, n, H, W, r0, Rv);
   };
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) issue(tile);
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();  // previous tile's LDS reads done
     sd.template commit<false, true>(d_s, W);
     sa.template commit<true, true>(a_s, W);
     if (ADD_SKIP) ss.template commit<false, false>(s_s, W);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
@@ -828,13 +866,14 @@ __host__ __device__ __forceinline__ void pooled_rows(int r_begin, int rows,
   *hi = h > Hp - 1 ? Hp - 1 : h;
 }
 
-template <int CIN, int COUT, bool NEED_DX>
+template <int CIN, int COUT, bool NEED_DX, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    int N, int H, int W, int R, int pb_h, int pb_w) {
+    int N, int H_, int W_, int R_, int pb_h, int pb_w, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   const int Wp = W + 2;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int d_elems = (R + 2) * Wp * COUT;
@@ -865,9 +904,10 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
              (hi - lo + 1) * prow_bytes * 2);
     sg.issue(argmax, prow0 * prow_bytes, (hi - lo + 1) * prow_bytes);
   };
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) issue(tile);
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
@@ -876,7 +916,7 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
     sg.commit(g_s);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
     gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
                                Rv + 2, d_s);
     __syncthreads();
@@ -896,12 +936,15 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
 // ky, D[m = 4 kx + ci][co] += X4[p + (ky-1, kx-1)][ci] dY[p][co]; the A tile
 // (4 pixels x 16 contiguous values = kx 0..3 x ci 0..3) and dY both come from
 // transposed LDS reads.  Scaled by 1/255 at the flush.
+template <int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const uint8_t* __restrict__ x, float* __restrict__ dw,
-    float* __restrict__ db, int N, int H, int W, int R, int pb_h, int pb_w) {
+    float* __restrict__ db, int N, int H_, int W_, int R_, int pb_h, int pb_w,
+    int xcd) {
   constexpr int COUT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   const int Wp = W + 2;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int d_elems = (R + 2) * Wp * COUT;
@@ -934,9 +977,10 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
              (hi - lo + 1) * prow_bytes * 2);
     sg.issue(argmax, prow0 * prow_bytes, (hi - lo + 1) * prow_bytes);
   };
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) issue(tile);
+  for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
@@ -945,7 +989,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
     sg.commit(g_s);
     __syncthreads();
-    if (tile + gridDim.x < ntiles) issue(tile + gridDim.x);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
     gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
                                Rv + 2, d_s);
@@ -1008,46 +1052,191 @@ void set_smem(K kernel, size_t bytes) {
                         static_cast<int>(bytes));
 }
 
+// ----- tile-height rules (constexpr: the same rule picks the compiled
+// geometry at build time and the runtime tile height at launch) -----------
+
 // rows per tile such that the staged halo fits NREG*256 16-B chunks per
 // stream and the tile holds ~target pixels
-int rows_for(int H, int W, int C, int target) {
+constexpr int rows_for(int H, int W, int C, int target) {
   int R = target / W;
   if (R < 1) R = 1;
   while (R > 1 && (R + 2) * W * C / 8 > NREG * kThreads) --R;
   return R < H ? R : H;
 }
+constexpr int rows_pool_fwd(int H, int W, int CIN, int px) {
+  const int Hp = (H + 1) / 2;
+  int Rp = (px / W - 1) / 2;
+  if (Rp < 1) Rp = 1;
+  while (Rp > 1 && (2 * Rp + 3) * W * CIN / 8 > NREG * kThreads) --Rp;
+  return Rp > Hp ? Hp : Rp;
+}
+constexpr int rows_conv1_fwd(int H, int W, int px) {
+  const int Hp = (H + 1) / 2;
+  int Rp = (px / W - 1) / 2;
+  if (Rp < 1) Rp = 1;
+  while (Rp > 1 && ((2 * Rp + 3) * W * 3 + 3) / 4 > NREG * kThreads) --Rp;
+  return Rp > Hp ? Hp : Rp;
+}
+constexpr int rows_pool_bwd(int H, int W, int CIN, int COUT, int px) {
+  const int Wo = (W + 1) / 2;
+  int R = rows_for(H, W, CIN, px);
+  while (R > 1 && ((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16) --R;
+  return R;
+}
+constexpr int rows_conv1_bwd(int H, int W, int px) {
+  const int Wo = (W + 1) / 2;
+  int R = px / W;
+  if (R < 1) R = 1;
+  while (R > 1 && (((R + 2) / 2 + 2) * Wo * 16 * 2 > NREG * kThreads * 16 ||
+                   ((R + 2) * W * 3 + 3) / 4 > NREG * kThreads))
+    --R;
+  return R > H ? H : R;
+}
 
 }  // namespace
 
 // ----------------------------------------------------------------- launchers
-int res_conv_rows(int H, int W) { return rows_for(H, W, 32, 192); }
+// Launch-shape knobs (defaults = the tuned configuration); exposed for
+// measurement through conv_tune_set (tools/conv_bench.py).  Changing a tile
+// knob away from its default makes the launchers fall back to the
+// runtime-geometry kernels.
+struct ConvTune {
+  int xcd = 1;            // XCD-aware contiguous tile ranges
+  int cap_fwd = 4;        // max resident workgroups per CU, forward kernels
+  int cap_bwd = 2;        // ... backward kernels
+  int px_res_fwd = 384;   // target pixels per tile
+  int px_res_bwd = 384;
+  int px_pool_fwd = 400;  // conv pixels per tile (pre-pool)
+  int px_conv1_fwd = 480;
+  int px_pool_bwd = 256;
+  int px_conv1_bwd = 384;
+  int specialize = 1;     // use compile-time-geometry kernels when they match
+};
+constexpr ConvTune kDef{};
+static ConvTune g_tune;
+
+int conv_tune_set(const char* key, int value) {
+  struct { const char* k; int* v; } table[] = {
+      {"xcd", &g_tune.xcd}, {"cap_fwd", &g_tune.cap_fwd},
+      {"cap_bwd", &g_tune.cap_bwd}, {"px_res_fwd", &g_tune.px_res_fwd},
+      {"px_res_bwd", &g_tune.px_res_bwd}, {"px_pool_fwd", &g_tune.px_pool_fwd},
+      {"px_conv1_fwd", &g_tune.px_conv1_fwd},
+      {"px_pool_bwd", &g_tune.px_pool_bwd},
+      {"px_conv1_bwd", &g_tune.px_conv1_bwd},
+      {"specialize", &g_tune.specialize}};
+  for (auto& e : table) {
+    if (std::strcmp(e.k, key) == 0) {
+      const int old = *e.v;
+      if (value >= 0) *e.v = value;
+      return old;
+    }
+  }
+  return -1;
+}
+
+namespace {
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// Compiled geometries: the IMPALA frame (72x96) and the Doom frame (72x128)
+// at every torso stage.  f(IC<H>, IC<W>, IC<R>) is called with the matching
+// compile-time geometry, or with zeros (runtime shapes).
+template <int HH, int WW, int RR, typename F>
+bool geo_try(int H, int W, int R, F& f) {
+  if (H == HH && W == WW && R == RR) {
+    f(IC<HH>{}, IC<WW>{}, IC<RR>{});
+    return true;
+  }
+  return false;
+}
+
+enum Stage { kConv1, kStage1, kStage2, kStage3 };
+
+// R(H, W) for a kernel family, as a constexpr functor.
+template <int STAGE, typename RF, typename F>
+void with_geo(int H, int W, int R, F&& f) {
+  if (g_tune.specialize) {
+    if constexpr (STAGE == kConv1) {
+      if (geo_try<72, 96, RF::rows(72, 96)>(H, W, R, f)) return;
+      if (geo_try<72, 128, RF::rows(72, 128)>(H, W, R, f)) return;
+    } else if constexpr (STAGE == kStage1) {
+      if (geo_try<36, 48, RF::rows(36, 48)>(H, W, R, f)) return;
+      if (geo_try<36, 64, RF::rows(36, 64)>(H, W, R, f)) return;
+    } else if constexpr (STAGE == kStage2) {
+      if (geo_try<18, 24, RF::rows(18, 24)>(H, W, R, f)) return;
+      if (geo_try<18, 32, RF::rows(18, 32)>(H, W, R, f)) return;
+    } else {
+      if (geo_try<9, 12, RF::rows(9, 12)>(H, W, R, f)) return;
+      if (geo_try<9, 16, RF::rows(9, 16)>(H, W, R, f)) return;
+    }
+  }
+  f(IC<0>{}, IC<0>{}, IC<0>{});
+}
+
+template <int C>
+struct RowsResFwd {
+  static constexpr int rows(int H, int W) { return rows_for(H, W, C, kDef.px_res_fwd); }
+};
+template <int C>
+struct RowsResBwd {
+  static constexpr int rows(int H, int W) { return rows_for(H, W, C, kDef.px_res_bwd); }
+};
+template <int CIN>
+struct RowsPoolFwd {
+  static constexpr int rows(int H, int W) { return rows_pool_fwd(H, W, CIN, kDef.px_pool_fwd); }
+};
+struct RowsConv1Fwd {
+  static constexpr int rows(int H, int W) { return rows_conv1_fwd(H, W, kDef.px_conv1_fwd); }
+};
+template <int CIN, int COUT>
+struct RowsPoolBwd {
+  static constexpr int rows(int H, int W) {
+    return rows_pool_bwd(H, W, CIN, COUT, kDef.px_pool_bwd);
+  }
+};
+struct RowsConv1Bwd {
+  static constexpr int rows(int H, int W) { return rows_conv1_bwd(H, W, kDef.px_conv1_bwd); }
+};
+
+}  // namespace
+
+int res_conv_rows(int H, int W) { return rows_for(H, W, 32, g_tune.px_res_fwd); }
 
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
                          int C, bool post_relu, hipStream_t s) {
-  const int R = rows_for(H, W, C, 192);
+  const int R = rows_for(H, W, C, g_tune.px_res_fwd);
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C + R * W * C) * sizeof(bf16_t);
-  const int grid = grid_for(ntiles, smem, 4);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
   auto Y = static_cast<bf16_t*>(y);
-#define SA_RF(CC, RE, PR)                                                     \
-  {                                                                           \
-    auto k = res_conv_fwd_kernel<CC, RE, PR>;                                 \
-    set_smem(k, smem);                                                        \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, X, w, b, RS,   \
-                       Y, N, H, W, R);                                        \
-  }
+  const int xcd = g_tune.xcd;
+  auto go = [&](auto kernel) {
+    set_smem(kernel, smem);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w, b,
+                       RS, Y, N, H, W, R, xcd);
+  };
+#define SA_RF(CC, RE, PR, STG)                                                 \
+  with_geo<STG, RowsResFwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {        \
+    go(res_conv_fwd_kernel<CC, RE, PR, decltype(h)::value,                     \
+                           decltype(ww)::value, decltype(r)::value>);          \
+  })
   const bool re = resid != nullptr;
   if (C == 16) {
-    if (re && post_relu) SA_RF(16, true, true)
-    else if (re) SA_RF(16, true, false)
-    else SA_RF(16, false, false)
+    if (re && post_relu) SA_RF(16, true, true, kStage1);
+    else if (re) SA_RF(16, true, false, kStage1);
+    else SA_RF(16, false, false, kStage1);
+  } else if (H * 2 > 18 + 9) {
+    if (re && post_relu) SA_RF(32, true, true, kStage2);
+    else if (re) SA_RF(32, true, false, kStage2);
+    else SA_RF(32, false, false, kStage2);
   } else {
-    if (re && post_relu) SA_RF(32, true, true)
-    else if (re) SA_RF(32, true, false)
-    else SA_RF(32, false, false)
+    if (re && post_relu) SA_RF(32, true, true, kStage3);
+    else if (re) SA_RF(32, true, false, kStage3);
+    else SA_RF(32, false, false, kStage3);
   }
 #undef SA_RF
 }
@@ -1056,27 +1245,27 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           void* pooled, uint8_t* argmax, int N, int H, int W,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
-  // ~400 conv pixels per tile; staged halo (2Rp+3 rows) within NREG*256 chunks
-  int Rp = (400 / W - 1) / 2;
-  if (Rp < 1) Rp = 1;
-  while (Rp > 1 && (2 * Rp + 3) * W * CIN / 8 > NREG * kThreads) --Rp;
-  if (Rp > Hp) Rp = Hp;
+  const int Rp = rows_pool_fwd(H, W, CIN, g_tune.px_pool_fwd);
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (9 * CIN * COUT + (2 * Rp + 3) * (W + 2) * CIN +
                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
-  const int grid = grid_for(ntiles, smem, 4);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto P = static_cast<bf16_t*>(pooled);
-#define SA_CP(CI, CO)                                                          \
-  {                                                                            \
-    auto k = conv_pool_fwd_kernel<CI, CO>;                                     \
-    set_smem(k, smem);                                                         \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, X, w, b, P,     \
-                       argmax, N, H, W, Rp, pb_h, pb_w);                       \
-  }
-  if (CIN == 16 && COUT == 32) SA_CP(16, 32)
-  else if (CIN == 32 && COUT == 32) SA_CP(32, 32)
-  else if (CIN == 16 && COUT == 16) SA_CP(16, 16)
+  const int xcd = g_tune.xcd;
+  auto go = [&](auto kernel) {
+    set_smem(kernel, smem);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w, b,
+                       P, argmax, N, H, W, Rp, pb_h, pb_w, xcd);
+  };
+#define SA_CP(CI, CO, STG)                                                     \
+  with_geo<STG, RowsPoolFwd<CI>>(H, W, Rp, [&](auto h, auto ww, auto r) {      \
+    go(conv_pool_fwd_kernel<CI, CO, decltype(h)::value, decltype(ww)::value,   \
+                            decltype(r)::value>);                              \
+  })
+  if (CIN == 16 && COUT == 32) SA_CP(16, 32, kStage1);
+  else if (CIN == 32 && COUT == 32) SA_CP(32, 32, kStage2);
+  else if (CIN == 16 && COUT == 16) SA_CP(16, 16, kStage1);
 #undef SA_CP
 }
 
@@ -1084,43 +1273,54 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                            void* pooled, uint8_t* argmax, int N, int H, int W,
                            int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
-  int Rp = (480 / W - 1) / 2;
-  if (Rp < 1) Rp = 1;
-  while (Rp > 1 && ((2 * Rp + 3) * W * 3 + 3) / 4 > NREG * kThreads) --Rp;
-  if (Rp > Hp) Rp = Hp;
+  const int Rp = rows_conv1_fwd(H, W, g_tune.px_conv1_fwd);
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (3 * 16 * 16 + (2 * Rp + 1) * W * 16 +
                        ((2 * Rp + 3) * (W + 2) + 4) * 4) * sizeof(bf16_t);
-  const int grid = grid_for(ntiles, smem, 4);
-  set_smem(conv1_pool_fwd_kernel, smem);
-  hipLaunchKernelGGL(conv1_pool_fwd_kernel, dim3(grid), dim3(kThreads), smem,
-                     s, x, w, b, static_cast<bf16_t*>(pooled), argmax, N, H, W,
-                     Rp, pb_h, pb_w);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
+  auto P = static_cast<bf16_t*>(pooled);
+  const int xcd = g_tune.xcd;
+  with_geo<kConv1, RowsConv1Fwd>(H, W, Rp, [&](auto h, auto ww, auto r) {
+    auto k = conv1_pool_fwd_kernel<decltype(h)::value, decltype(ww)::value,
+                                   decltype(r)::value>;
+    set_smem(k, smem);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, x, w, b, P,
+                       argmax, N, H, W, Rp, pb_h, pb_w, xcd);
+  });
 }
 
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
                          int H, int W, int C, hipStream_t s) {
-  const int R = rows_for(H, W, C, 192);
+  const int R = rows_for(H, W, C, g_tune.px_res_bwd);
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C) + R * W * C) *
                       sizeof(bf16_t);
-  const int grid = grid_for(ntiles, smem, 2);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DY = static_cast<const bf16_t*>(dy);
   auto A = static_cast<const bf16_t*>(act);
   auto SK = static_cast<const bf16_t*>(skip);
   auto DX = static_cast<bf16_t*>(dx);
-#define SA_RB(CC, SKP)                                                         \
-  {                                                                            \
-    auto k = res_conv_bwd_kernel<CC, SKP>;                                     \
-    set_smem(k, smem);                                                         \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, DY, A, SK, w,   \
-                       DX, dw, db, N, H, W, R);                                \
-  }
+  const int xcd = g_tune.xcd;
+  auto go = [&](auto kernel) {
+    set_smem(kernel, smem);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DY, A, SK,
+                       w, DX, dw, db, N, H, W, R, xcd);
+  };
+#define SA_RB(CC, SKP, STG)                                                    \
+  with_geo<STG, RowsResBwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {        \
+    go(res_conv_bwd_kernel<CC, SKP, decltype(h)::value, decltype(ww)::value,   \
+                           decltype(r)::value>);                               \
+  })
   if (C == 16) {
-    if (skip) SA_RB(16, true) else SA_RB(16, false)
+    if (skip) SA_RB(16, true, kStage1);
+    else SA_RB(16, false, kStage1);
+  } else if (H * 2 > 18 + 9) {
+    if (skip) SA_RB(32, true, kStage2);
+    else SA_RB(32, false, kStage2);
   } else {
-    if (skip) SA_RB(32, true) else SA_RB(32, false)
+    if (skip) SA_RB(32, true, kStage3);
+    else SA_RB(32, false, kStage3);
   }
 #undef SA_RB
 }
@@ -1130,32 +1330,37 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           int H, int W, int CIN, int COUT, int pb_h, int pb_w,
                           hipStream_t s) {
   const int Wo = (W + 1) / 2;
-  int R = rows_for(H, W, CIN, 256);
-  // pooled rows staged: ((R+2)/2+2) * Wo * COUT * 2 bytes within NREG*256*16
-  while (R > 1 && ((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16) --R;
+  const int R = rows_pool_bwd(H, W, CIN, COUT, g_tune.px_pool_bwd);
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * CIN * COUT + (R + 2) * (W + 2) * (CIN + COUT) +
                        CIN + COUT + prow_max * Wo * COUT) * sizeof(bf16_t) +
                       prow_max * Wo * COUT;
-  const int grid = grid_for(ntiles, smem, 2);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DP = static_cast<const bf16_t*>(dP);
   auto X = static_cast<const bf16_t*>(x);
   auto DX = static_cast<bf16_t*>(dx);
-#define SA_PB(CI, CO, NDX)                                                     \
-  {                                                                            \
-    auto k = pool_conv_bwd_kernel<CI, CO, NDX>;                                \
-    set_smem(k, smem);                                                         \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, DP, argmax, X,  \
-                       w, DX, dw, db, N, H, W, R, pb_h, pb_w);                 \
-  }
+  const int xcd = g_tune.xcd;
+  auto go = [&](auto kernel) {
+    set_smem(kernel, smem);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DP, argmax,
+                       X, w, DX, dw, db, N, H, W, R, pb_h, pb_w, xcd);
+  };
+#define SA_PB(CI, CO, NDX, STG)                                                \
+  with_geo<STG, RowsPoolBwd<CI, CO>>(H, W, R, [&](auto h, auto ww, auto r) {   \
+    go(pool_conv_bwd_kernel<CI, CO, NDX, decltype(h)::value,                   \
+                            decltype(ww)::value, decltype(r)::value>);         \
+  })
   const bool ndx = dx != nullptr;
   if (CIN == 16 && COUT == 32) {
-    if (ndx) SA_PB(16, 32, true) else SA_PB(16, 32, false)
+    if (ndx) SA_PB(16, 32, true, kStage1);
+    else SA_PB(16, 32, false, kStage1);
   } else if (CIN == 32 && COUT == 32) {
-    if (ndx) SA_PB(32, 32, true) else SA_PB(32, 32, false)
+    if (ndx) SA_PB(32, 32, true, kStage2);
+    else SA_PB(32, 32, false, kStage2);
   } else if (CIN == 16 && COUT == 16) {
-    if (ndx) SA_PB(16, 16, true) else SA_PB(16, 16, false)
+    if (ndx) SA_PB(16, 16, true, kStage1);
+    else SA_PB(16, 16, false, kStage1);
   }
 #undef SA_PB
 }
@@ -1164,22 +1369,22 @@ void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
                            int H, int W, int pb_h, int pb_w, hipStream_t s) {
   const int Wo = (W + 1) / 2;
-  int R = 384 / W;
-  if (R < 1) R = 1;
-  while (R > 1 && (((R + 2) / 2 + 2) * Wo * 16 * 2 > NREG * kThreads * 16 ||
-                   ((R + 2) * W * 3 + 3) / 4 > NREG * kThreads))
-    --R;
-  if (R > H) R = H;
+  const int R = rows_conv1_bwd(H, W, g_tune.px_conv1_bwd);
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = ((R + 2) * (W + 2) * 16 + 16 + (((R + 2) * (W + 2) + 5) & ~1) * 4 +
                        prow_max * Wo * 16) * sizeof(bf16_t) +
                       prow_max * Wo * 16;
-  const int grid = grid_for(ntiles, smem, 2);
-  set_smem(conv1_pool_bwd_kernel, smem);
-  hipLaunchKernelGGL(conv1_pool_bwd_kernel, dim3(grid), dim3(kThreads), smem,
-                     s, static_cast<const bf16_t*>(dP), argmax, x, dw, db, N,
-                     H, W, R, pb_h, pb_w);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
+  auto DP = static_cast<const bf16_t*>(dP);
+  const int xcd = g_tune.xcd;
+  with_geo<kConv1, RowsConv1Bwd>(H, W, R, [&](auto h, auto ww, auto r) {
+    auto k = conv1_pool_bwd_kernel<decltype(h)::value, decltype(ww)::value,
+                                   decltype(r)::value>;
+    set_smem(k, smem);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, DP, argmax, x,
+                       dw, db, N, H, W, R, pb_h, pb_w, xcd);
+  });
 }
 
 }  // namespace conv
