@@ -42,7 +42,7 @@ constexpr int GPW = 4;  // 16-pixel groups per wave per chunk
 struct TileIter {
   int first, stride, end;
   __device__ __forceinline__ TileIter(int ntiles, int xcd) {
-    if (!xcd) {
+    if (!(xcd & 1)) {
       first = blockIdx.x;
       stride = gridDim.x;
       end = ntiles;
@@ -286,16 +286,23 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
   }
 }
 
-// wgrad accumulators: wave w owns taps {w, w+4, w+8}; wave 1 (2 taps) also
-// owns the bias pseudo-tap.  D[m=ci][n=co] per (tap, ci-half, co-half).
+// wgrad accumulators.  The 9 taps are split into TG tap groups (TG = 1 for
+// 16x16 weights, 2 for the larger ones to bound accumulator registers); wave w
+// owns tap group w % TG and visits every (4/TG)-th 16-pixel group, so the dY
+// operand and the pixel addressing are read/computed 4/TG times less often
+// than with one tap set per wave.  D[m=ci][n=co] per (tap, ci-half,
+// co-half); the waves' partial sums are reduced through LDS once per
+// workgroup (flush_wgrad).
 template <int CIN, int COUT>
 struct WgradAcc {
   static constexpr int HC = CIN / 16, HO = COUT / 16;
-  f4 w[3][HC][HO];
+  static constexpr int TG = CIN * COUT > 512 ? 2 : 1;  // tap groups
+  static constexpr int TPG = (9 + TG - 1) / TG;        // taps per group
+  f4 w[TPG][HC][HO];
   f4 b[HO];
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < TPG; ++t)
 #pragma unroll
       for (int c = 0; c < HC; ++c)
 #pragma unroll
@@ -314,9 +321,12 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
                                                 int npix, int zero_a,
                                                 int zero_d,
                                                 WgradAcc<CIN, COUT>& acc) {
-  constexpr int HC = CIN / 16, HO = COUT / 16;
+  using A = WgradAcc<CIN, COUT>;
+  constexpr int HC = A::HC, HO = A::HO, TG = A::TG, TPG = A::TPG;
+  constexpr int GSTRIDE = kWaves / TG;
   const int lane = lane_id();
   const int wave = wave_id();
+  const int tg = wave % TG;
   const int Wp = Wt + 2;
   const int ngroups = (npix + 15) / 16;
   const int sub = lane & 15;
@@ -324,7 +334,7 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
   const int pcol = (sub & 3) * 4;  // 4-element column chunk
   s4 ones;
   ones[0] = ones[1] = ones[2] = ones[3] = 0x3F80;  // bf16 1.0
-  for (int g = 0; g < ngroups; ++g) {
+  for (int g = wave / TG; g < ngroups; g += GSTRIDE) {
     const int q = g * 16 + 4 * (lane >> 4) + qrow;
     const bool valid = q < npix;
     const int qr = valid ? q / Wt : 0;
@@ -332,11 +342,13 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
     const int pos = (qr + 1) * Wp + (qc + 1);
     s4 bd[HO];
 #pragma unroll
-    for (int o = 0; o < HO; ++o)
+    for (int o = 0; o < HO; ++o) {
       bd[o] = lds_tr4(d_s + (valid ? pos * COUT : zero_d) + 16 * o + pcol);
+      if (tg == 0) acc.b[o] = mfma16(ones, bd[o], acc.b[o]);
+    }
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int tap = wave + 4 * t;
+    for (int k = 0; k < TPG; ++k) {
+      const int tap = tg * TPG + k;
       if (tap < 9) {
         const int ky = tap / 3, kx = tap % 3;
         const int apos = pos + (ky - 1) * Wp + (kx - 1);
@@ -344,43 +356,61 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
         for (int c = 0; c < HC; ++c) {
           const s4 aa = lds_tr4(a_s + (valid ? apos * CIN : zero_a) + 16 * c + pcol);
 #pragma unroll
-          for (int o = 0; o < HO; ++o) acc.w[t][c][o] = mfma16(aa, bd[o], acc.w[t][c][o]);
+          for (int o = 0; o < HO; ++o) acc.w[k][c][o] = mfma16(aa, bd[o], acc.w[k][c][o]);
         }
       }
-    }
-    if (wave == 1) {
-#pragma unroll
-      for (int o = 0; o < HO; ++o) acc.b[o] = mfma16(ones, bd[o], acc.b[o]);
     }
   }
 }
 
+// Sums the waves' accumulators through LDS (scratch: >= 4*CIN*COUT floats,
+// 16-B aligned; all tile work must be finished) and adds the workgroup's
+// total to dw/db with one float atomic per element.
 template <int CIN, int COUT>
 __device__ __forceinline__ void flush_wgrad(const WgradAcc<CIN, COUT>& acc,
                                             float scale, float* __restrict__ dw,
-                                            float* __restrict__ db) {
-  constexpr int HC = CIN / 16, HO = COUT / 16;
+                                            float* __restrict__ db,
+                                            float* scratch) {
+  using A = WgradAcc<CIN, COUT>;
+  constexpr int HC = A::HC, HO = A::HO, TG = A::TG, TPG = A::TPG;
+  constexpr int PER = CIN * COUT;  // floats per wave per tap
   const int lane = lane_id();
   const int wave = wave_id();
+  __syncthreads();
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int tap = wave + 4 * t;
-    if (tap < 9) {
+  for (int k = 0; k <= TPG; ++k) {  // k == TPG: bias pseudo-tap
+    // [wave][c][o][i][lane]: conflict-free writes
 #pragma unroll
-      for (int c = 0; c < HC; ++c)
+    for (int c = 0; c < HC; ++c)
 #pragma unroll
-        for (int o = 0; o < HO; ++o)
+      for (int o = 0; o < HO; ++o)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int ci = 16 * c + 4 * (lane >> 4) + i;
-            const int co = 16 * o + (lane & 15);
-            atomicAdd(dw + (tap * CIN + ci) * COUT + co, acc.w[t][c][o][i] * scale);
-          }
+        for (int i = 0; i < 4; ++i) {
+          const float v = k < TPG ? acc.w[k < TPG ? k : 0][c][o][i]
+                                  : (c == 0 ? acc.b[o][i] : 0.f);
+          scratch[wave * PER + ((c * HO + o) * 4 + i) * 64 + lane] = v;
+        }
+    __syncthreads();
+    for (int e = threadIdx.x; e < TG * PER; e += kThreads) {
+      const int tg = e / PER;
+      const int r = e - tg * PER;
+      float v = 0.f;
+#pragma unroll
+      for (int w = tg; w < kWaves; w += TG) v += scratch[w * PER + r];
+      const int l = r & 63;
+      const int i = (r >> 6) & 3;
+      const int co_h = (r >> 8) % HO;
+      const int ci_h = (r >> 8) / HO;
+      const int ci = 16 * ci_h + 4 * (l >> 4) + i;
+      const int co = 16 * co_h + (l & 15);
+      const int tap = tg * TPG + k;
+      if (k < TPG) {
+        if (tap < 9) atomicAdd(dw + (tap * CIN + ci) * COUT + co, v * scale);
+      } else if (tg == 0 && ci_h == 0 && (l >> 4) == 0 && i == 0) {
+        atomicAdd(db + co, v);  // bias: every D row holds the column sum
+      }
     }
-  }
-  if (wave == 1 && (lane >> 4) == 0) {
-#pragma unroll
-    for (int o = 0; o < HO; ++o) atomicAdd(db + 16 * o + (lane & 15), acc.b[o][0]);
+    __syncthreads();
   }
 }
 
@@ -603,7 +633,9 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();
+    if (!((xcd >> 8) & 8))
     sx.template commit<true, true>(x_s, W);
+    if (!((xcd >> 8) & 8))
     if (RESID) sr.template commit<false, false>(r_s, W);
     __syncthreads();
     const int nt = it.next(tile);
@@ -613,6 +645,7 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
       if (RESID) sr.issue(resid, n2, H, W, r2, Rv2);
     }
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    if (!((xcd >> 8) & 4))
     conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
@@ -659,15 +692,18 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     const int cr0 = 2 * i0 - pb_h;
     const int Rc = 2 * Rpv + 1;
     __syncthreads();
+    if (!((xcd >> 8) & 8))
     sx.template commit<false, true>(x_s, W);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
+    if (!((xcd >> 8) & 4))
     conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
       store4(y_s + q * COUT + co0, v);
     });
     __syncthreads();
+    if (!((xcd >> 8) & 1))
     pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
                     argmax);
   }
@@ -718,6 +754,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     const int Rc = 2 * Rpv + 1;
     const int npix = Rc * W;
     __syncthreads();
+    if (!((xcd >> 8) & 8))
     commit_x4(sx, x4, W, Rc + 2, 4);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
@@ -727,7 +764,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       a[ky] = *reinterpret_cast<const s4*>(w_s + (ky * 16 + (lane & 15)) * 16 +
                                            4 * (lane >> 4));
     const int ngroups = (npix + 15) / 16;
-    for (int g = wave; g < ngroups; g += kWaves) {
+    for (int g = wave; g < (((xcd >> 8) & 4) ? 0 : ngroups); g += kWaves) {
       int q = g * 16 + (lane & 15);
       const bool valid = q < npix;
       if (!valid) q = 0;
@@ -745,6 +782,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       }
     }
     __syncthreads();
+    if (!((xcd >> 8) & 1))
     pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
                     argmax);
   }
@@ -786,13 +824,17 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();  // previous tile's LDS reads done
+    if (!((xcd >> 8) & 8))
     sd.template commit<false, true>(d_s, W);
+    if (!((xcd >> 8) & 8))
     sa.template commit<true, true>(a_s, W);
+    if (!((xcd >> 8) & 8))
     if (ADD_SKIP) ss.template commit<false, false>(s_s, W);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    if (!((xcd >> 8) & 4))
     conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
       const int qr = q / W, qc = q - (q / W) * W;
       float m[4];
@@ -803,9 +845,10 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
       for (int i = 0; i < 4; ++i) v[i] = s[i] + (m[i] > 0.f ? v[i] : 0.f);
       store4(dx + (img0 + q) * C + ci0, v);
     });
+    if (!((xcd >> 8) & 2))
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
   }
-  flush_wgrad<C, C>(acc, 1.f, dw, db);
+  flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
 }
 
 // dY of the conv feeding a max-pool, for the halo tile rows [r_begin,
@@ -912,24 +955,30 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
+    if (!((xcd >> 8) & 8))
     sx.template commit<false, true>(x_s, W);
+    if (!((xcd >> 8) & 8))
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
+    if (!((xcd >> 8) & 8))
     sg.commit(g_s);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
+    if (!((xcd >> 8) & 1))
     gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
                                Rv + 2, d_s);
     __syncthreads();
     const int npix = Rv * W;
     if (NEED_DX) {
       const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    if (!((xcd >> 8) & 4))
       conv_tile_dgrad<CIN, COUT>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
         store4(dx + (img0 + q) * CIN + ci0, v);
       });
     }
+    if (!((xcd >> 8) & 2))
     conv_tile_wgrad<CIN, COUT>(x_s, d_s, W, npix, x_elems, d_elems, acc);
   }
-  flush_wgrad<CIN, COUT>(acc, 1.f, dw, db);
+  flush_wgrad<CIN, COUT>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
 }
 
 // First-layer weight gradient on the bf16x4 frame tile: for each kernel row
@@ -985,17 +1034,21 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
+    if (!((xcd >> 8) & 8))
     commit_x4(sx, x4, W, Rv + 2, 4);  // (contains a barrier)
+    if (!((xcd >> 8) & 8))
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
+    if (!((xcd >> 8) & 8))
     sg.commit(g_s);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
+    if (!((xcd >> 8) & 1))
     gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
                                Rv + 2, d_s);
     __syncthreads();
     const int ngroups = (npix + 15) / 16;
-    for (int g = wave; g < ngroups; g += kWaves) {
+    for (int g = wave; g < (((xcd >> 8) & 2) ? 0 : ngroups); g += kWaves) {
       const int qb = g * 16 + 4 * (lane >> 4) + (sub >> 2);
       const bool vb = qb < npix;
       const int qbr = vb ? qb / W : 0, qbc = vb ? qb - qbr * W : 0;
@@ -1111,6 +1164,7 @@ struct ConvTune {
   int px_pool_bwd = 256;
   int px_conv1_bwd = 384;
   int specialize = 1;     // use compile-time-geometry kernels when they match
+  int ablate = 0;         // timing-only: skip phases (1 pool, 2 wgrad, 4 conv, 8 LDS commit)
 };
 constexpr ConvTune kDef{};
 static ConvTune g_tune;
@@ -1123,7 +1177,7 @@ int conv_tune_set(const char* key, int value) {
       {"px_conv1_fwd", &g_tune.px_conv1_fwd},
       {"px_pool_bwd", &g_tune.px_pool_bwd},
       {"px_conv1_bwd", &g_tune.px_conv1_bwd},
-      {"specialize", &g_tune.specialize}};
+      {"specialize", &g_tune.specialize}, {"ablate", &g_tune.ablate}};
   for (auto& e : table) {
     if (std::strcmp(e.k, key) == 0) {
       const int old = *e.v;
@@ -1213,7 +1267,7 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
   auto Y = static_cast<bf16_t*>(y);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w, b,
@@ -1252,7 +1306,7 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto P = static_cast<bf16_t*>(pooled);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w, b,
@@ -1279,7 +1333,7 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                        ((2 * Rp + 3) * (W + 2) + 4) * 4) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto P = static_cast<bf16_t*>(pooled);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   with_geo<kConv1, RowsConv1Fwd>(H, W, Rp, [&](auto h, auto ww, auto r) {
     auto k = conv1_pool_fwd_kernel<decltype(h)::value, decltype(ww)::value,
                                    decltype(r)::value>;
@@ -1301,7 +1355,7 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
   auto A = static_cast<const bf16_t*>(act);
   auto SK = static_cast<const bf16_t*>(skip);
   auto DX = static_cast<bf16_t*>(dx);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DY, A, SK,
@@ -1340,7 +1394,7 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
   auto DP = static_cast<const bf16_t*>(dP);
   auto X = static_cast<const bf16_t*>(x);
   auto DX = static_cast<bf16_t*>(dx);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DP, argmax,
@@ -1377,7 +1431,7 @@ void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                       prow_max * Wo * 16;
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DP = static_cast<const bf16_t*>(dP);
-  const int xcd = g_tune.xcd;
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
   with_geo<kConv1, RowsConv1Bwd>(H, W, R, [&](auto h, auto ww, auto r) {
     auto k = conv1_pool_bwd_kernel<decltype(h)::value, decltype(ww)::value,
                                    decltype(r)::value>;
