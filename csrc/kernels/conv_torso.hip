@@ -220,6 +220,7 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
                                                 int npix, Epi epi) {
   static_assert(COUT == 16 || COUT == 32, "COUT");
   constexpr int NH = CIN / 16;
+  constexpr int GPW = NH == 2 ? 2 : ::sa::conv::GPW;  // bound accumulator registers
   const int lane = lane_id();
   const int wave = wave_id();
   const int Wp = Wt + 2;
@@ -610,7 +611,7 @@ __device__ __forceinline__ void load_weights4(const float* __restrict__ w,
 constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
 
 template <int C, bool RESID, bool POST_RELU, int HC, int WC, int RC>
-__global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_conv_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, const bf16_t* __restrict__ resid,
     bf16_t* __restrict__ y, int N, int H_, int W_, int R_, int xcd) {
@@ -618,31 +619,26 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* x_s = w_s + 9 * C * C;
-  bf16_t* r_s = x_s + (R + 2) * (W + 2) * C;
   load_weights4<C, C, true>(w, w_s);
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
-  RowStager<C, NREG> sx, sr;
+  RowStager<C, NREG> sx;
   const TileIter it(ntiles, xcd);
   int tile = it.first;
   if (it.valid(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     sx.issue(x, n, H, W, r0 - 1, Rv + 2);
-    if (RESID) sr.issue(resid, n, H, W, r0, Rv);
   }
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();
     if (!((xcd >> 8) & 8))
     sx.template commit<true, true>(x_s, W);
-    if (!((xcd >> 8) & 8))
-    if (RESID) sr.template commit<false, false>(r_s, W);
     __syncthreads();
     const int nt = it.next(tile);
     if (it.valid(nt)) {
       const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
       sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
-      if (RESID) sr.issue(resid, n2, H, W, r2, Rv2);
     }
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     if (!((xcd >> 8) & 4))
@@ -650,8 +646,10 @@ __global__ __launch_bounds__(kThreads) void res_conv_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
       if (RESID) {
+        // residual read straight from HBM (8 B/lane, 32-B runs per pixel):
+        // no staging registers or LDS for it
         float r[4];
-        load4(r_s + q * C + co0, r);
+        load4(resid + (img0 + q) * C + co0, r);
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] += r[i];
       }
@@ -789,7 +787,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
 }
 
 template <int C, bool ADD_SKIP, int HC, int WC, int RC>
-__global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_conv_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ act,
     const bf16_t* __restrict__ skip, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
@@ -801,7 +799,6 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* d_s = w_s + 9 * C * C;
   bf16_t* a_s = d_s + tile_elems + C;  // + one zero pixel each
-  bf16_t* s_s = a_s + tile_elems + C;  // skip interior [R][W][C]
   load_weights4<C, C, false>(w, w_s);
   for (int e = threadIdx.x; e < C; e += blockDim.x) {
     d_s[tile_elems + e] = 0;
@@ -811,12 +808,11 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
   acc.zero();
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
-  RowStager<C, NREG> sd, sa, ss;
+  RowStager<C, NREG> sd, sa;
   auto issue = [&](int t) {
     const int n = t / tpi, r0 = (t - n * tpi) * R, Rv = min(R, H - r0);
     sd.issue(dy, n, H, W, r0 - 1, Rv + 2);
     sa.issue(act, n, H, W, r0 - 1, Rv + 2);
-    if (ADD_SKIP) ss.issue(skip, n, H, W, r0, Rv);
   };
   const TileIter it(ntiles, xcd);
   int tile = it.first;
@@ -828,8 +824,6 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
     sd.template commit<false, true>(d_s, W);
     if (!((xcd >> 8) & 8))
     sa.template commit<true, true>(a_s, W);
-    if (!((xcd >> 8) & 8))
-    if (ADD_SKIP) ss.template commit<false, false>(s_s, W);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
@@ -840,7 +834,7 @@ __global__ __launch_bounds__(kThreads) void res_conv_bwd_kernel(
       float m[4];
       load4(a_s + ((qr + 1) * Wp + qc + 1) * C + ci0, m);
       float s[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ADD_SKIP) load4(s_s + q * C + ci0, s);
+      if (ADD_SKIP) load4(skip + (img0 + q) * C + ci0, s);  // from HBM
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = s[i] + (m[i] > 0.f ? v[i] : 0.f);
       store4(dx + (img0 + q) * C + ci0, v);
@@ -900,6 +894,89 @@ __device__ __forceinline__ void gather_pool_grad_lds(
   }
 }
 
+// The same dY tile, built per 2x2 block of conv positions.  Block (i, j)
+// holds conv rows 2i-pb_h+{0,1} x cols 2j-pb_w+{0,1}; its cells can only be
+// the argmax of pooled windows (i,j), (i-1,j), (i,j-1), (i-1,j-1) (a window's
+// dy/dx = 2 cells are the next block's offset-0 cells).  Each thread loads
+// those 4 windows once and writes 4 cells:
+//   (1,1) <- (i,j):4       (0,1) <- (i,j):1 + (i-1,j):7
+//   (1,0) <- (i,j):3 + (i,j-1):5
+//   (0,0) <- (i,j):0 + (i-1,j):6 + (i,j-1):2 + (i-1,j-1):8
+// (window:code).  ~2x fewer VALU ops and 4x fewer LDS reads than checking
+// every window of every cell.  Halo columns are zeroed separately.
+template <int COUT>
+__device__ __forceinline__ void gather_pool_grad_blocks(
+    const bf16_t* p_s, const uint8_t* g_s, int i_lo, int i_hi, int W, int Wo,
+    int pb_h, int pb_w, int r_begin, int rows, bf16_t* d_s) {
+  constexpr int CH = COUT / 8;
+  const int Wp = W + 2;
+  // halo columns -1 and W
+  for (int e = threadIdx.x; e < rows * 2 * CH; e += blockDim.x) {
+    const int part = e % CH;
+    const int side = (e / CH) & 1;
+    const int rr = e / (2 * CH);
+    *reinterpret_cast<uint4*>(d_s + (rr * Wp + (side ? W + 1 : 0)) * COUT +
+                              part * 8) = make_uint4(0, 0, 0, 0);
+  }
+  // blocks whose rows intersect [r_begin, r_begin + rows)
+  const int t0 = r_begin + pb_h;
+  const int ib0 = t0 >= 0 ? t0 / 2 : -((1 - t0) / 2);  // floor(t0 / 2)
+  const int ib1 = (r_begin + rows - 1 + pb_h) / 2;
+  const int nbr = ib1 - ib0 + 1;
+  const int total = nbr * Wo * CH;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int part = e % CH;
+    const int jb = (e / CH) % Wo;
+    const int ib = ib0 + e / (CH * Wo);
+    uint32_t cw[4][2];  // codes of windows (i,j), (i-1,j), (i,j-1), (i-1,j-1)
+    uint32_t vw[4][4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int i = ib - (w & 1), j = jb - (w >> 1);
+      if (i >= i_lo && i <= i_hi && j >= 0) {
+        const int o = ((i - i_lo) * Wo + j) * COUT + part * 8;
+        const uint2 c = *reinterpret_cast<const uint2*>(g_s + o);
+        const uint4 v = *reinterpret_cast<const uint4*>(p_s + o);
+        cw[w][0] = c.x; cw[w][1] = c.y;
+        vw[w][0] = v.x; vw[w][1] = v.y; vw[w][2] = v.z; vw[w][3] = v.w;
+      } else {
+        cw[w][0] = cw[w][1] = 0xFFFFFFFFu;  // matches no code
+        vw[w][0] = vw[w][1] = vw[w][2] = vw[w][3] = 0;
+      }
+    }
+    float cell[4][8];  // (a,b) = (0,0), (0,1), (1,0), (1,1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v[4];
+      int code[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t u = vw[w][k >> 1];
+        v[w] = __uint_as_float((k & 1) ? (u & 0xFFFF0000u) : (u << 16));
+        code[w] = (cw[w][k >> 2] >> (8 * (k & 3))) & 0xFF;
+      }
+      cell[3][k] = code[0] == 4 ? v[0] : 0.f;
+      cell[1][k] = (code[0] == 1 ? v[0] : 0.f) + (code[1] == 7 ? v[1] : 0.f);
+      cell[2][k] = (code[0] == 3 ? v[0] : 0.f) + (code[2] == 5 ? v[2] : 0.f);
+      cell[0][k] = (code[0] == 0 ? v[0] : 0.f) + (code[1] == 6 ? v[1] : 0.f) +
+                   (code[2] == 2 ? v[2] : 0.f) + (code[3] == 8 ? v[3] : 0.f);
+    }
+#pragma unroll
+    for (int cidx = 0; cidx < 4; ++cidx) {
+      const int rr = 2 * ib - pb_h + (cidx >> 1) - r_begin;
+      const int cc = 2 * jb - pb_w + (cidx & 1);
+      if (rr >= 0 && rr < rows && cc >= 0 && cc < W) {
+        uint4 o;
+        o.x = f2bf(cell[cidx][0]) | (static_cast<uint32_t>(f2bf(cell[cidx][1])) << 16);
+        o.y = f2bf(cell[cidx][2]) | (static_cast<uint32_t>(f2bf(cell[cidx][3])) << 16);
+        o.z = f2bf(cell[cidx][4]) | (static_cast<uint32_t>(f2bf(cell[cidx][5])) << 16);
+        o.w = f2bf(cell[cidx][6]) | (static_cast<uint32_t>(f2bf(cell[cidx][7])) << 16);
+        *reinterpret_cast<uint4*>(d_s + (rr * Wp + cc + 1) * COUT + part * 8) = o;
+      }
+    }
+  }
+}
+
 __host__ __device__ __forceinline__ void pooled_rows(int r_begin, int rows,
                                                      int pb_h, int Hp, int* lo,
                                                      int* hi) {
@@ -910,7 +987,7 @@ __host__ __device__ __forceinline__ void pooled_rows(int r_begin, int rows,
 }
 
 template <int CIN, int COUT, bool NEED_DX, int HC, int WC, int RC>
-__global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void pool_conv_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
@@ -964,8 +1041,8 @@ __global__ __launch_bounds__(kThreads) void pool_conv_bwd_kernel(
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     if (!((xcd >> 8) & 1))
-    gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
-                               Rv + 2, d_s);
+    gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
+                                  Rv + 2, d_s);
     __syncthreads();
     const int npix = Rv * W;
     if (NEED_DX) {
@@ -1044,8 +1121,8 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
     if (!((xcd >> 8) & 1))
-    gather_pool_grad_lds<COUT>(p_s, g_s, lo, H, W, Hp, Wo, pb_h, pb_w, r0 - 1,
-                               Rv + 2, d_s);
+    gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
+                                  Rv + 2, d_s);
     __syncthreads();
     const int ngroups = (npix + 15) / 16;
     for (int g = wave; g < (((xcd >> 8) & 2) ? 0 : ngroups); g += kWaves) {
@@ -1262,7 +1339,7 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          int C, bool post_relu, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_fwd);
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C + R * W * C) * sizeof(bf16_t);
+  const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
@@ -1348,8 +1425,7 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          int H, int W, int C, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C) + R * W * C) *
-                      sizeof(bf16_t);
+  const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DY = static_cast<const bf16_t*>(dy);
   auto A = static_cast<const bf16_t*>(act);
