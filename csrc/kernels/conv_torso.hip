@@ -1237,9 +1237,9 @@ struct ConvTune {
   int px_res_fwd = 384;   // target pixels per tile
   int px_res_bwd = 384;
   int px_pool_fwd = 400;  // conv pixels per tile (pre-pool)
-  int px_conv1_fwd = 480;
-  int px_pool_bwd = 256;
-  int px_conv1_bwd = 384;
+  int px_conv1_fwd = 960;
+  int px_pool_bwd = 512;
+  int px_conv1_bwd = 1152;
   int specialize = 1;     // use compile-time-geometry kernels when they match
   int ablate = 0;         // timing-only: skip phases (1 pool, 2 wgrad, 4 conv, 8 LDS commit)
 };
