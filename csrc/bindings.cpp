@@ -26,19 +26,26 @@ const uint8_t* u8ptr(const at::Tensor& t) {
 
 void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
              at::Tensor frames, double lr0, double total_frames, double decay,
-             double momentum, double eps) {
+             double momentum, double eps, c10::optional<at::Tensor> guard) {
   SA_CHECK(w); SA_CHECK(g); SA_CHECK(ms); SA_CHECK(mom); SA_CHECK_CUDA(frames);
   SA_CHECK_F32(w); SA_CHECK_F32(g); SA_CHECK_F32(ms); SA_CHECK_F32(mom);
   TORCH_CHECK(frames.scalar_type() == at::kLong, "frames must be int64");
   TORCH_CHECK(w.numel() % 4 == 0, "flat buffer must be a multiple of 4");
   TORCH_CHECK(g.numel() == w.numel() && ms.numel() == w.numel() &&
               mom.numel() == w.numel(), "size mismatch");
-  const c10::DeviceGuard guard(w.device());
+  int* gp = nullptr;
+  if (guard.has_value()) {
+    SA_CHECK_CUDA(*guard);
+    TORCH_CHECK(guard->scalar_type() == at::kInt && guard->numel() >= 2,
+                "guard must be int32[2] (flag, skipped)");
+    gp = guard->data_ptr<int>();
+  }
+  const c10::DeviceGuard dguard(w.device());
   sa::rmsprop_launch(w.data_ptr<float>(), g.data_ptr<float>(),
                      ms.data_ptr<float>(), mom.data_ptr<float>(),
                      frames.data_ptr<int64_t>(), w.numel(), (float)lr0,
                      total_frames, (float)decay, (float)momentum, (float)eps,
-                     cur_stream());
+                     gp, cur_stream());
 }
 
 std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
@@ -165,7 +172,11 @@ void register_conv_ops(pybind11::module& m);  // conv_bindings.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "scalable_agent_amd gfx950 HIP kernels";
-  m.def("rmsprop", &rmsprop);
+  m.def("rmsprop", &rmsprop, pybind11::arg("w"), pybind11::arg("g"),
+        pybind11::arg("ms"), pybind11::arg("mom"), pybind11::arg("frames"),
+        pybind11::arg("lr0"), pybind11::arg("total_frames"),
+        pybind11::arg("decay"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("guard") = pybind11::none());
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd);

@@ -14,7 +14,7 @@ namespace sa {
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, hipStream_t stream);
+                    float eps, int* guard, hipStream_t stream);
 
 // ---- vtrace_loss.hip -------------------------------------------------------
 // Fused V-trace (from logits) + IMPALA loss + analytic gradients.

@@ -5,6 +5,11 @@
 //   mom = momentum * mom + lr * g / sqrt(ms + eps)
 //   w  -= mom
 //
+// Non-finite guard (optional): a check kernel ORs "some gradient is NaN/inf"
+// into guard[0] (zeroed by a memset node each step); the update kernel then
+// leaves every parameter and slot untouched and counts the skipped step in
+// guard[1].  One extra 8-MB read per step, no host synchronisation.
+//
 // Memory-bound: 5 streams of 4 B (w, g, ms, mom read; w, ms, mom written) per
 // element, float4 vectorised, grid-stride with a grid sized for 256 CUs.  The
 // learning rate is computed on the device from the int64 frame counter so the
@@ -14,11 +19,28 @@
 namespace sa {
 namespace {
 
+__global__ __launch_bounds__(256) void finite_check_kernel(
+    const float4* __restrict__ g, int64_t n4, int* __restrict__ guard) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  bool bad = false;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       i < n4; i += stride) {
+    const float4 v = g[i];
+    bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(guard, 1);
+}
+
 __global__ __launch_bounds__(256) void rmsprop_kernel(
     float4* __restrict__ w, const float4* __restrict__ g,
     float4* __restrict__ ms, float4* __restrict__ mom,
     const int64_t* __restrict__ frames, int64_t n4, float lr0,
-    double total_frames, float one_minus_decay, float momentum, float eps) {
+    double total_frames, float one_minus_decay, float momentum, float eps,
+    int* __restrict__ guard) {
+  if (guard != nullptr && *guard) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(guard + 1, 1);
+    return;
+  }
   const double f = fmin(static_cast<double>(*frames), total_frames);
   const float lr = static_cast<float>(lr0 * (1.0 - f / total_frames));
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -45,18 +67,23 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, hipStream_t stream) {
+                    float eps, int* guard, hipStream_t stream) {
   const int64_t n4 = n / 4;  // FlatParams pads every tensor to 64 elements
   const int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
+  if (guard != nullptr) {
+    (void)hipMemsetAsync(guard, 0, sizeof(int), stream);
+    hipLaunchKernelGGL(finite_check_kernel, dim3(blocks), dim3(threads), 0,
+                       stream, reinterpret_cast<const float4*>(g), n4, guard);
+  }
   hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(threads), 0, stream,
                      reinterpret_cast<float4*>(w),
                      reinterpret_cast<const float4*>(g),
                      reinterpret_cast<float4*>(ms),
                      reinterpret_cast<float4*>(mom), frames, n4, lr0,
-                     total_frames, 1.0f - decay, momentum, eps);
+                     total_frames, 1.0f - decay, momentum, eps, guard);
 }
 
 }  // namespace sa

@@ -11,9 +11,14 @@ agent output - and every unroll:
 Output arrays are numpy, time-major, without the batch dimension.
 """
 
+import logging
+import time
+
 import numpy as np
 
 from .models.instruction import tokenize
+from .py_process import EnvRestartedError
+from .utils.tracing import trace
 from .structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
 
 INSTR_LEN = 16  # max words kept per instruction (batcher rows need one shape)
@@ -33,7 +38,7 @@ class Actor(object):
   """One actor = one env + persistent recurrent state."""
 
   def __init__(self, env, infer_fn, level_name, action_set, unroll_length,
-               num_actions, core_size=256, use_instruction=True):
+               num_actions, core_size=256, use_instruction=True, stall_ms=0):
     """env: FlowEnvironment; infer_fn(last_action, reward, done, frame,
     instr_ids, instr_len, c, h) on batch-1 numpy arrays -> (action, logits,
     baseline, c, h)."""
@@ -46,6 +51,8 @@ class Actor(object):
     self._core = core_size
     self._use_instr = use_instruction
     self._env_output = None
+    self._stall_s = stall_ms / 1000.0  # fault injection: slow actor
+    self.env_restarts = 0
 
   def _reset(self):
     env_output, env_state = self._env.initial()
@@ -61,12 +68,13 @@ class Actor(object):
     frame, instr = eo.observation
     ids, n = encode_instruction(instr if self._use_instr else None)
     c, h = self._agent_state
-    out = self._infer(
-        np.asarray([self._agent_output.action], np.int64),
-        np.asarray([eo.reward], np.float32),
-        np.asarray([eo.done], np.bool_),
-        np.asarray(frame, np.uint8)[None],
-        ids[None], np.asarray([n], np.int64), c[None], h[None])
+    with trace('actor_inference'):
+      out = self._infer(
+          np.asarray([self._agent_output.action], np.int64),
+          np.asarray([eo.reward], np.float32),
+          np.asarray([eo.done], np.bool_),
+          np.asarray(frame, np.uint8)[None],
+          ids[None], np.asarray([n], np.int64), c[None], h[None])
     action, logits, baseline, c2, h2 = out
     self._agent_state = (np.asarray(c2[0], np.float32),
                          np.asarray(h2[0], np.float32))
@@ -75,7 +83,22 @@ class Actor(object):
                                      np.float32(baseline[0]))
 
   def unroll(self):
-    """Runs one unroll; returns an ActorOutput of numpy arrays [T+1, ...]."""
+    """Runs one unroll; returns an ActorOutput of numpy arrays [T+1, ...].
+
+    If the env worker dies or hangs mid-unroll (EnvRestartedError), the
+    partial unroll is dropped and a fresh episode starts."""
+    while True:
+      try:
+        return self._unroll()
+      except EnvRestartedError as e:
+        self.env_restarts += 1
+        logging.getLogger('scalable_agent_amd').warning(
+            'actor %s: %s; dropping the in-flight unroll', self.level_name, e)
+        self._env_output = None
+
+  def _unroll(self):
+    if self._stall_s:
+      time.sleep(self._stall_s)
     if self._env_output is None:
       self._reset()
     T1 = self._T + 1

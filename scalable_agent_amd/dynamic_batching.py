@@ -207,7 +207,17 @@ def batch_fn_with_options(minimum_batch_size=1, maximum_batch_size=1024,
       if state['runner'] is not None and state['started']:
         state['runner'].join(timeout)
 
+    def stats():
+      """{'batches', 'requests'} served so far (mean batch = ratio)."""
+      b = state['batcher']
+      impl = getattr(b, '_impl', None)
+      if impl is None:
+        return {'batches': 0, 'requests': 0}
+      return {'batches': int(impl.num_batches),
+              'requests': int(impl.num_requests)}
+
     wrapper.start = start
+    wrapper.stats = stats
     wrapper.close = close
     wrapper.cancel = cancel
     wrapper.join = join

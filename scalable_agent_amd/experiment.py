@@ -67,20 +67,29 @@ def action_set_for(flags, level_name):
   return environments.DEFAULT_ACTION_SET
 
 
+def _supervision(flags, seed):
+  """EnvProcess keyword args: hang watchdog + env-side fault injection."""
+  from .runtime.faults import FaultSpec
+  return dict(timeout=flags.env_timeout_secs,
+              fault_inject=FaultSpec(flags.fault_inject).env_spec(),
+              fault_seed=seed)
+
+
 def create_environment(flags, level_name, seed, is_test=False):
   """Returns an unstarted EnvProcess (reference create_environment :430-459)."""
   kind = env_kind(flags, level_name)
   shape = frame_shape_for(flags, level_name)
+  sup = _supervision(flags, seed)
   if kind == 'doom':
     from .envs.doom import PyProcessDoom
     return py_process.EnvProcess(PyProcessDoom, shape, level_name, None,
-                                 flags.num_action_repeats, seed)
+                                 flags.num_action_repeats, seed, **sup)
   if kind == 'synthetic':
     from .envs.synthetic import SyntheticEnv
     cfg = {'benchmark_mode': flags.benchmark_mode}
     return py_process.EnvProcess(
         SyntheticEnv, shape, level_name, cfg, flags.num_action_repeats, seed,
-        frame_shape=shape, episode_length=flags.synthetic_episode_length)
+        frame_shape=shape, episode_length=flags.synthetic_episode_length, **sup)
   if level_name in dmlab30.ALL_LEVELS:
     level_name = 'contributed/dmlab30/' + level_name
   config = {
@@ -93,7 +102,7 @@ def create_environment(flags, level_name, seed, is_test=False):
     config['allowHoldOutLevels'] = 'true'
     config['mixerSeed'] = 0x600D5EED
   return py_process.EnvProcess(environments.PyProcessDmLab, shape, level_name,
-                               config, flags.num_action_repeats, seed)
+                               config, flags.num_action_repeats, seed, **sup)
 
 
 def level_names_for(flags):
@@ -171,6 +180,22 @@ class EpisodeLogger(object):
 
 
 # --------------------------------------------------------------- train
+class _Terminated(BaseException):
+  """Raised in the main thread by SIGTERM: stop cleanly and checkpoint."""
+
+
+def _install_sigterm_handler():
+  import signal
+  if threading.current_thread() is not threading.main_thread():
+    return
+
+  def handler(signum, frame):
+    del signum, frame
+    raise _Terminated()
+
+  signal.signal(signal.SIGTERM, handler)
+
+
 def train(flags):
   """Single-machine or data-parallel learner(s) with local actors."""
   import torch
@@ -179,9 +204,12 @@ def train(flags):
   from . import parallel
   from .actor import Actor, stack_unrolls
   from .learner import Learner, batch_to_device
+  from .runtime.faults import FaultSpec
   from .summary import SummaryWriter
   from .utils.timing import StepTimer
+  from .utils.tracing import trace
 
+  faults = FaultSpec(flags.fault_inject)
   level_names = level_names_for(flags)
   action_set = action_set_for(flags, level_names[0])
   num_actions = len(action_set)
@@ -205,8 +233,10 @@ def train(flags):
       actors_levels.append(level)
     py_process.start_all(envs)
 
-  rank, world, local_rank = parallel.init_distributed()
+  rank, world, local_rank = parallel.init_distributed(
+      timeout_s=flags.collective_timeout_secs)
   device = _device(flags, local_rank)
+  _install_sigterm_handler()
   if device.type == 'cuda':
     torch.cuda.set_device(device)
   torch.manual_seed(flags.seed + rank)
@@ -230,6 +260,7 @@ def train(flags):
                                          flags.num_actors))
   stop = threading.Event()
   threads = []
+  actors = []
   transport = None
   infer = None
   if distributed_actors:
@@ -267,13 +298,17 @@ def train(flags):
     for i, env in enumerate(envs):
       actor = Actor(environments.FlowEnvironment(env), infer,
                     actors_levels[i], action_set, flags.unroll_length,
-                    num_actions, use_instruction=use_instr)
+                    num_actions, use_instruction=use_instr,
+                    stall_ms=faults.get('actor_stall'))
+      actors.append(actor)
       t = threading.Thread(target=actor_loop, args=(actor,), daemon=True,
                            name='actor-%d' % i)
       t.start()
       threads.append(t)
 
   episode_logger = EpisodeLogger(flags, level_names, writer)
+  if flags.deterministic:
+    torch.use_deterministic_algorithms(True, warn_only=True)
   timer = StepTimer(learner.frames_per_step)
   last_summary = time.time()
   last_log_frames = int(learner.frames.item())
@@ -295,17 +330,29 @@ def train(flags):
               (flags.queue_timeout_secs,
                [t.is_alive() for t in threads] or 'remote'))
       timer.add_wait(time.time() - t_wait)
+      if flags.deterministic:
+        # batch order independent of actor timing: sort by actor identity
+        unrolls.sort(key=lambda u: (u.level_name, float(u.agent_state[0][0])))
       host = stack_unrolls(unrolls, use_instruction=use_instr,
                            pin=device.type == 'cuda')
-      data = batch_to_device(host, device)
-      if use_graph:
-        if learner._graph is None:
-          learner.capture(data)
-        learner.load_static(data)
-        loss = learner.graph_step()
-      else:
-        loss = learner.step(data)
+      if faults.get('learner_nan') == steps + 1:
+        host.env_outputs.reward[1:, 0] = float('nan')  # poisoned batch
+      with trace('h2d'):
+        data = batch_to_device(host, device)
+      with trace('learner_step'):
+        if use_graph:
+          if learner._graph is None:
+            learner.capture(data)
+          learner.load_static(data)
+          loss = learner.graph_step()
+        else:
+          loss = learner.step(data)
       steps += 1
+      if (world > 1 and flags.consistency_check_steps and
+          steps % flags.consistency_check_steps == 0 and
+          not parallel.param_checksum_consistent(learner.flat.params)):
+        raise RuntimeError('data-parallel replicas diverged at step %d' %
+                           steps)
       if infer is not None:
         model.publish(learner.flat.params)
       elif transport is not None:
@@ -321,12 +368,20 @@ def train(flags):
                                  flags.save_summaries_secs):
         last_summary = time.time()
         lr = learner.opt.current_lr(frames - learner.frames_per_step)
-        writer.add_scalars({'learning_rate': lr,
-                            'total_loss': float(loss),
-                            'frames_per_sec': timer.frames_per_sec(),
-                            'learner_steps_per_sec': timer.steps_per_sec(),
-                            'queue_wait_frac': timer.wait_fraction()},
-                           frames)
+        scalars = {'learning_rate': lr,
+                   'total_loss': float(loss),
+                   'frames_per_sec': timer.frames_per_sec(),
+                   'learner_steps_per_sec': timer.steps_per_sec(),
+                   'queue_wait_frac': timer.wait_fraction(),
+                   'skipped_updates': learner.opt.skipped_steps,
+                   'env_restarts': sum(a.env_restarts for a in actors)}
+        if infer is not None and infer.stats()['batches']:
+          st = infer.stats()
+          scalars['inference_batch_size_mean'] = (st['requests'] /
+                                                  st['batches'])
+        if learner.grad_sync is not None:
+          scalars['allreduce_ms'] = 1e3 * learner.grad_sync.last_time_s
+        writer.add_scalars(scalars, frames)
         writer.add_histogram('action',
                              host.agent_outputs.action[1:].numpy(), frames)
         writer.flush()
@@ -338,6 +393,9 @@ def train(flags):
                  100 * timer.wait_fraction())
       if saver is not None:
         saver.maybe_save()
+  except _Terminated:
+    log.warning('SIGTERM: stopping and checkpointing at %d frames',
+                int(learner.frames.item()))
   finally:
     stop.set()
     if infer is not None:

@@ -103,6 +103,17 @@ def build_parser() -> argparse.ArgumentParser:
                  help='Stop after N learner steps (0 = frames limit only).')
   p.add_argument('--queue_timeout_secs', type=float, default=600.,
                  help='Learner starvation timeout (diagnostic failure).')
+  p.add_argument('--env_timeout_secs', type=float, default=0.,
+                 help='Env-call watchdog: a worker that does not answer in '
+                      'time is killed and respawned (0 = off).')
+  p.add_argument('--consistency_check_steps', type=int, default=1000,
+                 help='Data-parallel: every N steps all-reduce a parameter '
+                      'checksum and fail on divergence (0 = off).')
+  p.add_argument('--collective_timeout_secs', type=float, default=600.,
+                 help='RCCL/gloo collective timeout: a hung rank aborts the '
+                      'job (restart it to resume from the last checkpoint).')
+  p.add_argument('--skip_nonfinite', type=_str2bool, default=True,
+                 help='Skip (and count) optimizer steps with NaN/inf grads.')
   return p
 
 

@@ -26,6 +26,7 @@ from . import losses as losses_lib
 from . import vtrace as vtrace_lib
 from .optim import FlatParams, RMSProp
 from .structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
+from .utils.tracing import trace
 
 
 def compute_loss(agent, data, flags, use_fused=False):
@@ -110,14 +111,18 @@ class Learner:
   # ------------------------------------------------------------ eager step
   def _fwd_bwd(self, data):
     self.flat.zero_grad()
-    loss = compute_loss(self.agent, data, self.flags, self.use_fused)
-    loss.backward()
+    with trace('forward'):
+      loss = compute_loss(self.agent, data, self.flags, self.use_fused)
+    with trace('backward'):
+      loss.backward()
     return loss
 
   def _apply(self):
     if self.grad_sync is not None:
-      self.grad_sync.all_reduce()
-    self.opt.step(self.frames)
+      with trace('allreduce'):
+        self.grad_sync.all_reduce()
+    with trace('optimizer'):
+      self.opt.step(self.frames)
     self.frames.add_(self.frames_per_step)
 
   def step(self, data):

@@ -81,7 +81,8 @@ class RMSProp:
   """TF RMSProp over a FlatParams buffer with on-device LR schedule."""
 
   def __init__(self, flat: FlatParams, learning_rate, decay=0.99, momentum=0.,
-               epsilon=0.1, total_frames=int(1e9), use_hip=None):
+               epsilon=0.1, total_frames=int(1e9), use_hip=None,
+               skip_nonfinite=True):
     self.flat = flat
     self.lr0 = float(learning_rate)
     self.decay = float(decay)
@@ -94,6 +95,14 @@ class RMSProp:
     if use_hip is None:
       use_hip = dev.type == 'cuda'
     self.use_hip = use_hip
+    # (flag, skipped steps): a step with NaN/inf gradients leaves the
+    # parameters and slots untouched (SURVEY §5.3 failure detection).
+    self.skip_nonfinite = skip_nonfinite
+    self.guard = torch.zeros(2, dtype=torch.int32, device=dev)
+
+  @property
+  def skipped_steps(self):
+    return int(self.guard[1].item())
 
   def step(self, frames):
     """frames: int64 0-d tensor on the param device (read-only here)."""
@@ -101,9 +110,13 @@ class RMSProp:
       from . import ops
       ops.rmsprop_step(self.flat.params, self.flat.grads, self.ms, self.mom,
                        frames, self.lr0, self.total_frames, self.decay,
-                       self.momentum, self.epsilon)
+                       self.momentum, self.epsilon,
+                       self.guard if self.skip_nonfinite else None)
       return
     g = self.flat.grads
+    if self.skip_nonfinite and not bool(torch.isfinite(g).all()):
+      self.guard[1] += 1
+      return
     lr = polynomial_decay(self.lr0, frames, self.total_frames).to(torch.float32)
     self.ms.add_((g * g - self.ms) * (1 - self.decay))
     self.mom.mul_(self.momentum).add_(lr * g / torch.sqrt(self.ms +

@@ -43,6 +43,9 @@ def init_distributed(backend=None, timeout_s=600):
     kwargs = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
     if backend == 'nccl':
+      # a collective that times out aborts the process (instead of hanging
+      # the job); torchrun --max-restarts + checkpoint auto-restore resume it
+      os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
       torch.cuda.set_device(local)
       kwargs['device_id'] = torch.device('cuda', local)
     dist.init_process_group(**kwargs)
@@ -94,12 +97,22 @@ class GradientSynchronizer:
     self.buckets = bounds
     self.overlap = overlap
     self._pending = []
-    self.last_time_s = 0.0
+    self._events = None
+    self.last_time_s = 0.0  # device time of the latest finished all-reduce
 
   def all_reduce(self):
     if self.world <= 1:
       return
     g = self.flat.grads
+    timed = g.is_cuda
+    if timed:
+      if self._events is None:
+        self._events = (torch.cuda.Event(enable_timing=True),
+                        torch.cuda.Event(enable_timing=True))
+      elif self._events[1].query():
+        # previous step's collective has finished: harvest its duration
+        self.last_time_s = self._events[0].elapsed_time(self._events[1]) / 1e3
+      self._events[0].record()
     if len(self.buckets) == 1:
       dist.all_reduce(g, group=self.group)
     else:
@@ -109,3 +122,5 @@ class GradientSynchronizer:
         w.wait()
     if self.reduce == 'mean':
       g.div_(self.world)
+    if timed:
+      self._events[1].record()

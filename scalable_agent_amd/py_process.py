@@ -177,32 +177,74 @@ def close_all(processes):
 
 
 # --------------------------------------------------------------------------
-# Environment worker with shared-memory observation frames.
+# Environment worker with shared-memory observation frames, supervised.
+#
+# EnvProcess forks a small single-threaded SUPERVISOR before the learner
+# initialises the GPU; the supervisor forks the actual env worker and
+# re-forks a fresh one whenever it dies abnormally (signal, os._exit, a
+# segfault in a simulator, or a kill by the caller's hang watchdog).  The
+# replacement announces itself with a 'restarted' message; the caller raises
+# EnvRestartedError so the actor can drop its in-flight unroll and start a
+# new episode (env-worker watchdog).  Requests carry sequence
+# numbers so a reply that belongs to a request the dead worker never answered
+# can never be mistaken for a later one.  Env exceptions are NOT restarts:
+# they are re-raised in the caller (reference py_process.py:171-177).
 
-def _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape):
+
+class EnvRestartedError(Exception):
+  """The env worker died or hung and was replaced; its episode is lost."""
+
+
+class _Faults(object):
+  """Env-side fault injection: `env_crash:p` hard-kills the worker with
+  probability p per step (tests the supervisor/respawn path)."""
+
+  def __init__(self, spec, seed):
+    self.crash_p = 0.0
+    self.hang_p = 0.0
+    for part in filter(None, (spec or '').split(',')):
+      k, _, v = part.partition(':')
+      if k == 'env_crash':
+        self.crash_p = float(v)
+      elif k == 'env_hang':
+        self.hang_p = float(v)
+    self._rng = np.random.RandomState(seed % (2 ** 32))
+
+  def on_step(self):
+    import os
+    import time
+    if self.crash_p and self._rng.rand() < self.crash_p:
+      os._exit(17)
+    if self.hang_p and self._rng.rand() < self.hang_p:
+      time.sleep(3600)
+
+
+def _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape,
+                restarted, faults):
   env = None
   frames = np.frombuffer(frame_buf, dtype=np.uint8).reshape(frame_shape)
   try:
     env = env_ctor(*args, **kwargs)
-    conn.send(('ready', None))
+    conn.send(('restarted' if restarted else 'ready', -1, None))
     while True:
       msg = conn.recv()
       if msg is None:
         env.close()
         conn.close()
         return
-      name, margs = msg
+      seq, name, margs = msg
       if name == 'initial':
         frame, instr = env.initial()
         frames[...] = frame
-        conn.send(('ok', (instr,)))
+        conn.send(('ok', seq, (instr,)))
       elif name == 'step':
+        faults.on_step()
         reward, done, (frame, instr) = env.step(*margs)
         frames[...] = frame
-        conn.send(('ok', (float(reward), bool(done), instr)))
+        conn.send(('ok', seq, (float(reward), bool(done), instr)))
       else:
-        conn.send(('ok', getattr(env, name)(*margs)))
-  except (EOFError, KeyboardInterrupt):
+        conn.send(('ok', seq, getattr(env, name)(*margs)))
+  except (EOFError, KeyboardInterrupt, BrokenPipeError):
     pass
   except Exception as e:  # pylint: disable=broad-except
     if env is not None:
@@ -210,52 +252,120 @@ def _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape):
         env.close()
       except Exception:  # pylint: disable=broad-except
         pass
-    conn.send(('error', e))
+    try:
+      conn.send(('error', -1, e))
+    except Exception:  # pylint: disable=broad-except
+      conn.send(('error', -1, _RemoteError(repr(e))))
+
+
+def _supervisor(env_ctor, args, kwargs, conn, frame_buf, frame_shape, pid_box,
+                restarts_box, fault_spec, seed, max_restarts):
+  import os
+  import signal
+  signal.signal(signal.SIGINT, signal.SIG_IGN)
+  restarts = 0
+  while True:
+    pid = os.fork()
+    if pid == 0:
+      code = 0
+      try:
+        _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape,
+                    restarts > 0, _Faults(fault_spec, seed * 7919 + restarts))
+      except BaseException:  # pylint: disable=broad-except
+        code = 1
+      os._exit(code)
+    pid_box.value = pid
+    _, status = os.waitpid(pid, 0)
+    if os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0:
+      return  # closed (or the caller went away): done
+    restarts += 1
+    restarts_box.value = restarts
+    if restarts > max_restarts:
+      try:
+        conn.send(('error', -1, RuntimeError(
+            'env worker died %d times; giving up' % restarts)))
+      except Exception:  # pylint: disable=broad-except
+        pass
+      return
 
 
 class EnvProcess(object):
-  """Env in a child process; frames cross via shared memory, not pickle.
+  """Env in a supervised child process; frames cross via shared memory.
 
   The env must follow the reference protocol: `initial() -> [frame, instr]`,
-  `step(action) -> (reward, done, [frame, instr])`.
+  `step(action) -> (reward, done, [frame, instr])`.  `timeout` (seconds, 0 =
+  none) bounds every call: a worker that does not answer in time is killed
+  and replaced (EnvRestartedError).
   """
 
   def __init__(self, env_ctor, obs_shape, *args, **kwargs):
+    self._timeout = float(kwargs.pop('timeout', 0) or 0)
+    self._fault_spec = kwargs.pop('fault_inject', '')
+    self._fault_seed = int(kwargs.pop('fault_seed', 0))
+    self._max_restarts = int(kwargs.pop('max_restarts', 100))
     self._ctor = env_ctor
     self._shape = tuple(obs_shape)
     self._args = args
     self._kwargs = kwargs
     self._buf = _CTX.RawArray('B', int(np.prod(self._shape)))
     self._frames = np.frombuffer(self._buf, dtype=np.uint8).reshape(self._shape)
+    self._pid = _CTX.RawValue('i', 0)
+    self._restarts = _CTX.RawValue('i', 0)
     self._conn = None
     self._process = None
     self._closed = False
+    self._seq = 0
+
+  @property
+  def restarts(self):
+    return self._restarts.value
 
   def start(self):
     self._conn, child = _CTX.Pipe()
     self._process = _CTX.Process(
-        target=_env_worker,
+        target=_supervisor,
         args=(self._ctor, self._args, self._kwargs, child, self._buf,
-              self._shape), daemon=True)
+              self._shape, self._pid, self._restarts, self._fault_spec,
+              self._fault_seed, self._max_restarts), daemon=True)
     self._process.start()
     child.close()
-    status, payload = self._conn.recv()
+    status, _, payload = self._conn.recv()
     if status == 'error':
       self._process.join()
       raise payload
     return self
 
+  def _kill_worker(self):
+    import os
+    import signal
+    pid = self._pid.value
+    if pid > 0:
+      try:
+        os.kill(pid, signal.SIGKILL)
+      except ProcessLookupError:
+        pass
+
   def _rpc(self, name, *args):
     if self._closed:
       raise OutOfRangeError('env process closed')
+    self._seq += 1
+    seq = self._seq
     try:
-      self._conn.send((name, args))
-      status, payload = self._conn.recv()
+      self._conn.send((seq, name, args))
+      while True:
+        if self._timeout and not self._conn.poll(self._timeout):
+          self._kill_worker()  # hung: the supervisor forks a replacement
+        status, rseq, payload = self._conn.recv()
+        if status == 'restarted':
+          raise EnvRestartedError('env worker replaced (restart %d)' %
+                                  self._restarts.value)
+        if status == 'error':
+          raise payload
+        if rseq == seq:
+          return payload
+        # a stale reply to a request issued before a restart: drop it
     except (EOFError, OSError):
       raise OutOfRangeError('env process closed')
-    if status == 'error':
-      raise payload
-    return payload
 
   def initial(self):
     (instr,) = self._rpc('initial')
@@ -276,6 +386,7 @@ class EnvProcess(object):
       pass
     self._process.join(timeout=30)
     if self._process.is_alive():
+      self._kill_worker()
       self._process.terminate()
       self._process.join()
 

@@ -40,6 +40,28 @@ def test_rmsprop_matches_tf_formula(cuda):
   torch.testing.assert_close(w, w_ref, rtol=1e-6, atol=1e-6)
 
 
+def test_rmsprop_nonfinite_guard(cuda):
+  """A NaN/inf anywhere in the gradient skips the whole update on the
+  device and counts it; the next finite step applies normally."""
+  ops = _ops()
+  n = 64 * 300
+  w = torch.randn(n, device=cuda)
+  ms = torch.ones(n, device=cuda)
+  mom = torch.zeros(n, device=cuda)
+  frames = torch.zeros((), device=cuda, dtype=torch.int64)
+  guard = torch.zeros(2, dtype=torch.int32, device=cuda)
+  g = torch.randn(n, device=cuda)
+  g[n - 7] = float('inf')
+  w0, ms0 = w.clone(), ms.clone()
+  ops.rmsprop_step(w, g, ms, mom, frames, 1e-3, 1e6, 0.99, 0., 0.1, guard)
+  assert torch.equal(w, w0) and torch.equal(ms, ms0)
+  assert guard.tolist() == [1, 1]
+  g[n - 7] = 0.5
+  ops.rmsprop_step(w, g, ms, mom, frames, 1e-3, 1e6, 0.99, 0., 0.1, guard)
+  assert not torch.equal(w, w0)
+  assert guard.tolist() == [0, 1]
+
+
 def _ref_loss(bl, tl, a, r, done, v, boot, clip, bc, ec):
   cr = L.clip_rewards(r, clip)
   disc = (~done).float() * 0.99
