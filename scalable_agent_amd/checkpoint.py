@@ -67,6 +67,8 @@ def save(logdir, learner, flags=None, keep=5, extra=None):
       'torch_rng': torch.get_rng_state(),
       'time': time.time(),
   }
+  if getattr(learner, 'popart', None) is not None:
+    state['popart'] = _to_cpu(learner.popart.state_dict())
   if extra:
     state['extra'] = _to_cpu(extra)
   name = 'checkpoint_%d.pt' % frames
@@ -112,6 +114,8 @@ def restore(logdir, learner):
   learner.opt.ms.copy_(state['rmsprop']['ms'].to(learner.opt.ms.device))
   learner.opt.mom.copy_(state['rmsprop']['mom'].to(learner.opt.mom.device))
   learner.frames.fill_(int(state['num_environment_frames']))
+  if getattr(learner, 'popart', None) is not None and 'popart' in state:
+    learner.popart.load_state_dict(state['popart'])
   if 'torch_rng' in state:
     torch.set_rng_state(state['torch_rng'])
   return int(state['num_environment_frames'])

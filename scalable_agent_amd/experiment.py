@@ -126,6 +126,11 @@ def _device(flags, local_rank=0):
   return torch.device(flags.device)
 
 
+def num_value_heads(flags):
+  """PopArt: one normalised value output per task (level)."""
+  return len(level_names_for(flags)) if flags.popart else 1
+
+
 def _make_agent(flags, num_actions, frame_shape, device, seed):
   import torch
   from .models import Agent
@@ -136,7 +141,8 @@ def _make_agent(flags, num_actions, frame_shape, device, seed):
     backend = 'hip'
   cdt = torch.bfloat16 if flags.dtype == 'bf16' else torch.float32
   return Agent(num_actions, torso=flags.torso, frame_shape=frame_shape,
-               seed=seed, backend=backend, compute_dtype=cdt)
+               seed=seed, backend=backend, compute_dtype=cdt,
+               num_value_heads=num_value_heads(flags))
 
 
 class EpisodeLogger(object):
@@ -211,6 +217,7 @@ def train(flags):
 
   faults = FaultSpec(flags.fault_inject)
   level_names = level_names_for(flags)
+  task_index = {l: i for i, l in enumerate(level_names)}
   action_set = action_set_for(flags, level_names[0])
   num_actions = len(action_set)
   frame_shape = frame_shape_for(flags, level_names[0])
@@ -337,8 +344,13 @@ def train(flags):
                            pin=device.type == 'cuda')
       if faults.get('learner_nan') == steps + 1:
         host.env_outputs.reward[1:, 0] = float('nan')  # poisoned batch
+      dev_batch = host
+      if learner.popart is not None:
+        # PopArt: the device batch carries task indices instead of names
+        dev_batch = host._replace(level_name=torch.tensor(
+            [task_index[l] for l in host.level_name], dtype=torch.int64))
       with trace('h2d'):
-        data = batch_to_device(host, device)
+        data = batch_to_device(dev_batch, device)
       with trace('learner_step'):
         if use_graph:
           if learner._graph is None:

@@ -29,12 +29,20 @@ from .structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
 from .utils.tracing import trace
 
 
-def compute_loss(agent, data, flags, use_fused=False):
-  """Total loss for one time-major batch (ActorOutput of tensors)."""
+def compute_loss(agent, data, flags, use_fused=False, popart=None,
+                 aux=None):
+  """Total loss for one time-major batch (ActorOutput of tensors).
+
+  popart: optional PopArt; then data.level_name is a [B] task-index tensor,
+  values are normalised per task, and the V-trace targets are left in
+  aux['targets'] for the post-step statistics update.
+  """
   env_outputs = data.env_outputs
   agent_outputs = data.agent_outputs
+  task_ids = data.level_name if popart is not None else None
   learner_outputs, _ = agent.unroll(agent_outputs.action, env_outputs,
-                                    data.agent_state, sample=False)
+                                    data.agent_state, sample=False,
+                                    task_ids=task_ids)
   bootstrap_value = learner_outputs.baseline[-1]
 
   behaviour_logits = agent_outputs.policy_logits[1:]
@@ -44,13 +52,19 @@ def compute_loss(agent, data, flags, use_fused=False):
   target_logits = learner_outputs.policy_logits[:-1]
   values = learner_outputs.baseline[:-1]
 
-  if use_fused:
+  if use_fused and popart is None:
     from . import ops
     return ops.vtrace_loss(
         behaviour_logits, target_logits, actions, rewards, done, values,
         bootstrap_value, discounting=flags.discounting,
         reward_clipping=flags.reward_clipping,
         baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost)
+
+  norm_values = values
+  if popart is not None:
+    sigma, mu = popart.stats_for(task_ids)          # [B] each, no grad
+    values = values * sigma + mu                     # unnormalised
+    bootstrap_value = bootstrap_value * sigma + mu
 
   clipped_rewards = losses_lib.clip_rewards(rewards, flags.reward_clipping)
   discounts = (~done.to(torch.bool)).to(torch.float32) * flags.discounting
@@ -59,10 +73,18 @@ def compute_loss(agent, data, flags, use_fused=False):
       target_policy_logits=target_logits, actions=actions,
       discounts=discounts, rewards=clipped_rewards, values=values,
       bootstrap_value=bootstrap_value)
+  pg_advantages = vt.pg_advantages
+  if popart is None:
+    baseline_err = vt.vs - values
+  else:
+    baseline_err = (vt.vs - mu) / sigma - norm_values
+    pg_advantages = pg_advantages / sigma
+    if aux is not None:
+      aux['targets'] = vt.vs.detach()
   total = losses_lib.compute_policy_gradient_loss(target_logits, actions,
-                                                  vt.pg_advantages)
+                                                  pg_advantages)
   total = total + flags.baseline_cost * losses_lib.compute_baseline_loss(
-      vt.vs - values)
+      baseline_err)
   total = total + flags.entropy_cost * losses_lib.compute_entropy_loss(
       target_logits)
   return total
@@ -103,6 +125,12 @@ class Learner:
     self._static_in = None
     self._static_loss = None
     self.grad_sync = None
+    self.popart = None
+    self._aux = {}
+    if getattr(flags, 'popart', False):
+      from .popart import PopArt
+      self.popart = PopArt(self.agent.num_value_heads, flags.popart_beta,
+                           self.device)
     if world_size > 1:
       from .parallel import GradientSynchronizer
       self.grad_sync = GradientSynchronizer(self.flat, process_group,
@@ -112,7 +140,8 @@ class Learner:
   def _fwd_bwd(self, data):
     self.flat.zero_grad()
     with trace('forward'):
-      loss = compute_loss(self.agent, data, self.flags, self.use_fused)
+      loss = compute_loss(self.agent, data, self.flags, self.use_fused,
+                          self.popart, self._aux)
     with trace('backward'):
       loss.backward()
     return loss
@@ -123,10 +152,20 @@ class Learner:
         self.grad_sync.all_reduce()
     with trace('optimizer'):
       self.opt.step(self.frames)
+    if self.popart is not None:
+      # data-parallel: every rank applies the same update from its own
+      # targets; ranks stay consistent because the statistics are all-reduced
+      targets = self._aux['targets']
+      tasks = self._popart_tasks
+      if self.grad_sync is not None:
+        targets, tasks = _gather_targets(targets, tasks)
+      self.popart.update(targets, tasks, self.agent.baseline_w.data,
+                         self.agent.baseline_b.data)
     self.frames.add_(self.frames_per_step)
 
   def step(self, data):
     """One learner update from a device-resident time-major batch."""
+    self._popart_tasks = data.level_name if self.popart is not None else None
     loss = self._fwd_bwd(data)
     self.flat.rebind_grads()
     self._apply()
@@ -158,6 +197,8 @@ class Learner:
     _copy_into(self._static_in, data, non_blocking)
 
   def graph_step(self):
+    if self.popart is not None:
+      self._popart_tasks = self._static_in.level_name
     self._graph.replay()
     self._apply()
     self.last_loss = self._static_loss
@@ -165,13 +206,29 @@ class Learner:
 
   # ------------------------------------------------------------ state
   def state_dict(self):
-    return {'params': self.flat.state_dict(), 'opt': self.opt.state_dict(),
-            'frames': int(self.frames.item())}
+    sd = {'params': self.flat.state_dict(), 'opt': self.opt.state_dict(),
+          'frames': int(self.frames.item())}
+    if self.popart is not None:
+      sd['popart'] = self.popart.state_dict()
+    return sd
 
   def load_state_dict(self, sd):
     self.flat.load_state_dict(sd['params'])
     self.opt.load_state_dict(sd['opt'])
     self.frames.fill_(int(sd['frames']))
+    if self.popart is not None and 'popart' in sd:
+      self.popart.load_state_dict(sd['popart'])
+
+
+def _gather_targets(targets, tasks):
+  """All ranks' PopArt targets/tasks (so every replica updates identically)."""
+  import torch.distributed as dist
+  world = dist.get_world_size()
+  t_all = [torch.empty_like(targets) for _ in range(world)]
+  k_all = [torch.empty_like(tasks) for _ in range(world)]
+  dist.all_gather(t_all, targets.contiguous())
+  dist.all_gather(k_all, tasks.contiguous())
+  return torch.cat(t_all, 1), torch.cat(k_all, 0)
 
 
 def _map_tensors(x, fn):

@@ -83,9 +83,12 @@ class Agent(nn.Module):
   """IMPALA agent (see module docstring)."""
 
   def __init__(self, num_actions, torso='shallow', frame_shape=(72, 96, 3),
-               seed=None, backend='torch', compute_dtype=torch.float32):
+               seed=None, backend='torch', compute_dtype=torch.float32,
+               num_value_heads=1):
     super().__init__()
     self.num_actions = num_actions
+    # > 1: one (PopArt-normalised) value output per task (popart.py)
+    self.num_value_heads = int(num_value_heads)
     self.torso_kind = torso
     self.frame_shape = tuple(frame_shape)
     self.backend = backend
@@ -130,9 +133,9 @@ class Agent(nn.Module):
     self.policy_w = nn.Parameter(
         layers.sonnet_linear_init_(torch.empty(CORE_SIZE, num_actions), gen))
     self.policy_b = nn.Parameter(torch.zeros(num_actions))
-    self.baseline_w = nn.Parameter(
-        layers.sonnet_linear_init_(torch.empty(CORE_SIZE, 1), gen))
-    self.baseline_b = nn.Parameter(torch.zeros(1))
+    self.baseline_w = nn.Parameter(layers.sonnet_linear_init_(
+        torch.empty(CORE_SIZE, self.num_value_heads), gen))
+    self.baseline_b = nn.Parameter(torch.zeros(self.num_value_heads))
 
   # ------------------------------------------------------------------ naming
   def tf_variable_names(self):
@@ -253,14 +256,21 @@ class Agent(nn.Module):
       outs.append(h)
     return torch.stack(outs), (c, h)
 
-  def heads(self, core_out):
+  def heads(self, core_out, task_ids=None):
+    """task_ids: optional [B] task index per batch column (multi-head value
+    with PopArt); without it a multi-head agent reports head 0."""
     logits = core_out @ self.policy_w + self.policy_b
-    baseline = (core_out @ self.baseline_w + self.baseline_b).squeeze(-1)
-    return logits, baseline
+    values = core_out @ self.baseline_w + self.baseline_b
+    if self.num_value_heads == 1:
+      return logits, values.squeeze(-1)
+    if task_ids is None:
+      return logits, values[..., 0]
+    idx = task_ids.long().view(1, -1, 1).expand(values.shape[0], -1, 1)
+    return logits, values.gather(-1, idx).squeeze(-1)
 
   # ------------------------------------------------------------------ API
   def unroll(self, actions, env_outputs, core_state, sample=True,
-             generator=None):
+             generator=None, task_ids=None):
     """Unrolls over T steps (experiment.py:219-237).
 
     actions: [T,B] last actions; env_outputs: StepOutput with [T,B,...]
@@ -276,7 +286,7 @@ class Agent(nn.Module):
     x = x.view(T, B, -1)
     done = done.to(torch.bool).view(T, B)
     core_out, core_state = self.core_unroll(x, done, core_state)
-    logits, baseline = self.heads(core_out)
+    logits, baseline = self.heads(core_out, task_ids)
     if sample:
       probs = torch.softmax(logits.reshape(T * B, -1).float(), -1)
       action = torch.multinomial(probs, 1, generator=generator).view(T, B)

@@ -203,8 +203,9 @@ def run_actor_process(flags, level_names, action_set, frame_shape, use_instr):
   level = level_names[flags.task % len(level_names)]
   env = create_environment(flags, level, seed=flags.task + 1)
   env.start()
+  from ..experiment import num_value_heads
   agent = Agent(len(action_set), torso=flags.torso, frame_shape=frame_shape,
-                seed=flags.seed)
+                seed=flags.seed, num_value_heads=num_value_heads(flags))
   flat = FlatParams(agent)
   layout = UnrollLayout(flags.unroll_length + 1, frame_shape, len(action_set))
   ring_name, w_name = segment_names(flags.logdir)

@@ -77,3 +77,16 @@ def test_train_doom_benchmark_sim(tmp_path):
   assert r.returncode == 0, r.stderr[-3000:]
   assert 'Level: doom_benchmark Episode return' in r.stderr or \
       os.path.exists(str(tmp_path / 'd' / 'checkpoint'))
+
+
+def test_train_popart(tmp_path):
+  logdir = str(tmp_path / 'popart')
+  r = _run(['--logdir=' + logdir, '--num_actors=2', '--batch_size=2',
+            '--total_environment_frames=240', '--popart=true',
+            '--popart_beta=0.1'])
+  assert r.returncode == 0, r.stderr[-3000:]
+  import torch
+  from scalable_agent_amd import checkpoint as ckpt
+  sd = ckpt.load_state(ckpt.latest_checkpoint(logdir))
+  assert 'popart' in sd and sd['popart']['mu'].shape == (1,)
+  assert float(sd['popart']['mu'].abs().sum()) > 0

@@ -134,3 +134,47 @@ def test_agent_step_sampling_shapes():
   assert out.action.shape == (B,) and out.policy_logits.shape == (B, 9)
   assert out.baseline.shape == (B,) and c.shape == (B, 256)
   assert int(out.action.max()) < 9
+
+
+def test_popart_preserves_outputs_and_normalises():
+  """PopArt: the statistics move towards the targets and the value head is
+  rescaled so unnormalised outputs are preserved exactly."""
+  import torch
+  from scalable_agent_amd.popart import PopArt
+  torch.manual_seed(0)
+  pa = PopArt(3, beta=0.5)
+  w = torch.randn(8, 3)
+  b = torch.randn(3)
+  x = torch.randn(5, 8)
+
+  def unnorm(w, b):
+    return (x @ w + b) * pa.sigma() + pa.mu
+
+  before = unnorm(w, b)
+  targets = torch.randn(4, 6) * 10 + 50  # [T, B]
+  tasks = torch.tensor([0, 0, 1, 1, 0, 1])
+  pa.update(targets, tasks, w, b)
+  torch.testing.assert_close(unnorm(w, b), before, rtol=1e-4, atol=1e-3)
+  assert pa.mu[0] > 10 and pa.mu[1] > 10 and pa.mu[2] == 0  # task 2 absent
+  assert pa.sigma()[2] == 1.0
+
+
+def test_learner_popart_step_cpu():
+  import torch
+  from scalable_agent_amd import flags as flags_lib
+  from scalable_agent_amd.envs.synthetic import make_synthetic_batch
+  from scalable_agent_amd.learner import Learner
+  from scalable_agent_amd.models import Agent
+  f = flags_lib.default_flags(batch_size=2, unroll_length=4, popart=True,
+                              popart_beta=0.1)
+  agent = Agent(9, torso='shallow', frame_shape=(24, 32, 3), seed=1,
+                num_value_heads=2)
+  learner = Learner(agent, f, 'cpu')
+  batch = make_synthetic_batch(2, 4, (24, 32, 3), 9, seed=0)
+  batch = batch._replace(level_name=torch.tensor([0, 1]))
+  for _ in range(3):
+    loss = learner.step(batch)
+    assert torch.isfinite(loss)
+  assert float(learner.popart.mu.abs().sum()) > 0
+  sd = learner.state_dict()
+  assert 'popart' in sd
