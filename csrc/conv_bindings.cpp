@@ -65,8 +65,10 @@ std::vector<at::Tensor> conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
   return {pooled, arg};
 }
 
+// y = conv(relu_in ? relu(x) : x) + b [+ resid] [then relu]
 at::Tensor res_conv_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
-                        c10::optional<at::Tensor> resid, bool post_relu) {
+                        c10::optional<at::Tensor> resid, bool post_relu,
+                        bool relu_in) {
   const int64_t C = x.size(3);
   TORCH_CHECK(supported(C), "channels must be 16/32");
   check_act(x, "x", C);
@@ -77,17 +79,17 @@ at::Tensor res_conv_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
     TORCH_CHECK(resid->sizes() == x.sizes(), "resid shape");
     rp = resid->data_ptr();
   }
-  TORCH_CHECK(!post_relu || rp, "post_relu requires a residual");
   const c10::DeviceGuard g(x.device());
   auto y = at::empty_like(x);
   sa::conv::res_conv_fwd_launch(x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
                                 rp, y.data_ptr(), x.size(0), x.size(1), x.size(2), C,
-                                post_relu, stream());
+                                post_relu, relu_in, stream());
   return y;
 }
 
+// dx = [skip +] dgrad(dy) * (act > 0); dW += relu?(act)^T dy; db += sum dy
 at::Tensor res_conv_bwd(at::Tensor dy, at::Tensor act, c10::optional<at::Tensor> skip,
-                        at::Tensor w, at::Tensor dw, at::Tensor db) {
+                        at::Tensor w, at::Tensor dw, at::Tensor db, bool relu_act) {
   const int64_t C = act.size(3);
   TORCH_CHECK(supported(C), "channels must be 16/32");
   check_act(dy, "dy", C);
@@ -105,7 +107,8 @@ at::Tensor res_conv_bwd(at::Tensor dy, at::Tensor act, c10::optional<at::Tensor>
   auto dx = at::empty_like(act);
   sa::conv::res_conv_bwd_launch(dy.data_ptr(), act.data_ptr(), sp, w.data_ptr<float>(),
                                 dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
-                                act.size(0), act.size(1), act.size(2), C, stream());
+                                act.size(0), act.size(1), act.size(2), C, relu_act,
+                                stream());
   return dx;
 }
 
@@ -160,8 +163,10 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_pool_fwd", &conv_pool_fwd);
   m.def("res_conv_fwd", &res_conv_fwd, pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("b"), pybind11::arg("resid") = pybind11::none(),
-        pybind11::arg("post_relu") = false);
-  m.def("res_conv_bwd", &res_conv_bwd);
+        pybind11::arg("post_relu") = false, pybind11::arg("relu_in") = true);
+  m.def("res_conv_bwd", &res_conv_bwd, pybind11::arg("dy"), pybind11::arg("act"),
+        pybind11::arg("skip"), pybind11::arg("w"), pybind11::arg("dw"),
+        pybind11::arg("db"), pybind11::arg("relu_act") = true);
   m.def("pool_conv_bwd", &pool_conv_bwd);
   m.def("conv1_pool_bwd", &conv1_pool_bwd);
   m.def("conv_tune", [](const std::string& key, int64_t value) {

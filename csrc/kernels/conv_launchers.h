@@ -22,10 +22,10 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s);
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
-                         int C, bool post_relu, hipStream_t s);
+                         int C, bool post_relu, bool relu_in, hipStream_t s);
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
-                         int H, int W, int C, hipStream_t s);
+                         int H, int W, int C, bool relu_act, hipStream_t s);
 void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           const float* w, void* dx, float* dw, float* db, int N,
                           int H, int W, int CIN, int COUT, int pb_h, int pb_w,

@@ -610,7 +610,7 @@ __device__ __forceinline__ void load_weights4(const float* __restrict__ w,
 // ----------------------------------------------------------------- kernels
 constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
 
-template <int C, bool RESID, bool POST_RELU, int HC, int WC, int RC>
+template <int C, bool RESID, bool POST_RELU, bool RELU_IN, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_conv_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, const bf16_t* __restrict__ resid,
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();
     if (!((xcd >> 8) & 8))
-    sx.template commit<true, true>(x_s, W);
+    sx.template commit<RELU_IN, true>(x_s, W);
     __syncthreads();
     const int nt = it.next(tile);
     if (it.valid(nt)) {
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   }
 }
 
-template <int C, bool ADD_SKIP, int HC, int WC, int RC>
+template <int C, bool ADD_SKIP, bool RELU_ACT, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_conv_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ act,
     const bf16_t* __restrict__ skip, const float* __restrict__ w,
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if (!((xcd >> 8) & 8))
     sd.template commit<false, true>(d_s, W);
     if (!((xcd >> 8) & 8))
-    sa.template commit<true, true>(a_s, W);
+    sa.template commit<RELU_ACT, true>(a_s, W);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
@@ -1336,7 +1336,7 @@ int res_conv_rows(int H, int W) { return rows_for(H, W, 32, g_tune.px_res_fwd); 
 
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
-                         int C, bool post_relu, hipStream_t s) {
+                         int C, bool post_relu, bool relu_in, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_fwd);
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C) * sizeof(bf16_t);
@@ -1350,25 +1350,31 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w, b,
                        RS, Y, N, H, W, R, xcd);
   };
-#define SA_RF(CC, RE, PR, STG)                                                 \
+#define SA_RF(CC, RE, PR, RI, STG)                                             \
   with_geo<STG, RowsResFwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {        \
-    go(res_conv_fwd_kernel<CC, RE, PR, decltype(h)::value,                     \
+    go(res_conv_fwd_kernel<CC, RE, PR, RI, decltype(h)::value,                 \
                            decltype(ww)::value, decltype(r)::value>);          \
   })
+  // Instantiated combinations: (relu_in, resid, post_relu) in
+  //   {(1,0,*): block conv 1, (0,1,*): block conv 2, (1,1,*): reference form}
   const bool re = resid != nullptr;
+#define SA_RF_C(CC, STG)                                                       \
+  if (relu_in && !re && !post_relu) SA_RF(CC, false, false, true, STG);        \
+  else if (relu_in && !re) SA_RF(CC, false, true, true, STG);                  \
+  else if (relu_in && !post_relu) SA_RF(CC, true, false, true, STG);           \
+  else if (relu_in) SA_RF(CC, true, true, true, STG);                          \
+  else if (re && !post_relu) SA_RF(CC, true, false, false, STG);               \
+  else if (re) SA_RF(CC, true, true, false, STG);                              \
+  else if (!post_relu) SA_RF(CC, false, false, false, STG);                   \
+  else SA_RF(CC, false, true, false, STG)
   if (C == 16) {
-    if (re && post_relu) SA_RF(16, true, true, kStage1);
-    else if (re) SA_RF(16, true, false, kStage1);
-    else SA_RF(16, false, false, kStage1);
+    SA_RF_C(16, kStage1);
   } else if (H * 2 > 18 + 9) {
-    if (re && post_relu) SA_RF(32, true, true, kStage2);
-    else if (re) SA_RF(32, true, false, kStage2);
-    else SA_RF(32, false, false, kStage2);
+    SA_RF_C(32, kStage2);
   } else {
-    if (re && post_relu) SA_RF(32, true, true, kStage3);
-    else if (re) SA_RF(32, true, false, kStage3);
-    else SA_RF(32, false, false, kStage3);
+    SA_RF_C(32, kStage3);
   }
+#undef SA_RF_C
 #undef SA_RF
 }
 
@@ -1422,7 +1428,7 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
 
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
-                         int H, int W, int C, hipStream_t s) {
+                         int H, int W, int C, bool relu_act, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
@@ -1437,21 +1443,24 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DY, A, SK,
                        w, DX, dw, db, N, H, W, R, xcd);
   };
-#define SA_RB(CC, SKP, STG)                                                    \
+#define SA_RB(CC, SKP, RA, STG)                                                \
   with_geo<STG, RowsResBwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {        \
-    go(res_conv_bwd_kernel<CC, SKP, decltype(h)::value, decltype(ww)::value,   \
-                           decltype(r)::value>);                               \
+    go(res_conv_bwd_kernel<CC, SKP, RA, decltype(h)::value,                    \
+                           decltype(ww)::value, decltype(r)::value>);          \
   })
+#define SA_RB_C(CC, STG)                                                       \
+  if (skip && relu_act) SA_RB(CC, true, true, STG);                            \
+  else if (skip) SA_RB(CC, true, false, STG);                                  \
+  else if (relu_act) SA_RB(CC, false, true, STG);                              \
+  else SA_RB(CC, false, false, STG)
   if (C == 16) {
-    if (skip) SA_RB(16, true, kStage1);
-    else SA_RB(16, false, kStage1);
+    SA_RB_C(16, kStage1);
   } else if (H * 2 > 18 + 9) {
-    if (skip) SA_RB(32, true, kStage2);
-    else SA_RB(32, false, kStage2);
+    SA_RB_C(32, kStage2);
   } else {
-    if (skip) SA_RB(32, true, kStage3);
-    else SA_RB(32, false, kStage3);
+    SA_RB_C(32, kStage3);
   }
+#undef SA_RB_C
 #undef SA_RB
 }
 

@@ -3,8 +3,8 @@
 Forward per stage s (reference experiment.py:156-176):
   conv_pool_fwd      conv3x3 + bias + maxpool3x3/2 SAME (stage 1 straight from
                      the uint8 frame, x/255 folded into the weights)
-  2 x [res_conv_fwd  t = conv(relu(x)) + b
-       res_conv_fwd  y = conv(relu(t)) + b + x   (+ final ReLU on the last)]
+  2 x [res_conv_fwd  t = relu(conv(relu(x)) + b)     (stored ReLU'd)
+       res_conv_fwd  y = conv(t) + b + x   (+ final ReLU on the last)]
 Backward per residual block: two fused dgrad+wgrad+bias passes; per stage head
 one pass that gathers the pooled gradient through the saved argmax in LDS.
 All activations NHWC bf16; weights/biases fp32 master copies (TF HWIO); their
@@ -64,9 +64,12 @@ class _DeepTorso(torch.autograd.Function):
       for blk in range(2):
         w1, b1, w2, b2 = params[p:p + 4]
         p += 4
-        t = C.res_conv_fwd(xa, w1, b1)
+        # t is stored ReLU'd: it is only ever consumed as relu(t) (conv 2's
+        # input, and the (t > 0) mask in backward), so conv 2 skips its
+        # input ReLU and its backward skips the activation ReLU.
+        t = C.res_conv_fwd(xa, w1, b1, None, True, True)
         last = (s == 2 and blk == 1)
-        y = C.res_conv_fwd(t, w2, b2, xa, last)
+        y = C.res_conv_fwd(t, w2, b2, xa, last, False)
         saved += [xa, t]
         xa = y
       if s < 2:
@@ -115,8 +118,9 @@ class _DeepTorso(torch.autograd.Function):
         xa, tt = blocks[blk]
         i1 = pb + 2 + 4 * blk
         w1, w2 = params[i1], params[i1 + 2]
-        dt = C.res_conv_bwd(dy, tt, None, w2, gviews[i1 + 2], gviews[i1 + 3])
-        dy = C.res_conv_bwd(dt, xa, dy, w1, gviews[i1], gviews[i1 + 1])
+        dt = C.res_conv_bwd(dy, tt, None, w2, gviews[i1 + 2], gviews[i1 + 3],
+                            False)
+        dy = C.res_conv_bwd(dt, xa, dy, w1, gviews[i1], gviews[i1 + 1], True)
       H, W, pb_h, pb_w = ctx.shapes[s]
       if s == 0:
         C.conv1_pool_bwd(dy, arg, frames, gviews[pb], gviews[pb + 1], pb_h,

@@ -53,18 +53,24 @@ def close(a, b, tol):
   assert err <= tol * scale, 'max err %.4g vs scale %.4g' % (err, scale)
 
 
-@pytest.mark.parametrize('C,H,W,resid,post', [
-    (16, 36, 48, False, False), (16, 36, 48, True, False),
-    (32, 18, 24, True, True), (32, 9, 12, False, False), (32, 18, 24, False, False)])
-def test_res_conv_fwd(cuda, C, H, W, resid, post):
+@pytest.mark.parametrize('C,H,W,resid,post,relu_in', [
+    (16, 36, 48, False, False, True), (16, 36, 48, True, False, True),
+    (32, 18, 24, True, True, True), (32, 9, 12, False, False, True),
+    (32, 18, 24, False, False, True),
+    # block forms used by the torso: conv1 = relu-in + post-relu, conv2 =
+    # plain input + residual (+ post-relu on the last block)
+    (16, 36, 48, False, True, True), (16, 36, 48, True, False, False),
+    (32, 18, 24, False, True, True), (32, 9, 12, True, True, False),
+    (16, 10, 14, True, False, False)])
+def test_res_conv_fwd(cuda, C, H, W, resid, post, relu_in):
   torch.manual_seed(0)
   N = 3
   x = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
   w = bf(torch.randn(3, 3, C, C, device=cuda) * 0.1)
   b = torch.randn(C, device=cuda) * 0.1
   r = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16) if resid else None
-  y = _C().res_conv_fwd(x, w, b, r, post)
-  ref = conv_ref(F.relu(x.float()), w, b)
+  y = _C().res_conv_fwd(x, w, b, r, post, relu_in)
+  ref = conv_ref(F.relu(x.float()) if relu_in else x.float(), w, b)
   if resid:
     ref = ref + r.float()
   if post:
@@ -112,9 +118,12 @@ def test_conv1_pool_fwd(cuda, H, W):
   close(pooled, ref, 2e-2)
 
 
-@pytest.mark.parametrize('C,H,W,skip', [(16, 36, 48, False), (16, 36, 48, True),
-                                        (32, 18, 24, True), (32, 9, 12, False)])
-def test_res_conv_bwd(cuda, C, H, W, skip):
+@pytest.mark.parametrize('C,H,W,skip,relu_act', [
+    (16, 36, 48, False, True), (16, 36, 48, True, True),
+    (32, 18, 24, True, True), (32, 9, 12, False, True),
+    (16, 36, 48, False, False), (32, 18, 24, False, False),
+    (32, 9, 12, False, False), (16, 10, 14, False, False)])
+def test_res_conv_bwd(cuda, C, H, W, skip, relu_act):
   torch.manual_seed(3)
   N = 3
   act = torch.randn(N, H, W, C, device=cuda).to(torch.bfloat16)
@@ -123,7 +132,9 @@ def test_res_conv_bwd(cuda, C, H, W, skip):
   w = bf(torch.randn(3, 3, C, C, device=cuda) * 0.1)
   dw = torch.zeros(3, 3, C, C, device=cuda)
   db = torch.zeros(C, device=cuda)
-  dx = _C().res_conv_bwd(dy, act, sk, w, dw, db)
+  if not relu_act:
+    act = F.relu(act.float()).to(torch.bfloat16)  # stored post-ReLU
+  dx = _C().res_conv_bwd(dy, act, sk, w, dw, db, relu_act)
   a = act.float().requires_grad_(True)
   wr = w.clone().requires_grad_(True)
   br = torch.zeros(C, device=cuda, requires_grad=True)
@@ -238,12 +249,16 @@ def test_specialized_geometry_matches_generic(cuda, frame):
     out.append(C.res_conv_fwd(x16, w16, b16, x16, False))
     out.append(C.res_conv_fwd(x32, w32, b32, None, False))
     out.append(C.res_conv_fwd(x9, w32, b32, x9, True))
+    out.append(C.res_conv_fwd(x16, w16, b16, None, True, True))
+    out.append(C.res_conv_fwd(x32, w32, b32, x32, False, False))
     p2, a2 = C.conv_pool_fwd(x16, w1632, b32, 0, 0)
     p3, a3 = C.conv_pool_fwd(x32, w32, b32, 0, 0)
     out += [p2, a2, p3, a3]
     for x, w, b in ((x16, w16, b16), (x32, w32, b32), (x9, w32, b32)):
       dw, db = torch.zeros_like(w, dtype=torch.float32), torch.zeros_like(b)
       out += [C.res_conv_bwd(x, x, x, w, dw, db), dw, db]
+      dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
+      out += [C.res_conv_bwd(x, x, None, w, dw2, db2, False), dw2, db2]
     for (pp, aa, x, w, b) in ((p2, a2, x16, w1632, b32), (p3, a3, x32, w32, b32)):
       dw, db = torch.zeros_like(w, dtype=torch.float32), torch.zeros_like(b)
       out += [C.pool_conv_bwd(pp, aa, x, w, dw, db, True, 0, 0), dw, db]

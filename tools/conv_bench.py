@@ -54,33 +54,33 @@ def cases(n):
   return [
       ('conv1_pool_fwd', 1, F + B16 + B16 // 2,
        lambda: C.conv1_pool_fwd(frames, w1, b1, 0, 0)),
-      ('res_fwd16', 2, 2 * B16, lambda: C.res_conv_fwd(x16, w16, b16)),
+      ('res_fwd16', 2, 2 * B16, lambda: C.res_conv_fwd(x16, w16, b16, None, True, True)),
       ('res_fwd16_resid', 2, 3 * B16,
-       lambda: C.res_conv_fwd(x16, w16, b16, x16, False)),
+       lambda: C.res_conv_fwd(x16, w16, b16, x16, False, False)),
       ('conv_pool_fwd16_32', 1, B16 + B32 * 3 // 2,
        lambda: C.conv_pool_fwd(x16, w1632, b32, 0, 0)),
-      ('res_fwd32', 2, 2 * B32, lambda: C.res_conv_fwd(x32, w32_, b32)),
+      ('res_fwd32', 2, 2 * B32, lambda: C.res_conv_fwd(x32, w32_, b32, None, True, True)),
       ('res_fwd32_resid', 2, 3 * B32,
-       lambda: C.res_conv_fwd(x32, w32_, b32, x32, False)),
+       lambda: C.res_conv_fwd(x32, w32_, b32, x32, False, False)),
       ('conv_pool_fwd32_32', 1, B32 + B9 * 3 // 2,
        lambda: C.conv_pool_fwd(x32, w32_, b32, 0, 0)),
-      ('res_fwd9', 2, 2 * B9, lambda: C.res_conv_fwd(x9, w32_, b32)),
+      ('res_fwd9', 2, 2 * B9, lambda: C.res_conv_fwd(x9, w32_, b32, None, True, True)),
       ('res_fwd9_resid', 2, 3 * B9,
-       lambda: C.res_conv_fwd(x9, w32_, b32, x9, True)),
+       lambda: C.res_conv_fwd(x9, w32_, b32, x9, True, False)),
       ('res_bwd9', 2, 3 * B9,
-       lambda: C.res_conv_bwd(d9, x9, None, w32_, dw32, db32)),
+       lambda: C.res_conv_bwd(d9, x9, None, w32_, dw32, db32, False)),
       ('res_bwd9_skip', 2, 4 * B9,
        lambda: C.res_conv_bwd(d9, x9, d9, w32_, dw32, db32)),
       ('pool_bwd32_32', 1, B9 * 3 // 2 + 2 * B32,
        lambda: C.pool_conv_bwd(dp3, a3, x32, w32_, dw32, db32, True, 0, 0)),
       ('res_bwd32', 2, 3 * B32,
-       lambda: C.res_conv_bwd(d32, x32, None, w32_, dw32, db32)),
+       lambda: C.res_conv_bwd(d32, x32, None, w32_, dw32, db32, False)),
       ('res_bwd32_skip', 2, 4 * B32,
        lambda: C.res_conv_bwd(d32, x32, d32, w32_, dw32, db32)),
       ('pool_bwd16_32', 1, B32 * 3 // 2 + 2 * B16,
        lambda: C.pool_conv_bwd(dp2, a2, x16, w1632, dw1632, db32, True, 0, 0)),
       ('res_bwd16', 2, 3 * B16,
-       lambda: C.res_conv_bwd(d16, x16, None, w16, dw16, db16)),
+       lambda: C.res_conv_bwd(d16, x16, None, w16, dw16, db16, False)),
       ('res_bwd16_skip', 2, 4 * B16,
        lambda: C.res_conv_bwd(d16, x16, d16, w16, dw16, db16)),
       ('conv1_pool_bwd', 1, B16 * 3 // 4 + F,
