@@ -501,86 +501,84 @@ struct SpanStager {
   }
 };
 
-// uint8 RGB frame rows -> LDS rows of stride U8_STRIDE(W) bytes: byte
-// 4 + 3c + ci holds pixel c (c = -1..W, halo zero), channel ci.
-__host__ __device__ __forceinline__ int u8_stride(int W) { return (3 * W + 8 + 3) & ~3; }
+// uint8 RGB frame rows, staged as groups of 4 pixels (12 bytes = 3 dwords)
+// per lane: when the rows are dword aligned (W % 4 == 0, the usual frame
+// widths) a group is three dword loads; otherwise it falls back to bytes.
+constexpr int kU8Groups = 2;  // 4-pixel groups per lane per tile
 
-template <int NREG>
+template <int NG>
 struct U8Stager {
-  uint32_t v[NREG];
-  int total;  // dword chunks over the row span
-  int span;   // bytes in the (clipped) row span
+  uint32_t v[3 * NG];
+  int npix;   // pixels in the (clipped) row span
   int row0;   // first staged row (tile coordinates)
+  int nrows;  // staged image rows
   __device__ __forceinline__ void issue(const uint8_t* __restrict__ src, int n,
                                         int H, int W, int r_begin, int rows) {
     const int rlo = max(r_begin, 0), rhi = min(r_begin + rows, H);
     row0 = rlo - r_begin;
-    span = rhi > rlo ? (rhi - rlo) * W * 3 : 0;
-    total = (span + 3) / 4;
+    nrows = rhi > rlo ? rhi - rlo : 0;
+    npix = nrows * W;
     const uint8_t* base = src + (static_cast<int64_t>(n) * H + rlo) * W * 3;
+    const bool aligned =
+        ((W & 3) | (reinterpret_cast<uintptr_t>(src) & 3)) == 0;
 #pragma unroll
-    for (int k = 0; k < NREG; ++k) {
-      const int e = threadIdx.x + k * kThreads;
-      uint32_t x = 0;
-      if (e < total) {
+    for (int k = 0; k < NG; ++k) {
+      const int g = threadIdx.x + k * kThreads;
+      v[3 * k] = v[3 * k + 1] = v[3 * k + 2] = 0;
+      if (4 * g < npix) {
+        if (aligned) {
+          const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base) + 3 * g;
+          v[3 * k] = b32[0];
+          v[3 * k + 1] = b32[1];
+          v[3 * k + 2] = b32[2];
+        } else {
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if (4 * e + b < span) x |= static_cast<uint32_t>(base[4 * e + b]) << (8 * b);
-      }
-      v[k] = x;
-    }
-  }
-  __device__ __forceinline__ void commit(uint8_t* lds, int W, int rows) const {
-    const int S = u8_stride(W);
-    // zero the whole tile first (halo pixels, rows outside the image)
-    for (int e = threadIdx.x; e < rows * S / 4; e += kThreads)
-      reinterpret_cast<uint32_t*>(lds)[e] = 0;
-    __syncthreads();
-    const int rb = 3 * W;
-#pragma unroll
-    for (int k = 0; k < NREG; ++k) {
-      const int e = threadIdx.x + k * kThreads;
-      if (e < total) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int i = 4 * e + b;
-          if (i < span) {
-            const int rr = i / rb;
-            lds[(row0 + rr) * S + 4 + (i - rr * rb)] = (v[k] >> (8 * b)) & 0xFF;
-          }
+          for (int b = 0; b < 12; ++b)
+            if (12 * g + b < 3 * npix)
+              v[3 * k + b / 4] |= static_cast<uint32_t>(base[12 * g + b]) << (8 * (b % 4));
         }
       }
     }
   }
 };
 
-// uint8 rows -> bf16x4 halo tile [rows][W+2][4] (channel 3 and halo zero);
-// `pad` extra zero pixels follow the tile (MFMA reads may run 3 pixels past
-// the last row into weights-zero columns).
-template <int NREG>
-__device__ __forceinline__ void commit_x4(const U8Stager<NREG>& st, bf16_t* x4,
+// Staged uint8 rows -> bf16x4 halo tile [rows][W+2][4] (channel 3 and halo
+// zero); `pad` extra zero pixels follow the tile (MFMA reads may run 3 pixels
+// past the last row into weights-zero columns).  Every LDS pixel is written
+// exactly once (data, halo or zero row), so no barrier is needed inside.
+template <int NG>
+__device__ __forceinline__ void commit_x4(const U8Stager<NG>& st, bf16_t* x4,
                                           int W, int rows, int pad) {
   const int Wp = W + 2;
-  const int nq = (rows * Wp + pad) * 4 / 8;  // uint4 = 8 bf16
-  for (int e = threadIdx.x; e < nq; e += kThreads)
-    reinterpret_cast<uint4*>(x4)[e] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  const int rb = 3 * W;
+  uint2* px4 = reinterpret_cast<uint2*>(x4);
+  const uint2 z = make_uint2(0, 0);
+  // halo columns of every row, then the trailing pad pixels
+  for (int e = threadIdx.x; e < 2 * rows + pad; e += kThreads)
+    px4[e < 2 * rows ? (e >> 1) * Wp + (e & 1) * (W + 1) : rows * Wp + e - 2 * rows] = z;
+  // rows outside the image
+  const int top = st.row0 * W, bot = (rows - st.row0 - st.nrows) * W;
+  for (int e = threadIdx.x; e < top + bot; e += kThreads) {
+    const int r = e < top ? e / W : st.row0 + st.nrows + (e - top) / W;
+    const int c = e < top ? e - (e / W) * W : (e - top) - ((e - top) / W) * W;
+    px4[r * Wp + c + 1] = z;
+  }
 #pragma unroll
-  for (int k = 0; k < NREG; ++k) {
-    const int e = threadIdx.x + k * kThreads;
-    if (e < st.total) {
+  for (int k = 0; k < NG; ++k) {
+    const int g = threadIdx.x + k * kThreads;
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int i = 4 * e + b;
-        if (i < st.span) {
-          const int rr = i / rb;
-          const int rem = i - rr * rb;
-          const int px = rem / 3;
-          const int ci = rem - px * 3;
-          x4[((st.row0 + rr) * Wp + px + 1) * 4 + ci] =
-              f2bf(static_cast<float>((st.v[k] >> (8 * b)) & 0xFF));
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * g + j;
+      if (p < st.npix) {
+        const int rr = p / W, c = p - rr * W;
+        uint32_t ch[3];
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) {
+          const int b = 3 * j + ci;  // byte within the 12-byte group
+          // byte values are exact in bf16: take the top half of the fp32
+          ch[ci] = __float_as_uint(static_cast<float>(
+                       (st.v[3 * k + b / 4] >> (8 * (b % 4))) & 0xFF)) >> 16;
         }
+        px4[(st.row0 + rr) * Wp + c + 1] = make_uint2(ch[0] | (ch[1] << 16), ch[2]);
       }
     }
   }
@@ -736,7 +734,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   const int wave = wave_id();
   const int tpi = (Hp + Rp - 1) / Rp;
   const int ntiles = N * tpi;
-  U8Stager<NREG> sx;
+  U8Stager<kU8Groups> sx;
   auto issue = [&](int t) {
     const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
@@ -1090,7 +1088,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
   ones[0] = ones[1] = ones[2] = ones[3] = 0x3F80;
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
-  U8Stager<NREG> sx;
+  U8Stager<kU8Groups> sx;
   SpanStager<NREG> sp, sg;
   const int prow_bytes = Wo * COUT;
   auto issue = [&](int t) {
@@ -1112,7 +1110,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
     if (!((xcd >> 8) & 8))
-    commit_x4(sx, x4, W, Rv + 2, 4);  // (contains a barrier)
+    commit_x4(sx, x4, W, Rv + 2, 4);
     if (!((xcd >> 8) & 8))
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
     if (!((xcd >> 8) & 8))
@@ -1204,7 +1202,7 @@ constexpr int rows_conv1_fwd(int H, int W, int px) {
   const int Hp = (H + 1) / 2;
   int Rp = (px / W - 1) / 2;
   if (Rp < 1) Rp = 1;
-  while (Rp > 1 && ((2 * Rp + 3) * W * 3 + 3) / 4 > NREG * kThreads) --Rp;
+  while (Rp > 1 && ((2 * Rp + 3) * W + 3) / 4 > kU8Groups * kThreads) --Rp;
   return Rp > Hp ? Hp : Rp;
 }
 constexpr int rows_pool_bwd(int H, int W, int CIN, int COUT, int px) {
@@ -1218,7 +1216,7 @@ constexpr int rows_conv1_bwd(int H, int W, int px) {
   int R = px / W;
   if (R < 1) R = 1;
   while (R > 1 && (((R + 2) / 2 + 2) * Wo * 16 * 2 > NREG * kThreads * 16 ||
-                   ((R + 2) * W * 3 + 3) / 4 > NREG * kThreads))
+                   ((R + 2) * W + 3) / 4 > kU8Groups * kThreads))
     --R;
   return R > H ? H : R;
 }
