@@ -150,9 +150,26 @@ __device__ __forceinline__ void load4(const bf16_t* src, float v[4]) {
   v[3] = __uint_as_float(o.y & 0xFFFF0000u);
 }
 
-// Max-pool 3x3/2 (TF SAME: pad_before pb, -inf padding) over a conv tile held
-// in LDS y_s [Rc][W][COUT] whose row 0 is conv row cr0; writes pooled rows
-// [i0, i0+Rpv).  8 channels per thread-iteration.
+// Pre-pool conv outputs are stored in LDS as order-preserving 16-bit keys
+// (bf16 bits with the magnitude bits of negatives flipped, so signed-int16
+// order == float order).  The pooling then needs one v_and_or/v_lshl_or and
+// one v_max_i32 per channel and tap: key32 = ord16 << 16 | (15 - tap code),
+// so the max also yields the first maximal tap of the 3x3 window.
+__device__ __forceinline__ uint32_t bf2_to_ord(uint32_t u) {
+  return u ^ (((u >> 15) & 0x00010001u) * 0x7FFFu);
+}
+__device__ __forceinline__ void store4_ord(bf16_t* dst, const float v[4]) {
+  uint2 o;
+  o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+  o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+  o.x = bf2_to_ord(o.x);
+  o.y = bf2_to_ord(o.y);
+  *reinterpret_cast<uint2*>(dst) = o;
+}
+
+// 3x3/2 max-pool (TF SAME padding offsets pb_h/pb_w) of the conv tile in
+// y_s (order keys, [conv rows from cr0][W][COUT]) -> pooled bf16 + argmax
+// code dy*3+dx, one 8-channel slice per thread.
 template <int COUT>
 __device__ __forceinline__ void pool_tile(const bf16_t* y_s, int cr0, int H,
                                           int W, int Wo, int pb_h, int pb_w,
@@ -165,13 +182,9 @@ __device__ __forceinline__ void pool_tile(const bf16_t* y_s, int cr0, int H,
     const int part = e % CH;
     const int pj = (e / CH) % Wo;
     const int pi = e / (CH * Wo);
-    float best[8];
-    uint8_t arg[8];
+    int best[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      best[c] = -INFINITY;
-      arg[c] = 0;
-    }
+    for (int c = 0; c < 8; ++c) best[c] = -0x7FFFFFFF - 1;
     const int crow0 = 2 * (i0 + pi) - pb_h;  // first conv row of the window
     const int ccol0 = 2 * pj - pb_w;
 #pragma unroll
@@ -185,27 +198,32 @@ __device__ __forceinline__ void pool_tile(const bf16_t* y_s, int cr0, int H,
         const uint4 v = *reinterpret_cast<const uint4*>(
             y_s + ((cr - cr0) * W + cc) * COUT + part * 8);
         const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t K = 15 - (dy * 3 + dx);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const float f = __uint_as_float((c & 1) ? (u[c >> 1] & 0xFFFF0000u)
-                                                  : (u[c >> 1] << 16));
-          if (f > best[c]) {
-            best[c] = f;
-            arg[c] = static_cast<uint8_t>(dy * 3 + dx);
-          }
+          const uint32_t key = (c & 1) ? ((u[c >> 1] & 0xFFFF0000u) | K)
+                                       : ((u[c >> 1] << 16) | K);
+          best[c] = max(best[c], static_cast<int>(key));
         }
       }
     }
+    uint32_t bits[8], arg[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int o16 = best[c] >> 16;  // arithmetic: sign-extended ord
+      bits[c] = static_cast<uint32_t>(o16 ^ ((o16 >> 15) & 0x7FFF)) & 0xFFFFu;
+      arg[c] = 15u - (static_cast<uint32_t>(best[c]) & 15u);
+    }
     const int64_t o = ((static_cast<int64_t>(n) * Hp + i0 + pi) * Wo + pj) * COUT + part * 8;
     uint4 pv;
-    pv.x = f2bf(best[0]) | (static_cast<uint32_t>(f2bf(best[1])) << 16);
-    pv.y = f2bf(best[2]) | (static_cast<uint32_t>(f2bf(best[3])) << 16);
-    pv.z = f2bf(best[4]) | (static_cast<uint32_t>(f2bf(best[5])) << 16);
-    pv.w = f2bf(best[6]) | (static_cast<uint32_t>(f2bf(best[7])) << 16);
+    pv.x = bits[0] | (bits[1] << 16);
+    pv.y = bits[2] | (bits[3] << 16);
+    pv.z = bits[4] | (bits[5] << 16);
+    pv.w = bits[6] | (bits[7] << 16);
     *reinterpret_cast<uint4*>(pooled + o) = pv;
     uint2 av;
-    av.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (static_cast<uint32_t>(arg[3]) << 24);
-    av.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (static_cast<uint32_t>(arg[7]) << 24);
+    av.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    av.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
     *reinterpret_cast<uint2*>(argmax + o) = av;
   }
 }
@@ -696,7 +714,7 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
-      store4(y_s + q * COUT + co0, v);
+      store4_ord(y_s + q * COUT + co0, v);
     });
     __syncthreads();
     if (!((xcd >> 8) & 1))
@@ -774,7 +792,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       }
       if (valid) {
         const float v[4] = {acc[0] + b0, acc[1] + b1, acc[2] + b2, acc[3] + b3};
-        store4(y_s + q * COUT + 4 * (lane >> 4), v);
+        store4_ord(y_s + q * COUT + 4 * (lane >> 4), v);
       }
     }
     __syncthreads();
