@@ -24,6 +24,8 @@
 #include "conv_launchers.h"
 
 #include <cstring>
+#include <stdexcept>
+#include <string>
 #include <type_traits>
 
 namespace sa {
@@ -31,8 +33,22 @@ namespace conv {
 namespace {
 
 constexpr int kThreads = 256;
+// Phase ablation for timing studies (tools/conv_bench.py, knob "ablate":
+// 1 pool/gather, 2 wgrad, 4 conv, 8 LDS commit) exists only in builds with
+// -DSA_CONV_ABLATE: the runtime branches around the staging commit make the
+// compiler's vmcnt bookkeeping conservative (it then drains the prefetch).
+#ifdef SA_CONV_ABLATE
+__device__ __forceinline__ bool kKeep(int xcd, int bit) { return !((xcd >> 8) & bit); }
+#else
+__device__ __forceinline__ constexpr bool kKeep(int, int) { return true; }
+#endif
 constexpr int kWaves = kThreads / 64;
 constexpr int GPW = 4;  // 16-pixel groups per wave per chunk
+constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
+// Largest tile (output pixels) of a conv whose staged input has C channels:
+// the tile-height rules keep the staged halo rows within NREG*kThreads 16-B
+// chunks, i.e. at most NREG*kThreads*8/C pixels.
+constexpr int kMaxTilePx(int C) { return NREG * kThreads * 8 / C; }
 
 // Persistent tile schedule.  xcd == 0: tile = blockIdx.x + k * gridDim.x.
 // xcd == 1: XCD-aware - workgroups are dispatched round-robin over the 8 XCDs
@@ -61,59 +77,148 @@ struct TileIter {
 };
 
 // ----------------------------------------------------------------- forward
-// Per-wave implicit GEMM over a chunk of up to GPW groups. x_s: halo tile
+// Calls f(IC<n>) with n = nv in [1, N] as a compile-time constant, so chunk
+// bodies are branch-free (every LDS read of a chunk can be issued ahead of
+// its MFMAs) without computing padding groups.
+template <int N, typename F>
+__device__ __forceinline__ void for_count(int nv, F&& f) {
+  if constexpr (N > 1) {
+    if (nv < N) {
+      for_count<N - 1>(nv, f);
+      return;
+    }
+  }
+  f(std::integral_constant<int, N>{});
+}
+
+// Chunking of a tile's 16-pixel groups over the waves: wave w computes
+// groups w + kWaves * (c * gpw + gi) (chunk c, gi < gpw).  The chunk loop is
+// unrolled over the kChunks a tile can need (the tile-height rules bound a
+// tile to kMaxTilePx pixels): with a real loop holding global stores, the
+// compiler drains vmcnt in the preheader, i.e. waits for the next tile's
+// prefetch before computing this one.
+template <int GP, int MAXPX>
+struct Chunking {
+  static constexpr int kGpw = GP;
+  static constexpr int kChunks = (MAXPX / 16 + kWaves * GP - 1) / (kWaves * GP);
+  static constexpr int kSlots = kChunks * GP;  // groups per wave, max
+};
+template <int CIN, int COUT>
+using FwdChunks = Chunking<GPW, kMaxTilePx(CIN)>;
+template <int CIN, int COUT>
+using DgradChunks = Chunking<(CIN == 32 ? 2 : GPW), kMaxTilePx(CIN < COUT ? CIN : COUT)>;
+
+// Per-lane copy of a global [pixels][C] bf16 operand for the epilogue of
+// this wave's groups (4 channels per 16-channel half), loaded BEFORE the
+// next tile's prefetch is issued: vmcnt is in order, so a global load in the
+// epilogue would otherwise also wait for the whole prefetch.
+template <int C, typename CH>
+struct EpiOperand {
+  static constexpr int NH = C / 16;
+  uint2 v[CH::kSlots][NH];
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ src,
+                                       int64_t img0, int npix) {
+    const int lane = lane_id();
+    const int wave = wave_id();
+#pragma unroll
+    for (int k = 0; k < CH::kSlots; ++k) {
+      const int q = (wave + kWaves * k) * 16 + (lane & 15);
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        v[k][h] = q < npix ? *reinterpret_cast<const uint2*>(
+                                 src + (img0 + q) * C + 16 * h + 4 * (lane >> 4))
+                           : make_uint2(0, 0);
+    }
+  }
+  __device__ __forceinline__ void get(int slot, int co0, float f[4]) const {
+    const uint2 o = v[slot][co0 >> 4];
+    f[0] = __uint_as_float(o.x << 16);
+    f[1] = __uint_as_float(o.x & 0xFFFF0000u);
+    f[2] = __uint_as_float(o.y << 16);
+    f[3] = __uint_as_float(o.y & 0xFFFF0000u);
+  }
+};
+
+// Bias of this lane's output channels (co0 = 16 h + 4 (lane >> 4)) into
+// registers, bounced through LDS `scratch` (contains a barrier; scratch is
+// free again after the caller's next barrier).  Loading them with a global
+// load straight into the registers used inside the tile loop makes the
+// compiler re-check vmcnt there, which (in-order counter) also waits for
+// the next tile's prefetch.
+template <int COUT>
+__device__ __forceinline__ void bias_regs(const float* __restrict__ bias,
+                                          float* scratch, float breg[COUT / 16][4]) {
+  for (int e = threadIdx.x; e < COUT; e += blockDim.x) scratch[e] = bias[e];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < COUT / 16; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) breg[h][i] = scratch[16 * h + 4 * (lane_id() >> 4) + i];
+}
+
+// Per-wave implicit GEMM over the tile (FwdChunks). x_s: halo tile
 // [rows][Wt+2][CIN]; output pixel q=(qr,qc) reads x_s[(qr+ky)*(Wt+2)+qc+kx].
-// epi(q, co0, v[4]) is called for every valid (pixel, 4-channel slice).
+// epi(q, co0, v[4], slot) is called for every valid (pixel, 4-channel slice);
+// slot = the group's index in this wave's list (compile-time after unrolling).
 template <int CIN, int COUT, typename Epi>
 __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
                                               const bf16_t* w_s, int Wt,
                                               int npix, Epi epi) {
   static_assert(CIN == 16 || CIN == 32, "CIN");
   constexpr int NH = COUT / 16;
+  // Keep the per-tap weight fragments in LDS (re-read per chunk) unless
+  // they are small: hoisting 9 taps of 32-wide fragments out of the loop
+  // costs 72 VGPRs and halves occupancy.
+  constexpr bool kReloadW = CIN == 32 || NH == 2;
   const int lane = lane_id();
   const int wave = wave_id();
   const int Wp = Wt + 2;
   const int ngroups = (npix + 15) / 16;
-  for (int g0 = wave; g0 < ngroups; g0 += kWaves * GPW) {
-    f4 acc[GPW][NH];
-    int base[GPW];
+  using CH = FwdChunks<CIN, COUT>;
 #pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
+  for (int c = 0; c < CH::kChunks; ++c) {
+    const int g0 = wave + c * kWaves * CH::kGpw;
+    if (g0 >= ngroups) break;
+    if constexpr (kReloadW) asm volatile("" ::: "memory");
+    const int nv = (ngroups - g0 + kWaves - 1) / kWaves;
+    for_count<CH::kGpw>(nv, [&](auto NCc) {
+      constexpr int NC = decltype(NCc)::value;
+      f4 acc[NC][NH];
+      int base[NC];
 #pragma unroll
-      for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
-      int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-      if (q >= npix) q = 0;
-      const int qr = q / Wt, qc = q - (q / Wt) * Wt;
-      base[gi] = (qr * Wp + qc) * CIN;
-    }
+      for (int gi = 0; gi < NC; ++gi) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
-      const int toff = (ky * Wp + kx) * CIN;
-      if constexpr (CIN == 16) {
-        s4 a[NH];
+        for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
+        int q = (g0 + kWaves * gi) * 16 + (lane & 15);
+        if (q >= npix) q = 0;
+        const int qr = q / Wt, qc = q - (q / Wt) * Wt;
+        base[gi] = (qr * Wp + qc) * CIN;
+      }
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
-          a[h] = *reinterpret_cast<const s4*>(
-              w_s + (tap * COUT + (lane & 15) + 16 * h) * CIN + 4 * (lane >> 4));
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const int toff = (ky * Wp + kx) * CIN;
+        if constexpr (CIN == 16) {
+          s4 a[NH];
 #pragma unroll
-        for (int gi = 0; gi < GPW; ++gi) {
-          if (g0 + kWaves * gi < ngroups) {
+          for (int h = 0; h < NH; ++h)
+            a[h] = *reinterpret_cast<const s4*>(
+                w_s + (tap * COUT + (lane & 15) + 16 * h) * CIN + 4 * (lane >> 4));
+#pragma unroll
+          for (int gi = 0; gi < NC; ++gi) {
             const s4 b = *reinterpret_cast<const s4*>(x_s + base[gi] + toff +
                                                       4 * (lane >> 4));
 #pragma unroll
             for (int h = 0; h < NH; ++h) acc[gi][h] = mfma16(a[h], b, acc[gi][h]);
           }
-        }
-      } else {
-        bf8 a[NH];
+        } else {
+          bf8 a[NH];
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
-          a[h] = *reinterpret_cast<const bf8*>(
-              w_s + (tap * COUT + (lane & 15) + 16 * h) * CIN + 8 * (lane >> 4));
+          for (int h = 0; h < NH; ++h)
+            a[h] = *reinterpret_cast<const bf8*>(
+                w_s + (tap * COUT + (lane & 15) + 16 * h) * CIN + 8 * (lane >> 4));
 #pragma unroll
-        for (int gi = 0; gi < GPW; ++gi) {
-          if (g0 + kWaves * gi < ngroups) {
+          for (int gi = 0; gi < NC; ++gi) {
             const bf8 b = *reinterpret_cast<const bf8*>(x_s + base[gi] + toff +
                                                         8 * (lane >> 4));
 #pragma unroll
@@ -121,18 +226,18 @@ __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
           }
         }
       }
-    }
 #pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-      const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-      if (g0 + kWaves * gi < ngroups && q < npix) {
+      for (int gi = 0; gi < NC; ++gi) {
+        const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
+        if (q < npix) {
 #pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
-          epi(q, 16 * h + 4 * (lane >> 4), v);
+          for (int h = 0; h < NH; ++h) {
+            float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
+            epi(q, 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
+          }
         }
       }
-    }
+    });
   }
 }
 
@@ -238,51 +343,57 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
                                                 int npix, Epi epi) {
   static_assert(COUT == 16 || COUT == 32, "COUT");
   constexpr int NH = CIN / 16;
-  constexpr int GPW = NH == 2 ? 2 : ::sa::conv::GPW;  // bound accumulator registers
+  using CH = DgradChunks<CIN, COUT>;  // gpw 2 for CIN 32: bound accumulators
+  constexpr int GPWD = CH::kGpw;
+  constexpr bool kReloadW = COUT == 32 || NH == 2;  // see conv_tile_fwd
   const int lane = lane_id();
   const int wave = wave_id();
   const int Wp = Wt + 2;
   const int ngroups = (npix + 15) / 16;
-  for (int g0 = wave; g0 < ngroups; g0 += kWaves * GPW) {
-    f4 acc[GPW][NH];
-    int base[GPW];
 #pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
+  for (int c = 0; c < CH::kChunks; ++c) {  // unrolled: see Chunking
+    const int g0 = wave + c * kWaves * GPWD;
+    if (g0 >= ngroups) break;
+    if constexpr (kReloadW) asm volatile("" ::: "memory");
+    const int nv = (ngroups - g0 + kWaves - 1) / kWaves;
+    for_count<GPWD>(nv, [&](auto NCc) {
+      constexpr int NC = decltype(NCc)::value;
+      f4 acc[NC][NH];
+      int base[NC];
 #pragma unroll
-      for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
-      int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-      if (q >= npix) q = 0;
-      const int qr = q / Wt, qc = q - (q / Wt) * Wt;
-      base[gi] = (qr * Wp + qc) * COUT;  // + ((2-ky)*Wp + (2-kx))*COUT per tap
-    }
+      for (int gi = 0; gi < NC; ++gi) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
-      const int toff = ((2 - ky) * Wp + (2 - kx)) * COUT;
-      if constexpr (COUT == 16) {
-        s4 a[NH];
+        for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
+        int q = (g0 + kWaves * gi) * 16 + (lane & 15);
+        if (q >= npix) q = 0;
+        const int qr = q / Wt, qc = q - (q / Wt) * Wt;
+        base[gi] = (qr * Wp + qc) * COUT;  // + ((2-ky)*Wp + (2-kx))*COUT per tap
+      }
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
-          a[h] = *reinterpret_cast<const s4*>(
-              w_s + (tap * CIN + (lane & 15) + 16 * h) * COUT + 4 * (lane >> 4));
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const int toff = ((2 - ky) * Wp + (2 - kx)) * COUT;
+        if constexpr (COUT == 16) {
+          s4 a[NH];
 #pragma unroll
-        for (int gi = 0; gi < GPW; ++gi) {
-          if (g0 + kWaves * gi < ngroups) {
+          for (int h = 0; h < NH; ++h)
+            a[h] = *reinterpret_cast<const s4*>(
+                w_s + (tap * CIN + (lane & 15) + 16 * h) * COUT + 4 * (lane >> 4));
+#pragma unroll
+          for (int gi = 0; gi < NC; ++gi) {
             const s4 b = *reinterpret_cast<const s4*>(d_s + base[gi] + toff +
                                                       4 * (lane >> 4));
 #pragma unroll
             for (int h = 0; h < NH; ++h) acc[gi][h] = mfma16(a[h], b, acc[gi][h]);
           }
-        }
-      } else {
-        bf8 a[NH];
+        } else {
+          bf8 a[NH];
 #pragma unroll
-        for (int h = 0; h < NH; ++h)
-          a[h] = *reinterpret_cast<const bf8*>(
-              w_s + (tap * CIN + (lane & 15) + 16 * h) * COUT + 8 * (lane >> 4));
+          for (int h = 0; h < NH; ++h)
+            a[h] = *reinterpret_cast<const bf8*>(
+                w_s + (tap * CIN + (lane & 15) + 16 * h) * COUT + 8 * (lane >> 4));
 #pragma unroll
-        for (int gi = 0; gi < GPW; ++gi) {
-          if (g0 + kWaves * gi < ngroups) {
+          for (int gi = 0; gi < NC; ++gi) {
             const bf8 b = *reinterpret_cast<const bf8*>(d_s + base[gi] + toff +
                                                         8 * (lane >> 4));
 #pragma unroll
@@ -290,18 +401,18 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
           }
         }
       }
-    }
 #pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-      const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-      if (g0 + kWaves * gi < ngroups && q < npix) {
+      for (int gi = 0; gi < NC; ++gi) {
+        const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
+        if (q < npix) {
 #pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
-          epi(q, 16 * h + 4 * (lane >> 4), v);
+          for (int h = 0; h < NH; ++h) {
+            float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
+            epi(q, 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
+          }
         }
       }
-    }
+    });
   }
 }
 
@@ -624,7 +735,6 @@ __device__ __forceinline__ void load_weights4(const float* __restrict__ w,
 }
 
 // ----------------------------------------------------------------- kernels
-constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
 
 template <int C, bool RESID, bool POST_RELU, bool RELU_IN, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_conv_fwd_kernel(
@@ -636,6 +746,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* x_s = w_s + 9 * C * C;
   load_weights4<C, C, true>(w, w_s);
+  float breg[C / 16][4];
+  bias_regs<C>(bias, reinterpret_cast<float*>(x_s), breg);
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
   RowStager<C, NREG> sx;
@@ -648,24 +760,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sx.template commit<RELU_IN, true>(x_s, W);
     __syncthreads();
+    const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    // residual straight from HBM into registers (no staging LDS), issued
+    // before the prefetch so the epilogue does not wait for the prefetch
+    EpiOperand<C, FwdChunks<C, C>> rop;
+    if (RESID) rop.load(resid, img0, Rv * W);
     const int nt = it.next(tile);
     if (it.valid(nt)) {
       const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
       sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
     }
-    const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
-    if (!((xcd >> 8) & 4))
-    conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4]) {
+    if (kKeep(xcd, 4))
+    conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4], int slot) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
+      for (int i = 0; i < 4; ++i) v[i] += breg[co0 >> 4][i];
       if (RESID) {
-        // residual read straight from HBM (8 B/lane, 32-B runs per pixel):
-        // no staging registers or LDS for it
         float r[4];
-        load4(resid + (img0 + q) * C + co0, r);
+        rop.get(slot, co0, r);
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] += r[i];
       }
@@ -691,6 +805,8 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
   bf16_t* x_s = w_s + 9 * CIN * COUT;
   bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN;
   load_weights4<CIN, COUT, true>(w, w_s);
+  float breg[COUT / 16][4];
+  bias_regs<COUT>(bias, reinterpret_cast<float*>(x_s), breg);
   const int tpi = (Hp + Rp - 1) / Rp;
   const int ntiles = N * tpi;
   RowStager<CIN, NREG> sx;
@@ -706,18 +822,18 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     const int cr0 = 2 * i0 - pb_h;
     const int Rc = 2 * Rpv + 1;
     __syncthreads();
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sx.template commit<false, true>(x_s, W);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
-    if (!((xcd >> 8) & 4))
-    conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4]) {
+    if (kKeep(xcd, 4))
+    conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4], int) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] += bias[co0 + i];
+      for (int i = 0; i < 4; ++i) v[i] += breg[co0 >> 4][i];
       store4_ord(y_s + q * COUT + co0, v);
     });
     __syncthreads();
-    if (!((xcd >> 8) & 1))
+    if (kKeep(xcd, 1))
     pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
                     argmax);
   }
@@ -757,18 +873,19 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
   };
+  float breg[1][4];
+  bias_regs<COUT>(bias, reinterpret_cast<float*>(y_s), breg);
+  const float b0 = breg[0][0], b1 = breg[0][1], b2 = breg[0][2], b3 = breg[0][3];
   const TileIter it(ntiles, xcd);
   int tile = it.first;
   if (it.valid(tile)) issue(tile);
-  const float b0 = bias[4 * (lane >> 4)], b1 = bias[4 * (lane >> 4) + 1],
-              b2 = bias[4 * (lane >> 4) + 2], b3 = bias[4 * (lane >> 4) + 3];
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, i0 = (tile - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     const int cr0 = 2 * i0 - pb_h;
     const int Rc = 2 * Rpv + 1;
     const int npix = Rc * W;
     __syncthreads();
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     commit_x4(sx, x4, W, Rc + 2, 4);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
@@ -778,7 +895,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       a[ky] = *reinterpret_cast<const s4*>(w_s + (ky * 16 + (lane & 15)) * 16 +
                                            4 * (lane >> 4));
     const int ngroups = (npix + 15) / 16;
-    for (int g = wave; g < (((xcd >> 8) & 4) ? 0 : ngroups); g += kWaves) {
+    for (int g = wave; g < (kKeep(xcd, 4) ? ngroups : 0); g += kWaves) {
       int q = g * 16 + (lane & 15);
       const bool valid = q < npix;
       if (!valid) q = 0;
@@ -796,7 +913,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       }
     }
     __syncthreads();
-    if (!((xcd >> 8) & 1))
+    if (kKeep(xcd, 1))
     pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
                     argmax);
   }
@@ -836,26 +953,28 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   for (; it.valid(tile); tile = it.next(tile)) {
     const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
     __syncthreads();  // previous tile's LDS reads done
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sd.template commit<false, true>(d_s, W);
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sa.template commit<RELU_ACT, true>(a_s, W);
     __syncthreads();
-    if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
-    if (!((xcd >> 8) & 4))
-    conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
+    EpiOperand<C, DgradChunks<C, C>> sop;  // skip grad, before the prefetch
+    if (ADD_SKIP) sop.load(skip, img0, npix);
+    if (it.valid(it.next(tile))) issue(it.next(tile));
+    if (kKeep(xcd, 4))
+    conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4], int slot) {
       const int qr = q / W, qc = q - (q / W) * W;
       float m[4];
       load4(a_s + ((qr + 1) * Wp + qc + 1) * C + ci0, m);
       float s[4] = {0.f, 0.f, 0.f, 0.f};
-      if (ADD_SKIP) load4(skip + (img0 + q) * C + ci0, s);  // from HBM
+      if (ADD_SKIP) sop.get(slot, ci0, s);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = s[i] + (m[i] > 0.f ? v[i] : 0.f);
       store4(dx + (img0 + q) * C + ci0, v);
     });
-    if (!((xcd >> 8) & 2))
+    if (kKeep(xcd, 2))
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
   }
   flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
@@ -1048,27 +1167,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sx.template commit<false, true>(x_s, W);
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sg.commit(g_s);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
-    if (!((xcd >> 8) & 1))
+    if (kKeep(xcd, 1))
     gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
                                   Rv + 2, d_s);
     __syncthreads();
     const int npix = Rv * W;
     if (NEED_DX) {
       const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
-    if (!((xcd >> 8) & 4))
-      conv_tile_dgrad<CIN, COUT>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4]) {
+    if (kKeep(xcd, 4))
+      conv_tile_dgrad<CIN, COUT>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4], int) {
         store4(dx + (img0 + q) * CIN + ci0, v);
       });
     }
-    if (!((xcd >> 8) & 2))
+    if (kKeep(xcd, 2))
     conv_tile_wgrad<CIN, COUT>(x_s, d_s, W, npix, x_elems, d_elems, acc);
   }
   flush_wgrad<CIN, COUT>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
@@ -1127,21 +1246,21 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     int lo, hi;
     pooled_rows(r0 - 1, Rv + 2, pb_h, Hp, &lo, &hi);
     __syncthreads();
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     commit_x4(sx, x4, W, Rv + 2, 4);
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sp.commit(reinterpret_cast<uint8_t*>(p_s));
-    if (!((xcd >> 8) & 8))
+    if (kKeep(xcd, 8))
     sg.commit(g_s);
     __syncthreads();
     if (it.valid(it.next(tile))) issue(it.next(tile));
     const int npix = Rv * W;
-    if (!((xcd >> 8) & 1))
+    if (kKeep(xcd, 1))
     gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
                                   Rv + 2, d_s);
     __syncthreads();
     const int ngroups = (npix + 15) / 16;
-    for (int g = wave; g < (((xcd >> 8) & 2) ? 0 : ngroups); g += kWaves) {
+    for (int g = wave; g < (kKeep(xcd, 2) ? ngroups : 0); g += kWaves) {
       const int qb = g * 16 + 4 * (lane >> 4) + (sub >> 2);
       const bool vb = qb < npix;
       const int qbr = vb ? qb / W : 0, qbc = vb ? qb - qbr * W : 0;
@@ -1239,6 +1358,15 @@ constexpr int rows_conv1_bwd(int H, int W, int px) {
   return R > H ? H : R;
 }
 
+// Host-side guard: the tile-height rules stop at one row, so a frame too wide
+// for even a one-row tile must be rejected (the kernels assume the staged
+// halo fits their staging registers and kMaxTilePx).
+void require_fit(bool ok, const char* what) {
+  if (!ok)
+    throw std::invalid_argument(std::string(what) +
+                                ": frame too wide for the conv tile staging");
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- launchers
@@ -1257,7 +1385,7 @@ struct ConvTune {
   int px_pool_bwd = 512;
   int px_conv1_bwd = 1152;
   int specialize = 1;     // use compile-time-geometry kernels when they match
-  int ablate = 0;         // timing-only: skip phases (1 pool, 2 wgrad, 4 conv, 8 LDS commit)
+  int ablate = 0;         // timing-only, -DSA_CONV_ABLATE builds: skip phases
 };
 constexpr ConvTune kDef{};
 static ConvTune g_tune;
@@ -1354,6 +1482,7 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
                          int C, bool post_relu, bool relu_in, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_fwd);
+  require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_fwd");
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
@@ -1399,6 +1528,7 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
   const int Rp = rows_pool_fwd(H, W, CIN, g_tune.px_pool_fwd);
+  require_fit((2 * Rp + 3) * W * CIN / 8 <= NREG * kThreads, "conv_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (9 * CIN * COUT + (2 * Rp + 3) * (W + 2) * CIN +
                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
@@ -1427,6 +1557,7 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                            int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
   const int Rp = rows_conv1_fwd(H, W, g_tune.px_conv1_fwd);
+  require_fit(((2 * Rp + 3) * W + 3) / 4 <= kU8Groups * kThreads, "conv1_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (3 * 16 * 16 + (2 * Rp + 1) * W * 16 +
                        ((2 * Rp + 3) * (W + 2) + 4) * 4) * sizeof(bf16_t);
@@ -1446,6 +1577,7 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
                          int H, int W, int C, bool relu_act, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
+  require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_bwd");
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
@@ -1486,6 +1618,9 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           hipStream_t s) {
   const int Wo = (W + 1) / 2;
   const int R = rows_pool_bwd(H, W, CIN, COUT, g_tune.px_pool_bwd);
+  require_fit((R + 2) * W * CIN / 8 <= NREG * kThreads &&
+                  ((R + 2) / 2 + 2) * Wo * COUT * 2 <= NREG * kThreads * 16,
+              "pool_conv_bwd");
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = (9 * CIN * COUT + (R + 2) * (W + 2) * (CIN + COUT) +
@@ -1525,6 +1660,9 @@ void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            int H, int W, int pb_h, int pb_w, hipStream_t s) {
   const int Wo = (W + 1) / 2;
   const int R = rows_conv1_bwd(H, W, g_tune.px_conv1_bwd);
+  require_fit(((R + 2) * W + 3) / 4 <= kU8Groups * kThreads &&
+                  ((R + 2) / 2 + 2) * ((W + 1) / 2) * 16 * 2 <= NREG * kThreads * 16,
+              "conv1_pool_bwd");
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
   const size_t smem = ((R + 2) * (W + 2) * 16 + 16 + (((R + 2) * (W + 2) + 5) & ~1) * 4 +
