@@ -37,6 +37,10 @@ constexpr int kThreads = 256;
 // 1 pool/gather, 2 wgrad, 4 conv, 8 LDS commit) exists only in builds with
 // -DSA_CONV_ABLATE: the runtime branches around the staging commit make the
 // compiler's vmcnt bookkeeping conservative (it then drains the prefetch).
+#ifndef SA_LATE_PREFETCH
+#define SA_LATE_PREFETCH 0
+#endif
+constexpr bool kLatePrefetch = SA_LATE_PREFETCH;
 #ifdef SA_CONV_ABLATE
 __device__ __forceinline__ bool kKeep(int xcd, int bit) { return !((xcd >> 8) & bit); }
 #else
@@ -122,12 +126,12 @@ struct EpiOperand {
     const int wave = wave_id();
 #pragma unroll
     for (int k = 0; k < CH::kSlots; ++k) {
-      const int q = (wave + kWaves * k) * 16 + (lane & 15);
+      // unconditional (clamped) loads: see RowStager
+      const int q = min((wave + kWaves * k) * 16 + (lane & 15), npix - 1);
 #pragma unroll
       for (int h = 0; h < NH; ++h)
-        v[k][h] = q < npix ? *reinterpret_cast<const uint2*>(
-                                 src + (img0 + q) * C + 16 * h + 4 * (lane >> 4))
-                           : make_uint2(0, 0);
+        v[k][h] = *reinterpret_cast<const uint2*>(src + (img0 + q) * C + 16 * h +
+                                                  4 * (lane >> 4));
     }
   }
   __device__ __forceinline__ void get(int slot, int co0, float f[4]) const {
@@ -199,17 +203,24 @@ __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
         const int ky = tap / 3, kx = tap % 3;
         const int toff = (ky * Wp + kx) * CIN;
         if constexpr (CIN == 16) {
-          s4 a[NH];
+          // paired taps: K = 32 = (kx0, kx0 + 1) x 16 ci, i.e. two
+          // neighbouring pixels read as ONE conflict-free ds_read_b128 per
+          // lane (6 MFMA 16x16x32 per group instead of 9 16x16x16; the
+          // compiler fuses 8-byte reads into ds_read2_b64, which banks mod
+          // 32 and serialises 4-way on this 32-byte pixel stride)
+          if (kx == 1) continue;  // covered by the (0, 1) pair
+          const int pr = kx >> 1;  // pair 0: kx 0,1; pair 1: kx 2,(3 = zero weights)
+          bf8 a[NH];
 #pragma unroll
           for (int h = 0; h < NH; ++h)
-            a[h] = *reinterpret_cast<const s4*>(
-                w_s + (tap * COUT + (lane & 15) + 16 * h) * CIN + 4 * (lane >> 4));
+            a[h] = *reinterpret_cast<const bf8*>(
+                w_s + (((ky * 2 + pr) * COUT + (lane & 15) + 16 * h) * 32) + 8 * (lane >> 4));
 #pragma unroll
           for (int gi = 0; gi < NC; ++gi) {
-            const s4 b = *reinterpret_cast<const s4*>(x_s + base[gi] + toff +
-                                                      4 * (lane >> 4));
+            const bf8 b = *reinterpret_cast<const bf8*>(x_s + base[gi] + toff +
+                                                        8 * (lane >> 4));
 #pragma unroll
-            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma16(a[h], b, acc[gi][h]);
+            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma32(a[h], b, acc[gi][h]);
           }
         } else {
           bf8 a[NH];
@@ -374,17 +385,22 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
         const int ky = tap / 3, kx = tap % 3;
         const int toff = ((2 - ky) * Wp + (2 - kx)) * COUT;
         if constexpr (COUT == 16) {
-          s4 a[NH];
+          // paired column offsets (see conv_tile_fwd): offsets o = 2 - kx in
+          // (0, 1) and (2, 3 = zero weights), one ds_read_b128 per lane
+          const int o = 2 - kx;
+          if (o == 1 || o == 3) continue;
+          const int pr = o >> 1, ro = 2 - ky;
+          bf8 a[NH];
 #pragma unroll
           for (int h = 0; h < NH; ++h)
-            a[h] = *reinterpret_cast<const s4*>(
-                w_s + (tap * CIN + (lane & 15) + 16 * h) * COUT + 4 * (lane >> 4));
+            a[h] = *reinterpret_cast<const bf8*>(
+                w_s + (((ro * 2 + pr) * CIN + (lane & 15) + 16 * h) * 32) + 8 * (lane >> 4));
 #pragma unroll
           for (int gi = 0; gi < NC; ++gi) {
-            const s4 b = *reinterpret_cast<const s4*>(d_s + base[gi] + toff +
-                                                      4 * (lane >> 4));
+            const bf8 b = *reinterpret_cast<const bf8*>(d_s + base[gi] + toff +
+                                                        8 * (lane >> 4));
 #pragma unroll
-            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma16(a[h], b, acc[gi][h]);
+            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma32(a[h], b, acc[gi][h]);
           }
         } else {
           bf8 a[NH];
@@ -555,23 +571,26 @@ __device__ __forceinline__ void flush_wgrad(const WgradAcc<CIN, COUT>& acc,
 template <int C, int NREG>
 struct RowStager {
   uint4 v[NREG];
-  int total;
+  int total, r_begin, H;
+  // Every lane issues all NREG loads (addresses clamped into the image) and
+  // commit() zeroes what lies outside: the staging registers are then always
+  // written by a load and always read after the wait, so the compiler's
+  // vmcnt bookkeeping stays exact (a zero-init of a register that may still
+  // have a load in flight costs a full vmcnt(0) drain).
   __device__ __forceinline__ void issue(const bf16_t* __restrict__ src, int n,
-                                        int H, int W, int r_begin, int rows) {
+                                        int H_, int W, int r_begin_, int rows) {
     constexpr int CH = C / 8;
     const int rc = W * CH;
     total = rows * rc;
+    r_begin = r_begin_;
+    H = H_;
 #pragma unroll
     for (int k = 0; k < NREG; ++k) {
-      const int e = threadIdx.x + k * kThreads;
-      v[k] = make_uint4(0, 0, 0, 0);
-      if (e < total) {
-        const int rr = e / rc;
-        const int r = r_begin + rr;
-        if (r >= 0 && r < H)
-          v[k] = *reinterpret_cast<const uint4*>(
-              src + (static_cast<int64_t>(n) * H + r) * W * C + (e - rr * rc) * 8);
-      }
+      const int e = min(static_cast<int>(threadIdx.x) + k * kThreads, total - 1);
+      const int rr = e / rc;
+      const int r = min(max(r_begin + rr, 0), H - 1);
+      v[k] = *reinterpret_cast<const uint4*>(
+          src + (static_cast<int64_t>(n) * H + r) * W * C + (e - rr * rc) * 8);
     }
   }
   template <bool RELU, bool HALO>
@@ -587,15 +606,18 @@ struct RowStager {
         const int rem = e - rr * rc;
         const int px = rem / CH;
         const int part = rem - px * CH;
-        uint4 x = v[k];
+        const int r = r_begin + rr;
+        uint4 x = (r >= 0 && r < H) ? v[k] : make_uint4(0, 0, 0, 0);
         if (RELU) x = relu8(x);
         *reinterpret_cast<uint4*>(lds + (rr * Wl + px + (HALO ? 1 : 0)) * C +
                                   part * 8) = x;
       }
     }
     if (HALO) {
+      // halo columns of every row, plus the first pixel after the last row
+      // (read, with zero weights, by the paired-tap MFMAs of the last row)
       const int rows = total / rc;
-      for (int e = threadIdx.x; e < rows * 2 * CH; e += kThreads) {
+      for (int e = threadIdx.x; e < (rows * 2 + 1) * CH; e += kThreads) {
         const int rr = e / (2 * CH);
         const int side = (e / CH) & 1;
         const int part = e % CH;
@@ -713,10 +735,36 @@ __device__ __forceinline__ void commit_x4(const U8Stager<NG>& st, bf16_t* x4,
   }
 }
 
+// LDS elements of a weight image (paired-tap layouts are 6 x 32 x M).
+__host__ __device__ constexpr int w_lds_elems(int CIN, int COUT, bool FWD) {
+  return (FWD && CIN == 16) ? 192 * COUT : (!FWD && COUT == 16) ? 192 * CIN : 9 * CIN * COUT;
+}
+
 // Fast fp32 [3][3][CIN][COUT] -> LDS bf16 weight load (float4 over co).
 template <int CIN, int COUT, bool FWD>
 __device__ __forceinline__ void load_weights4(const float* __restrict__ w,
                                               bf16_t* lds) {
+  if constexpr ((FWD && CIN == 16) || (!FWD && COUT == 16)) {
+    // paired-tap layouts (conv_tile_fwd / conv_tile_dgrad, 16-wide K):
+    //  FWD : [ky][pair][co][32], k < 16: kx = 2 pair, ci = k; else kx + 1
+    //  !FWD: [2-ky][pair][ci][32] over column offsets o = 2 - kx (o = 2 pair
+    //        + (k >= 16)), co = k & 15; kx outside 0..2 -> zero
+    constexpr int M = FWD ? COUT : CIN;
+    for (int e = threadIdx.x; e < 6 * M * 32; e += blockDim.x) {
+      const int kk = e & 31, m = (e >> 5) % M, pair = e / (32 * M);
+      const int r = pair >> 1, pr = pair & 1;
+      float v = 0.f;
+      if (FWD) {
+        const int kx = 2 * pr + (kk >> 4), ci = kk & 15;
+        if (kx < 3) v = w[((r * 3 + kx) * CIN + ci) * COUT + m];
+      } else {
+        const int kx = 2 - (2 * pr + (kk >> 4)), co = kk & 15, ky = 2 - r;
+        if (kx >= 0) v = w[((ky * 3 + kx) * CIN + m) * COUT + co];
+      }
+      lds[e] = f2bf(v);
+    }
+    return;
+  }
   const int total = 9 * CIN * COUT / 4;
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
     const float4 v = reinterpret_cast<const float4*>(w)[e];
@@ -744,7 +792,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* x_s = w_s + 9 * C * C;
+  bf16_t* x_s = w_s + w_lds_elems(C, C, true);  // + one pad pixel (paired taps)
   load_weights4<C, C, true>(w, w_s);
   float breg[C / 16][4];
   bias_regs<C>(bias, reinterpret_cast<float*>(x_s), breg);
@@ -769,10 +817,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     EpiOperand<C, FwdChunks<C, C>> rop;
     if (RESID) rop.load(resid, img0, Rv * W);
     const int nt = it.next(tile);
-    if (it.valid(nt)) {
-      const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
-      sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
-    }
+    auto prefetch = [&]() {
+      if (it.valid(nt)) {
+        const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
+        sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
+      }
+    };
+    if (!kLatePrefetch) prefetch();
     if (kKeep(xcd, 4))
     conv_tile_fwd<C, C>(x_s, w_s, W, Rv * W, [&](int q, int co0, float v[4], int slot) {
 #pragma unroll
@@ -789,6 +840,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       }
       store4(y + (img0 + q) * C + co0, v);
     });
+    if (kLatePrefetch) prefetch();
   }
 }
 
@@ -802,8 +854,8 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
   const int H = HC ? HC : H_, W = WC ? WC : W_, Rp = RC ? RC : Rp_;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* x_s = w_s + 9 * CIN * COUT;
-  bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN;
+  bf16_t* x_s = w_s + w_lds_elems(CIN, COUT, true);
+  bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN + CIN;  // + pad pixel
   load_weights4<CIN, COUT, true>(w, w_s);
   float breg[COUT / 16][4];
   bias_regs<COUT>(bias, reinterpret_cast<float*>(x_s), breg);
@@ -930,7 +982,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   const int Wp = W + 2;
   const int tile_elems = (R + 2) * Wp * C;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* d_s = w_s + 9 * C * C;
+  bf16_t* d_s = w_s + w_lds_elems(C, C, false);
   bf16_t* a_s = d_s + tile_elems + C;  // + one zero pixel each
   load_weights4<C, C, false>(w, w_s);
   for (int e = threadIdx.x; e < C; e += blockDim.x) {
@@ -962,7 +1014,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     EpiOperand<C, DgradChunks<C, C>> sop;  // skip grad, before the prefetch
     if (ADD_SKIP) sop.load(skip, img0, npix);
-    if (it.valid(it.next(tile))) issue(it.next(tile));
+    if (!kLatePrefetch && it.valid(it.next(tile))) issue(it.next(tile));
     if (kKeep(xcd, 4))
     conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4], int slot) {
       const int qr = q / W, qc = q - (q / W) * W;
@@ -976,6 +1028,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     });
     if (kKeep(xcd, 2))
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
+    if (kLatePrefetch && it.valid(it.next(tile))) issue(it.next(tile));
   }
   flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
 }
@@ -1135,7 +1188,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   const int x_elems = (R + 2) * Wp * CIN;
   const int prow_max = (R + 2) / 2 + 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* d_s = w_s + 9 * CIN * COUT;
+  bf16_t* d_s = w_s + w_lds_elems(CIN, COUT, false);
   bf16_t* x_s = d_s + d_elems + COUT;
   bf16_t* p_s = x_s + x_elems + CIN;
   uint8_t* g_s = reinterpret_cast<uint8_t*>(p_s + prow_max * Wo * COUT);
@@ -1484,7 +1537,7 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
   const int R = rows_for(H, W, C, g_tune.px_res_fwd);
   require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_fwd");
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (9 * C * C + (R + 2) * (W + 2) * C) * sizeof(bf16_t);
+  const size_t smem = (w_lds_elems(C, C, true) + (R + 2) * (W + 2) * C + C) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
@@ -1530,7 +1583,7 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
   const int Rp = rows_pool_fwd(H, W, CIN, g_tune.px_pool_fwd);
   require_fit((2 * Rp + 3) * W * CIN / 8 <= NREG * kThreads, "conv_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
-  const size_t smem = (9 * CIN * COUT + (2 * Rp + 3) * (W + 2) * CIN +
+  const size_t smem = (w_lds_elems(CIN, COUT, true) + (2 * Rp + 3) * (W + 2) * CIN + CIN +
                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
@@ -1579,7 +1632,7 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
   require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_bwd");
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (9 * C * C + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
+  const size_t smem = (w_lds_elems(C, C, false) + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DY = static_cast<const bf16_t*>(dy);
   auto A = static_cast<const bf16_t*>(act);
@@ -1623,7 +1676,7 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
               "pool_conv_bwd");
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (9 * CIN * COUT + (R + 2) * (W + 2) * (CIN + COUT) +
+  const size_t smem = (w_lds_elems(CIN, COUT, false) + (R + 2) * (W + 2) * (CIN + COUT) +
                        CIN + COUT + prow_max * Wo * COUT) * sizeof(bf16_t) +
                       prow_max * Wo * COUT;
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
