@@ -54,6 +54,48 @@ constexpr int NREG = 4;  // staging registers (uint4) per lane per stream
 // chunks, i.e. at most NREG*kThreads*8/C pixels.
 constexpr int kMaxTilePx(int C) { return NREG * kThreads * 8 / C; }
 
+// LDS halo images [rows][W+2][C].  32-channel images (64-B pixels) get 32 B
+// of padding per row, so a row starts 2 slots (mod 4) after the previous
+// one; their MFMA column groups are 2 rows x 8 pixels (GroupMap).  A
+// ds_read_b128 of such a group (16 lanes x one 16-B chunk) is then
+// conflict-free for any starting pixel; 16 consecutive 64-B pixels of one row
+// would be 2-way conflicted.  16-channel images are unpadded, their groups
+// 16 consecutive pixels (paired-tap reads of 32-B pixels are conflict-free).
+__host__ __device__ constexpr int row_pitch(int C, int W) {
+  return (W + 2) * C + (C == 32 ? 16 : 0);
+}
+__host__ __device__ constexpr int ceil_div(int a, int b) { return (a + b - 1) / b; }
+// MFMA column groups of a tile of `rows` x W output pixels.
+__host__ __device__ constexpr int tile_groups(int C, int rows, int W) {
+  return C == 32 ? ceil_div(rows, 2) * ceil_div(W, 8) : ceil_div(rows * W, 16);
+}
+
+template <int C>
+struct GroupMap {
+  int Wt, rows, ncb, ngroups;
+  __device__ __forceinline__ GroupMap(int Wt_, int npix) : Wt(Wt_), rows(npix / Wt_) {
+    ncb = (Wt + 7) >> 3;
+    ngroups = tile_groups(C, rows, Wt);
+  }
+  // pixel (r, c) of lane i of group g; invalid lanes get (0, 0)
+  __device__ __forceinline__ bool pixel(int g, int i, int& r, int& c) const {
+    bool valid;
+    if constexpr (C == 32) {
+      const int rp = g / ncb, cb = g - rp * ncb;
+      r = 2 * rp + (i >> 3);
+      c = cb * 8 + (i & 7);
+      valid = r < rows && c < Wt;
+    } else {
+      const int q = g * 16 + i;
+      valid = q < rows * Wt;
+      r = q / Wt;
+      c = q - r * Wt;
+    }
+    if (!valid) r = c = 0;
+    return valid;
+  }
+};
+
 // Persistent tile schedule.  xcd == 0: tile = blockIdx.x + k * gridDim.x.
 // xcd == 1: XCD-aware - workgroups are dispatched round-robin over the 8 XCDs
 // (b % 8), so each XCD gets one CONTIGUOUS range of tiles (proportional to
@@ -101,16 +143,19 @@ __device__ __forceinline__ void for_count(int nv, F&& f) {
 // tile to kMaxTilePx pixels): with a real loop holding global stores, the
 // compiler drains vmcnt in the preheader, i.e. waits for the next tile's
 // prefetch before computing this one.
-template <int GP, int MAXPX>
+template <int GP, int MAXPX, int MAPC>
 struct Chunking {
   static constexpr int kGpw = GP;
-  static constexpr int kChunks = (MAXPX / 16 + kWaves * GP - 1) / (kWaves * GP);
+  static constexpr int kMapC = MAPC;  // GroupMap of the image the MFMAs read
+  static constexpr int kMaxGroups = MAXPX / 16;  // enforced by the tile rules
+  static constexpr int kChunks = (kMaxGroups + kWaves * GP - 1) / (kWaves * GP);
   static constexpr int kSlots = kChunks * GP;  // groups per wave, max
 };
 template <int CIN, int COUT>
-using FwdChunks = Chunking<GPW, kMaxTilePx(CIN)>;
+using FwdChunks = Chunking<GPW, kMaxTilePx(CIN), CIN>;
 template <int CIN, int COUT>
-using DgradChunks = Chunking<(CIN == 32 ? 2 : GPW), kMaxTilePx(CIN < COUT ? CIN : COUT)>;
+using DgradChunks =
+    Chunking<(CIN == 32 ? 2 : GPW), kMaxTilePx(CIN < COUT ? CIN : COUT), COUT>;
 
 // Per-lane copy of a global [pixels][C] bf16 operand for the epilogue of
 // this wave's groups (4 channels per 16-channel half), loaded BEFORE the
@@ -121,13 +166,16 @@ struct EpiOperand {
   static constexpr int NH = C / 16;
   uint2 v[CH::kSlots][NH];
   __device__ __forceinline__ void load(const bf16_t* __restrict__ src,
-                                       int64_t img0, int npix) {
+                                       int64_t img0, int npix, int Wt) {
     const int lane = lane_id();
     const int wave = wave_id();
+    const GroupMap<CH::kMapC> gm(Wt, npix);
 #pragma unroll
     for (int k = 0; k < CH::kSlots; ++k) {
-      // unconditional (clamped) loads: see RowStager
-      const int q = min((wave + kWaves * k) * 16 + (lane & 15), npix - 1);
+      // unconditional loads (invalid lanes read pixel 0): see RowStager
+      int r, c;
+      gm.pixel(wave + kWaves * k, lane & 15, r, c);
+      const int q = r * Wt + c;
 #pragma unroll
       for (int h = 0; h < NH; ++h)
         v[k][h] = *reinterpret_cast<const uint2*>(src + (img0 + q) * C + 16 * h +
@@ -176,8 +224,9 @@ __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
   constexpr bool kReloadW = CIN == 32 || NH == 2;
   const int lane = lane_id();
   const int wave = wave_id();
-  const int Wp = Wt + 2;
-  const int ngroups = (npix + 15) / 16;
+  const int RP = row_pitch(CIN, Wt);
+  const GroupMap<CIN> gm(Wt, npix);
+  const int ngroups = gm.ngroups;
   using CH = FwdChunks<CIN, COUT>;
 #pragma unroll
   for (int c = 0; c < CH::kChunks; ++c) {
@@ -188,20 +237,20 @@ __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
     for_count<CH::kGpw>(nv, [&](auto NCc) {
       constexpr int NC = decltype(NCc)::value;
       f4 acc[NC][NH];
-      int base[NC];
+      int base[NC], qv[NC];
 #pragma unroll
       for (int gi = 0; gi < NC; ++gi) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
-        int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-        if (q >= npix) q = 0;
-        const int qr = q / Wt, qc = q - (q / Wt) * Wt;
-        base[gi] = (qr * Wp + qc) * CIN;
+        int qr, qc;
+        const bool valid = gm.pixel(g0 + kWaves * gi, lane & 15, qr, qc);
+        qv[gi] = valid ? qr * Wt + qc : -1;
+        base[gi] = qr * RP + qc * CIN;
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int ky = tap / 3, kx = tap % 3;
-        const int toff = (ky * Wp + kx) * CIN;
+        const int toff = ky * RP + kx * CIN;
         if constexpr (CIN == 16) {
           // paired taps: K = 32 = (kx0, kx0 + 1) x 16 ci, i.e. two
           // neighbouring pixels read as ONE conflict-free ds_read_b128 per
@@ -239,12 +288,11 @@ __device__ __forceinline__ void conv_tile_fwd(const bf16_t* x_s,
       }
 #pragma unroll
       for (int gi = 0; gi < NC; ++gi) {
-        const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-        if (q < npix) {
+        if (qv[gi] >= 0) {
 #pragma unroll
           for (int h = 0; h < NH; ++h) {
             float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
-            epi(q, 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
+            epi(qv[gi], 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
           }
         }
       }
@@ -359,8 +407,9 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
   constexpr bool kReloadW = COUT == 32 || NH == 2;  // see conv_tile_fwd
   const int lane = lane_id();
   const int wave = wave_id();
-  const int Wp = Wt + 2;
-  const int ngroups = (npix + 15) / 16;
+  const int RP = row_pitch(COUT, Wt);
+  const GroupMap<COUT> gm(Wt, npix);
+  const int ngroups = gm.ngroups;
 #pragma unroll
   for (int c = 0; c < CH::kChunks; ++c) {  // unrolled: see Chunking
     const int g0 = wave + c * kWaves * GPWD;
@@ -370,20 +419,20 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
     for_count<GPWD>(nv, [&](auto NCc) {
       constexpr int NC = decltype(NCc)::value;
       f4 acc[NC][NH];
-      int base[NC];
+      int base[NC], qv[NC];
 #pragma unroll
       for (int gi = 0; gi < NC; ++gi) {
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
-        int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-        if (q >= npix) q = 0;
-        const int qr = q / Wt, qc = q - (q / Wt) * Wt;
-        base[gi] = (qr * Wp + qc) * COUT;  // + ((2-ky)*Wp + (2-kx))*COUT per tap
+        int qr, qc;
+        const bool valid = gm.pixel(g0 + kWaves * gi, lane & 15, qr, qc);
+        qv[gi] = valid ? qr * Wt + qc : -1;
+        base[gi] = qr * RP + qc * COUT;  // + (2-ky, 2-kx) per tap
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int ky = tap / 3, kx = tap % 3;
-        const int toff = ((2 - ky) * Wp + (2 - kx)) * COUT;
+        const int toff = (2 - ky) * RP + (2 - kx) * COUT;
         if constexpr (COUT == 16) {
           // paired column offsets (see conv_tile_fwd): offsets o = 2 - kx in
           // (0, 1) and (2, 3 = zero weights), one ds_read_b128 per lane
@@ -419,12 +468,11 @@ __device__ __forceinline__ void conv_tile_dgrad(const bf16_t* d_s,
       }
 #pragma unroll
       for (int gi = 0; gi < NC; ++gi) {
-        const int q = (g0 + kWaves * gi) * 16 + (lane & 15);
-        if (q < npix) {
+        if (qv[gi] >= 0) {
 #pragma unroll
           for (int h = 0; h < NH; ++h) {
             float v[4] = {acc[gi][h][0], acc[gi][h][1], acc[gi][h][2], acc[gi][h][3]};
-            epi(q, 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
+            epi(qv[gi], 16 * h + 4 * (lane >> 4), v, c * CH::kGpw + gi);
           }
         }
       }
@@ -473,7 +521,7 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
   const int lane = lane_id();
   const int wave = wave_id();
   const int tg = wave % TG;
-  const int Wp = Wt + 2;
+  const int RPa = row_pitch(CIN, Wt), RPd = row_pitch(COUT, Wt);
   const int ngroups = (npix + 15) / 16;
   const int sub = lane & 15;
   const int qrow = sub >> 2;       // row of the 4x16 tr block
@@ -485,11 +533,10 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
     const bool valid = q < npix;
     const int qr = valid ? q / Wt : 0;
     const int qc = valid ? q - qr * Wt : 0;
-    const int pos = (qr + 1) * Wp + (qc + 1);
     s4 bd[HO];
 #pragma unroll
     for (int o = 0; o < HO; ++o) {
-      bd[o] = lds_tr4(d_s + (valid ? pos * COUT : zero_d) + 16 * o + pcol);
+      bd[o] = lds_tr4(d_s + (valid ? (qr + 1) * RPd + (qc + 1) * COUT : zero_d) + 16 * o + pcol);
       if (tg == 0) acc.b[o] = mfma16(ones, bd[o], acc.b[o]);
     }
 #pragma unroll
@@ -497,10 +544,10 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
       const int tap = tg * TPG + k;
       if (tap < 9) {
         const int ky = tap / 3, kx = tap % 3;
-        const int apos = pos + (ky - 1) * Wp + (kx - 1);
+        const int aoff = (qr + ky) * RPa + (qc + kx) * CIN;
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
-          const s4 aa = lds_tr4(a_s + (valid ? apos * CIN : zero_a) + 16 * c + pcol);
+          const s4 aa = lds_tr4(a_s + (valid ? aoff : zero_a) + 16 * c + pcol);
 #pragma unroll
           for (int o = 0; o < HO; ++o) acc.w[k][c][o] = mfma16(aa, bd[o], acc.w[k][c][o]);
         }
@@ -597,7 +644,7 @@ struct RowStager {
   __device__ __forceinline__ void commit(bf16_t* lds, int W) const {
     constexpr int CH = C / 8;
     const int rc = W * CH;
-    const int Wl = HALO ? W + 2 : W;
+    const int RP = HALO ? row_pitch(C, W) : W * C;
 #pragma unroll
     for (int k = 0; k < NREG; ++k) {
       const int e = threadIdx.x + k * kThreads;
@@ -609,7 +656,7 @@ struct RowStager {
         const int r = r_begin + rr;
         uint4 x = (r >= 0 && r < H) ? v[k] : make_uint4(0, 0, 0, 0);
         if (RELU) x = relu8(x);
-        *reinterpret_cast<uint4*>(lds + (rr * Wl + px + (HALO ? 1 : 0)) * C +
+        *reinterpret_cast<uint4*>(lds + rr * RP + (px + (HALO ? 1 : 0)) * C +
                                   part * 8) = x;
       }
     }
@@ -621,7 +668,7 @@ struct RowStager {
         const int rr = e / (2 * CH);
         const int side = (e / CH) & 1;
         const int part = e % CH;
-        *reinterpret_cast<uint4*>(lds + (rr * Wl + (side ? W + 1 : 0)) * C +
+        *reinterpret_cast<uint4*>(lds + rr * RP + (side ? W + 1 : 0) * C +
                                   part * 8) = make_uint4(0, 0, 0, 0);
       }
     }
@@ -815,7 +862,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     // residual straight from HBM into registers (no staging LDS), issued
     // before the prefetch so the epilogue does not wait for the prefetch
     EpiOperand<C, FwdChunks<C, C>> rop;
-    if (RESID) rop.load(resid, img0, Rv * W);
+    if (RESID) rop.load(resid, img0, Rv * W, W);
     const int nt = it.next(tile);
     auto prefetch = [&]() {
       if (it.valid(nt)) {
@@ -855,7 +902,7 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* x_s = w_s + w_lds_elems(CIN, COUT, true);
-  bf16_t* y_s = x_s + (2 * Rp + 3) * (W + 2) * CIN + CIN;  // + pad pixel
+  bf16_t* y_s = x_s + (2 * Rp + 3) * row_pitch(CIN, W) + CIN;  // + pad pixel
   load_weights4<CIN, COUT, true>(w, w_s);
   float breg[COUT / 16][4];
   bias_regs<COUT>(bias, reinterpret_cast<float*>(x_s), breg);
@@ -979,8 +1026,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     int N, int H_, int W_, int R_, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
-  const int Wp = W + 2;
-  const int tile_elems = (R + 2) * Wp * C;
+  const int RP = row_pitch(C, W);
+  const int tile_elems = (R + 2) * RP;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* d_s = w_s + w_lds_elems(C, C, false);
   bf16_t* a_s = d_s + tile_elems + C;  // + one zero pixel each
@@ -1013,13 +1060,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const int npix = Rv * W;
     const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     EpiOperand<C, DgradChunks<C, C>> sop;  // skip grad, before the prefetch
-    if (ADD_SKIP) sop.load(skip, img0, npix);
+    if (ADD_SKIP) sop.load(skip, img0, npix, W);
     if (!kLatePrefetch && it.valid(it.next(tile))) issue(it.next(tile));
     if (kKeep(xcd, 4))
     conv_tile_dgrad<C, C>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4], int slot) {
       const int qr = q / W, qc = q - (q / W) * W;
       float m[4];
-      load4(a_s + ((qr + 1) * Wp + qc + 1) * C + ci0, m);
+      load4(a_s + (qr + 1) * RP + (qc + 1) * C + ci0, m);
       float s[4] = {0.f, 0.f, 0.f, 0.f};
       if (ADD_SKIP) sop.get(slot, ci0, s);
 #pragma unroll
@@ -1033,56 +1080,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
 }
 
-// dY of the conv feeding a max-pool, for the halo tile rows [r_begin,
-// r_begin+rows) x cols [-1, W], gathered from LDS copies of the pooled grads
-// p_s and argmax g_s holding pooled rows [i_lo, ...).
-template <int COUT>
-__device__ __forceinline__ void gather_pool_grad_lds(
-    const bf16_t* p_s, const uint8_t* g_s, int i_lo, int H, int W, int Hp,
-    int Wo, int pb_h, int pb_w, int r_begin, int rows, bf16_t* d_s) {
-  constexpr int CH = COUT / 8;
-  const int Wp = W + 2;
-  const int total = rows * Wp * CH;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int part = e % CH;
-    const int pix = e / CH;
-    const int rr = pix / Wp;
-    const int cc = pix - rr * Wp;
-    const int r = r_begin + rr, c = cc - 1;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (r >= 0 && r < H && c >= 0 && c < W) {
-      const int ilo = max(0, (r + pb_h - 1) / 2);
-      const int ihi = min(Hp - 1, (r + pb_h) / 2);
-      const int jlo = max(0, (c + pb_w - 1) / 2);
-      const int jhi = min(Wo - 1, (c + pb_w) / 2);
-      for (int i = ilo; i <= ihi; ++i) {
-        const int dyy = r - (2 * i - pb_h);
-        for (int j = jlo; j <= jhi; ++j) {
-          const int code = dyy * 3 + (c - (2 * j - pb_w));
-          const int o = ((i - i_lo) * Wo + j) * COUT + part * 8;
-          const uint2 a = *reinterpret_cast<const uint2*>(g_s + o);
-          const uint4 d = *reinterpret_cast<const uint4*>(p_s + o);
-          const uint32_t du[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t ab = ((k < 4 ? a.x : a.y) >> (8 * (k & 3))) & 0xFF;
-            if (static_cast<int>(ab) == code)
-              acc[k] += __uint_as_float((k & 1) ? (du[k >> 1] & 0xFFFF0000u)
-                                                : (du[k >> 1] << 16));
-          }
-        }
-      }
-    }
-    uint4 v;
-    v.x = f2bf(acc[0]) | (static_cast<uint32_t>(f2bf(acc[1])) << 16);
-    v.y = f2bf(acc[2]) | (static_cast<uint32_t>(f2bf(acc[3])) << 16);
-    v.z = f2bf(acc[4]) | (static_cast<uint32_t>(f2bf(acc[5])) << 16);
-    v.w = f2bf(acc[6]) | (static_cast<uint32_t>(f2bf(acc[7])) << 16);
-    *reinterpret_cast<uint4*>(d_s + pix * COUT + part * 8) = v;
-  }
-}
-
-// The same dY tile, built per 2x2 block of conv positions.  Block (i, j)
+// dY of the conv feeding a max-pool as an LDS halo tile (rows [r_begin,
+// r_begin+rows) x cols [-1, W], pitch row_pitch(COUT, W)), built per 2x2
+// block of conv positions.  Block (i, j)
 // holds conv rows 2i-pb_h+{0,1} x cols 2j-pb_w+{0,1}; its cells can only be
 // the argmax of pooled windows (i,j), (i-1,j), (i,j-1), (i-1,j-1) (a window's
 // dy/dx = 2 cells are the next block's offset-0 cells).  Each thread loads
@@ -1097,13 +1097,13 @@ __device__ __forceinline__ void gather_pool_grad_blocks(
     const bf16_t* p_s, const uint8_t* g_s, int i_lo, int i_hi, int W, int Wo,
     int pb_h, int pb_w, int r_begin, int rows, bf16_t* d_s) {
   constexpr int CH = COUT / 8;
-  const int Wp = W + 2;
+  const int RPd = row_pitch(COUT, W);
   // halo columns -1 and W
   for (int e = threadIdx.x; e < rows * 2 * CH; e += blockDim.x) {
     const int part = e % CH;
     const int side = (e / CH) & 1;
     const int rr = e / (2 * CH);
-    *reinterpret_cast<uint4*>(d_s + (rr * Wp + (side ? W + 1 : 0)) * COUT +
+    *reinterpret_cast<uint4*>(d_s + rr * RPd + (side ? W + 1 : 0) * COUT +
                               part * 8) = make_uint4(0, 0, 0, 0);
   }
   // blocks whose rows intersect [r_begin, r_begin + rows)
@@ -1159,7 +1159,7 @@ __device__ __forceinline__ void gather_pool_grad_blocks(
         o.y = f2bf(cell[cidx][2]) | (static_cast<uint32_t>(f2bf(cell[cidx][3])) << 16);
         o.z = f2bf(cell[cidx][4]) | (static_cast<uint32_t>(f2bf(cell[cidx][5])) << 16);
         o.w = f2bf(cell[cidx][6]) | (static_cast<uint32_t>(f2bf(cell[cidx][7])) << 16);
-        *reinterpret_cast<uint4*>(d_s + (rr * Wp + cc + 1) * COUT + part * 8) = o;
+        *reinterpret_cast<uint4*>(d_s + rr * RPd + (cc + 1) * COUT + part * 8) = o;
       }
     }
   }
@@ -1182,10 +1182,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     int N, int H_, int W_, int R_, int pb_h, int pb_w, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
-  const int Wp = W + 2;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
-  const int d_elems = (R + 2) * Wp * COUT;
-  const int x_elems = (R + 2) * Wp * CIN;
+  const int d_elems = (R + 2) * row_pitch(COUT, W);
+  const int x_elems = (R + 2) * row_pitch(CIN, W);
   const int prow_max = (R + 2) / 2 + 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);
   bf16_t* d_s = w_s + w_lds_elems(CIN, COUT, false);
@@ -1378,14 +1377,18 @@ void set_smem(K kernel, size_t bytes) {
 constexpr int rows_for(int H, int W, int C, int target) {
   int R = target / W;
   if (R < 1) R = 1;
-  while (R > 1 && (R + 2) * W * C / 8 > NREG * kThreads) --R;
+  while (R > 1 && ((R + 2) * W * C / 8 > NREG * kThreads ||
+                   tile_groups(C, R, W) > kMaxTilePx(C) / 16))
+    --R;
   return R < H ? R : H;
 }
 constexpr int rows_pool_fwd(int H, int W, int CIN, int px) {
   const int Hp = (H + 1) / 2;
   int Rp = (px / W - 1) / 2;
   if (Rp < 1) Rp = 1;
-  while (Rp > 1 && (2 * Rp + 3) * W * CIN / 8 > NREG * kThreads) --Rp;
+  while (Rp > 1 && ((2 * Rp + 3) * W * CIN / 8 > NREG * kThreads ||
+                    tile_groups(CIN, 2 * Rp + 1, W) > kMaxTilePx(CIN) / 16))
+    --Rp;
   return Rp > Hp ? Hp : Rp;
 }
 constexpr int rows_conv1_fwd(int H, int W, int px) {
@@ -1398,7 +1401,9 @@ constexpr int rows_conv1_fwd(int H, int W, int px) {
 constexpr int rows_pool_bwd(int H, int W, int CIN, int COUT, int px) {
   const int Wo = (W + 1) / 2;
   int R = rows_for(H, W, CIN, px);
-  while (R > 1 && ((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16) --R;
+  while (R > 1 && (((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16 ||
+                   tile_groups(COUT, R, W) > kMaxTilePx(CIN < COUT ? CIN : COUT) / 16))
+    --R;
   return R;
 }
 constexpr int rows_conv1_bwd(int H, int W, int px) {
@@ -1535,9 +1540,11 @@ void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
                          int C, bool post_relu, bool relu_in, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_fwd);
-  require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_fwd");
+  require_fit((R + 2) * W * C / 8 <= NREG * kThreads &&
+                  tile_groups(C, R, W) <= kMaxTilePx(C) / 16,
+              "res_conv_fwd");
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (w_lds_elems(C, C, true) + (R + 2) * (W + 2) * C + C) * sizeof(bf16_t);
+  const size_t smem = (w_lds_elems(C, C, true) + (R + 2) * row_pitch(C, W) + C) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto RS = static_cast<const bf16_t*>(resid);
@@ -1581,9 +1588,11 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
   const int Rp = rows_pool_fwd(H, W, CIN, g_tune.px_pool_fwd);
-  require_fit((2 * Rp + 3) * W * CIN / 8 <= NREG * kThreads, "conv_pool_fwd");
+  require_fit((2 * Rp + 3) * W * CIN / 8 <= NREG * kThreads &&
+                  tile_groups(CIN, 2 * Rp + 1, W) <= kMaxTilePx(CIN) / 16,
+              "conv_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
-  const size_t smem = (w_lds_elems(CIN, COUT, true) + (2 * Rp + 3) * (W + 2) * CIN + CIN +
+  const size_t smem = (w_lds_elems(CIN, COUT, true) + (2 * Rp + 3) * row_pitch(CIN, W) + CIN +
                        (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
@@ -1630,9 +1639,11 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
                          int H, int W, int C, bool relu_act, hipStream_t s) {
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
-  require_fit((R + 2) * W * C / 8 <= NREG * kThreads, "res_conv_bwd");
+  require_fit((R + 2) * W * C / 8 <= NREG * kThreads &&
+                  tile_groups(C, R, W) <= kMaxTilePx(C) / 16,
+              "res_conv_bwd");
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (w_lds_elems(C, C, false) + 2 * ((R + 2) * (W + 2) * C + C)) * sizeof(bf16_t);
+  const size_t smem = (w_lds_elems(C, C, false) + 2 * ((R + 2) * row_pitch(C, W) + C)) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DY = static_cast<const bf16_t*>(dy);
   auto A = static_cast<const bf16_t*>(act);
@@ -1672,11 +1683,13 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
   const int Wo = (W + 1) / 2;
   const int R = rows_pool_bwd(H, W, CIN, COUT, g_tune.px_pool_bwd);
   require_fit((R + 2) * W * CIN / 8 <= NREG * kThreads &&
+                  tile_groups(COUT, R, W) <= kMaxTilePx(CIN < COUT ? CIN : COUT) / 16 &&
                   ((R + 2) / 2 + 2) * Wo * COUT * 2 <= NREG * kThreads * 16,
               "pool_conv_bwd");
   const int prow_max = (R + 2) / 2 + 2;
   const int ntiles = N * ((H + R - 1) / R);
-  const size_t smem = (w_lds_elems(CIN, COUT, false) + (R + 2) * (W + 2) * (CIN + COUT) +
+  const size_t smem = (w_lds_elems(CIN, COUT, false) +
+                       (R + 2) * (row_pitch(CIN, W) + row_pitch(COUT, W)) +
                        CIN + COUT + prow_max * Wo * COUT) * sizeof(bf16_t) +
                       prow_max * Wo * COUT;
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
