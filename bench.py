@@ -53,6 +53,8 @@ def main():
   ap.add_argument('--graph', type=int, default=1)
   ap.add_argument('--device', default='auto')
   ap.add_argument('--profile_steps', type=int, default=0)
+  ap.add_argument('--pipeline_chunks', type=int, default=1,
+                  help='time chunks of the torso || LSTM pipeline (1 = off)')
   args = ap.parse_args()
 
   rank, world, local = parallel.init_distributed()
@@ -78,7 +80,8 @@ def main():
   frame_shape = (args.height, args.width, 3)
   cdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
   agent = Agent(num_actions, torso=args.torso, frame_shape=frame_shape,
-                seed=flags.seed, backend=backend, compute_dtype=cdt)
+                seed=flags.seed, backend=backend, compute_dtype=cdt,
+                pipeline_chunks=args.pipeline_chunks)
   learner = Learner(agent, flags, device, world_size=world)
   if world > 1:
     parallel.broadcast_params(learner.flat.params)
@@ -169,6 +172,7 @@ def main():
                    'frame': '%dx%dx3' % (args.height, args.width),
                    'parallelism': 'dp%d' % world, 'backend': backend,
                    'hip_graph': use_graph, 'loss_finite': ok,
+                   'pipeline_chunks': args.pipeline_chunks,
                    'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
                                    'frames/s (BASELINE.md B)'},
     }

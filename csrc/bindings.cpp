@@ -91,18 +91,8 @@ std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
   return {loss, dlogits, dvalues};
 }
 
-// Operand packing shared by the fwd/bwd step kernels (see lstm.hip):
-// fwd A:  [RT][8 waves][2 mt][NS=H/32][64 lanes] of h (rows padded to 32)
-// bwd A:  [RT][16 waves][2 mt][NS=H/16][64 lanes] of dG
-at::Tensor pack_rows(const at::Tensor& x, int64_t nwaves) {
-  // x [B, K] -> packed [RT][nwaves][2][NS][4 q][16 rr]
-  const int64_t B = x.size(0), K = x.size(1), RT = (B + 31) / 32;
-  const int64_t NS = K / nwaves / 4;
-  auto xp = at::zeros({RT * 32, K}, x.options());
-  xp.narrow(0, 0, B).copy_(x);
-  return xp.view({RT, 2, 16, nwaves, NS, 4}).permute({0, 3, 1, 4, 5, 2}).contiguous();
-}
-
+// Returns {hs, cs, acts, hpm, wt}: hpm[t] = keep_t * h_{t-1} (A operand of
+// the dW_h GEMM), wt = W_h^T packed for lstm_bwd.
 std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
                                  at::Tensor h0, at::Tensor w_h) {
   SA_CHECK(xw); SA_CHECK(done); SA_CHECK(c0); SA_CHECK(h0); SA_CHECK(w_h);
@@ -116,50 +106,71 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   auto hs = at::empty({T, B, H}, xw.options());
   auto cs = at::empty({T, B, H}, xw.options());
   auto acts = at::empty({T, B, H4}, xw.options());
-  // weight slices packed per workgroup: [H/4][H][4 units][4 gates]
-  auto w4 = w_h.view({H, 4, H / 4, 4}).permute({2, 0, 3, 1}).contiguous();
+  auto hpm = at::empty({T, B, H}, xw.options());
+  auto w4 = at::empty({H * H4}, xw.options());
+  auto wt = at::empty({H * H4}, xw.options());
   const int64_t RT = (B + 31) / 32;
-  auto hpk = at::zeros({2, RT * 32 * H}, xw.options());
-  hpk[0].copy_(pack_rows(h0.reshape({B, H}), 8).reshape(-1));
+  auto hpk = at::empty({2, RT * 32 * H}, xw.options());
   auto s = cur_stream();
+  sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
+                               wt.data_ptr<float>(), H, s);
   const uint8_t* dn = u8ptr(done);
   for (int t = 0; t < T; ++t) {
     const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
-    sa::lstm_fwd_step_launch(xw[t].data_ptr<float>(), hpk[t & 1].data_ptr<float>(),
+    const float* hp = t == 0 ? h0.data_ptr<float>() : hs[t - 1].data_ptr<float>();
+    sa::lstm_fwd_step_launch(xw[t].data_ptr<float>(),
+                             t == 0 ? nullptr : hpk[t & 1].data_ptr<float>(), hp,
                              cp, dn + t * B, w4.data_ptr<float>(),
                              hs[t].data_ptr<float>(), hpk[(t + 1) & 1].data_ptr<float>(),
                              cs[t].data_ptr<float>(), acts[t].data_ptr<float>(),
-                             B, H, s);
+                             hpm[t].data_ptr<float>(), B, H, s);
   }
-  return {hs, cs, acts};
+  return {hs, cs, acts, hpm, wt};
 }
 
-at::Tensor lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor w_h,
-                    at::Tensor acts, at::Tensor cs, at::Tensor c0) {
-  SA_CHECK(dh_out); SA_CHECK(done); SA_CHECK(w_h); SA_CHECK(acts);
+// Returns {dG [T,B,4H] f32, dc0 [B,H], dG bf16 (or an empty tensor)}.
+// wt: the packed W_h^T from lstm_fwd.  dc_last (optional) is the gradient
+// w.r.t. the final cell state (a later time chunk's dc0); dc0 is the gradient
+// w.r.t. the initial cell state (already masked by keep_0).
+std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor wt,
+                                 at::Tensor acts, at::Tensor cs, at::Tensor c0,
+                                 c10::optional<at::Tensor> dc_last, bool want_bf16) {
+  SA_CHECK(dh_out); SA_CHECK(done); SA_CHECK(wt); SA_CHECK(acts);
   SA_CHECK(cs); SA_CHECK(c0);
+  SA_CHECK_F32(dh_out);
   const int T = acts.size(0), B = acts.size(1), H4 = acts.size(2), H = H4 / 4;
+  TORCH_CHECK(wt.numel() == H * H4, "packed W_h^T size");
+  TORCH_CHECK(dh_out.numel() == T * B * H, "dh shape");
+  if (dc_last.has_value()) {
+    SA_CHECK(*dc_last); SA_CHECK_F32(*dc_last);
+    TORCH_CHECK(dc_last->numel() == c0.numel(), "dc_last shape");
+  }
   const c10::DeviceGuard guard(acts.device());
   auto dg = at::empty({T, B, H4}, acts.options());
-  auto carry = at::zeros({2, B, H}, acts.options());
+  at::Tensor dg16;
+  if (want_bf16) dg16 = at::empty({T, B, H4}, acts.options().dtype(at::kBFloat16));
+  // every step writes its carry / packed dG before the next one reads it
+  auto carry = at::empty({2, B, H}, acts.options());
   const int64_t RT = (B + 31) / 32;
-  auto dgpk = at::zeros({2, RT * 32 * H4}, acts.options());
-  // W_h^T packed: [H/16 blk][16 waves][NS][4 q][16 rr] = W_h[16 blk + rr][64 w + 4 s + q]
-  auto wt = w_h.view({H / 16, 16, 16, H4 / 64, 4}).permute({0, 2, 3, 4, 1}).contiguous();
+  auto dgpk = at::empty({2, RT * 32 * H4}, acts.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
   for (int t = T - 1; t >= 0; --t) {
     const float* dgn = t == T - 1 ? nullptr : dgpk[(t + 1) & 1].data_ptr<float>();
     const uint8_t* dnext = t == T - 1 ? nullptr : dn + (t + 1) * B;
     const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
-    const float* cin = t == T - 1 ? nullptr : carry[(t + 1) & 1].data_ptr<float>();
+    const float* cin = t == T - 1
+        ? (dc_last.has_value() ? dc_last->data_ptr<float>() : nullptr)
+        : carry[(t + 1) & 1].data_ptr<float>();
     sa::lstm_bwd_step_launch(dh_out[t].data_ptr<float>(), dgn, dnext, dn + t * B,
                              wt.data_ptr<float>(), acts[t].data_ptr<float>(),
                              cs[t].data_ptr<float>(), cp, cin,
                              carry[t & 1].data_ptr<float>(), dg[t].data_ptr<float>(),
-                             dgpk[t & 1].data_ptr<float>(), B, H, s);
+                             dgpk[t & 1].data_ptr<float>(),
+                             want_bf16 ? dg16[t].data_ptr() : nullptr, B, H, s);
   }
-  return dg;
+  if (!want_bf16) dg16 = at::empty({0}, acts.options());
+  return {dg, carry[0], dg16};
 }
 
 void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
@@ -168,7 +179,8 @@ void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
 
 }  // namespace
 
-void register_conv_ops(pybind11::module& m);  // conv_bindings.cpp
+void register_conv_ops(pybind11::module& m);     // conv_bindings.cpp
+void register_learner_ops(pybind11::module& m);  // learner_bindings.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "scalable_agent_amd gfx950 HIP kernels";
@@ -179,7 +191,11 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("guard") = pybind11::none());
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd);
-  m.def("lstm_bwd", &lstm_bwd);
+  m.def("lstm_bwd", &lstm_bwd, pybind11::arg("dh_out"), pybind11::arg("done"),
+        pybind11::arg("wt"), pybind11::arg("acts"), pybind11::arg("cs"),
+        pybind11::arg("c0"), pybind11::arg("dc_last") = pybind11::none(),
+        pybind11::arg("want_bf16") = false);
   m.def("noop", &noop);
   register_conv_ops(m);
+  register_learner_ops(m);
 }

@@ -37,21 +37,63 @@ void vtrace_loss_launch(const float* behaviour, const float* target,
 // One LSTMBlockCell step over all B rows with done-reset (gate order i,c,f,o,
 // forget bias +1).  xw_t [B,4H] = x_t W_x + b precomputed; w4 = W_h [H,4H]
 // packed as [H/4 blocks][H k][4 units][4 gates]; h_pk = h_{t-1} in the fwd
-// MFMA-operand order (see lstm.hip), written for the next step as h_pk_out.
+// MFMA-operand order (see lstm.hip), written for the next step as h_pk_out;
+// h_pk_in == nullptr reads h_prev [B,H] unpacked instead (first step).
+// hpm_t (optional) = keep_t * h_prev for the dW_h GEMM.
 void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
-                          const float* c_prev, const uint8_t* done_t,
-                          const float* w4, float* h_t, float* h_pk_out,
-                          float* c_t, float* acts_t, int B, int H,
-                          hipStream_t stream);
+                          const float* h_prev, const float* c_prev,
+                          const uint8_t* done_t, const float* w4, float* h_t,
+                          float* h_pk_out, float* c_t, float* acts_t,
+                          float* hpm_t, int B, int H, hipStream_t stream);
 // Reverse step t: consumes dG_{t+1} (packed, null at t=T-1), writes dG_t
-// (plain [B,4H] and packed).  wt = W_h^T packed [H/16][16][4H/64][64].
+// (plain [B,4H] fp32, packed, and optionally bf16 for the bf16 dX GEMMs).
+// wt = W_h^T packed [H/16][16][4H/64][64].
 void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const uint8_t* done_next, const uint8_t* done_t,
                           const float* wt, const float* acts_t,
                           const float* c_t, const float* c_prev,
                           const float* dcarry_in, float* dcarry_out,
-                          float* dg_t, float* dg_pk_out, int B, int H,
-                          hipStream_t stream);
+                          float* dg_t, float* dg_pk_out, void* dg16_t, int B,
+                          int H, hipStream_t stream);
+// W_h [H,4H] -> fwd-packed w4 and bwd-packed wt (one launch per unroll).
+void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
+                              hipStream_t stream);
+
+// ---- learner_io.hip --------------------------------------------------------
+// Fused heads + V-trace + loss (one workgroup per batch column; see the file
+// header).  core [T+1,B,256]; behaviour/actions/rewards/done point at row 1
+// of the [T+1,B,...] batch tensors; dlogits [T,B,A], dvalues [T,B];
+// partial [B*3] scratch; ticket: zero-initialised persistent counter.
+size_t learner_head_fwd_smem(int T, int A);
+void learner_head_fwd_launch(const float* core, const float* wp, const float* bp,
+                             const float* wb, const float* bb,
+                             const float* behaviour, const int64_t* actions,
+                             const float* rewards, const uint8_t* done, int T,
+                             int B, int A, float discounting, int clip_mode,
+                             float clip_rho, float clip_pg_rho,
+                             float baseline_cost, float entropy_cost,
+                             float* dlogits, float* dvalues, float* partial,
+                             unsigned* ticket, float* loss, hipStream_t stream);
+// dcore [N1,256] = g (dlogits Wp^T + dv Wb^T) (rows >= Ng zero); heads'
+// gradients accumulated (atomics) into gwp [256,A], gbp [A], gwb [256], gbb.
+void learner_head_bwd_launch(const float* gscale, const float* core,
+                             const float* dlogits, const float* dvalues,
+                             const float* wp, const float* wb, int N1, int Ng,
+                             int A, float* dcore, float* gwp, float* gbp,
+                             float* gwb, float* gbb, hipStream_t stream);
+// h_aug (bf16 [N, ld]) <- [h (bf16 [N, c0]), clip(r), one_hot(a), 0...]
+void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
+                         const int64_t* actions, int N, int ld, int c0,
+                         int clip_mode, hipStream_t stream);
+// out[c] += sum_r x[r,c], x fp32 [N,C]
+void colsum_f32_launch(const float* x, int N, int C, float* out,
+                       hipStream_t stream);
+// dy bf16 [N,C] *= (y > 0) (y bf16 with row stride ldy); out[c] += colsum
+void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
+                            float* out, hipStream_t stream);
+// dx bf16 *= (x > 0), n % 8 == 0
+void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,
+                           hipStream_t stream);
 
 // ---- calibration ----------------------------------------------------------
 void noop_launch(int blocks, int threads, int* p, hipStream_t s);

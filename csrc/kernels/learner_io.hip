@@ -1,0 +1,640 @@
+// Learner glue kernels around the LSTM core: they replace ~40 small PyTorch
+// launches per learner step (slices, concats, one-hots, bias adds, column
+// sums, ReLU masks, the policy/baseline heads and their gradients) with a
+// handful of fused launches.
+//
+//  * learner_head_fwd  policy + baseline heads (experiment.py:200-210) for all
+//                      T+1 steps, then V-trace + IMPALA loss + their analytic
+//                      gradients (vtrace.py:71-280, experiment.py:324-407):
+//                      ONE workgroup per batch column b (the V-trace scan runs
+//                      along time inside the workgroup), the four loss sums
+//                      finished by the last workgroup to arrive (ticket) in a
+//                      fixed order, so the loss is deterministic.
+//  * learner_head_bwd  dcore = g (dlogits W_p^T + dv W_b^T) and the heads'
+//                      weight/bias gradients (fp32 atomics into the learner's
+//                      flat gradient buffer), g = the incoming loss gradient.
+//  * core_aug_fwd      [clip(r), one_hot(a), 0...] columns next to the torso
+//                      output, so the core-input concat (experiment.py:185-198)
+//                      and the x W_x projection are ONE GEMM.
+//  * colsum_f32        column sums of an fp32 matrix accumulated into a vector
+//                      (LSTM bias gradient).
+//  * relu_bwd_colsum   dY *= (Y > 0) in place on bf16 + column sums (torso FC
+//                      ReLU + bias gradient).
+//  * relu_mask_bf16    dX *= (X > 0) in place (the torso's final ReLU).
+#include "launchers.h"
+
+#include <hip/hip_bf16.h>
+
+namespace sa {
+namespace {
+
+typedef unsigned short bf16_t;  // raw bf16 bits
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(static_cast<unsigned>(v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {  // round to nearest even
+  unsigned u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<bf16_t>(u >> 16);
+}
+
+__device__ __forceinline__ float clip_reward(float r, int mode) {
+  if (mode == 0) return fminf(fmaxf(r, -1.f), 1.f);       // abs_one
+  const float sq = tanhf(r / 5.0f);                         // soft_asymmetric
+  return (r < 0.f ? 0.3f * sq : sq) * 5.0f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Phase timestamps of block 0 for tools/micro/head_trace.hip (compiled out).
+#ifdef SA_HEAD_TRACE
+}  // namespace
+__device__ unsigned long long sa_head_trace[16];
+namespace {
+#define HEAD_TRACE(i) \
+  if (threadIdx.x == 0 && blockIdx.x == 0) sa_head_trace[i] = __builtin_amdgcn_s_memtime()
+#else
+#define HEAD_TRACE(i)
+#endif
+
+constexpr int kHeadThreads = 1024;
+constexpr int kHeadWaves = kHeadThreads / 64;
+constexpr int kMaxA = 31;      // A + 1 head outputs <= 32
+
+// ------------------------------------------------------------ heads + V-trace
+// core [T1,B,H] (H == 256), Wp [H,A], Wb [H] (one value head).  The V-trace
+// inputs are the learner's time-shifted views (compute_loss): target logits
+// / values = heads at t < T, bootstrap = value at T, behaviour logits,
+// actions, rewards, done = rows 1..T of the batch (the caller passes
+// pointers to row 1).  Every global operand of the column is fetched in the
+// prologue with all loads in flight (one memory round trip), then the
+// phases run out of LDS.  The heads are fp32 MFMA (16x16x4): wave w owns
+// rows [16w, 16w+16) of the column, lane l sums k in [64(l>>4), +64), so its
+// A operand is 64 contiguous floats of one core row.  LDS (dynamic, 4-byte
+// words): W [H][MAXC] (zero-padded) | logits/values [T1][A+1] | behaviour
+// [T][A] | a_t, delta_t, pgrho_t [T] | vs_t [T+1] | reward [T] | action [T]
+// | done [T].
+template <int MAXC>
+__global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
+    const float* __restrict__ core, const float* __restrict__ wp,
+    const float* __restrict__ bp, const float* __restrict__ wb,
+    const float* __restrict__ bb, const float* __restrict__ behaviour,
+    const int64_t* __restrict__ actions, const float* __restrict__ rewards,
+    const uint8_t* __restrict__ done, int T, int B, int A, float discounting,
+    int clip_mode, float clip_rho, float clip_pg_rho, float baseline_cost,
+    float entropy_cost, float* __restrict__ dlogits, float* __restrict__ dvalues,
+    float* __restrict__ partial, unsigned* __restrict__ ticket,
+    float* __restrict__ loss) {
+  constexpr int H = 256;
+  extern __shared__ float smem[];
+  const int A1 = A + 1;
+  const int T1 = T + 1;
+  float* w_s = smem;                 // [H][MAXC] + 4 x 16 pad
+  float* lv_s = w_s + H * MAXC + 64; // [T1][A1]: logits then value
+  float* beh_s = lv_s + T1 * A1;     // [T][A]
+  float* a_s = beh_s + T * A;        // gamma_t c_t
+  float* d_s = a_s + T;              // delta_t
+  float* p_s = d_s + T;              // clipped pg rho
+  float* vs_s = p_s + T;             // vs_t, vs_s[T] = bootstrap
+  float* r_s = vs_s + T + 1;         // clipped reward
+  int* act_s = reinterpret_cast<int*>(r_s + T);
+  float* disc_s = reinterpret_cast<float*>(act_s + T);
+  __shared__ float scan_a[kHeadThreads], scan_b[kHeadThreads];
+  __shared__ float red[3][kHeadWaves];
+  __shared__ bool last_s;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  HEAD_TRACE(0);
+  // ---- prologue: every load of the column issued before any is consumed
+  constexpr int NCT = MAXC / 16;  // 16-wide output column tiles
+  const int ntiles = (T1 + 15) / 16;
+  const int arow = lane & 15, kq = lane >> 4;
+  float4 xa[16];  // A operand: core[16 tile + arow][64 kq + 4j .. +3]
+  auto load_a = [&](int tile) {
+    const int t = 16 * tile + arow;
+    const float4* src = reinterpret_cast<const float4*>(
+        core + (static_cast<int64_t>(t < T1 ? t : 0) * B + b) * H + 64 * kq);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) xa[j] = t < T1 ? src[j] : float4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (wave < ntiles) load_a(wave);
+  float bias[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int c = 16 * ct + arow;
+    bias[ct] = c < A ? bp[c] : (c == A ? bb[0] : 0.f);
+  }
+  // (register-staged: every load below is issued before the first LDS store)
+  constexpr int WPT = H * MAXC / kHeadThreads;
+  float wv[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int i = tid + j * kHeadThreads;
+    const int k = i / MAXC, c = i - k * MAXC;
+    wv[j] = c < A ? wp[k * A + c] : (c == A ? wb[k] : 0.f);
+  }
+  constexpr int BPT = 2;  // behaviour logits per thread staged in registers
+  float bv[BPT];
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * kHeadThreads;
+    const int t = i / A, jj = i - t * A;
+    bv[j] = i < T * A ? behaviour[(static_cast<int64_t>(t) * B + b) * A + jj] : 0.f;
+  }
+  float rv = 0.f, dn = 0.f;
+  int av = 0;
+  if (tid < T) {
+    const int64_t idx = static_cast<int64_t>(tid) * B + b;  // row t+1 of batch
+    rv = rewards[idx];
+    av = static_cast<int>(actions[idx]);
+    dn = done[idx] ? 0.f : discounting;
+  }
+  // W (k, c) at k MAXC + 16 (k / 64) + c: the 4 k-quarters of a wave's B
+  // operand reads land 16 banks apart
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int i = tid + j * kHeadThreads;
+    w_s[i + 16 * ((i / MAXC) >> 6)] = wv[j];
+  }
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int i = tid + j * kHeadThreads;
+    if (i < T * A) beh_s[i] = bv[j];
+  }
+  for (int i = tid + BPT * kHeadThreads; i < T * A; i += kHeadThreads) {
+    const int t = i / A, jj = i - t * A;  // long unrolls only
+    beh_s[i] = behaviour[(static_cast<int64_t>(t) * B + b) * A + jj];
+  }
+  if (tid < T) {
+    r_s[tid] = clip_reward(rv, clip_mode);
+    act_s[tid] = av;
+    disc_s[tid] = dn;
+  }
+  for (int t = tid + kHeadThreads; t < T; t += kHeadThreads) {
+    const int64_t idx = static_cast<int64_t>(t) * B + b;
+    r_s[t] = clip_reward(rewards[idx], clip_mode);
+    act_s[t] = static_cast<int>(actions[idx]);
+    disc_s[t] = done[idx] ? 0.f : discounting;
+  }
+  __syncthreads();
+  HEAD_TRACE(1);
+
+  // ---- heads: [16 rows x 256] x [256 x 16 cols] per wave on fp32 MFMA
+  for (int tile = wave; tile < ntiles; tile += kHeadWaves) {
+    if (tile != wave) load_a(tile);
+    f4v acc[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4v{0.f, 0.f, 0.f, 0.f};
+    const float* wk = w_s + (64 * kq) * MAXC + 16 * kq + arow;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float av[4] = {xa[j].x, xa[j].y, xa[j].z, xa[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              av[q], wk[(4 * j + q) * MAXC + 16 * ct], acc[ct], 0, 0, 0);
+      }
+    }
+    // D[row 4 kq + i][col arow]
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int c = 16 * ct + arow;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = 16 * tile + 4 * kq + i;
+        if (t < T1 && c < A1) lv_s[t * A1 + c] = acc[ct][i] + bias[ct];
+      }
+    }
+  }
+  __syncthreads();
+  HEAD_TRACE(2);
+
+  // ---- V-trace elementwise (vtrace.py:143-147, 235-262)
+  for (int t = tid; t < T; t += kHeadThreads) {
+    const float* zt = lv_s + t * A1;
+    const float* zb = beh_s + t * A;
+    const int a = act_s[t];
+    float mt = -INFINITY, mb = -INFINITY;
+    for (int j = 0; j < A; ++j) {
+      mt = fmaxf(mt, zt[j]);
+      mb = fmaxf(mb, zb[j]);
+    }
+    float st = 0.f, sb = 0.f;
+    for (int j = 0; j < A; ++j) {
+      st += __expf(zt[j] - mt);
+      sb += __expf(zb[j] - mb);
+    }
+    const float log_pi = zt[a] - mt - __logf(st);
+    const float log_mu = zb[a] - mb - __logf(sb);
+    const float rho = __expf(log_pi - log_mu);
+    const float disc = disc_s[t];
+    const float v = zt[A];
+    const float v1 = lv_s[(t + 1) * A1 + A];
+    a_s[t] = disc * fminf(1.0f, rho);
+    d_s[t] = fminf(clip_rho, rho) * (r_s[t] + disc * v1 - v);
+    p_s[t] = fminf(clip_pg_rho, rho);
+  }
+  __syncthreads();
+  HEAD_TRACE(3);
+
+  // ---- reverse recursion acc_t = delta_t + a_t acc_{t+1}: each thread
+  // composes a chunk of C steps, then a workgroup suffix scan of the maps
+  const int C = (T + kHeadThreads - 1) / kHeadThreads;
+  const int t0 = tid * C;
+  const int t1 = min(t0 + C, T);
+  float ca = 1.f, cb = 0.f;  // acc_{t0} = cb + ca * acc_{t1}
+  for (int t = t1 - 1; t >= t0; --t) {
+    cb = d_s[t] + a_s[t] * cb;
+    ca = a_s[t] * ca;
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {  // wave-level inclusive suffix
+    const float na = __shfl_down(ca, d, 64);
+    const float nb = __shfl_down(cb, d, 64);
+    if (lane + d < 64) {
+      cb = cb + ca * nb;
+      ca = ca * na;
+    }
+  }
+  scan_a[tid] = ca;
+  scan_b[tid] = cb;
+  __syncthreads();
+  HEAD_TRACE(4);
+  // acc entering this thread's chunk from the right: the later waves'
+  // totals, then the next lane's inclusive suffix in this wave
+  float acc = 0.f;
+  for (int w = kHeadWaves - 1; w > wave; --w) acc = scan_b[w * 64] + scan_a[w * 64] * acc;
+  if (lane < 63) acc = scan_b[tid + 1] + scan_a[tid + 1] * acc;
+  for (int t = t1 - 1; t >= t0; --t) {
+    acc = d_s[t] + a_s[t] * acc;
+    vs_s[t] = acc + lv_s[t * A1 + A];
+  }
+  if (tid == 0) vs_s[T] = lv_s[T * A1 + A];  // bootstrap
+  __syncthreads();
+  HEAD_TRACE(5);
+
+  // ---- advantages, loss terms and their gradients
+  float l_pg = 0.f, l_bl = 0.f, l_ent = 0.f;
+  for (int t = tid; t < T; t += kHeadThreads) {
+    const int64_t idx = static_cast<int64_t>(t) * B + b;
+    const float* zt = lv_s + t * A1;
+    float* dz = dlogits + idx * A;
+    const int a = act_s[t];
+    const float v = zt[A];
+    const float vs = vs_s[t];
+    const float pg_adv = p_s[t] * (r_s[t] + disc_s[t] * vs_s[t + 1] - v);
+    float m = -INFINITY;
+    for (int j = 0; j < A; ++j) m = fmaxf(m, zt[j]);
+    float s = 0.f;
+    for (int j = 0; j < A; ++j) s += __expf(zt[j] - m);
+    const float lse = m + __logf(s);
+    float Hn = 0.f;
+    for (int j = 0; j < A; ++j) {
+      const float lp = zt[j] - lse;
+      Hn -= __expf(lp) * lp;
+    }
+    for (int j = 0; j < A; ++j) {
+      const float lp = zt[j] - lse;
+      const float p = __expf(lp);
+      dz[j] = (p - (j == a ? 1.f : 0.f)) * pg_adv + entropy_cost * p * (lp + Hn);
+    }
+    dvalues[idx] = -baseline_cost * (vs - v);
+    l_pg += (lse - zt[a]) * pg_adv;
+    l_bl += 0.5f * (vs - v) * (vs - v);
+    l_ent -= Hn;
+  }
+  l_pg = wave_sum(l_pg);
+  l_bl = wave_sum(l_bl);
+  l_ent = wave_sum(l_ent);
+  if (lane == 0) {
+    red[0][wave] = l_pg;
+    red[1][wave] = l_bl;
+    red[2][wave] = l_ent;
+  }
+  __syncthreads();
+  HEAD_TRACE(6);
+  if (tid == 0) {
+    float pg = 0.f, bl = 0.f, en = 0.f;
+    for (int w = 0; w < kHeadWaves; ++w) {
+      pg += red[0][w];
+      bl += red[1][w];
+      en += red[2][w];
+    }
+    // publish the partials write-through (sc1), wait for them, then take a
+    // ticket; the last block reads them with sc1 loads after its add
+    // returned - no L2 write-back / invalidate fences (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, the one-lane sc1 hand-off)
+    __hip_atomic_store(partial + b * 3 + 0, pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partial + b * 3 + 1, bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partial + b * 3 + 2, en, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    last_s = (prev == static_cast<unsigned>(gridDim.x) - 1);
+  }
+  __syncthreads();
+  HEAD_TRACE(7);
+  if (last_s && tid == 0) {
+    float pg = 0.f, bl = 0.f, en = 0.f;
+    for (int j = 0; j < B; ++j) {  // fixed order: deterministic
+      pg += __hip_atomic_load(partial + j * 3 + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bl += __hip_atomic_load(partial + j * 3 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      en += __hip_atomic_load(partial + j * 3 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    loss[1] = pg;
+    loss[2] = bl;
+    loss[3] = en;
+    loss[0] = pg + baseline_cost * bl + entropy_cost * en;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  HEAD_TRACE(8);
+}
+
+// dcore [N1, H] = g (dlogits W_p^T + dv W_b^T) (rows >= Ng get zero), and
+// g core^T [dlogits | dv] and its column sums accumulated into the heads'
+// fp32 gradients.  Block = 16 hidden units x a chunk of kBwdRows rows
+// (thread = (unit kk, row lane rl), kBwdRows / 16 rows per thread, all core
+// and dlogits loads of the chunk in flight at once); the 16 row lanes are
+// reduced in registers/LDS, then ONE atomic per (unit, output) per block.
+constexpr int kBwdRows = 256;
+constexpr int kBwdRowsPerThread = kBwdRows / 16;
+
+template <int MAXC>
+__global__ __launch_bounds__(256) void learner_head_bwd_kernel(
+    const float* __restrict__ gscale, const float* __restrict__ core,
+    const float* __restrict__ dlogits, const float* __restrict__ dvalues,
+    const float* __restrict__ wp, const float* __restrict__ wb, int N1, int Ng,
+    int A, float* __restrict__ dcore, float* __restrict__ gwp,
+    float* __restrict__ gbp, float* __restrict__ gwb, float* __restrict__ gbb) {
+  constexpr int H = 256;
+  __shared__ float dl_s[kBwdRows][MAXC];
+  __shared__ float red_s[4][16][MAXC];
+  const int tid = threadIdx.x;
+  const int kk = tid & 15, rl = tid >> 4;
+  const int k = blockIdx.x * 16 + kk;
+  const int r0 = blockIdx.y * kBwdRows;
+  const int rows = min(kBwdRows, N1 - r0);
+  const int A1 = A + 1;
+  // prologue: this thread's core values, the chunk's dlogits, the weights
+  float x[kBwdRowsPerThread];
+#pragma unroll
+  for (int i = 0; i < kBwdRowsPerThread; ++i) {
+    const int rr = rl + 16 * i;
+    x[i] = rr < rows ? core[static_cast<int64_t>(r0 + rr) * H + k] : 0.f;
+  }
+  const float g = gscale ? *gscale : 1.f;
+  // dlogits/dv of the chunk: MAXC values per thread, all loads in flight
+  float dv_r[MAXC];
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int i = tid + 256 * j;
+    const int rr = i / MAXC, c = i - rr * MAXC;
+    const int r = r0 + rr;
+    float v = 0.f;
+    if (rr < rows && r < Ng && c < A1)
+      v = c < A ? dlogits[static_cast<int64_t>(r) * A + c] : dvalues[r];
+    dv_r[j] = v;
+  }
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int i = tid + 256 * j;
+    dl_s[i / MAXC][i % MAXC] = dv_r[j];
+  }
+  float w[MAXC], acc[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    w[c] = c < A ? wp[k * A + c] : (c == A ? wb[k] : 0.f);
+    acc[c] = 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kBwdRowsPerThread; ++i) {
+    const int rr = rl + 16 * i;
+    if (rr < rows) {
+      float d = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < A1) {
+          const float dc = dl_s[rr][c];
+          d += dc * w[c];
+          acc[c] += x[i] * dc;
+        }
+      }
+      dcore[static_cast<int64_t>(r0 + rr) * H + k] = g * d;
+    }
+  }
+  // reduce the 16 row lanes: lanes kk, kk+16, kk+32, kk+48 of a wave share
+  // a unit; then the 4 waves through LDS
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c < A1) {
+      float v = acc[c];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) red_s[wave][lane][c] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 16 * A1; i += 256) {
+    const int u = i / A1, c = i - u * A1;
+    const float v = g * (red_s[0][u][c] + red_s[1][u][c] + red_s[2][u][c] +
+                         red_s[3][u][c]);
+    const int ku = blockIdx.x * 16 + u;
+    atomicAdd(c < A ? gwp + ku * A + c : gwb + ku, v);
+  }
+  if (blockIdx.x == 0 && tid >= 256 - A1) {  // bias grads: column sums
+    const int c = tid - (256 - A1);
+    float s = 0.f;
+    for (int rr = 0; rr < rows; ++rr) s += dl_s[rr][c];
+    atomicAdd(c < A ? gbp + c : gbb, g * s);
+  }
+}
+
+// -------------------------------------------------------------- core input
+// h_aug [N, ld] bf16 <- [h (c0 columns), clip(r), one_hot(a), 0...]: the
+// core input row without the (empty) instruction encoding.
+__global__ __launch_bounds__(256) void core_aug_fwd_kernel(
+    bf16_t* __restrict__ h_aug, const bf16_t* __restrict__ h,
+    const float* __restrict__ rewards, const int64_t* __restrict__ actions,
+    int N, int ld, int c0, int clip_mode) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= static_cast<int64_t>(N) * ld) return;
+  const int n = static_cast<int>(i / ld);
+  const int j = static_cast<int>(i - static_cast<int64_t>(n) * ld);
+  bf16_t out;
+  if (j < c0) {
+    out = h[static_cast<int64_t>(n) * c0 + j];
+  } else {
+    float v = 0.f;
+    if (j == c0) v = clip_reward(rewards[n], clip_mode);
+    else if (j - c0 - 1 == static_cast<int>(actions[n])) v = 1.f;
+    out = f2bf(v);
+  }
+  h_aug[i] = out;
+}
+
+// out[c] += sum_r x[r, c] over an fp32 [N, C] matrix.  Block: 256 columns x
+// kColRows rows, loads batched 16 deep; one atomic per column per block.
+constexpr int kColRows = 64;
+constexpr int kColBatch = 16;
+
+__global__ __launch_bounds__(256) void colsum_f32_kernel(
+    const float* __restrict__ x, int N, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r0 = blockIdx.y * kColRows;
+  const int r1 = min(r0 + kColRows, N);
+  if (c >= C) return;
+  float s = 0.f;
+  for (int base = r0; base < r1; base += kColBatch) {
+    float v[kColBatch];
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j)
+      v[j] = base + j < r1 ? x[static_cast<int64_t>(base + j) * C + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j) s += v[j];
+  }
+  atomicAdd(out + c, s);
+}
+
+// dy [N, C] bf16 *= (y > 0); out[c] += sum_r dy[r, c] (after masking)
+__global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
+    bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int N, int C,
+    int ldy, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int r0 = blockIdx.y * kColRows;
+  const int r1 = min(r0 + kColRows, N);
+  if (c >= C) return;
+  float s = 0.f;
+  for (int base = r0; base < r1; base += kColBatch) {
+    bf16_t dv[kColBatch], yv[kColBatch];
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j) {
+      const bool in = base + j < r1;
+      dv[j] = in ? dy[static_cast<int64_t>(base + j) * C + c] : bf16_t(0);
+      yv[j] = in ? y[static_cast<int64_t>(base + j) * ldy + c] : bf16_t(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j) {
+      const bool on = bf2f(yv[j]) > 0.f;
+      if (base + j < r1) {
+        if (on) s += bf2f(dv[j]);
+        else dy[static_cast<int64_t>(base + j) * C + c] = 0;
+      }
+    }
+  }
+  if (out) atomicAdd(out + c, s);
+}
+
+// dx *= (x > 0), 8 bf16 per thread
+__global__ __launch_bounds__(256) void relu_mask_bf16_kernel(
+    uint4* __restrict__ dx, const uint4* __restrict__ x, int64_t n8) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  uint4 d = dx[i];
+  const uint4 v = x[i];
+  unsigned* dp = reinterpret_cast<unsigned*>(&d);
+  const unsigned* vp = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    // bf16 > 0  <=>  sign bit clear and not (+)0
+    const unsigned lo = vp[j] & 0xffffu, hi = vp[j] >> 16;
+    const unsigned mlo = (lo != 0u && !(lo & 0x8000u)) ? 0xffffu : 0u;
+    const unsigned mhi = (hi != 0u && !(hi & 0x8000u)) ? 0xffff0000u : 0u;
+    dp[j] &= (mlo | mhi);
+  }
+  dx[i] = d;
+}
+
+}  // namespace
+
+size_t learner_head_fwd_smem(int T, int A) {
+  const int maxc = (A + 1 <= 16) ? 16 : 32;
+  return sizeof(float) * (256 * maxc + 64 + (T + 1) * (A + 1) + T * A + 4 * T +
+                          1 + 3 * T);
+}
+
+void learner_head_fwd_launch(const float* core, const float* wp, const float* bp,
+                             const float* wb, const float* bb,
+                             const float* behaviour, const int64_t* actions,
+                             const float* rewards, const uint8_t* done, int T,
+                             int B, int A, float discounting, int clip_mode,
+                             float clip_rho, float clip_pg_rho,
+                             float baseline_cost, float entropy_cost,
+                             float* dlogits, float* dvalues, float* partial,
+                             unsigned* ticket, float* loss, hipStream_t stream) {
+  const size_t smem = learner_head_fwd_smem(T, A);
+  auto k16 = learner_head_fwd_kernel<16>;
+  auto k32 = learner_head_fwd_kernel<kMaxA + 1>;
+  auto kern = (A + 1 <= 16) ? k16 : k32;
+  if (smem > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(smem));
+  hipLaunchKernelGGL(kern, dim3(B), dim3(kHeadThreads), smem, stream, core, wp,
+                     bp, wb, bb, behaviour, actions, rewards, done, T, B, A,
+                     discounting, clip_mode, clip_rho, clip_pg_rho,
+                     baseline_cost, entropy_cost, dlogits, dvalues, partial,
+                     ticket, loss);
+}
+
+void learner_head_bwd_launch(const float* gscale, const float* core,
+                             const float* dlogits, const float* dvalues,
+                             const float* wp, const float* wb, int N1, int Ng,
+                             int A, float* dcore, float* gwp, float* gbp,
+                             float* gwb, float* gbb, hipStream_t stream) {
+  const dim3 grid(256 / 16, (N1 + kBwdRows - 1) / kBwdRows);
+  if (A + 1 <= 16)
+    hipLaunchKernelGGL(learner_head_bwd_kernel<16>, grid, dim3(256), 0, stream,
+                       gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, dcore,
+                       gwp, gbp, gwb, gbb);
+  else
+    hipLaunchKernelGGL(learner_head_bwd_kernel<kMaxA + 1>, grid, dim3(256), 0,
+                       stream, gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A,
+                       dcore, gwp, gbp, gwb, gbb);
+}
+
+void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
+                         const int64_t* actions, int N, int ld, int c0,
+                         int clip_mode, hipStream_t stream) {
+  const int64_t n = static_cast<int64_t>(N) * ld;
+  hipLaunchKernelGGL(core_aug_fwd_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     stream, static_cast<bf16_t*>(h_aug),
+                     static_cast<const bf16_t*>(h), rewards, actions, N, ld, c0,
+                     clip_mode);
+}
+
+void colsum_f32_launch(const float* x, int N, int C, float* out,
+                       hipStream_t stream) {
+  dim3 grid((C + 255) / 256, (N + kColRows - 1) / kColRows);
+  hipLaunchKernelGGL(colsum_f32_kernel, grid, dim3(256), 0, stream, x, N, C, out);
+}
+
+void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
+                            float* out, hipStream_t stream) {
+  dim3 grid((C + 255) / 256, (N + kColRows - 1) / kColRows);
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, stream,
+                     static_cast<bf16_t*>(dy), static_cast<const bf16_t*>(y), N,
+                     C, ldy, out);
+}
+
+void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,
+                           hipStream_t stream) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3((n8 + 255) / 256), dim3(256), 0,
+                     stream, static_cast<uint4*>(dx), static_cast<const uint4*>(x),
+                     n8);
+}
+
+}  // namespace sa

@@ -21,6 +21,8 @@
 // across the waves of the workgroup and reduced once through LDS.
 #include "launchers.h"
 
+#include <hip/hip_bf16.h>
+
 namespace sa {
 namespace {
 
@@ -37,13 +39,17 @@ __device__ __forceinline__ f4v mfma_f32(float a, float b, f4v c) {
 // h_pk_in / h_pk_out: h in MFMA-operand order, [row tile][wave][mt][s][lane]
 // with lane l <-> (row 16 mt + (l&15), k = KW w + 4 s + (l>>4)): every operand
 // load is one contiguous 256-B wave access.
+// h_pk_in == nullptr (the first step) reads the A operand straight from the
+// unpacked h_prev [B,H] (no host-side packing pass).  hpm_t (optional) gets
+// keep_t * h_prev, the A operand of the dW_h = sum_t hpm_t^T dG_t GEMM.
 template <int H>
 __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     const float* __restrict__ xw_t, const float* __restrict__ h_pk_in,
-    const float* __restrict__ c_prev, const uint8_t* __restrict__ done_t,
-    const float* __restrict__ w4, float* __restrict__ h_t,
-    float* __restrict__ h_pk_out, float* __restrict__ c_t,
-    float* __restrict__ acts_t, int B) {
+    const float* __restrict__ h_prev, const float* __restrict__ c_prev,
+    const uint8_t* __restrict__ done_t, const float* __restrict__ w4,
+    float* __restrict__ h_t, float* __restrict__ h_pk_out,
+    float* __restrict__ c_t, float* __restrict__ acts_t,
+    float* __restrict__ hpm_t, int B) {
   constexpr int NW = 8;
   constexpr int KW = H / NW;     // k per wave
   constexpr int NS = KW / 4;     // mfma k-steps per wave
@@ -58,7 +64,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   const int er = tid >> 2, eu = tid & 3;
   const int egr = r0 + er;
   const int ej = blk * 4 + eu;
-  float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, ekeep = 0.f;
+  float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, hp = 0.f, ekeep = 0.f;
   if (tid < 128 && egr < B) {
     const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
     xi = xw_t[g0];
@@ -66,6 +72,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     xf = xw_t[g0 + 2 * H];
     xo = xw_t[g0 + 3 * H];
     cp = c_prev[static_cast<int64_t>(egr) * H + ej];
+    if (hpm_t) hp = h_prev[static_cast<int64_t>(egr) * H + ej];
     ekeep = done_t[egr] ? 0.f : 1.f;
   }
   // B operand: W[k = kw0 + 4s + (l>>4)][n = l&15]
@@ -76,14 +83,25 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 4 * 16];
   // A operand: h[row = r0 + 16 mt + (l&15)][k = kw0 + 4s + (l>>4)] * keep
   float ha[2][NS];
-  const float* pk = h_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * H +
-                    wave * 2 * NS * 64 + lane;
+  if (h_pk_in != nullptr) {
+    const float* pk = h_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * H +
+                      wave * 2 * NS * 64 + lane;
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int row = r0 + 16 * mt + (lane & 15);
-    const float kf = (row < B && !done_t[row < B ? row : 0]) ? 1.f : 0.f;
+    for (int mt = 0; mt < 2; ++mt) {
+      const int row = r0 + 16 * mt + (lane & 15);
+      const float kf = (row < B && !done_t[row < B ? row : 0]) ? 1.f : 0.f;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) ha[mt][s] = pk[(mt * NS + s) * 64] * kf;
+      for (int s = 0; s < NS; ++s) ha[mt][s] = pk[(mt * NS + s) * 64] * kf;
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int row = r0 + 16 * mt + (lane & 15);
+      const bool ok = row < B && !done_t[row < B ? row : 0];
+      const float* hr = h_prev + static_cast<int64_t>(ok ? row : 0) * H + kw0 + (lane >> 4);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) ha[mt][s] = ok ? hr[4 * s] : 0.f;
+    }
   }
   f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -127,6 +145,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     acts_t[g0 + H] = g;
     acts_t[g0 + 2 * H] = f;
     acts_t[g0 + 3 * H] = o;
+    if (hpm_t) hpm_t[hj] = ekeep * hp;
   }
 }
 
@@ -142,7 +161,8 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     const float* __restrict__ wt, const float* __restrict__ acts_t,
     const float* __restrict__ c_t, const float* __restrict__ c_prev,
     const float* __restrict__ dcarry_in, float* __restrict__ dcarry_out,
-    float* __restrict__ dg_t, float* __restrict__ dg_pk_out, int B) {
+    float* __restrict__ dg_t, float* __restrict__ dg_pk_out,
+    __hip_bfloat16* __restrict__ dg16_t, int B) {
   const float* dg_next = dg_pk_in;
   constexpr int NW = 16;
   constexpr int NWID = 4 * H / NW;  // n per wave
@@ -224,6 +244,7 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       dg_t[g0 + g * H] = dgv[g];
+      if (dg16_t) dg16_t[g0 + g * H] = __float2bfloat16(dgv[g]);
       const int n = g * H + ej;
       const int w = n / NWID, s2 = (n % NWID) >> 2, q = n & 3;
       pko[((w * 2 + (rr >> 4)) * NS + s2) * 64 + (q << 4) + (rr & 15)] = dgv[g];
@@ -232,22 +253,50 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
   }
 }
 
+// W_h [H,4H] -> w4 (fwd B operand, [H/4][H][4 units][4 gates]) and wt (bwd
+// B operand, W_h^T [H/16][16 waves][4H/64][4][16]) in one pass.
+template <int H>
+__global__ __launch_bounds__(256) void lstm_pack_weights_kernel(
+    const float* __restrict__ w, float* __restrict__ w4, float* __restrict__ wt) {
+  constexpr int H4 = 4 * H;
+  constexpr int NWID = H4 / 16;  // bwd n per wave
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= H * H4) return;
+  const int k = idx / H4, n = idx - k * H4;
+  const float v = w[idx];
+  const int g = n / H, u = n - g * H;
+  w4[((static_cast<int64_t>(u >> 2) * H + k) * 4 + (u & 3)) * 4 + g] = v;
+  const int wv = n / NWID, r = n - wv * NWID, s2 = r >> 2, q = r & 3;
+  wt[(((static_cast<int64_t>(k >> 4) * 16 + wv) * (NWID / 4) + s2) * 4 + q) * 16 + (k & 15)] = v;
+}
+
 }  // namespace
 
+void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
+                              hipStream_t stream) {
+  const int n = H * 4 * H;
+  if (H == 256)
+    hipLaunchKernelGGL(lstm_pack_weights_kernel<256>, dim3((n + 255) / 256), dim3(256), 0,
+                       stream, w, w4, wt);
+  else if (H == 64)
+    hipLaunchKernelGGL(lstm_pack_weights_kernel<64>, dim3((n + 255) / 256), dim3(256), 0,
+                       stream, w, w4, wt);
+}
+
 void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
-                          const float* c_prev, const uint8_t* done_t,
-                          const float* w4, float* h_t, float* h_pk_out,
-                          float* c_t, float* acts_t, int B, int H,
-                          hipStream_t stream) {
+                          const float* h_prev, const float* c_prev,
+                          const uint8_t* done_t, const float* w4, float* h_t,
+                          float* h_pk_out, float* c_t, float* acts_t,
+                          float* hpm_t, int B, int H, hipStream_t stream) {
   dim3 grid(H / 4, (B + 31) / 32);
   if (H == 256) {
     hipLaunchKernelGGL(lstm_fwd_step_kernel<256>, grid, dim3(512), 0, stream,
-                       xw_t, h_pk_in, c_prev, done_t, w4, h_t, h_pk_out, c_t,
-                       acts_t, B);
+                       xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
+                       c_t, acts_t, hpm_t, B);
   } else if (H == 64) {
     hipLaunchKernelGGL(lstm_fwd_step_kernel<64>, grid, dim3(512), 0, stream,
-                       xw_t, h_pk_in, c_prev, done_t, w4, h_t, h_pk_out, c_t,
-                       acts_t, B);
+                       xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
+                       c_t, acts_t, hpm_t, B);
   }
 }
 
@@ -256,17 +305,18 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const float* wt, const float* acts_t,
                           const float* c_t, const float* c_prev,
                           const float* dcarry_in, float* dcarry_out,
-                          float* dg_t, float* dg_pk_out, int B, int H,
-                          hipStream_t stream) {
+                          float* dg_t, float* dg_pk_out, void* dg16_t, int B,
+                          int H, hipStream_t stream) {
   dim3 grid(H / 16, (B + 31) / 32);
+  __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
   if (H == 256) {
     hipLaunchKernelGGL(lstm_bwd_step_kernel<256>, grid, dim3(1024), 0, stream,
                        dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
-                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, B);
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B);
   } else if (H == 64) {
     hipLaunchKernelGGL(lstm_bwd_step_kernel<64>, grid, dim3(1024), 0, stream,
                        dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
-                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, B);
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B);
   }
 }
 

@@ -1,0 +1,156 @@
+// Torch bindings for the learner glue kernels (csrc/kernels/learner_io.hip).
+// Host-side shape/dtype checks; outputs come from the caching allocator and
+// everything launches on the current stream (hipGraph-capturable).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define LB_CHECK(t) TORCH_CHECK((t).is_cuda() && (t).is_contiguous(), #t " must be a contiguous GPU tensor")
+#define LB_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define LB_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+
+const uint8_t* mask_ptr(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBool || t.scalar_type() == at::kByte,
+              "done must be bool/uint8");
+  return reinterpret_cast<const uint8_t*>(t.data_ptr());
+}
+
+// core [T1,B,256]; behaviour [T1,B,A]; actions/rewards/done [T1,B] (full
+// batch tensors: the kernel reads rows 1..T).  ticket: persistent int32[1],
+// zero between launches.  -> {loss[4], dlogits [T,B,A], dvalues [T,B]}
+std::vector<at::Tensor> learner_head_fwd(
+    at::Tensor core, at::Tensor wp, at::Tensor bp, at::Tensor wb, at::Tensor bb,
+    at::Tensor behaviour, at::Tensor actions, at::Tensor rewards, at::Tensor done,
+    at::Tensor ticket, double discounting, int64_t clip_mode, double clip_rho,
+    double clip_pg_rho, double baseline_cost, double entropy_cost) {
+  LB_CHECK(core); LB_CHECK(wp); LB_CHECK(bp); LB_CHECK(wb); LB_CHECK(bb);
+  LB_CHECK(behaviour); LB_CHECK(actions); LB_CHECK(rewards); LB_CHECK(done);
+  LB_CHECK(ticket);
+  LB_F32(core); LB_F32(wp); LB_F32(bp); LB_F32(wb); LB_F32(bb);
+  LB_F32(behaviour); LB_F32(rewards);
+  TORCH_CHECK(actions.scalar_type() == at::kLong, "actions must be int64");
+  TORCH_CHECK(ticket.scalar_type() == at::kInt && ticket.numel() >= 1, "ticket");
+  TORCH_CHECK(core.dim() == 3 && core.size(2) == 256, "core must be [T+1,B,256]");
+  const int T1 = core.size(0), B = core.size(1), T = T1 - 1;
+  const int A = wp.size(1);
+  TORCH_CHECK(T >= 1, "need T >= 1");
+  TORCH_CHECK(wp.dim() == 2 && wp.size(0) == 256, "policy w must be [256,A]");
+  TORCH_CHECK(A >= 1 && A + 1 <= 32, "1 <= num_actions <= 31");
+  TORCH_CHECK(bp.numel() == A && wb.numel() == 256 && bb.numel() == 1,
+              "one value head");
+  TORCH_CHECK(behaviour.numel() == (int64_t)T1 * B * A, "behaviour logits shape");
+  TORCH_CHECK(actions.numel() == (int64_t)T1 * B && rewards.numel() == (int64_t)T1 * B &&
+              done.numel() == (int64_t)T1 * B, "[T+1,B] shape mismatch");
+  TORCH_CHECK(sa::learner_head_fwd_smem(T, A) <= 160 * 1024, "unroll too long");
+  const c10::DeviceGuard guard(core.device());
+  auto f32 = core.options();
+  auto loss = at::empty({4}, f32);
+  auto dlogits = at::empty({T, B, A}, f32);
+  auto dvalues = at::empty({T, B}, f32);
+  auto partial = at::empty({B * 3}, f32);
+  sa::learner_head_fwd_launch(
+      core.data_ptr<float>(), wp.data_ptr<float>(), bp.data_ptr<float>(),
+      wb.data_ptr<float>(), bb.data_ptr<float>(),
+      behaviour.data_ptr<float>() + (int64_t)B * A,
+      actions.data_ptr<int64_t>() + B, rewards.data_ptr<float>() + B,
+      mask_ptr(done) + B, T, B, A, (float)discounting, (int)clip_mode,
+      (float)clip_rho, (float)clip_pg_rho, (float)baseline_cost,
+      (float)entropy_cost, dlogits.data_ptr<float>(), dvalues.data_ptr<float>(),
+      partial.data_ptr<float>(), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
+      loss.data_ptr<float>(), stream());
+  return {loss, dlogits, dvalues};
+}
+
+// -> dcore [T1,B,256]; the heads' gradients are ACCUMULATED into gwp/gbp/gwb/gbb
+at::Tensor learner_head_bwd(at::Tensor gscale, at::Tensor core, at::Tensor dlogits,
+                            at::Tensor dvalues, at::Tensor wp, at::Tensor wb,
+                            at::Tensor gwp, at::Tensor gbp, at::Tensor gwb,
+                            at::Tensor gbb) {
+  LB_CHECK(gscale); LB_CHECK(core); LB_CHECK(dlogits); LB_CHECK(dvalues);
+  LB_CHECK(wp); LB_CHECK(wb); LB_CHECK(gwp); LB_CHECK(gbp); LB_CHECK(gwb);
+  LB_CHECK(gbb);
+  LB_F32(gscale); LB_F32(core); LB_F32(dlogits); LB_F32(dvalues); LB_F32(gwp);
+  LB_F32(gbp); LB_F32(gwb); LB_F32(gbb);
+  const int T1 = core.size(0), B = core.size(1), A = wp.size(1);
+  TORCH_CHECK(dlogits.numel() == (int64_t)(T1 - 1) * B * A, "dlogits shape");
+  TORCH_CHECK(gwp.numel() == wp.numel() && gbp.numel() == A &&
+              gwb.numel() == 256 && gbb.numel() == 1, "gradient sink shapes");
+  const c10::DeviceGuard guard(core.device());
+  auto dcore = at::empty_like(core);
+  sa::learner_head_bwd_launch(
+      gscale.data_ptr<float>(), core.data_ptr<float>(), dlogits.data_ptr<float>(),
+      dvalues.data_ptr<float>(), wp.data_ptr<float>(), wb.data_ptr<float>(),
+      T1 * B, (T1 - 1) * B, A, dcore.data_ptr<float>(), gwp.data_ptr<float>(),
+      gbp.data_ptr<float>(), gwb.data_ptr<float>(), gbb.data_ptr<float>(),
+      stream());
+  return dcore;
+}
+
+// -> h_aug bf16 [N, ld] = [h (bf16 [N, c0]), clip(r), one_hot(a), 0...]
+at::Tensor core_aug_fwd(at::Tensor h, at::Tensor rewards, at::Tensor actions,
+                        int64_t ld, int64_t clip_mode) {
+  LB_CHECK(h); LB_CHECK(rewards); LB_CHECK(actions);
+  LB_BF16(h); LB_F32(rewards);
+  TORCH_CHECK(actions.scalar_type() == at::kLong, "actions must be int64");
+  const int N = h.size(0), c0 = h.size(1);
+  TORCH_CHECK(rewards.numel() == N && actions.numel() == N, "row count");
+  TORCH_CHECK(ld > c0, "aug width");
+  const c10::DeviceGuard guard(h.device());
+  auto h_aug = at::empty({N, ld}, h.options());
+  sa::core_aug_fwd_launch(h_aug.data_ptr(), h.data_ptr(), rewards.data_ptr<float>(),
+                          actions.data_ptr<int64_t>(), N, (int)ld, c0,
+                          (int)clip_mode, stream());
+  return h_aug;
+}
+
+void colsum_f32_(at::Tensor x, at::Tensor out) {
+  LB_CHECK(x); LB_CHECK(out); LB_F32(x); LB_F32(out);
+  const int C = x.size(-1);
+  const int64_t N = x.numel() / C;
+  TORCH_CHECK(out.numel() == C, "out must have one entry per column");
+  const c10::DeviceGuard guard(x.device());
+  sa::colsum_f32_launch(x.data_ptr<float>(), (int)N, C, out.data_ptr<float>(),
+                        stream());
+}
+
+// dy bf16 [N,C] *= (y > 0); y may be a column slice (row stride >= C)
+void relu_bwd_colsum_(at::Tensor dy, at::Tensor y, c10::optional<at::Tensor> out) {
+  LB_CHECK(dy); LB_BF16(dy); LB_BF16(y);
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be row-major 2-D");
+  const int N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(y.size(0) == N && y.size(1) == C, "shape mismatch");
+  float* op = nullptr;
+  if (out.has_value()) {
+    LB_CHECK(*out); LB_F32(*out);
+    TORCH_CHECK(out->numel() == C, "out size");
+    op = out->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(dy.device());
+  sa::relu_bwd_colsum_launch(dy.data_ptr(), y.data_ptr(), N, C, (int)y.stride(0),
+                             op, stream());
+}
+
+void relu_mask_bf16_(at::Tensor dx, at::Tensor x) {
+  LB_CHECK(dx); LB_CHECK(x); LB_BF16(dx); LB_BF16(x);
+  TORCH_CHECK(dx.numel() == x.numel() && dx.numel() % 8 == 0, "size");
+  const c10::DeviceGuard guard(dx.device());
+  sa::relu_mask_bf16_launch(dx.data_ptr(), x.data_ptr(), dx.numel(), stream());
+}
+
+}  // namespace
+
+void register_learner_ops(pybind11::module& m) {
+  m.def("learner_head_fwd", &learner_head_fwd);
+  m.def("learner_head_bwd", &learner_head_bwd);
+  m.def("core_aug_fwd", &core_aug_fwd);
+  m.def("colsum_f32_", &colsum_f32_);
+  m.def("relu_bwd_colsum_", &relu_bwd_colsum_, pybind11::arg("dy"),
+        pybind11::arg("y"), pybind11::arg("out") = pybind11::none());
+  m.def("relu_mask_bf16_", &relu_mask_bf16_);
+}

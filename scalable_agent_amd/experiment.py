@@ -142,7 +142,8 @@ def _make_agent(flags, num_actions, frame_shape, device, seed):
   cdt = torch.bfloat16 if flags.dtype == 'bf16' else torch.float32
   return Agent(num_actions, torso=flags.torso, frame_shape=frame_shape,
                seed=seed, backend=backend, compute_dtype=cdt,
-               num_value_heads=num_value_heads(flags))
+               num_value_heads=num_value_heads(flags),
+               pipeline_chunks=getattr(flags, 'pipeline_chunks', 1))
 
 
 class EpisodeLogger(object):

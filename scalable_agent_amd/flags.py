@@ -96,6 +96,10 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--log_every_frames', type=int, default=50000,
                  help='Throughput log period (reference log_step_count_steps).')
   p.add_argument('--use_hip_graph', type=_str2bool, default=True)
+  p.add_argument('--pipeline_chunks', type=int, default=1,
+                 help='HIP learner: split the unroll into N time chunks and '
+                      'overlap chunk k\'s LSTM recurrence (side stream) with '
+                      'the conv torso of chunk k+1 (1 = off).')
   p.add_argument('--fault_inject', default='',
                  help='e.g. env_crash:0.01,actor_stall:50 (tests only).')
   p.add_argument('--deterministic', type=_str2bool, default=False)

@@ -39,6 +39,19 @@ def compute_loss(agent, data, flags, use_fused=False, popart=None,
   """
   env_outputs = data.env_outputs
   agent_outputs = data.agent_outputs
+  instr = env_outputs.observation[1]
+  if (use_fused and popart is None and agent.num_value_heads == 1 and
+      agent.fused_core_ready(instr)):
+    # HIP learner path: fused core + fused heads/V-trace/loss; same math
+    from . import ops
+    core_out, _ = agent.unroll_core(agent_outputs.action, env_outputs,
+                                    data.agent_state)
+    return ops.heads_vtrace_loss(
+        core_out, agent.policy_w, agent.policy_b, agent.baseline_w,
+        agent.baseline_b, agent_outputs.policy_logits, agent_outputs.action,
+        env_outputs.reward, env_outputs.done, discounting=flags.discounting,
+        reward_clipping=flags.reward_clipping,
+        baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost)
   task_ids = data.level_name if popart is not None else None
   learner_outputs, _ = agent.unroll(agent_outputs.action, env_outputs,
                                     data.agent_state, sample=False,
@@ -143,7 +156,9 @@ class Learner:
       loss = compute_loss(self.agent, data, self.flags, self.use_fused,
                           self.popart, self._aux)
     with trace('backward'):
-      loss.backward()
+      from .ops import grad_sink
+      with grad_sink.direct_grads(self.use_fused):
+        loss.backward()
     return loss
 
   def _apply(self):
@@ -189,7 +204,10 @@ class Learner:
     self.flat.rebind_grads()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-      self._static_loss = self._fwd_bwd(self._static_in)
+      # detached: holding the autograd graph would keep its AccumulateGrad
+      # nodes (and the streams they were created on) alive into later
+      # captures and eager steps
+      self._static_loss = self._fwd_bwd(self._static_in).detach()
     self.flat.params.copy_(saved_p)
     self._graph = g
 

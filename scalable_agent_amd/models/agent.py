@@ -84,8 +84,13 @@ class Agent(nn.Module):
 
   def __init__(self, num_actions, torso='shallow', frame_shape=(72, 96, 3),
                seed=None, backend='torch', compute_dtype=torch.float32,
-               num_value_heads=1):
+               num_value_heads=1, pipeline_chunks=1):
     super().__init__()
+    # > 1 (HIP backend on a GPU): the learner unroll is split into this many
+    # time chunks; chunk k's LSTM recurrence runs on a side stream while the
+    # conv torso of chunk k+1 runs on the main stream (see _pipelined_core).
+    self.pipeline_chunks = int(pipeline_chunks)
+    self._core_streams = {}
     self.num_actions = num_actions
     # > 1: one (PopArt-normalised) value output per task (popart.py)
     self.num_value_heads = int(num_value_heads)
@@ -256,6 +261,58 @@ class Agent(nn.Module):
       outs.append(h)
     return torch.stack(outs), (c, h)
 
+  def _core_stream(self, device):
+    s = self._core_streams.get(device)
+    if s is None:
+      s = torch.cuda.Stream(device)
+      self._core_streams[device] = s
+    return s
+
+  def _pipelined_core(self, frames, reward, actions, instr, done, state,
+                      chunks):
+    """Time-chunked torso || LSTM pipeline (HIP backend, GPU only).
+
+    The torso, FC and core-input assembly of time chunk k run on the current
+    (main) stream; the x W_x projection and the recurrence of chunk k run on
+    a side stream as soon as chunk k's inputs exist, overlapping the torso of
+    chunk k+1.  Autograd runs every backward node on its forward stream, so
+    the backward overlaps the same way in reverse: once the recurrence of the
+    last chunk has produced its input gradient, that chunk's torso backward
+    runs while the recurrence backward continues on earlier chunks.  Both
+    directions are fork/join DAGs that a captured hipGraph replays
+    concurrently (tools/micro/graph_fork.hip).  Same math as core_unroll.
+    """
+    from .. import ops
+    T, B = done.shape
+    dev = frames.device
+    main = torch.cuda.current_stream(dev)
+    side = self._core_stream(dev)
+    F_in = self.core_input_size
+    w_x = self.lstm_kernel[:F_in]
+    w_h = self.lstm_kernel[F_in:]
+    bounds = [(T * k) // chunks for k in range(chunks + 1)]
+    outs = []
+    for k in range(chunks):
+      t0, t1 = bounds[k], bounds[k + 1]
+      n0, n1 = t0 * B, t1 * B
+      ins = None
+      if instr is not None:
+        ins = (instr[0][n0:n1], instr[1][n0:n1])
+      x = self.core_inputs(frames[n0:n1], reward[n0:n1], actions[n0:n1], ins)
+      x = x.view(t1 - t0, B, -1)
+      side.wait_stream(main)
+      x.record_stream(side)
+      with torch.cuda.stream(side):
+        hs, state = ops.lstm_unroll(x, done[t0:t1], state, self.lstm_kernel,
+                                    self.lstm_bias, w_x=w_x, w_h=w_h)
+      outs.append(hs)
+    main.wait_stream(side)
+    for h in outs:
+      h.record_stream(main)
+    for t in state:
+      t.record_stream(main)
+    return torch.cat(outs, 0), state
+
   def heads(self, core_out, task_ids=None):
     """task_ids: optional [B] task index per batch column (multi-head value
     with PopArt); without it a multi-head agent reports head 0."""
@@ -269,6 +326,39 @@ class Agent(nn.Module):
     return logits, values.gather(-1, idx).squeeze(-1)
 
   # ------------------------------------------------------------------ API
+  def fused_core_ready(self, instr=None):
+    """True when the HIP learner path (fused torso-FC/core-input/LSTM op,
+    fused heads+V-trace loss) applies: HIP backend, HIP torso, no
+    instruction strings, bf16 compute."""
+    return (self.backend == 'hip' and _hip_torso_ready(self) and
+            instr is None and self.compute_dtype == torch.bfloat16)
+
+  def unroll_core(self, actions, env_outputs, core_state):
+    """Everything of `unroll` up to the LSTM output: -> (core_out [T,B,256],
+    core_state)."""
+    reward, _, done, (frame, instr) = env_outputs
+    T, B = actions.shape[0], actions.shape[1]
+    frames = frame.reshape((T * B,) + tuple(frame.shape[2:]))
+    if instr is not None:
+      instr = (instr[0].reshape(T * B, -1), instr[1].reshape(T * B))
+    done = done.to(torch.bool).view(T, B)
+    chunks = min(self.pipeline_chunks, T // 4)
+    if self.backend == 'hip' and frames.is_cuda and chunks > 1:
+      return self._pipelined_core(
+          frames, reward.reshape(T * B), actions.reshape(T * B), instr, done,
+          core_state, chunks)
+    if self.fused_core_ready(instr) and frames.is_cuda:
+      from .. import ops
+      feats = self.conv_features(frames)
+      return ops.core_lstm(feats, self.linear_w, self.linear_b,
+                           self.lstm_kernel, self.lstm_bias,
+                           reward.reshape(T * B), actions.reshape(T * B), done,
+                           core_state, self.num_actions)
+    x = self.core_inputs(frames, reward.reshape(T * B),
+                         actions.reshape(T * B), instr)
+    x = x.view(T, B, -1)
+    return self.core_unroll(x, done, core_state)
+
   def unroll(self, actions, env_outputs, core_state, sample=True,
              generator=None, task_ids=None):
     """Unrolls over T steps (experiment.py:219-237).
@@ -276,16 +366,8 @@ class Agent(nn.Module):
     actions: [T,B] last actions; env_outputs: StepOutput with [T,B,...]
     fields whose observation is (frame uint8 [T,B,H,W,C], instr or None).
     """
-    reward, _, done, (frame, instr) = env_outputs
     T, B = actions.shape[0], actions.shape[1]
-    frames = frame.reshape((T * B,) + tuple(frame.shape[2:]))
-    if instr is not None:
-      instr = (instr[0].reshape(T * B, -1), instr[1].reshape(T * B))
-    x = self.core_inputs(frames, reward.reshape(T * B),
-                         actions.reshape(T * B), instr)
-    x = x.view(T, B, -1)
-    done = done.to(torch.bool).view(T, B)
-    core_out, core_state = self.core_unroll(x, done, core_state)
+    core_out, core_state = self.unroll_core(actions, env_outputs, core_state)
     logits, baseline = self.heads(core_out, task_ids)
     if sample:
       probs = torch.softmax(logits.reshape(T * B, -1).float(), -1)

@@ -13,6 +13,7 @@ gradients accumulate in fp32 directly inside the kernels.
 
 import torch
 
+from . import grad_sink
 from ._ext import ext
 from ..models import layers
 
@@ -103,13 +104,15 @@ class _DeepTorso(torch.autograd.Function):
         stage_out = saved[k]
         k += 1
       stages.append((arg, blocks, stage_out))
-    # The kernels ACCUMULATE weight/bias gradients.  Where a parameter
-    # already holds a .grad buffer (the learner's flat gradient buffer), they
-    # accumulate straight into it and None is returned for that parameter -
-    # exactly AccumulateGrad's `grad += g`, minus one add kernel per tensor.
-    gviews, direct = _grad_sinks(params, out.device)
-    dy = grad_out.reshape(out.shape).to(torch.bfloat16)
-    dy = (dy * (out > 0)).contiguous()
+    # The kernels ACCUMULATE weight/bias gradients: inside
+    # grad_sink.direct_grads() straight into the learner's flat gradient
+    # buffer (None is returned for those parameters), else into fresh zeros.
+    gviews, direct = grad_sink.sinks(params)
+    # the torso's final ReLU: dy *= (out > 0), in place on our own bf16 copy
+    dy = grad_out.reshape(out.shape)
+    if dy.dtype != torch.bfloat16 or not dy.is_contiguous():
+      dy = dy.to(torch.bfloat16).contiguous()
+    C.relu_mask_bf16_(dy, out)
     p_base = [0, 10, 20]
     for s in reversed(range(3)):
       arg, blocks, _ = stages[s]
@@ -129,32 +132,7 @@ class _DeepTorso(torch.autograd.Function):
         x_in = stages[s - 1][2]
         dy = C.pool_conv_bwd(dy, arg, x_in, params[pb], gviews[pb],
                              gviews[pb + 1], True, pb_h, pb_w)
-    return (None,) + tuple(None if d else g for g, d in zip(gviews, direct))
-
-
-def _grad_sinks(params, device):
-  """-> (per-param fp32 accumulation buffers, per-param 'is p.grad')."""
-  views, direct = [], []
-  fresh = [q for q in params if not _is_sink(q)]
-  buf = (torch.zeros(sum(q.numel() for q in fresh), dtype=torch.float32,
-                     device=device) if fresh else None)
-  o = 0
-  for q in params:
-    if _is_sink(q):
-      views.append(q.grad)
-      direct.append(True)
-    else:
-      views.append(buf[o:o + q.numel()].view_as(q))
-      o += q.numel()
-      direct.append(False)
-  return views, direct
-
-
-def _is_sink(q):
-  g = q.grad
-  return (g is not None and g.dtype == torch.float32 and g.is_contiguous()
-          and g.shape == q.shape and g.device == q.device
-          and not torch.is_grad_enabled())
+    return (None,) + grad_sink.returned(gviews, direct)
 
 
 def torso_forward(agent, frames):

@@ -1,0 +1,115 @@
+"""Fused torso-FC -> core input -> LSTM-256 core (HIP backend learner path).
+
+Reference: experiment.py:185-198 (Linear(256)+ReLU on the flattened conv
+features; concat [torso, clip(reward, -1, 1), one_hot(last_action),
+instruction]) and :228-235 (LSTMBlockCell(256) unrolled with done-reset).
+
+Forward (one autograd node: 4 launches + the recurrence):
+  h      = relu(feats W_fc + b_fc)              hipBLASLt bf16, bias+ReLU epilogue
+  h_aug  = [h, clip(r), one_hot(a), 0...]      core_aug_fwd (the instruction
+                                               encoding is all-zero without
+                                               instructions, so its W_x rows
+                                               drop out of the product)
+  xw     = h_aug W_x[:K] + b_lstm               hipBLASLt bf16 in, fp32 out
+  hs, cs = LSTM recurrence                      lstm.hip fwd steps (fp32)
+Backward:
+  dG (fp32 + bf16)                              lstm.hip bwd steps
+  dW_h  += hpm^T dG        dW_x[:K] += h_aug^T dG        db_lstm += colsum dG
+  dh     = dG W_x[:256]^T ; dh *= (h > 0) ; db_fc += colsum dh
+  dfeats = dh W_fc^T       dW_fc += feats^T dh
+Weight gradients accumulate straight into the learner's flat fp32 gradient
+buffer inside grad_sink.direct_grads(); the pad rows of W_x[:K] past the
+one-hot (the first instruction rows) meet all-zero h_aug columns, so they
+receive exactly 0.  GEMMs are plain library GEMMs (hipBLASLt); the glue
+kernels are in csrc/kernels/learner_io.hip.
+"""
+
+import torch
+
+from . import grad_sink
+from ._ext import ext
+
+CORE = 256
+
+
+def aug_width(num_actions):
+  """Columns of [h, clip(r), one_hot(a)] padded to a multiple of 16."""
+  return (CORE + 1 + num_actions + 15) // 16 * 16
+
+
+class _CoreLSTM(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
+              done_u8, num_actions):
+    C = ext()
+    T, B = done_u8.shape
+    N = T * B
+    f_in = CORE + 1 + num_actions + 64
+    K = aug_width(num_actions)
+    assert K <= f_in and kernel.shape[0] == f_in + CORE
+    bf = torch.bfloat16
+    w16_fc = w_fc.to(bf)
+    wx16 = kernel[:K].to(bf)
+    h = torch._addmm_activation(b_fc.to(bf), feats, w16_fc)
+    # reward clipping of the core input is always abs_one (experiment.py:194)
+    h_aug = C.core_aug_fwd(h, rewards, actions, K, 0)
+    del h
+    xw = torch.addmm(bias, h_aug, wx16, out_dtype=torch.float32)
+    hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
+                                       kernel[f_in:])
+    ctx.save_for_backward(feats, w_fc, b_fc, kernel, bias, w16_fc, wx16, h_aug,
+                          wt, acts, cs, c0, hpm, done_u8)
+    ctx.f_in = f_in
+    ctx.K = K
+    return hs, cs[-1]
+
+  @staticmethod
+  def backward(ctx, dhs, dc_last):
+    C = ext()
+    (feats, w_fc, b_fc, kernel, bias, w16_fc, wx16, h_aug, wt, acts, cs, c0,
+     hpm, done_u8) = ctx.saved_tensors
+    f_in, K = ctx.f_in, ctx.K
+    T, B, G = acts.shape
+    N = T * B
+    if dhs is None:
+      dhs = torch.zeros(T, B, CORE, dtype=acts.dtype, device=acts.device)
+    if dc_last is not None:
+      dc_last = dc_last.contiguous()
+    dg, dc0, dg16 = C.lstm_bwd(dhs.contiguous(), done_u8, wt, acts, cs, c0,
+                               dc_last, True)
+    (gwfc, gbfc, gk, gb), direct = grad_sink.sinks([w_fc, b_fc, kernel, bias])
+    dg2 = dg.view(N, G)
+    dg16_2 = dg16.view(N, G)
+    f32 = torch.float32
+    gk[f_in:].addmm_(hpm.view(N, CORE).t(), dg2)                    # W_h
+    gxk = gk[:K]
+    torch.addmm(gxk, h_aug.t(), dg16_2, out_dtype=f32, out=gxk)     # W_x rows
+    C.colsum_f32_(dg2, gb)                                          # b_lstm
+    dh = torch.mm(dg16_2, wx16[:CORE].t())                          # [N,256]
+    C.relu_bwd_colsum_(dh, h_aug[:, :CORE], gbfc)                   # b_fc
+    dfeats = torch.mm(dh, w16_fc.t())
+    torch.addmm(gwfc, feats.t(), dh, out_dtype=f32, out=gwfc)       # W_fc
+    dh0 = None
+    if ctx.needs_input_grad[8]:
+      keep0 = (done_u8[0] == 0).to(f32).unsqueeze(-1)
+      dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
+    if not ctx.needs_input_grad[7]:
+      dc0 = None
+    g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
+    return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None)
+
+
+def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
+              num_actions):
+  """feats bf16 [T*B, F] (ReLU'd torso output), rewards [T*B] f32, actions
+  [T*B] (last actions), done [T,B] bool, state (c, h) [B,256] ->
+  (hs [T,B,256] f32, (c_T, h_T))."""
+  c0, h0 = state
+  hs, c_last = _CoreLSTM.apply(
+      feats.contiguous(), w_fc, b_fc, kernel, bias,
+      rewards.reshape(-1).to(torch.float32).contiguous(),
+      actions.reshape(-1).to(torch.int64).contiguous(),
+      c0.float().contiguous(), h0.float().contiguous(),
+      done.to(torch.uint8).contiguous(), int(num_actions))
+  return hs, (c_last, hs[-1])

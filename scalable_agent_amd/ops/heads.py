@@ -1,0 +1,71 @@
+"""Fused policy/baseline heads + V-trace + IMPALA loss (HIP learner path).
+
+Reference: heads experiment.py:200-210; learner loss :360-407 (bootstrap from
+the last baseline, one-step time shift, reward clipping, discounts, V-trace
+from logits vtrace.py:71-161, PG + baseline + entropy losses :324-343).
+
+Forward: ONE kernel (learner_head_fwd, a workgroup per batch column) computes
+the heads for all T+1 steps, V-trace, the loss sums and the analytic
+gradients w.r.t. the logits/values.  Backward: ONE kernel (learner_head_bwd)
+scales them by the incoming loss gradient, maps them through the heads
+(dcore) and accumulates the heads' weight/bias gradients (ops.grad_sink).
+Single value head only (PopArt multi-head runs the generic path).
+"""
+
+import torch
+
+from . import grad_sink
+from ._ext import ext
+
+_CLIP = {'abs_one': 0, 'soft_asymmetric': 1}
+_TICKETS = {}
+
+
+def _ticket(device):
+  """Per-device completion counter of the fwd kernel (self-resetting)."""
+  t = _TICKETS.get(device)
+  if t is None:
+    t = torch.zeros(1, dtype=torch.int32, device=device)
+    _TICKETS[device] = t
+  return t
+
+
+class _HeadsVTraceLoss(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, core, wp, bp, wb, bb, behaviour, actions, rewards, done,
+              cfg):
+    loss, dl, dv = ext().learner_head_fwd(
+        core, wp, bp, wb.reshape(-1), bb.reshape(-1), behaviour, actions,
+        rewards, done, _ticket(core.device), cfg['discounting'],
+        _CLIP[cfg['reward_clipping']], 1.0, 1.0, cfg['baseline_cost'],
+        cfg['entropy_cost'])
+    ctx.save_for_backward(core, dl, dv, wp, bp, wb, bb)
+    return loss[0]
+
+  @staticmethod
+  def backward(ctx, g):
+    core, dl, dv, wp, bp, wb, bb = ctx.saved_tensors
+    (gwp, gbp, gwb, gbb), direct = grad_sink.sinks([wp, bp, wb, bb])
+    gs = g.reshape(1).to(torch.float32).contiguous()
+    dcore = ext().learner_head_bwd(gs, core, dl, dv, wp, wb.reshape(-1), gwp,
+                                   gbp, gwb.view(-1), gbb.view(-1))
+    return (dcore,) + grad_sink.returned((gwp, gbp, gwb, gbb), direct) + (
+        None,) * 5
+
+
+def heads_vtrace_loss(core_out, policy_w, policy_b, baseline_w, baseline_b,
+                      behaviour_logits, actions, rewards, done, discounting,
+                      reward_clipping, baseline_cost, entropy_cost):
+  """core_out [T+1,B,256] f32 from the learner unroll; behaviour_logits /
+  actions / rewards / done: the FULL [T+1,B,...] batch tensors (rows 1..T
+  are used, as in experiment.py:360-375).  Returns the total loss (sum)."""
+  cfg = dict(discounting=float(discounting), reward_clipping=reward_clipping,
+             baseline_cost=float(baseline_cost),
+             entropy_cost=float(entropy_cost))
+  return _HeadsVTraceLoss.apply(
+      core_out.contiguous(), policy_w, policy_b, baseline_w, baseline_b,
+      behaviour_logits.to(torch.float32).contiguous(),
+      actions.to(torch.int64).contiguous(),
+      rewards.to(torch.float32).contiguous(),
+      done.to(torch.bool).contiguous(), cfg)

@@ -4,6 +4,12 @@ x W_x + b for all T steps is ONE GEMM (hipBLASLt via torch.matmul, autograd
 handles dX/dW_x/db); the serial recurrence runs as T fused step kernels
 (recurrent GEMV + gates + cell + done-reset) forward and T fused reverse step
 kernels backward; dW_h = sum_t (keep_t h_{t-1})^T dG_t is one GEMM.
+
+The recurrence is differentiable w.r.t. its initial state too (dc0 from the
+backward kernels' carry, dh0 = keep_0 * dG_0 W_h^T), so an unroll can be split
+into time chunks that chain their states - the pipelined learner unroll
+(models/agent.py) runs chunk k's recurrence on a side stream while the conv
+torso of chunk k+1 runs on the main stream.
 """
 
 import torch
@@ -17,31 +23,49 @@ class _LSTMRecurrence(torch.autograd.Function):
   def forward(ctx, xw, w_h, c0, h0, done_u8):
     xw = xw.contiguous()
     w_h_c = w_h.contiguous()
-    hs, cs, acts = ext().lstm_fwd(xw, done_u8, c0.contiguous(),
-                                  h0.contiguous(), w_h_c)
-    ctx.save_for_backward(w_h_c, acts, cs, c0, h0, hs, done_u8)
+    c0 = c0.contiguous()
+    h0 = h0.contiguous()
+    hs, cs, acts, hpm, wt = ext().lstm_fwd(xw, done_u8, c0, h0, w_h_c)
+    ctx.save_for_backward(w_h_c, wt, acts, cs, c0, hpm, done_u8)
     return hs, cs[-1]
 
   @staticmethod
   def backward(ctx, dhs, dc_last):
-    w_h, acts, cs, c0, h0, hs, done_u8 = ctx.saved_tensors
+    w_h, wt, acts, cs, c0, hpm, done_u8 = ctx.saved_tensors
+    T, B, H4 = acts.shape
+    H = H4 // 4
     if dhs is None:
-      dhs = torch.zeros_like(hs)
-    dg = ext().lstm_bwd(dhs.contiguous(), done_u8, w_h, acts, cs,
-                        c0.contiguous())
-    T, B, H = hs.shape
-    keep = (done_u8 == 0).to(hs.dtype).unsqueeze(-1)
-    h_prev = torch.cat([h0.unsqueeze(0), hs[:-1]], 0) * keep
-    dw_h = h_prev.reshape(T * B, H).t() @ dg.reshape(T * B, 4 * H)
-    return dg, dw_h, None, None, None
+      dhs = torch.zeros(T, B, H, dtype=acts.dtype, device=acts.device)
+    if dc_last is not None:
+      dc_last = dc_last.contiguous()
+    dg, dc0, _ = ext().lstm_bwd(dhs.contiguous(), done_u8, wt, acts, cs, c0,
+                                dc_last, False)
+    # dW_h = sum_t (keep_t h_{t-1})^T dG_t; hpm is saved by the fwd kernel
+    dw_h = hpm.reshape(T * B, H).t() @ dg.reshape(T * B, 4 * H)
+    dh0 = None
+    if ctx.needs_input_grad[3]:
+      keep0 = (done_u8[0] == 0).to(dg.dtype).unsqueeze(-1)
+      dh0 = (dg[0] @ w_h.t()) * keep0
+    if not ctx.needs_input_grad[2]:
+      dc0 = None
+    return dg, dw_h, dc0, dh0, None
 
 
-def lstm_unroll(x, done, state, kernel, bias):
-  """x [T,B,F] f32, done [T,B] bool, state (c,h) -> (h_all, (c_T, h_T))."""
+def lstm_unroll(x, done, state, kernel, bias, w_x=None, w_h=None):
+  """x [T,B,F] f32, done [T,B] bool, state (c,h) -> (h_all, (c_T, h_T)).
+
+  w_x / w_h: optional pre-sliced views of `kernel` (rows [:F] and [F:]); a
+  chunked unroll passes the same views to every chunk so the slice backward
+  runs once instead of once per chunk.
+  """
   c0, h0 = state
   check_cuda(x, kernel)
   F_in = x.shape[-1]
-  xw = torch.matmul(x.float(), kernel[:F_in]) + bias
-  hs, c_last = _LSTMRecurrence.apply(xw, kernel[F_in:], c0.float(), h0.float(),
+  if w_x is None:
+    w_x = kernel[:F_in]
+  if w_h is None:
+    w_h = kernel[F_in:]
+  xw = torch.matmul(x.float(), w_x) + bias
+  hs, c_last = _LSTMRecurrence.apply(xw, w_h, c0.float(), h0.float(),
                                      done.to(torch.uint8).contiguous())
   return hs, (c_last, hs[-1])

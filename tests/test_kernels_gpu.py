@@ -148,3 +148,44 @@ def test_lstm_unroll_fwd_bwd(cuda, T, B, H):
   torch.testing.assert_close(x.grad, gx, rtol=1e-3, atol=1e-4)
   torch.testing.assert_close(kernel.grad, gk, rtol=1e-3, atol=1e-3)
   torch.testing.assert_close(bias.grad, gb, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize('T,B,H', [(25, 32, 256), (7, 5, 64)])
+def test_lstm_state_grads_and_chunking(cuda, T, B, H):
+  """dc0/dh0 from the HIP recurrence match autograd through the fp32
+  reference, and an unroll split into chained time chunks (the pipelined
+  learner) gives the same outputs and gradients as one unroll."""
+  ops = _ops()
+  torch.manual_seed(3)
+  F_in = 330
+  x = torch.randn(T, B, F_in, device=cuda, requires_grad=True)
+  done = torch.rand(T, B, device=cuda) < 0.1
+  done[0, 0] = True
+  c0 = (torch.randn(B, H, device=cuda) * 0.5).requires_grad_()
+  h0 = (torch.randn(B, H, device=cuda) * 0.5).requires_grad_()
+  kernel = (torch.randn(F_in + H, 4 * H, device=cuda) * 0.05).requires_grad_()
+  bias = (torch.randn(4 * H, device=cuda) * 0.1).requires_grad_()
+  leaves = [x, c0, h0, kernel, bias]
+  hs_ref, c_ref = _ref_lstm(x, done, c0, h0, kernel, bias)
+  go = torch.randn_like(hs_ref)
+  gc = torch.randn_like(c_ref)
+  ((hs_ref * go).sum() + (c_ref * gc).sum()).backward()
+  ref = [t.grad.clone() for t in leaves]
+  for split in (None, [0, T // 3, T // 2 + 1, T]):
+    for t in leaves:
+      t.grad = None
+    if split is None:
+      hs, (c_last, _) = ops.lstm_unroll(x, done, (c0, h0), kernel, bias)
+    else:
+      state, outs = (c0, h0), []
+      w_x, w_h = kernel[:F_in], kernel[F_in:]
+      for a, b in zip(split[:-1], split[1:]):
+        h_k, state = ops.lstm_unroll(x[a:b], done[a:b], state, kernel, bias,
+                                     w_x=w_x, w_h=w_h)
+        outs.append(h_k)
+      hs, c_last = torch.cat(outs), state[0]
+    torch.testing.assert_close(hs, hs_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(c_last, c_ref, rtol=1e-4, atol=1e-5)
+    ((hs * go).sum() + (c_last * gc).sum()).backward()
+    for t, g in zip(leaves, ref):
+      torch.testing.assert_close(t.grad, g, rtol=1e-3, atol=1e-3)

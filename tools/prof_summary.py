@@ -31,7 +31,7 @@ def main():
   steps_arg = sys.argv[2] if len(sys.argv) > 2 else 'auto'
   top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
   if steps_arg == 'auto':
-    steps = max([r[1] for r in rows if 'vtrace_loss_kernel' in r[0]] or [1])
+    steps = max([r[1] for r in rows if 'vtrace_loss_kernel' in r[0] or 'learner_head_fwd' in r[0]] or [1])
   else:
     steps = float(steps_arg)
   tot = sum(r[2] for r in rows)
