@@ -6,6 +6,9 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <cstdlib>
+#include <map>
+
 #include "kernels/launchers.h"
 #include "kernels/conv_launchers.h"
 
@@ -91,6 +94,35 @@ std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
   return {loss, dlogits, dvalues};
 }
 
+// Persistent whole-unroll LSTM kernels (lstm_persistent.hip) for H == 256,
+// B <= 32 when enabled (SA_LSTM_PERSISTENT=1 or lstm_set_persistent(True)).
+// OFF by default: measured on MI355X (tools/micro/lstm_probe.py, T=101,
+// B=32) the granule all-gather of h / dG costs 9 / 27.6 us per step against
+// 4.4 / 6.9 us for the graph-replayed per-step kernels, whose operand loads
+// ride the normal L2/MALL path.
+bool g_lstm_persistent = [] {
+  const char* e = std::getenv("SA_LSTM_PERSISTENT");
+  return e && e[0] == '1';
+}();
+
+bool use_persistent(int H, int B) { return g_lstm_persistent && H == 256 && B <= 32; }
+
+// Sticky per-device timeout word of the persistent kernels (0 = healthy).
+at::Tensor lstm_err_word(const at::Device& dev) {
+  static std::map<int, at::Tensor> words;
+  auto it = words.find(dev.index());
+  if (it != words.end()) return it->second;
+  auto w = at::zeros({4}, at::TensorOptions().dtype(at::kInt).device(dev));
+  words[dev.index()] = w;
+  return w;
+}
+
+at::Tensor lstm_xbuf(bool bwd, const at::TensorOptions& o) {
+  // zeroed before EVERY launch (a memset node under graph replay): stale
+  // tags of an earlier call can never match
+  return at::zeros({(int64_t)sa::lstm_persistent_xbuf_granules(bwd)}, o.dtype(at::kLong));
+}
+
 // Returns {hs, cs, acts, hpm, wt}: hpm[t] = keep_t * h_{t-1} (A operand of
 // the dW_h GEMM), wt = W_h^T packed for lstm_bwd.
 std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
@@ -115,6 +147,15 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
                                wt.data_ptr<float>(), H, s);
   const uint8_t* dn = u8ptr(done);
+  if (use_persistent(H, B)) {
+    auto xbuf = lstm_xbuf(false, xw.options());
+    sa::lstm_fwd_persistent_launch(
+        xw.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), dn,
+        w4.data_ptr<float>(), hs.data_ptr<float>(), cs.data_ptr<float>(),
+        acts.data_ptr<float>(), hpm.data_ptr<float>(), xbuf.data_ptr(),
+        reinterpret_cast<unsigned*>(lstm_err_word(xw.device()).data_ptr<int>()), T, B, s);
+    return {hs, cs, acts, hpm, wt};
+  }
   for (int t = 0; t < T; ++t) {
     const float* cp = t == 0 ? c0.data_ptr<float>() : cs[t - 1].data_ptr<float>();
     const float* hp = t == 0 ? h0.data_ptr<float>() : hs[t - 1].data_ptr<float>();
@@ -155,6 +196,19 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
   auto dgpk = at::empty({2, RT * 32 * H4}, acts.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
+  if (use_persistent(H, B)) {
+    auto dc0 = at::empty({B, H}, acts.options());
+    auto xbuf = lstm_xbuf(true, acts.options());
+    sa::lstm_bwd_persistent_launch(
+        dh_out.data_ptr<float>(), dn, wt.data_ptr<float>(), acts.data_ptr<float>(),
+        cs.data_ptr<float>(), c0.data_ptr<float>(),
+        dc_last.has_value() ? dc_last->data_ptr<float>() : nullptr,
+        dg.data_ptr<float>(), want_bf16 ? dg16.data_ptr() : nullptr,
+        dc0.data_ptr<float>(), xbuf.data_ptr(),
+        reinterpret_cast<unsigned*>(lstm_err_word(acts.device()).data_ptr<int>()), T, B, s);
+    if (!want_bf16) dg16 = at::empty({0}, acts.options());
+    return {dg, dc0, dg16};
+  }
   for (int t = T - 1; t >= 0; --t) {
     const float* dgn = t == T - 1 ? nullptr : dgpk[(t + 1) & 1].data_ptr<float>();
     const uint8_t* dnext = t == T - 1 ? nullptr : dn + (t + 1) * B;
@@ -172,6 +226,10 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
   if (!want_bf16) dg16 = at::empty({0}, acts.options());
   return {dg, carry[0], dg16};
 }
+
+void lstm_set_persistent(bool on) { g_lstm_persistent = on; }
+bool lstm_get_persistent() { return g_lstm_persistent; }
+at::Tensor lstm_error(at::Tensor like) { return lstm_err_word(like.device()); }
 
 void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
   sa::noop_launch(blocks, threads, counter.data_ptr<int>(), cur_stream());
@@ -195,6 +253,9 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("wt"), pybind11::arg("acts"), pybind11::arg("cs"),
         pybind11::arg("c0"), pybind11::arg("dc_last") = pybind11::none(),
         pybind11::arg("want_bf16") = false);
+  m.def("lstm_set_persistent", &lstm_set_persistent);
+  m.def("lstm_get_persistent", &lstm_get_persistent);
+  m.def("lstm_error_word", &lstm_error);
   m.def("noop", &noop);
   register_conv_ops(m);
   register_learner_ops(m);

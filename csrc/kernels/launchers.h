@@ -59,6 +59,24 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
 void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                               hipStream_t stream);
 
+// ---- lstm_persistent.hip -------------------------------------------------
+// Whole-unroll LSTM-256 recurrence in one launch per direction (B <= 32).
+// xbuf: lstm_persistent_xbuf_granules(bwd) zeroed 8-byte granules (zero it
+// before EVERY launch); err: sticky timeout word (never reset by kernels).
+// fwd: w4 packed as for lstm_fwd_step; outputs as lstm.hip (hs, cs, acts,
+// hpm [T,B,...]).  bwd: wt packed W_h^T; dc_last may be null; dg16 / dc0
+// may be null.
+size_t lstm_persistent_xbuf_granules(bool bwd);
+void lstm_fwd_persistent_launch(const float* xw, const float* h0, const float* c0,
+                                const uint8_t* done, const float* w4, float* hs,
+                                float* cs, float* acts, float* hpm, void* xbuf,
+                                unsigned* err, int T, int B, hipStream_t stream);
+void lstm_bwd_persistent_launch(const float* dh_out, const uint8_t* done,
+                                const float* wt, const float* acts, const float* cs,
+                                const float* c0, const float* dc_last, float* dg,
+                                void* dg16, float* dc0, void* xbuf, unsigned* err,
+                                int T, int B, hipStream_t stream);
+
 // ---- learner_io.hip --------------------------------------------------------
 // Fused heads + V-trace + loss (one workgroup per batch column; see the file
 // header).  core [T+1,B,256]; behaviour/actions/rewards/done point at row 1

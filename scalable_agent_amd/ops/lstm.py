@@ -69,3 +69,19 @@ def lstm_unroll(x, done, state, kernel, bias, w_x=None, w_h=None):
   hs, c_last = _LSTMRecurrence.apply(xw, w_h, c0.float(), h0.float(),
                                      done.to(torch.uint8).contiguous())
   return hs, (c_last, hs[-1])
+
+
+def set_persistent(on):
+  """Selects the whole-unroll persistent kernels (B <= 32, H == 256; the
+  default) or the per-step kernels; returns the previous setting."""
+  prev = bool(ext().lstm_get_persistent())
+  ext().lstm_set_persistent(bool(on))
+  return prev
+
+
+def persistent_error(device):
+  """Sticky timeout word of the persistent kernels on `device` (0 = healthy;
+  nonzero means a workgroup could not co-reside and the unroll was
+  abandoned).  Reading it synchronises the device."""
+  like = torch.empty(0, device=device)
+  return int(ext().lstm_error_word(like)[0].item())

@@ -189,3 +189,45 @@ def test_lstm_state_grads_and_chunking(cuda, T, B, H):
     ((hs * go).sum() + (c_last * gc).sum()).backward()
     for t, g in zip(leaves, ref):
       torch.testing.assert_close(t.grad, g, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize('T,B', [(101, 32), (37, 7), (1, 32)])
+def test_lstm_persistent_matches_per_step(cuda, T, B):
+  """The opt-in whole-unroll persistent kernels (granule hand-offs between
+  workgroups) reproduce the per-step kernels to fp32 rounding, identically
+  over repeated launches (stale-tag / race check), and leave the error word
+  clear."""
+  ops = _ops()
+  from scalable_agent_amd.ops import lstm as lstm_ops
+  C = ops.ext()
+  torch.manual_seed(9)
+  H = 256
+  xw = torch.randn(T, B, 4 * H, device=cuda)
+  done = (torch.rand(T, B, device=cuda) < 0.1).to(torch.uint8)
+  c0 = torch.randn(B, H, device=cuda) * 0.5
+  h0 = torch.randn(B, H, device=cuda) * 0.5
+  w_h = torch.randn(H, 4 * H, device=cuda) * 0.05
+  dh = torch.randn(T, B, H, device=cuda)
+  dcl = torch.randn(B, H, device=cuda)
+  outs = {}
+  prev = lstm_ops.set_persistent(False)
+  try:
+    for mode in (False, True):
+      lstm_ops.set_persistent(mode)
+      runs = []
+      for _ in range(3 if mode else 1):
+        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
+        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True)
+        runs.append([hs, cs, acts, hpm, dg, dc0, dg16.float()])
+      for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+          assert torch.equal(a, b)
+      outs[mode] = runs[0]
+  finally:
+    lstm_ops.set_persistent(prev)
+  torch.cuda.synchronize()
+  assert lstm_ops.persistent_error(cuda) == 0
+  for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+    tol = 1e-2 if i == 6 else 1e-5  # bf16 copy of dG: one rounding step
+    torch.testing.assert_close(b, a, rtol=tol, atol=tol * 0.1,
+                               msg='output %d' % i)

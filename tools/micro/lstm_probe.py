@@ -1,0 +1,54 @@
+"""Times the LSTM recurrence kernels (persistent vs per-step) in a hipGraph."""
+import os
+import sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))))
+from scalable_agent_amd import ops  # noqa: E402
+from scalable_agent_amd.ops import lstm as lstm_ops  # noqa: E402
+
+
+def t_us(fn, reps=20):
+  s0 = torch.cuda.Stream()
+  s0.wait_stream(torch.cuda.current_stream())
+  with torch.cuda.stream(s0):
+    for _ in range(2):
+      fn()
+  torch.cuda.current_stream().wait_stream(s0)
+  torch.cuda.synchronize()
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    for _ in range(reps):
+      fn()
+  g.replay()
+  torch.cuda.synchronize()
+  s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+  s.record()
+  g.replay()
+  e.record()
+  torch.cuda.synchronize()
+  return s.elapsed_time(e) / reps * 1e3
+
+
+def main():
+  C = ops.load()
+  d = torch.device('cuda')
+  T, B, H = 101, 32, 256
+  xw = torch.randn(T, B, 4 * H, device=d)
+  done = (torch.rand(T, B, device=d) < 0.02).to(torch.uint8)
+  c0 = torch.randn(B, H, device=d) * 0.5
+  h0 = torch.randn(B, H, device=d) * 0.5
+  w_h = torch.randn(H, 4 * H, device=d) * 0.05
+  dh = torch.randn(T, B, H, device=d)
+  for mode in (False, True):
+    lstm_ops.set_persistent(mode)
+    hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
+    f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h)
+    b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True)
+    print('persistent=%d fwd %8.1f us  bwd %8.1f us' % (mode, t_us(f), t_us(b)),
+          flush=True)
+  print('error word', lstm_ops.persistent_error(d))
+
+
+if __name__ == '__main__':
+  main()
