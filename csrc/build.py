@@ -76,10 +76,12 @@ def _compile_all(jobs, workers):
       print('  compiled', os.path.relpath(futs[f], ROOT), flush=True)
 
 
-def build_hip(workers=8, force=False, extra_flags=()):
+def build_hip(workers=8, force=False, extra_flags=(), out=None):
   inc, lib, abi = _torch_paths()
   py_inc = sysconfig.get_paths()['include']
   digest = _headers_digest([CSRC])
+  if extra_flags:
+    digest += '-' + hashlib.sha1(' '.join(extra_flags).encode()).hexdigest()[:8]
   objdir = os.path.join(BUILD, 'hip-%s' % digest)
   os.makedirs(objdir, exist_ok=True)
   if force:
@@ -102,7 +104,7 @@ def build_hip(workers=8, force=False, extra_flags=()):
         '-Wno-unused-parameter', '-Wno-deprecated-declarations']
     jobs.append((src, obj, cmd))
   _compile_all(jobs, workers)
-  out = os.path.join(PKG, '_C.so')
+  out = out or os.path.join(PKG, '_C.so')
   objs = [o for _, o, _ in jobs]
   if (force or not os.path.exists(out) or
       max(os.path.getmtime(o) for o in objs) > os.path.getmtime(out)):

@@ -508,33 +508,57 @@ __global__ __launch_bounds__(256) void colsum_f32_kernel(
   atomicAdd(out + c, s);
 }
 
-// dy [N, C] bf16 *= (y > 0); out[c] += sum_r dy[r, c] (after masking)
+// dy [N, C] bf16 *= (y > 0); out[c] += sum_r dy[r, c] (after masking).
+// C even: thread = (column pair, row lane); a block covers C/2 pairs x
+// kRbRows rows (256 / (C/2) row lanes), every load of the block issued up
+// front; row lanes are reduced through LDS, then one atomic per column.
+constexpr int kRbRows = 32;
+
 __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
     bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int N, int C,
     int ldy, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  const int r0 = blockIdx.y * kColRows;
-  const int r1 = min(r0 + kColRows, N);
-  if (c >= C) return;
-  float s = 0.f;
-  for (int base = r0; base < r1; base += kColBatch) {
-    bf16_t dv[kColBatch], yv[kColBatch];
+  __shared__ float red[256][2];
+  const int pairs = C >> 1;
+  const int lanes = 256 / pairs;  // row lanes (host: C/2 divides 256)
+  const int cp = threadIdx.x % pairs, rl = threadIdx.x / pairs;
+  const int r0 = blockIdx.x * kRbRows;
+  constexpr int kMaxPer = kRbRows;  // lanes >= 1
+  const int per = kRbRows / lanes;
+  unsigned dv[kMaxPer], yv[kMaxPer];
 #pragma unroll
-    for (int j = 0; j < kColBatch; ++j) {
-      const bool in = base + j < r1;
-      dv[j] = in ? dy[static_cast<int64_t>(base + j) * C + c] : bf16_t(0);
-      yv[j] = in ? y[static_cast<int64_t>(base + j) * ldy + c] : bf16_t(0);
-    }
+  for (int i = 0; i < kMaxPer; ++i) {
+    const int r = r0 + rl + lanes * i;
+    const bool in = i < per && r < N;
+    dv[i] = in ? *reinterpret_cast<const unsigned*>(dy + static_cast<int64_t>(r) * C + 2 * cp) : 0u;
+    yv[i] = in ? *reinterpret_cast<const unsigned*>(y + static_cast<int64_t>(r) * ldy + 2 * cp) : 0u;
+  }
+  float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-    for (int j = 0; j < kColBatch; ++j) {
-      const bool on = bf2f(yv[j]) > 0.f;
-      if (base + j < r1) {
-        if (on) s += bf2f(dv[j]);
-        else dy[static_cast<int64_t>(base + j) * C + c] = 0;
-      }
+  for (int i = 0; i < kMaxPer; ++i) {
+    const int r = r0 + rl + lanes * i;
+    if (i < per && r < N) {
+      const bool on0 = bf2f(static_cast<bf16_t>(yv[i] & 0xffffu)) > 0.f;
+      const bool on1 = bf2f(static_cast<bf16_t>(yv[i] >> 16)) > 0.f;
+      const unsigned m = (on0 ? 0xffffu : 0u) | (on1 ? 0xffff0000u : 0u);
+      const unsigned d = dv[i] & m;
+      if (m != 0xffffffffu)
+        *reinterpret_cast<unsigned*>(dy + static_cast<int64_t>(r) * C + 2 * cp) = d;
+      s0 += bf2f(static_cast<bf16_t>(d & 0xffffu));
+      s1 += bf2f(static_cast<bf16_t>(d >> 16));
     }
   }
-  if (out) atomicAdd(out + c, s);
+  red[threadIdx.x][0] = s0;
+  red[threadIdx.x][1] = s1;
+  __syncthreads();
+  if (out && threadIdx.x < pairs) {
+    float t0 = 0.f, t1 = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      t0 += red[l * pairs + threadIdx.x][0];
+      t1 += red[l * pairs + threadIdx.x][1];
+    }
+    atomicAdd(out + 2 * threadIdx.x, t0);
+    atomicAdd(out + 2 * threadIdx.x + 1, t1);
+  }
 }
 
 // dx *= (x > 0), 8 bf16 per thread
@@ -623,10 +647,9 @@ void colsum_f32_launch(const float* x, int N, int C, float* out,
 
 void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
                             float* out, hipStream_t stream) {
-  dim3 grid((C + 255) / 256, (N + kColRows - 1) / kColRows);
-  hipLaunchKernelGGL(relu_bwd_colsum_kernel, grid, dim3(256), 0, stream,
-                     static_cast<bf16_t*>(dy), static_cast<const bf16_t*>(y), N,
-                     C, ldy, out);
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, dim3((N + kRbRows - 1) / kRbRows),
+                     dim3(256), 0, stream, static_cast<bf16_t*>(dy),
+                     static_cast<const bf16_t*>(y), N, C, ldy, out);
 }
 
 void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,

@@ -125,6 +125,8 @@ void relu_bwd_colsum_(at::Tensor dy, at::Tensor y, c10::optional<at::Tensor> out
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be row-major 2-D");
   const int N = dy.size(0), C = dy.size(1);
   TORCH_CHECK(y.size(0) == N && y.size(1) == C, "shape mismatch");
+  TORCH_CHECK(C % 2 == 0 && C <= 512 && 256 % (C / 2) == 0 && (C / 2) * 32 >= 256,
+              "relu_bwd_colsum_: C/2 must divide 256 and C >= 16");
   float* op = nullptr;
   if (out.has_value()) {
     LB_CHECK(*out); LB_F32(*out);

@@ -1,6 +1,7 @@
 """Loader for the in-tree HIP extension (`scalable_agent_amd/_C.so`)."""
 
 import importlib
+import importlib.util as importlib_util
 import os
 
 _EXT = None
@@ -14,7 +15,13 @@ def load():
     return _EXT
   try:
     import torch  # noqa: F401  (libtorch must be loaded first)
-    _EXT = importlib.import_module('scalable_agent_amd._C')
+    alt = os.environ.get('SA_EXT_PATH')  # experiment builds (e.g. ablation)
+    if alt:
+      spec = importlib_util.spec_from_file_location('scalable_agent_amd._C', alt)
+      _EXT = importlib_util.module_from_spec(spec)
+      spec.loader.exec_module(_EXT)
+    else:
+      _EXT = importlib.import_module('scalable_agent_amd._C')
   except Exception as e:  # pragma: no cover - depends on build state
     _ERR = e
     raise RuntimeError(

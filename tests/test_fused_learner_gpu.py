@@ -170,3 +170,36 @@ def test_fused_learner_loss_matches_generic_hip_path(cuda):
   (l1, g1), (l2, g2) = out
   torch.testing.assert_close(l1, l2, rtol=2e-3, atol=2e-2)
   assert _cos(g1, g2) > 0.999
+
+
+@pytest.mark.parametrize('N,C,ld', [(3232, 256, 272), (37, 16, 16), (5, 64, 80)])
+def test_glue_kernels_match_torch(cuda, N, C, ld):
+  """relu_bwd_colsum_ (masked in place + column sums, strided y), relu_mask,
+  colsum and core_aug against plain PyTorch."""
+  C_ = _ops().ext()
+  torch.manual_seed(N)
+  dy = torch.randn(N, C, device=cuda).bfloat16()
+  yfull = torch.randn(N, ld, device=cuda).bfloat16()
+  y = yfull[:, :C]
+  ref = dy.float() * (y.float() > 0)
+  out = torch.ones(C, device=cuda)
+  C_.relu_bwd_colsum_(dy, y, out)
+  torch.testing.assert_close(dy.float(), ref)
+  torch.testing.assert_close(out, 1 + ref.sum(0), rtol=1e-4, atol=1e-3)
+  x = torch.randn(N, C, device=cuda)
+  s = torch.zeros(C, device=cuda)
+  C_.colsum_f32_(x, s)
+  torch.testing.assert_close(s, x.sum(0), rtol=1e-4, atol=1e-3)
+  if (N * C) % 8 == 0:
+    d2 = torch.randn(N, C, device=cuda).bfloat16()
+    r2 = d2 * (yfull[:, :C].contiguous() > 0)
+    C_.relu_mask_bf16_(d2, yfull[:, :C].contiguous())
+    assert torch.equal(d2, r2)
+  h = torch.randn(N, C, device=cuda).bfloat16()
+  rw = torch.randn(N, device=cuda) * 3
+  act = torch.randint(0, 5, (N,), device=cuda)
+  aug = C_.core_aug_fwd(h, rw, act, C + 16, 0)
+  assert torch.equal(aug[:, :C], h)
+  assert torch.equal(aug[:, C].float(), rw.clamp(-1, 1).bfloat16().float())
+  oh = torch.nn.functional.one_hot(act, 15).bfloat16()
+  assert torch.equal(aug[:, C + 1:], oh)

@@ -56,5 +56,45 @@ def main():
   print('accumulate max err', float((g - ref).abs().max()), float(ref.abs().max()))
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and 'backends' not in __import__('sys').argv:
   main()
+
+
+def compare_backends():
+  """hipBLASLt (torch default) vs rocBLAS on the learner GEMM shapes."""
+  d = torch.device('cuda')
+  N, F, H, G, K = 3232, 3456, 256, 1024, 272
+  feats = torch.randn(N, F, device=d).bfloat16()
+  w = (torch.randn(F, H, device=d) * 0.02).bfloat16()
+  b = torch.randn(H, device=d).bfloat16()
+  h = torch.randn(N, K, device=d).relu().bfloat16()
+  wx = (torch.randn(K, G, device=d) * 0.05).bfloat16()
+  bias = torch.randn(G, device=d)
+  dg = torch.randn(N, G, device=d).bfloat16()
+  gx = torch.zeros(K, G, device=d)
+  gf = torch.zeros(F, H, device=d)
+  dh = torch.randn(N, H, device=d).bfloat16()
+  hp = torch.randn(N, 256, device=d)
+  dg32 = torch.randn(N, G, device=d)
+  gwh = torch.zeros(256, G, device=d)
+  shapes = [
+      ('fc fwd relu', lambda: torch._addmm_activation(b, feats, w)),
+      ('xproj fwd', lambda: torch.addmm(bias, h, wx, out_dtype=torch.float32)),
+      ('dWx', lambda: torch.addmm(gx, h.t(), dg, out_dtype=torch.float32, out=gx)),
+      ('dh', lambda: torch.mm(dg, wx[:256].t())),
+      ('dfeats', lambda: torch.mm(dh, w.t())),
+      ('dWfc', lambda: torch.addmm(gf, feats.t(), dh, out_dtype=torch.float32, out=gf)),
+      ('dWh fp32', lambda: gwh.addmm_(hp.t(), dg32)),
+  ]
+  for lib in ('hipblaslt', 'ck', 'hipblas'):
+    try:
+      torch.backends.cuda.preferred_blas_library(lib)
+    except Exception as ex:  # noqa
+      print(lib, 'unavailable', ex)
+      continue
+    for name, fn in shapes:
+      probe('%s %s' % (lib, name), fn)
+
+
+if __name__ == '__main__' and 'backends' in __import__('sys').argv:
+  compare_backends()
