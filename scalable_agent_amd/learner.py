@@ -18,6 +18,7 @@ static staging slots; the data-parallel gradient sum is one RCCL all-reduce on
 the flat gradient buffer.
 """
 
+import os
 import time
 
 import torch
@@ -140,6 +141,9 @@ class Learner:
     self.grad_sync = None
     self.popart = None
     self._aux = {}
+    # weight-gradient GEMMs on a side stream next to the torso backward
+    # (opt-in: measured within run-to-run noise, profiles/experiments.md)
+    self._overlap = os.environ.get('SA_OVERLAP_WGRAD', '0') == '1'
     if getattr(flags, 'popart', False):
       from .popart import PopArt
       self.popart = PopArt(self.agent.num_value_heads, flags.popart_beta,
@@ -157,7 +161,8 @@ class Learner:
                           self.popart, self._aux)
     with trace('backward'):
       from .ops import grad_sink
-      with grad_sink.direct_grads(self.use_fused):
+      with grad_sink.direct_grads(self.use_fused), \
+          grad_sink.overlap_weight_grads(self.use_fused and self._overlap):
         loss.backward()
     return loss
 

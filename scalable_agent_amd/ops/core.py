@@ -18,16 +18,22 @@ Backward:
   dh     = dG W_x[:256]^T ; dh *= (h > 0) ; db_fc += colsum dh
   dfeats = dh W_fc^T       dW_fc += feats^T dh
 Weight gradients accumulate straight into the learner's flat fp32 gradient
-buffer inside grad_sink.direct_grads(); the pad rows of W_x[:K] past the
+buffer inside grad_sink.direct_grads(), and inside
+grad_sink.overlap_weight_grads() the four weight-gradient products run on a
+side stream concurrently with the conv-torso backward; the pad rows of W_x[:K] past the
 one-hot (the first instruction rows) meet all-zero h_aug columns, so they
 receive exactly 0.  GEMMs are plain library GEMMs (hipBLASLt); the glue
 kernels are in csrc/kernels/learner_io.hip.
 """
 
+import contextlib
+
 import torch
 
 from . import grad_sink
 from ._ext import ext
+
+_nullctx = contextlib.nullcontext
 
 CORE = 256
 
@@ -82,14 +88,23 @@ class _CoreLSTM(torch.autograd.Function):
     dg2 = dg.view(N, G)
     dg16_2 = dg16.view(N, G)
     f32 = torch.float32
-    gk[f_in:].addmm_(hpm.view(N, CORE).t(), dg2)                    # W_h
-    gxk = gk[:K]
-    torch.addmm(gxk, h_aug.t(), dg16_2, out_dtype=f32, out=gxk)     # W_x rows
-    C.colsum_f32_(dg2, gb)                                          # b_lstm
+    # critical path: dfeats feeds the conv-torso backward
     dh = torch.mm(dg16_2, wx16[:CORE].t())                          # [N,256]
     C.relu_bwd_colsum_(dh, h_aug[:, :CORE], gbfc)                   # b_fc
     dfeats = torch.mm(dh, w16_fc.t())
-    torch.addmm(gwfc, feats.t(), dh, out_dtype=f32, out=gwfc)       # W_fc
+    # weight gradients only: on a side stream next to the torso backward
+    # when they accumulate into the learner's sinks (grad_sink overlap)
+    side = grad_sink.side_stream(dg.device) if all(direct) else None
+    if side is not None:
+      side.wait_stream(torch.cuda.current_stream(dg.device))
+      for t in (hpm, dg, dg16, h_aug, feats, dh):
+        t.record_stream(side)
+    with torch.cuda.stream(side) if side is not None else _nullctx():
+      gk[f_in:].addmm_(hpm.view(N, CORE).t(), dg2)                  # W_h
+      gxk = gk[:K]
+      torch.addmm(gxk, h_aug.t(), dg16_2, out_dtype=f32, out=gxk)   # W_x rows
+      C.colsum_f32_(dg2, gb)                                        # b_lstm
+      torch.addmm(gwfc, feats.t(), dh, out_dtype=f32, out=gwfc)     # W_fc
     dh0 = None
     if ctx.needs_input_grad[8]:
       keep0 = (done_u8[0] == 0).to(f32).unsqueeze(-1)

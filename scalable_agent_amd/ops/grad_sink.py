@@ -66,3 +66,46 @@ def sinks(params):
 def returned(views, direct):
   """Gradients to hand back to autograd: None where accumulated in place."""
   return tuple(None if d else g for g, d in zip(views, direct))
+
+
+# ---- off-critical-path weight-gradient GEMMs -------------------------------
+# Inside overlap_weight_grads(), ops may enqueue work that only produces
+# parameter gradients (into direct sinks) on a side stream, forked from the
+# current stream; the context joins every side stream back into the caller's
+# current stream on exit, so the optimizer (and a graph capture's end) sees
+# the finished gradients.  The fused core uses it to run dW_h / dW_x / dW_fc
+# / db_lstm next to the conv-torso backward instead of in front of it.
+_OVERLAP = False
+_SIDE_STREAMS = {}
+_PENDING = []
+
+
+@contextlib.contextmanager
+def overlap_weight_grads(on=True):
+  global _OVERLAP
+  prev = _OVERLAP
+  _OVERLAP = bool(on)
+  try:
+    yield
+  finally:
+    _OVERLAP = prev
+    join_side_streams()
+
+
+def side_stream(device):
+  """The side stream for gradient-only work, or None when not overlapping."""
+  if not (_OVERLAP and _DIRECT) or device.type != 'cuda':
+    return None
+  s = _SIDE_STREAMS.get(device)
+  if s is None:
+    s = torch.cuda.Stream(device)
+    _SIDE_STREAMS[device] = s
+  if s not in _PENDING:
+    _PENDING.append(s)
+  return s
+
+
+def join_side_streams():
+  while _PENDING:
+    s = _PENDING.pop()
+    torch.cuda.current_stream(s.device).wait_stream(s)
