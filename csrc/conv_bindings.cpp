@@ -87,6 +87,24 @@ at::Tensor res_conv_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
   return y;
 }
 
+// -> {t, y}: t = relu(conv1(relu(x)) + b1), y = conv2(t) + b2 + x [+ relu]
+std::vector<at::Tensor> res_block_fwd(at::Tensor x, at::Tensor w1, at::Tensor b1,
+                                      at::Tensor w2, at::Tensor b2, bool post_relu) {
+  const int64_t C = x.size(3);
+  TORCH_CHECK(supported(C), "channels must be 16/32");
+  check_act(x, "x", C);
+  check_w(w1, b1, C, C);
+  check_w(w2, b2, C, C);
+  const c10::DeviceGuard g(x.device());
+  auto t = at::empty_like(x);
+  auto y = at::empty_like(x);
+  sa::conv::res_block_fwd_launch(x.data_ptr(), w1.data_ptr<float>(), b1.data_ptr<float>(),
+                                 w2.data_ptr<float>(), b2.data_ptr<float>(), t.data_ptr(),
+                                 y.data_ptr(), x.size(0), x.size(1), x.size(2), C,
+                                 post_relu, stream());
+  return {t, y};
+}
+
 // dx = [skip +] dgrad(dy) * (act > 0); dW += relu?(act)^T dy; db += sum dy
 at::Tensor res_conv_bwd(at::Tensor dy, at::Tensor act, c10::optional<at::Tensor> skip,
                         at::Tensor w, at::Tensor dw, at::Tensor db, bool relu_act) {
@@ -161,6 +179,7 @@ void conv1_pool_bwd(at::Tensor dP, at::Tensor arg, at::Tensor x, at::Tensor dw,
 void register_conv_ops(pybind11::module& m) {
   m.def("conv1_pool_fwd", &conv1_pool_fwd);
   m.def("conv_pool_fwd", &conv_pool_fwd);
+  m.def("res_block_fwd", &res_block_fwd);
   m.def("res_conv_fwd", &res_conv_fwd, pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("b"), pybind11::arg("resid") = pybind11::none(),
         pybind11::arg("post_relu") = false, pybind11::arg("relu_in") = true);

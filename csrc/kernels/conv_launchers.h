@@ -23,6 +23,12 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,
                          int C, bool post_relu, bool relu_in, hipStream_t s);
+// Whole residual block: t = relu(conv1(relu(x)) + b1) (written, for the
+// backward), y = conv2(t) + b2 + x [then relu].
+void res_block_fwd_launch(const void* x, const float* w1, const float* b1,
+                          const float* w2, const float* b2, void* t, void* y,
+                          int N, int H, int W, int C, bool post_relu,
+                          hipStream_t s);
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
                          int H, int W, int C, bool relu_act, hipStream_t s);

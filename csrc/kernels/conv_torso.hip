@@ -891,6 +891,93 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   }
 }
 
+// Whole residual block forward in one pass (reference experiment.py:170-175):
+//   t = relu(conv1(relu(x)) + b1)          (stored ReLU'd, for the backward)
+//   y = conv2(t) + b2 + x  [+ final relu]
+// A tile of R output rows stages x rows [r0-2, r0+R+2) once, computes t for
+// rows [r0-1, r0+R+1) into an LDS halo image (the two halo rows are
+// recomputed by the neighbouring tiles too; rows outside the image are the
+// zero padding of conv2), writes t rows [r0, r0+R) to HBM and y straight
+// from conv2's epilogue.  Against two res_conv_fwd launches this removes the
+// HBM write+read of t by conv2 and one launch per block.
+template <int C, bool POST_RELU, int HC, int WC, int RC>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void res_block_fwd_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ b2, bf16_t* __restrict__ t_out,
+    bf16_t* __restrict__ y, int N, int H_, int W_, int R_, int xcd) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
+  const int RP = row_pitch(C, W);
+  bf16_t* w1_s = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* w2_s = w1_s + w_lds_elems(C, C, true);
+  bf16_t* x_s = w2_s + w_lds_elems(C, C, true);   // (R+4) rows + pad pixel
+  bf16_t* t_s = x_s + (R + 4) * RP + C;           // (R+2) rows + pad pixel
+  load_weights4<C, C, true>(w1, w1_s);
+  load_weights4<C, C, true>(w2, w2_s);
+  float bq1[C / 16][4], bq2[C / 16][4];
+  bias_regs<C>(b1, reinterpret_cast<float*>(x_s), bq1);
+  __syncthreads();
+  bias_regs<C>(b2, reinterpret_cast<float*>(x_s) + C, bq2);
+  // t_s halo columns stay zero for the whole kernel (epilogues write only
+  // interior pixels)
+  for (int e = threadIdx.x; e < (R + 2) * 2 * (C / 8); e += kThreads) {
+    const int rr = e / (2 * (C / 8)), side = (e / (C / 8)) & 1, part = e % (C / 8);
+    *reinterpret_cast<uint4*>(t_s + rr * RP + (side ? W + 1 : 0) * C + part * 8) =
+        make_uint4(0, 0, 0, 0);
+  }
+  const int tpi = (H + R - 1) / R;
+  const int ntiles = N * tpi;
+  RowStager<C, NREG> sx;
+  const TileIter it(ntiles, xcd);
+  int tile = it.first;
+  if (it.valid(tile)) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    sx.issue(x, n, H, W, r0 - 2, Rv + 4);
+  }
+  for (; it.valid(tile); tile = it.next(tile)) {
+    const int n = tile / tpi, r0 = (tile - n * tpi) * R, Rv = min(R, H - r0);
+    __syncthreads();
+    if (kKeep(xcd, 8))
+    sx.template commit<true, true>(x_s, W);
+    // zero pixel after t's last row (read with zero weights by paired taps)
+    for (int e = threadIdx.x; e < C / 8; e += kThreads)
+      *reinterpret_cast<uint4*>(t_s + (Rv + 2) * RP + e * 8) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
+    EpiOperand<C, FwdChunks<C, C>> rop;  // skip = raw x rows [r0, r0+Rv)
+    rop.load(x, img0, Rv * W, W);
+    const int nt = it.next(tile);
+    if (it.valid(nt)) {
+      const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
+      sx.issue(x, n2, H, W, r2 - 2, Rv2 + 4);
+    }
+    if (kKeep(xcd, 4))
+    conv_tile_fwd<C, C>(x_s, w1_s, W, (Rv + 2) * W, [&](int q, int co0, float v[4], int) {
+      const int qr = q / W, qc = q - qr * W;
+      const int r = r0 - 1 + qr;  // image row of this t pixel
+      const bool in = r >= 0 && r < H;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = in ? fmaxf(v[i] + bq1[co0 >> 4][i], 0.f) : 0.f;
+      store4(t_s + qr * RP + (qc + 1) * C + co0, v);
+      if (qr >= 1 && qr <= Rv) store4(t_out + (img0 + q - W) * C + co0, v);
+    });
+    __syncthreads();
+    if (kKeep(xcd, 4))
+    conv_tile_fwd<C, C>(t_s, w2_s, W, Rv * W, [&](int q, int co0, float v[4], int slot) {
+      float r[4];
+      rop.get(slot, co0, r);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] += bq2[co0 >> 4][i];  // same rounding order as res_conv_fwd
+        v[i] += r[i];
+        if (POST_RELU) v[i] = fmaxf(v[i], 0.f);
+      }
+      store4(y + (img0 + q) * C + co0, v);
+    });
+  }
+}
+
 template <int CIN, int COUT, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ w,
@@ -1382,6 +1469,16 @@ constexpr int rows_for(int H, int W, int C, int target) {
     --R;
   return R < H ? R : H;
 }
+// fused residual block: x staged with 2 halo rows each side, t computed
+// for R + 2 rows
+constexpr int rows_block(int H, int W, int C, int target) {
+  int R = target / W;
+  if (R < 1) R = 1;
+  while (R > 1 && ((R + 4) * W * C / 8 > NREG * kThreads ||
+                   tile_groups(C, R + 2, W) > kMaxTilePx(C) / 16))
+    --R;
+  return R < H ? R : H;
+}
 constexpr int rows_pool_fwd(int H, int W, int CIN, int px) {
   const int Hp = (H + 1) / 2;
   int Rp = (px / W - 1) / 2;
@@ -1512,6 +1609,10 @@ struct RowsResFwd {
   static constexpr int rows(int H, int W) { return rows_for(H, W, C, kDef.px_res_fwd); }
 };
 template <int C>
+struct RowsBlockFwd {
+  static constexpr int rows(int H, int W) { return rows_block(H, W, C, kDef.px_res_fwd); }
+};
+template <int C>
 struct RowsResBwd {
   static constexpr int rows(int H, int W) { return rows_for(H, W, C, kDef.px_res_bwd); }
 };
@@ -1535,6 +1636,42 @@ struct RowsConv1Bwd {
 }  // namespace
 
 int res_conv_rows(int H, int W) { return rows_for(H, W, 32, g_tune.px_res_fwd); }
+
+void res_block_fwd_launch(const void* x, const float* w1, const float* b1,
+                          const float* w2, const float* b2, void* t, void* y,
+                          int N, int H, int W, int C, bool post_relu,
+                          hipStream_t s) {
+  const int R = rows_block(H, W, C, g_tune.px_res_fwd);
+  require_fit((R + 4) * W * C / 8 <= NREG * kThreads &&
+                  tile_groups(C, R + 2, W) <= kMaxTilePx(C) / 16,
+              "res_block_fwd");
+  const int ntiles = N * ((H + R - 1) / R);
+  const size_t smem = (2 * w_lds_elems(C, C, true) + (R + 4) * row_pitch(C, W) + C +
+                       (R + 2) * row_pitch(C, W) + C) * sizeof(bf16_t);
+  const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
+  auto X = static_cast<const bf16_t*>(x);
+  auto Tt = static_cast<bf16_t*>(t);
+  auto Y = static_cast<bf16_t*>(y);
+  const int xcd = g_tune.xcd | (g_tune.ablate << 8);
+  auto go = [&](auto kernel) {
+    set_smem(kernel, smem);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, X, w1, b1,
+                       w2, b2, Tt, Y, N, H, W, R, xcd);
+  };
+#define SA_RB(CC, PR, STG)                                                     \
+  with_geo<STG, RowsBlockFwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {      \
+    go(res_block_fwd_kernel<CC, PR, decltype(h)::value, decltype(ww)::value,   \
+                            decltype(r)::value>);                              \
+  })
+  if (C == 16) {
+    if (post_relu) SA_RB(16, true, kStage1); else SA_RB(16, false, kStage1);
+  } else if (H * 2 > 18 + 9) {
+    if (post_relu) SA_RB(32, true, kStage2); else SA_RB(32, false, kStage2);
+  } else {
+    if (post_relu) SA_RB(32, true, kStage3); else SA_RB(32, false, kStage3);
+  }
+#undef SA_RB
+}
 
 void res_conv_fwd_launch(const void* x, const float* w, const float* b,
                          const void* resid, void* y, int N, int H, int W,

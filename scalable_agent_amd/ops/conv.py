@@ -11,6 +11,8 @@ All activations NHWC bf16; weights/biases fp32 master copies (TF HWIO); their
 gradients accumulate in fp32 directly inside the kernels.
 """
 
+import os
+
 import torch
 
 from . import grad_sink
@@ -18,6 +20,11 @@ from ._ext import ext
 from ..models import layers
 
 TORSO_READY = True
+# whole-residual-block forward kernel (res_block_fwd) instead of two
+# res_conv_fwd launches: opt-in (SA_FUSED_BLOCK=1) - bitwise identical but
+# measured slower (206 vs 169 us at 36x48x16, 143 vs 102 at 18x24x32): the
+# convs are latency/issue bound, not HBM bound (profiles/experiments.md)
+FUSED_BLOCK = os.environ.get('SA_FUSED_BLOCK', '0') == '1'
 
 
 def supports(agent):
@@ -68,9 +75,13 @@ class _DeepTorso(torch.autograd.Function):
         # t is stored ReLU'd: it is only ever consumed as relu(t) (conv 2's
         # input, and the (t > 0) mask in backward), so conv 2 skips its
         # input ReLU and its backward skips the activation ReLU.
-        t = C.res_conv_fwd(xa, w1, b1, None, True, True)
         last = (s == 2 and blk == 1)
-        y = C.res_conv_fwd(t, w2, b2, xa, last, False)
+        if FUSED_BLOCK:
+          # both convs of the block in one pass (t never re-read from HBM)
+          t, y = C.res_block_fwd(xa, w1, b1, w2, b2, last)
+        else:
+          t = C.res_conv_fwd(xa, w1, b1, None, True, True)
+          y = C.res_conv_fwd(t, w2, b2, xa, last, False)
         saved += [xa, t]
         xa = y
       if s < 2:

@@ -278,3 +278,22 @@ def test_specialized_geometry_matches_generic(cuda, frame):
       close(a, b, 1e-4)
     else:
       assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('C,H,W,last', [(16, 36, 48, False), (32, 18, 24, False),
+                                        (32, 9, 12, True), (16, 10, 14, False),
+                                        (32, 7, 5, True)])
+def test_res_block_fwd_matches_two_convs(cuda, C, H, W, last):
+  """The fused residual-block forward reproduces the two-launch form
+  (conv1 with ReLU-in/ReLU-out, conv2 with the skip) exactly."""
+  torch.manual_seed(C + H)
+  x = torch.randn(3, H, W, C, device=cuda).to(torch.bfloat16)
+  w1 = torch.randn(3, 3, C, C, device=cuda) * 0.2
+  w2 = torch.randn(3, 3, C, C, device=cuda) * 0.2
+  b1 = torch.randn(C, device=cuda) * 0.1
+  b2 = torch.randn(C, device=cuda) * 0.1
+  t_ref = _C().res_conv_fwd(x, w1, b1, None, True, True)
+  y_ref = _C().res_conv_fwd(t_ref, w2, b2, x, last, False)
+  t, y = _C().res_block_fwd(x, w1, b1, w2, b2, last)
+  assert torch.equal(t, t_ref)
+  assert torch.equal(y, y_ref)

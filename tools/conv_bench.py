@@ -57,16 +57,22 @@ def cases(n):
       ('res_fwd16', 2, 2 * B16, lambda: C.res_conv_fwd(x16, w16, b16, None, True, True)),
       ('res_fwd16_resid', 2, 3 * B16,
        lambda: C.res_conv_fwd(x16, w16, b16, x16, False, False)),
+      ('block_fwd16 (fused)', 0, 3 * B16,
+       lambda: C.res_block_fwd(x16, w16, b16, w16, b16, False)),
       ('conv_pool_fwd16_32', 1, B16 + B32 * 3 // 2,
        lambda: C.conv_pool_fwd(x16, w1632, b32, 0, 0)),
       ('res_fwd32', 2, 2 * B32, lambda: C.res_conv_fwd(x32, w32_, b32, None, True, True)),
       ('res_fwd32_resid', 2, 3 * B32,
        lambda: C.res_conv_fwd(x32, w32_, b32, x32, False, False)),
+      ('block_fwd32 (fused)', 0, 3 * B32,
+       lambda: C.res_block_fwd(x32, w32_, b32, w32_, b32, False)),
       ('conv_pool_fwd32_32', 1, B32 + B9 * 3 // 2,
        lambda: C.conv_pool_fwd(x32, w32_, b32, 0, 0)),
       ('res_fwd9', 2, 2 * B9, lambda: C.res_conv_fwd(x9, w32_, b32, None, True, True)),
       ('res_fwd9_resid', 2, 3 * B9,
        lambda: C.res_conv_fwd(x9, w32_, b32, x9, True, False)),
+      ('block_fwd9 (fused)', 0, 3 * B9,
+       lambda: C.res_block_fwd(x9, w32_, b32, w32_, b32, True)),
       ('res_bwd9', 2, 3 * B9,
        lambda: C.res_conv_bwd(d9, x9, None, w32_, dw32, db32, False)),
       ('res_bwd9_skip', 2, 4 * B9,
@@ -130,7 +136,7 @@ def main():
     print('config %s: torso kernels %.1f us/step' % (json.dumps(cfg), tot),
           flush=True)
     for name, calls, us, gbs in rows:
-      print('  %-20s x%d %8.1f us  %6.0f GB/s' % (name, calls, us, gbs))
+      print('  %-20s x%d %8.1f us  %6.0f GB/s' % (name[:20], calls, us, gbs))
     results[json.dumps(cfg)] = tot
     for k, v in old.items():
       C.conv_tune(k, v)
