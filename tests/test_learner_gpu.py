@@ -85,3 +85,30 @@ def test_pipelined_unroll_matches_serial(cuda):
   torch.cuda.synchronize()
   torch.testing.assert_close(lg.float(), l4.float(), rtol=1e-3, atol=1e-3)
   assert not torch.equal(before, lrn4.flat.params)
+
+
+def test_experiment_train_and_test_on_gpu(tmp_path):
+  """The full driver on the GPU: actor threads with batched GPU inference
+  (fused core at T=1), the HIP-graph learner on the fused path, checkpoint,
+  then --mode=test from the checkpoint (reference Dockerfile smoke, deep
+  torso)."""
+  import os
+  import subprocess
+  import sys
+  if not torch.cuda.is_available():
+    pytest.skip('no GPU')
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  common = [sys.executable, os.path.join(root, 'experiment.py'),
+            '--level_name=synthetic', '--torso=deep', '--unroll_length=8',
+            '--synthetic_episode_length=10', '--logdir=' + str(tmp_path)]
+  env = dict(os.environ, PYTHONPATH=root)
+  r = subprocess.run(common + ['--num_actors=4', '--batch_size=4',
+                               '--total_environment_frames=1280',
+                               '--save_summaries_secs=0'],
+                     capture_output=True, text=True, timeout=100, env=env)
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Episode return' in r.stderr
+  r = subprocess.run(common + ['--mode=test', '--test_num_episodes=2'],
+                     capture_output=True, text=True, timeout=100, env=env)
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Mean episode return' in r.stderr
