@@ -256,6 +256,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_set_persistent", &lstm_set_persistent);
   m.def("lstm_get_persistent", &lstm_get_persistent);
   m.def("lstm_error_word", &lstm_error);
+  m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);
   register_conv_ops(m);
   register_learner_ops(m);

@@ -55,6 +55,10 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const float* dcarry_in, float* dcarry_out,
                           float* dg_t, float* dg_pk_out, void* dg16_t, int B,
                           int H, hipStream_t stream);
+// Step-kernel placement knob: 1 = plain grid; 8 = launch 8x the blocks and let
+// only every 8th work, i.e. all working blocks on one XCD (SA_LSTM_XPACK).
+// v outside [1, 8] only queries.  Returns the previous value.
+int lstm_xpack(int v);
 // W_h [H,4H] -> fwd-packed w4 and bwd-packed wt (one launch per unroll).
 void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                               hipStream_t stream);

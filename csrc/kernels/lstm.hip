@@ -23,6 +23,8 @@
 
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+
 namespace sa {
 namespace {
 
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     const uint8_t* __restrict__ done_t, const float* __restrict__ w4,
     float* __restrict__ h_t, float* __restrict__ h_pk_out,
     float* __restrict__ c_t, float* __restrict__ acts_t,
-    float* __restrict__ hpm_t, int B) {
+    float* __restrict__ hpm_t, int B, int xpack) {
   constexpr int NW = 8;
   constexpr int KW = H / NW;     // k per wave
   constexpr int NS = KW / 4;     // mfma k-steps per wave
@@ -58,7 +60,10 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int blk = blockIdx.x;
+  // xpack > 1: only every xpack-th block works, so with round-robin XCD
+  // dispatch all working blocks share one XCD (and its L2)
+  if (blockIdx.x % xpack) return;
+  const int blk = blockIdx.x / xpack;
   const int r0 = blockIdx.y * 32;
   // epilogue operands (thread = (row r, unit u) for tid < 128)
   const int er = tid >> 2, eu = tid & 3;
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     const float* __restrict__ c_t, const float* __restrict__ c_prev,
     const float* __restrict__ dcarry_in, float* __restrict__ dcarry_out,
     float* __restrict__ dg_t, float* __restrict__ dg_pk_out,
-    __hip_bfloat16* __restrict__ dg16_t, int B) {
+    __hip_bfloat16* __restrict__ dg16_t, int B, int xpack) {
   const float* dg_next = dg_pk_in;
   constexpr int NW = 16;
   constexpr int NWID = 4 * H / NW;  // n per wave
@@ -172,7 +177,9 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int u0 = blockIdx.x * 16;
+  if (blockIdx.x % xpack) return;
+  const int bx = blockIdx.x / xpack;
+  const int u0 = bx * 16;
   const int r0 = blockIdx.y * 32;
   // epilogue operands: thread = (row er, unit eu) for tid < 512
   const int er = tid >> 4, eu = tid & 15;
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
   if (dg_next != nullptr) {
     // B[k = n][col = unit]: W_h[u0 + (l&15)][n0 + 4s + (l>>4)] (packed)
     float wb[NS];
-    const float* wsrc = wt + (static_cast<int64_t>(blockIdx.x) * NW + wave) * NS * 64 + lane;
+    const float* wsrc = wt + (static_cast<int64_t>(bx) * NW + wave) * NS * 64 + lane;
 #pragma unroll
     for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 64];
     float da[2][NS];
@@ -283,20 +290,35 @@ void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                        stream, w, w4, wt);
 }
 
+// Default 4 (working blocks on 2 of the 8 XCDs): measured 469 -> 448 us fwd
+// and 739 -> 724 us bwd per T=101 unroll at B=32 (tools/micro/lstm_probe.py,
+// two runs); 8 (one XCD) oversubscribes its 32 CUs in the fwd (533 us).
+static int g_xpack = [] {
+  const char* e = std::getenv("SA_LSTM_XPACK");
+  const int v = e ? std::atoi(e) : 4;
+  return v >= 1 && v <= 8 ? v : 4;
+}();
+int lstm_xpack(int v) {
+  const int old = g_xpack;
+  if (v >= 1 && v <= 8) g_xpack = v;
+  return old;
+}
+
 void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           const float* h_prev, const float* c_prev,
                           const uint8_t* done_t, const float* w4, float* h_t,
                           float* h_pk_out, float* c_t, float* acts_t,
                           float* hpm_t, int B, int H, hipStream_t stream) {
-  dim3 grid(H / 4, (B + 31) / 32);
+  const int xp = g_xpack;
+  dim3 grid(H / 4 * xp, (B + 31) / 32);
   if (H == 256) {
     hipLaunchKernelGGL(lstm_fwd_step_kernel<256>, grid, dim3(512), 0, stream,
                        xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
-                       c_t, acts_t, hpm_t, B);
+                       c_t, acts_t, hpm_t, B, xp);
   } else if (H == 64) {
     hipLaunchKernelGGL(lstm_fwd_step_kernel<64>, grid, dim3(512), 0, stream,
                        xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
-                       c_t, acts_t, hpm_t, B);
+                       c_t, acts_t, hpm_t, B, xp);
   }
 }
 
@@ -307,16 +329,17 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const float* dcarry_in, float* dcarry_out,
                           float* dg_t, float* dg_pk_out, void* dg16_t, int B,
                           int H, hipStream_t stream) {
-  dim3 grid(H / 16, (B + 31) / 32);
+  const int xp = g_xpack;
+  dim3 grid(H / 16 * xp, (B + 31) / 32);
   __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
   if (H == 256) {
     hipLaunchKernelGGL(lstm_bwd_step_kernel<256>, grid, dim3(1024), 0, stream,
                        dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
-                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B);
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B, xp);
   } else if (H == 64) {
     hipLaunchKernelGGL(lstm_bwd_step_kernel<64>, grid, dim3(1024), 0, stream,
                        dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
-                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B);
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B, xp);
   }
 }
 

@@ -40,12 +40,13 @@ def main():
   h0 = torch.randn(B, H, device=d) * 0.5
   w_h = torch.randn(H, 4 * H, device=d) * 0.05
   dh = torch.randn(T, B, H, device=d)
-  for mode in (False, True):
+  for mode, xp in ((False, 1), (False, 2), (False, 4), (False, 8), (True, 1)):
     lstm_ops.set_persistent(mode)
+    C.lstm_xpack(xp)
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
     f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h)
     b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True)
-    print('persistent=%d fwd %8.1f us  bwd %8.1f us' % (mode, t_us(f), t_us(b)),
+    print('persistent=%d xpack=%d fwd %8.1f us  bwd %8.1f us' % (mode, xp, t_us(f), t_us(b)),
           flush=True)
   print('error word', lstm_ops.persistent_error(d))
 
