@@ -37,7 +37,9 @@ def init_distributed(backend=None, timeout_s=600):
     return 0, 1, 0
   if not dist.is_initialized():
     if backend is None:
-      backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+      # SA_DIST_BACKEND=gloo: rehearse the multi-rank GPU path on one card
+      backend = os.environ.get('SA_DIST_BACKEND') or (
+          'nccl' if torch.cuda.is_available() else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     os.environ.setdefault('MASTER_PORT', '29500')
     kwargs = dict(backend=backend, rank=rank, world_size=world,
