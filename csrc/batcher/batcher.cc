@@ -263,6 +263,51 @@ Status Batcher::GetInputsInto(const std::vector<void*>& dst,
   return Status::OK();
 }
 
+Status Batcher::GetInputsPacked(void* dst, size_t cap, size_t align,
+                                std::vector<TensorMeta>* metas,
+                                std::vector<size_t>* offsets, size_t* used,
+                                int64_t* batch_size, int64_t* computation_id) {
+  std::vector<Request*> reqs;
+  int64_t id = -1;
+  Status st = TakeBatch(&reqs, &id);
+  if (!st.ok()) return st;
+  const auto& first = *reqs[0]->inputs;
+  const int64_t n = static_cast<int64_t>(reqs.size());
+  if (align == 0) align = 1;
+  metas->clear();
+  offsets->clear();
+  size_t off = 0;
+  for (size_t k = 0; k < first.size(); ++k) {
+    TensorMeta m = first[k].meta;
+    m.shape[0] = n;
+    off = (off + align - 1) / align * align;
+    offsets->push_back(off);
+    off += m.nbytes();
+    metas->push_back(m);
+  }
+  if (off > cap) {
+    st = Status::Invalid("GetInputsPacked: staging slab too small (" +
+                         std::to_string(off) + " > " + std::to_string(cap) + " bytes)");
+    MutexLock l(&mu_);
+    copying_.erase(id);
+    CancelAndCloseLocked();
+    return st;
+  }
+  uint8_t* base = static_cast<uint8_t*>(dst);
+  for (size_t k = 0; k < first.size(); ++k) {
+    const size_t row = (*metas)[k].row_bytes();
+    uint8_t* seg = base + (*offsets)[k];
+    for (int64_t i = 0; i < n; ++i)
+      std::memcpy(seg + i * row, (*reqs[i]->inputs)[k].data, row);
+  }
+  EndCopy(id, &st);
+  if (!st.ok()) return st;
+  *used = off;
+  *batch_size = n;
+  *computation_id = id;
+  return Status::OK();
+}
+
 Status Batcher::SetOutputs(const std::vector<TensorView>& outputs,
                            int64_t computation_id) {
   std::vector<Request*> reqs;

@@ -96,6 +96,16 @@ class Batcher {
                        std::vector<TensorMeta>* metas, int64_t* batch_size,
                        int64_t* computation_id) SA_EXCLUDES(mu_);
 
+  // Packed staging: the n rows of input k land at dst + offsets[k], the
+  // segments back to back (each start aligned to `align` bytes), so the
+  // whole batched input is ONE contiguous range [0, *used) of the slab and
+  // reaches the GPU with a single host->device copy.
+  Status GetInputsPacked(void* dst, size_t cap, size_t align,
+                         std::vector<TensorMeta>* metas,
+                         std::vector<size_t>* offsets, size_t* used,
+                         int64_t* batch_size, int64_t* computation_id)
+      SA_EXCLUDES(mu_);
+
   Status SetOutputs(const std::vector<TensorView>& outputs,
                     int64_t computation_id) SA_EXCLUDES(mu_);
 

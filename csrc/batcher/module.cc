@@ -131,6 +131,26 @@ class PyBatcher {
     return py::make_tuple(n, id, m);
   }
 
+  // Packed variant: one slab (address, capacity); returns (batch_size, id,
+  // used_bytes, [(dtype, shape, offset)]).
+  py::tuple GetInputsPacked(uintptr_t addr, size_t cap, size_t align) {
+    std::vector<TensorMeta> metas;
+    std::vector<size_t> offs;
+    size_t used = 0;
+    int64_t n = 0, id = -1;
+    Status s;
+    {
+      py::gil_scoped_release nogil;
+      s = b_.GetInputsPacked(reinterpret_cast<void*>(addr), cap, align, &metas,
+                             &offs, &used, &n, &id);
+    }
+    if (!s.ok()) Raise(s);
+    py::list m;
+    for (size_t k = 0; k < metas.size(); ++k)
+      m.append(py::make_tuple(metas[k].dtype, py::cast(metas[k].shape), offs[k]));
+    return py::make_tuple(n, id, used, m);
+  }
+
   void SetOutputs(const py::list& outputs, int64_t id) {
     std::vector<py::array> keep;
     std::vector<TensorView> views;
@@ -185,6 +205,8 @@ PYBIND11_MODULE(_native, m) {
       .def("compute", &PyBatcher::Compute)
       .def("get_inputs", &PyBatcher::GetInputs)
       .def("get_inputs_into", &PyBatcher::GetInputsInto)
+      .def("get_inputs_packed", &PyBatcher::GetInputsPacked, py::arg("address"),
+           py::arg("capacity"), py::arg("align") = 256)
       .def("set_outputs", &PyBatcher::SetOutputs)
       .def("close", &PyBatcher::Close)
       .def("cancel", &PyBatcher::Cancel)

@@ -1,0 +1,103 @@
+// Actor-inference head: policy logits + baseline + categorical sample in ONE
+// launch (reference experiment.py:200-210: Linear(A) policy, Linear(1)
+// baseline, tf.multinomial(logits, 1); SURVEY.md §2.3 K10 + K11).
+//
+// One 64-lane wavefront per batch row.  Lane l holds h[4l..4l+3] (one 16-byte
+// load), forms its 4-term partial dot product for every output column and the
+// row's A+1 sums are finished with a butterfly (every lane ends with every
+// logit; no LDS, no barriers).  Lane a < A then draws u_a from Philox4x32-10
+// (key = seed, counter = (row, a, offset)) and the action is the Gumbel-max
+// argmax_a (logit_a - log(-log u_a)), reduced across the wave with the lower
+// index winning ties - an exact sample from softmax(logits), reproducible for
+// a given (seed, offset) whatever the batch composition of the other rows.
+#include "launchers.h"
+
+namespace sa {
+namespace {
+
+constexpr int kMaxA = 32;
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(256) void actor_head_sample_kernel(
+    const float* __restrict__ h, const float* __restrict__ wp,
+    const float* __restrict__ bp, const float* __restrict__ wb,
+    const float* __restrict__ bb, float* __restrict__ logits,
+    float* __restrict__ baseline, int64_t* __restrict__ action, int B, int A,
+    unsigned long long seed, unsigned long long offset) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;  // whole wave exits together
+  const float4 x = reinterpret_cast<const float4*>(h + (int64_t)row * 256)[lane];
+  const float* w0 = wp + (4 * lane) * A;
+  float acc[kMaxA + 1];
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a)
+    acc[a] = a < A ? x.x * w0[a] + x.y * w0[A + a] + x.z * w0[2 * A + a] +
+                         x.w * w0[3 * A + a]
+                   : 0.f;
+  const float4 wv = reinterpret_cast<const float4*>(wb)[lane];
+  acc[kMaxA] = x.x * wv.x + x.y * wv.y + x.z * wv.z + x.w * wv.w;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+#pragma unroll
+    for (int a = 0; a <= kMaxA; ++a)
+      if (a < A || a == kMaxA) acc[a] += __shfl_xor(acc[a], m, 64);
+  }
+  float mine = -INFINITY;
+#pragma unroll
+  for (int a = 0; a < kMaxA; ++a)
+    if (a == lane) mine = acc[a];
+  float key = -INFINITY;
+  if (lane < A) {
+    mine += bp[lane];
+    logits[(int64_t)row * A + lane] = mine;
+    const uint4 r = philox4x32_10(
+        make_uint4((unsigned)row, (unsigned)lane, (unsigned)offset,
+                   (unsigned)(offset >> 32)),
+        make_uint2((unsigned)seed, (unsigned)(seed >> 32)));
+    const float u = ((r.x >> 8) + 0.5f) * (1.0f / 16777216.0f);  // (0,1)
+    key = mine - __logf(-__logf(u));
+  }
+  int idx = lane;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const float ok = __shfl_xor(key, m, 64);
+    const int oi = __shfl_xor(idx, m, 64);
+    if (ok > key || (ok == key && oi < idx)) {
+      key = ok;
+      idx = oi;
+    }
+  }
+  if (lane == 0) {
+    baseline[row] = acc[kMaxA] + bb[0];
+    action[row] = idx;
+  }
+}
+
+}  // namespace
+
+int actor_head_max_actions() { return kMaxA; }
+
+void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
+                              const float* wb, const float* bb, float* logits,
+                              float* baseline, int64_t* action, int B, int A,
+                              unsigned long long seed, unsigned long long offset,
+                              hipStream_t stream) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(actor_head_sample_kernel, dim3((B + 3) / 4), dim3(256), 0,
+                     stream, h, wp, bp, wb, bb, logits, baseline, action, B, A,
+                     seed, offset);
+}
+
+}  // namespace sa

@@ -117,6 +117,17 @@ void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
 void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,
                            hipStream_t stream);
 
+// ---- actor_io.hip ----------------------------------------------------------
+// Actor inference head: logits [B,A] = h Wp + bp, baseline [B] = h Wb + bb,
+// action [B] ~ Categorical(softmax(logits)) by Gumbel-max over Philox4x32-10
+// (key = seed, counter = (row, a, offset)).  h fp32 [B,256], A <= 32.
+int actor_head_max_actions();
+void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
+                              const float* wb, const float* bb, float* logits,
+                              float* baseline, int64_t* action, int B, int A,
+                              unsigned long long seed, unsigned long long offset,
+                              hipStream_t stream);
+
 // ---- calibration ----------------------------------------------------------
 void noop_launch(int blocks, int threads, int* p, hipStream_t s);
 

@@ -145,6 +145,37 @@ void relu_mask_bf16_(at::Tensor dx, at::Tensor x) {
   sa::relu_mask_bf16_launch(dx.data_ptr(), x.data_ptr(), dx.numel(), stream());
 }
 
+// Actor inference head + sampler: h [B,256] f32 -> {logits [B,A], baseline
+// [B], action [B] int64}.  (seed, offset) select the Philox stream; the
+// caller advances offset once per call.
+std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tensor bp,
+                                          at::Tensor wb, at::Tensor bb, int64_t seed,
+                                          int64_t offset) {
+  LB_CHECK(h); LB_CHECK(wp); LB_CHECK(bp); LB_CHECK(wb); LB_CHECK(bb);
+  LB_F32(h); LB_F32(wp); LB_F32(bp); LB_F32(wb); LB_F32(bb);
+  TORCH_CHECK(h.dim() == 2 && h.size(1) == 256, "h must be [B,256]");
+  TORCH_CHECK(wp.dim() == 2 && wp.size(0) == 256, "policy w must be [256,A]");
+  const int B = h.size(0), A = wp.size(1);
+  TORCH_CHECK(A >= 1 && A <= sa::actor_head_max_actions(), "1 <= num_actions <= 32");
+  TORCH_CHECK(bp.numel() == A && wb.numel() == 256 && bb.numel() == 1,
+              "one value head");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(wb.data_ptr()) % 16 == 0,
+              "h / baseline w must be 16-byte aligned");
+  const c10::DeviceGuard guard(h.device());
+  auto logits = at::empty({B, A}, h.options());
+  auto baseline = at::empty({B}, h.options());
+  auto action = at::empty({B}, h.options().dtype(at::kLong));
+  sa::actor_head_sample_launch(h.data_ptr<float>(), wp.data_ptr<float>(),
+                               bp.data_ptr<float>(), wb.data_ptr<float>(),
+                               bb.data_ptr<float>(), logits.data_ptr<float>(),
+                               baseline.data_ptr<float>(),
+                               action.data_ptr<int64_t>(), B, A,
+                               static_cast<unsigned long long>(seed),
+                               static_cast<unsigned long long>(offset), stream());
+  return {logits, baseline, action};
+}
+
 }  // namespace
 
 void register_learner_ops(pybind11::module& m) {
@@ -155,4 +186,5 @@ void register_learner_ops(pybind11::module& m) {
   m.def("relu_bwd_colsum_", &relu_bwd_colsum_, pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("out") = pybind11::none());
   m.def("relu_mask_bf16_", &relu_mask_bf16_);
+  m.def("actor_head_sample", &actor_head_sample);
 }

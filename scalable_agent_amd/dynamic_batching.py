@@ -52,6 +52,13 @@ class Batcher(object):
     """buffers: list of (address, nbytes). Returns (batch, id, metas)."""
     return self._impl.get_inputs_into(list(buffers))
 
+  def get_inputs_packed(self, address, capacity, align=256):
+    """Gathers the batch into ONE slab at `address` (capacity bytes), input
+    k at an `align`-aligned offset.  Returns (batch, id, used_bytes,
+    [(dtype, shape, offset)])."""
+    return self._impl.get_inputs_packed(int(address), int(capacity),
+                                        int(align))
+
   def set_outputs(self, flat_result, computation_id):
     self._impl.set_outputs([np.require(r, requirements='C') for r in flat_result],
                            int(computation_id))

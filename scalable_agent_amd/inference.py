@@ -5,11 +5,18 @@ experiment.py:534-546 + dynamic_batching.py).
 versioned weight snapshot): the learner publishes new
 weights after every update with one device-to-device copy of the flat buffer,
 so an inference batch never reads half-updated weights.  Inference runs on a
-dedicated HIP stream, concurrently with the learner stream.
+dedicated HIP stream, concurrently with the learner stream.  On the HIP
+backend the heads and the categorical sample are one kernel (actor_io.hip,
+Gumbel-max over a device-side Philox stream).
 
 `make_batched_infer` wraps it with the C++ dynamic batcher: actor threads call
-it with batch-1 numpy arrays; the runner thread executes batches of up to
-`max_batch` rows (timeout `timeout_ms`).
+it with batch-1 numpy arrays; a runner thread executes batches of up to
+`max_batch` rows (timeout `timeout_ms`).  On a GPU the runner is
+`StagedBatchedInfer`: the native batcher gathers the request rows straight into
+ONE pinned host slab (`GetInputsPacked`), the batch goes to the device with ONE
+async copy, the five outputs come back packed in ONE device->host copy into a
+pinned slab, and one stream synchronisation ends the batch (SURVEY.md §2.2
+"beyond the reference").
 """
 
 import threading
@@ -34,7 +41,15 @@ class InferenceModel(object):
     self._lock = threading.Lock()
     self._stream = (torch.cuda.Stream(self.device)
                     if self.device.type == 'cuda' else None)
-    self._gen = torch.Generator(device=self.device).manual_seed(seed)
+    if self.device.type == 'cuda' and getattr(agent, 'backend', '') == 'hip':
+      from .ops.heads import PhiloxStream
+      self._gen = PhiloxStream(seed)
+    else:
+      self._gen = torch.Generator(device=self.device).manual_seed(seed)
+
+  @property
+  def stream(self):
+    return self._stream
 
   def publish(self, flat_params, version=None):
     """Copies the learner's flat parameter buffer into the snapshot."""
@@ -50,6 +65,19 @@ class InferenceModel(object):
       self.version = self.version + 1 if version is None else version
 
   @torch.no_grad()
+  def step_device(self, last_action, reward, done, frame, instr_ids,
+                  instr_len, c, h, has_instr):
+    """Device tensors in -> device tensors (action, logits, baseline, c, h).
+    Call under `self._lock` on `self.stream`."""
+    instr = (instr_ids, instr_len) if (self.use_instruction and
+                                       has_instr) else None
+    env_output = StepOutput(reward, StepOutputInfo(None, None), done,
+                            (frame, instr))
+    out, (c2, h2) = self.agent.step(last_action, env_output, (c, h),
+                                    generator=self._gen)
+    return [out.action, out.policy_logits, out.baseline, c2, h2]
+
+  @torch.no_grad()
   def infer(self, last_action, reward, done, frame, instr_ids, instr_len, c,
             h):
     """Batched numpy in -> numpy out (action, logits, baseline, c, h)."""
@@ -60,14 +88,10 @@ class InferenceModel(object):
       with ctx:
         t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(
             dev, non_blocking=True)
-        instr = None
-        if self.use_instruction and int(np.max(instr_len, initial=0)) > 0:
-          instr = (t(instr_ids), t(instr_len))
-        env_output = StepOutput(t(reward), StepOutputInfo(None, None),
-                                t(done), (t(frame), instr))
-        out, (c2, h2) = self.agent.step(t(last_action), env_output,
-                                        (t(c), t(h)), generator=self._gen)
-        res = [out.action, out.policy_logits, out.baseline, c2, h2]
+        has_instr = int(np.max(instr_len, initial=0)) > 0
+        res = self.step_device(t(last_action), t(reward), t(done), t(frame),
+                               t(instr_ids), t(instr_len), t(c), t(h),
+                               has_instr)
         res = [r.to('cpu', non_blocking=False) for r in res]
     return tuple(r.numpy() for r in res)
 
@@ -80,7 +104,149 @@ class _null(object):
     return False
 
 
-def make_batched_infer(model, min_batch=1, max_batch=1024, timeout_ms=100):
+_ALIGN = 256
+
+
+def _torch_dtype(np_dtype):
+  return torch.from_numpy(np.empty(0, np.dtype(np_dtype))).dtype
+
+
+class StagedBatchedInfer(object):
+  """GPU inference server over the native batcher with pinned staging slabs.
+
+  Same calling convention as `dynamic_batching.batch_fn` wrappers:
+  `infer(last_action, reward, done, frame, instr_ids, instr_len, c, h)` on
+  batch-1 numpy arrays from any number of actor threads, plus
+  start/close/cancel/join/stats.
+  """
+
+  def __init__(self, model, min_batch=1, max_batch=1024, timeout_ms=100):
+    self.model = model
+    self.max_batch = int(max_batch)
+    self._batcher = dynamic_batching.Batcher(min_batch, max_batch, timeout_ms)
+    self._lock = threading.Lock()
+    self._thread = None
+    self._error = None
+    self._stop_requested = False
+    self._in_host = self._in_dev = None
+    self._out_host = self._out_dev = None
+    self.state = {'batcher': self._batcher}
+
+  # ---- slabs -------------------------------------------------------------
+  def _pinned(self, nbytes):
+    t = torch.empty(nbytes, dtype=torch.uint8)
+    return t.pin_memory() if self.model.device.type == 'cuda' else t
+
+  def _ensure_in_slabs(self, args):
+    if self._in_host is not None:
+      return
+    per_row = sum((np.asarray(a).nbytes + _ALIGN) for a in args)
+    cap = self.max_batch * per_row + _ALIGN * len(args)
+    self._in_host = self._pinned(cap)
+    self._in_dev = torch.empty(cap, dtype=torch.uint8,
+                               device=self.model.device)
+
+  def _out_slabs(self, nbytes):
+    if self._out_dev is None or self._out_dev.numel() < nbytes:
+      cap = max(nbytes, 1 << 16)
+      self._out_host = self._pinned(cap)
+      self._out_dev = torch.empty(cap, dtype=torch.uint8,
+                                  device=self.model.device)
+    return self._out_host, self._out_dev
+
+  # ---- runner ------------------------------------------------------------
+  def _serve_one(self):
+    m = self.model
+    host = self._in_host
+    n, cid, used, metas = self._batcher.get_inputs_packed(
+        host.data_ptr(), host.numel(), _ALIGN)
+    hnp = host.numpy()
+    ctx = torch.cuda.stream(m.stream) if m.stream is not None else _null()
+    with m._lock, ctx:
+      self._in_dev[:used].copy_(host[:used], non_blocking=True)
+      views, hviews = [], []
+      for dt, shape, off in metas:
+        nb = int(np.prod(shape)) * np.dtype(dt).itemsize
+        views.append(self._in_dev[off:off + nb].view(
+            _torch_dtype(dt)).view(*shape))
+        hviews.append(hnp[off:off + nb].view(np.dtype(dt)).reshape(shape))
+      has_instr = int(np.max(hviews[5], initial=0)) > 0
+      outs = m.step_device(*views, has_instr=has_instr)
+      outs = [o.contiguous() for o in outs]
+      layout, off = [], 0
+      for o in outs:
+        layout.append((o.dtype, tuple(o.shape), off))
+        off += (o.numel() * o.element_size() + _ALIGN - 1) // _ALIGN * _ALIGN
+      ohost, odev = self._out_slabs(off)
+      for o, (_, _, oo) in zip(outs, layout):
+        odev[oo:oo + o.numel() * o.element_size()].copy_(
+            o.view(-1).view(torch.uint8))
+      ohost[:off].copy_(odev[:off], non_blocking=True)
+      if m.stream is not None:
+        m.stream.synchronize()
+    onp = ohost.numpy()
+    result = []
+    for (dt, shape, oo), o in zip(layout, outs):
+      npdt = torch.empty(0, dtype=dt).numpy().dtype
+      nb = o.numel() * o.element_size()
+      result.append(onp[oo:oo + nb].view(npdt).reshape(shape))
+    self._batcher.set_outputs(result, cid)
+
+  def _run(self):
+    try:
+      while True:
+        self._serve_one()
+    except dynamic_batching.CancelledError as e:
+      if not self._stop_requested and 'Batcher is closed' not in str(e):
+        self._error = e
+    except BaseException as e:  # pylint: disable=broad-except
+      self._error = e
+      try:
+        self._batcher.cancel()
+      except Exception:  # pragma: no cover
+        pass
+
+  # ---- batch_fn-style API ------------------------------------------------
+  def start(self):
+    with self._lock:
+      if self._thread is None:
+        self._thread = threading.Thread(target=self._run, daemon=True,
+                                        name='staged-inference')
+        self._thread.start()
+
+  def __call__(self, *args):
+    if self._in_host is None:
+      with self._lock:
+        self._ensure_in_slabs(args)
+    self.start()
+    out = self._batcher.compute([np.asarray(a) for a in args])
+    return tuple(out)
+
+  def close(self):
+    self._stop_requested = True
+    self._batcher.close()
+
+  def cancel(self):
+    self._batcher.cancel()
+
+  def join(self, timeout=None):
+    if self._thread is not None:
+      self._thread.join(timeout)
+    if self._error is not None:
+      raise self._error
+
+  def stats(self):
+    return {'batches': int(self._batcher.num_batches),
+            'requests': int(self._batcher.num_requests)}
+
+
+def make_batched_infer(model, min_batch=1, max_batch=1024, timeout_ms=100,
+                       staged=None):
+  """staged: None = pinned-slab server on a GPU, batch_fn runner on CPU."""
+  if staged is None:
+    staged = model.device.type == 'cuda'
+  if staged:
+    return StagedBatchedInfer(model, min_batch, max_batch, timeout_ms)
   return dynamic_batching.batch_fn_with_options(
       minimum_batch_size=min_batch, maximum_batch_size=max_batch,
       timeout_ms=timeout_ms)(model.infer)

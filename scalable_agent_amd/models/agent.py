@@ -218,6 +218,18 @@ class Agent(nn.Module):
     if lengths.numel() == 0 or int(lengths.max()) == 0:
       return torch.zeros(n, INSTR_LSTM, device=device)
     emb = F.embedding(ids, self.embed)  # [N, L, 20]
+    if self.backend == 'hip' and emb.is_cuda:
+      # words are the time axis of the fused H=64 LSTM step kernels (K7
+      # shares K9's kernels); the output is h at the last valid word
+      from .. import ops
+      z = torch.zeros(n, INSTR_LSTM, device=device)
+      done = torch.zeros(ids.shape[1], n, dtype=torch.bool, device=device)
+      hs, _ = ops.lstm_unroll(emb.transpose(0, 1).contiguous(), done, (z, z),
+                              self.language_lstm_kernel,
+                              self.language_lstm_bias)
+      last = (lengths - 1).clamp(min=0).view(1, n, 1).expand(1, n, INSTR_LSTM)
+      out = hs.gather(0, last).squeeze(0)
+      return out * (lengths > 0).unsqueeze(-1).to(out.dtype)
     c = torch.zeros(n, INSTR_LSTM, device=device)
     h = torch.zeros_like(c)
     out = torch.zeros_like(c)
@@ -359,6 +371,14 @@ class Agent(nn.Module):
     x = x.view(T, B, -1)
     return self.core_unroll(x, done, core_state)
 
+  def _fused_sampler_ready(self, core_out, task_ids, generator):
+    """Heads + Gumbel-max sampling as one HIP kernel (actor_io.hip) when the
+    caller drives a device-side PhiloxStream."""
+    from ..ops.heads import PhiloxStream
+    return (isinstance(generator, PhiloxStream) and self.backend == 'hip' and
+            core_out.is_cuda and self.num_value_heads == 1 and
+            task_ids is None and self.num_actions <= 32)
+
   def unroll(self, actions, env_outputs, core_state, sample=True,
              generator=None, task_ids=None):
     """Unrolls over T steps (experiment.py:219-237).
@@ -368,6 +388,13 @@ class Agent(nn.Module):
     """
     T, B = actions.shape[0], actions.shape[1]
     core_out, core_state = self.unroll_core(actions, env_outputs, core_state)
+    if sample and self._fused_sampler_ready(core_out, task_ids, generator):
+      from .. import ops
+      action, logits, baseline = ops.actor_heads_sample(
+          core_out.reshape(T * B, -1), self.policy_w, self.policy_b,
+          self.baseline_w, self.baseline_b, generator)
+      return AgentOutput(action.view(T, B), logits.view(T, B, -1),
+                         baseline.view(T, B)), core_state
     logits, baseline = self.heads(core_out, task_ids)
     if sample:
       probs = torch.softmax(logits.reshape(T * B, -1).float(), -1)

@@ -13,5 +13,5 @@ from .vtrace_loss import vtrace_loss, vtrace_fused_forward  # noqa: F401
 from .lstm import lstm_unroll  # noqa: F401
 from .conv import torso_forward, linear_relu  # noqa: F401
 from .core import core_lstm  # noqa: F401
-from .heads import heads_vtrace_loss  # noqa: F401
+from .heads import heads_vtrace_loss, actor_heads_sample, PhiloxStream  # noqa: F401
 from .grad_sink import direct_grads  # noqa: F401

@@ -69,3 +69,36 @@ def heads_vtrace_loss(core_out, policy_w, policy_b, baseline_w, baseline_b,
       actions.to(torch.int64).contiguous(),
       rewards.to(torch.float32).contiguous(),
       done.to(torch.bool).contiguous(), cfg)
+
+
+class PhiloxStream(object):
+  """(seed, offset) counter for the actor sampler: every call draws from a
+  fresh Philox4x32-10 counter block, so samples never repeat and a run is
+  reproducible from its seed (the device-side analogue of a torch
+  Generator)."""
+
+  def __init__(self, seed):
+    self.seed = int(seed) & ((1 << 63) - 1)
+    self.offset = 0
+
+  def manual_seed(self, seed):
+    self.seed = int(seed) & ((1 << 63) - 1)
+    self.offset = 0
+    return self
+
+  def next_offset(self):
+    o = self.offset
+    self.offset += 1
+    return o
+
+
+def actor_heads_sample(core_out, policy_w, policy_b, baseline_w, baseline_b,
+                       stream):
+  """Actor inference heads + sampling in one kernel (actor_io.hip):
+  core_out [B,256] f32 -> (action [B] int64, logits [B,A], baseline [B]).
+  `stream`: a PhiloxStream (advanced by one)."""
+  logits, baseline, action = ext().actor_head_sample(
+      core_out.float().contiguous(), policy_w.contiguous(),
+      policy_b.contiguous(), baseline_w.reshape(-1).contiguous(),
+      baseline_b.reshape(-1).contiguous(), stream.seed, stream.next_offset())
+  return action, logits, baseline
