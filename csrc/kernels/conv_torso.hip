@@ -322,73 +322,91 @@ __device__ __forceinline__ void load4(const bf16_t* src, float v[4]) {
 __device__ __forceinline__ uint32_t bf2_to_ord(uint32_t u) {
   return u ^ (((u >> 15) & 0x00010001u) * 0x7FFFu);
 }
-__device__ __forceinline__ void store4_ord(bf16_t* dst, const float v[4]) {
+
+// Pre-pool LDS image y_s: order keys [Rc conv rows from cr0][W + 2][COUT],
+// columns -1 and W are permanent pad columns holding kOrdMin keys (written
+// once per kernel by init_pool_pads), and conv rows outside the image are
+// stored as kOrdMin keys by the conv epilogue (store4_ord_in).  A pad key
+// (0x8000 as int16) is below every real key (-inf is 0x807F), so the window
+// max needs no bounds checks and the first maximal tap is unchanged.
+constexpr uint32_t kOrdMin2 = 0x80008000u;
+
+__device__ __forceinline__ void store4_ord_in(bf16_t* dst, const float v[4],
+                                              bool in_image) {
   uint2 o;
   o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
   o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
-  o.x = bf2_to_ord(o.x);
-  o.y = bf2_to_ord(o.y);
+  o.x = in_image ? bf2_to_ord(o.x) : kOrdMin2;
+  o.y = in_image ? bf2_to_ord(o.y) : kOrdMin2;
   *reinterpret_cast<uint2*>(dst) = o;
 }
 
-// 3x3/2 max-pool (TF SAME padding offsets pb_h/pb_w) of the conv tile in
-// y_s (order keys, [conv rows from cr0][W][COUT]) -> pooled bf16 + argmax
-// code dy*3+dx, one 8-channel slice per thread.
 template <int COUT>
-__device__ __forceinline__ void pool_tile(const bf16_t* y_s, int cr0, int H,
-                                          int W, int Wo, int pb_h, int pb_w,
-                                          int n, int Hp, int i0, int Rpv,
-                                          bf16_t* __restrict__ pooled,
+__device__ __forceinline__ void init_pool_pads(bf16_t* y_s, int rows, int W) {
+  constexpr int CH = COUT / 8;
+  for (int e = threadIdx.x; e < rows * 2 * CH; e += blockDim.x) {
+    const int part = e % CH, side = (e / CH) & 1, r = e / (2 * CH);
+    *reinterpret_cast<uint4*>(y_s + (r * (W + 2) + (side ? W + 1 : 0)) * COUT +
+                              part * 8) =
+        make_uint4(kOrdMin2, kOrdMin2, kOrdMin2, kOrdMin2);
+  }
+}
+
+// 3x3/2 max-pool (TF SAME padding offsets pb_h/pb_w) of the padded conv tile
+// in y_s -> pooled bf16 + argmax code dy*3+dx, one 8-channel slice per
+// thread.  key32 = ord16 << 16 | (15 - tap): one v_lshl_or / v_and_or and one
+// v_max_i32 per channel and tap; the 9 taps are immediate-offset ds_read_b128
+// from one base address.  The epilogue unpacks two channels per v_perm.
+template <int COUT>
+__device__ __forceinline__ void pool_tile(const bf16_t* y_s, int W, int Wo,
+                                          int pb_w, int n, int Hp, int i0,
+                                          int Rpv, bf16_t* __restrict__ pooled,
                                           uint8_t* __restrict__ argmax) {
   constexpr int CH = COUT / 8;
+  const int Wt = W + 2;
   const int total = Rpv * Wo * CH;
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
     const int part = e % CH;
     const int pj = (e / CH) % Wo;
     const int pi = e / (CH * Wo);
+    // window origin: local conv row 2 pi, padded column 2 pj - pb_w + 1
+    const bf16_t* base = y_s + ((2 * pi) * Wt + 2 * pj - pb_w) * COUT + COUT + part * 8;
     int best[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) best[c] = -0x7FFFFFFF - 1;
-    const int crow0 = 2 * (i0 + pi) - pb_h;  // first conv row of the window
-    const int ccol0 = 2 * pj - pb_w;
-#pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
-      const int cr = crow0 + dy;
-      if (cr < 0 || cr >= H) continue;
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        const int cc = ccol0 + dx;
-        if (cc < 0 || cc >= W) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(
-            y_s + ((cr - cr0) * W + cc) * COUT + part * 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(base + (dy * Wt + dx) * COUT);
         const uint32_t u[4] = {v.x, v.y, v.z, v.w};
         const uint32_t K = 15 - (dy * 3 + dx);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const uint32_t key = (c & 1) ? ((u[c >> 1] & 0xFFFF0000u) | K)
-                                       : ((u[c >> 1] << 16) | K);
-          best[c] = max(best[c], static_cast<int>(key));
+          const int key = static_cast<int>((c & 1) ? ((u[c >> 1] & 0xFFFF0000u) | K)
+                                                   : ((u[c >> 1] << 16) | K));
+          best[c] = (dy | dx) ? max(best[c], key) : key;
         }
       }
     }
-    uint32_t bits[8], arg[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int o16 = best[c] >> 16;  // arithmetic: sign-extended ord
-      bits[c] = static_cast<uint32_t>(o16 ^ ((o16 >> 15) & 0x7FFF)) & 0xFFFFu;
-      arg[c] = 15u - (static_cast<uint32_t>(best[c]) & 15u);
-    }
     const int64_t o = ((static_cast<int64_t>(n) * Hp + i0 + pi) * Wo + pj) * COUT + part * 8;
-    uint4 pv;
-    pv.x = bits[0] | (bits[1] << 16);
-    pv.y = bits[2] | (bits[3] << 16);
-    pv.z = bits[4] | (bits[5] << 16);
-    pv.w = bits[6] | (bits[7] << 16);
-    *reinterpret_cast<uint4*>(pooled + o) = pv;
-    uint2 av;
-    av.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
-    av.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
-    *reinterpret_cast<uint2*>(argmax + o) = av;
+    uint32_t pv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)  // high halves of best[2k], best[2k+1]
+      pv[k] = bf2_to_ord(__builtin_amdgcn_perm(static_cast<uint32_t>(best[2 * k + 1]),
+                                               static_cast<uint32_t>(best[2 * k]),
+                                               0x07060302u));
+    *reinterpret_cast<uint4*>(pooled + o) = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+    uint32_t lo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // low bytes (15 - tap) of best[4k..4k+3]
+      const uint32_t a = __builtin_amdgcn_perm(static_cast<uint32_t>(best[4 * k + 1]),
+                                               static_cast<uint32_t>(best[4 * k]),
+                                               0x0c0c0400u);
+      const uint32_t b = __builtin_amdgcn_perm(static_cast<uint32_t>(best[4 * k + 3]),
+                                               static_cast<uint32_t>(best[4 * k + 2]),
+                                               0x0c0c0400u);
+      lo[k] = 0x0F0F0F0Fu - (a | (b << 16));
+    }
+    *reinterpret_cast<uint2*>(argmax + o) = make_uint2(lo[0], lo[1]);
   }
 }
 
@@ -993,6 +1011,7 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
   load_weights4<CIN, COUT, true>(w, w_s);
   float breg[COUT / 16][4];
   bias_regs<COUT>(bias, reinterpret_cast<float*>(x_s), breg);
+  init_pool_pads<COUT>(y_s, 2 * Rp + 1, W);
   const int tpi = (Hp + Rp - 1) / Rp;
   const int ntiles = N * tpi;
   RowStager<CIN, NREG> sx;
@@ -1016,12 +1035,13 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4], int) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += breg[co0 >> 4][i];
-      store4_ord(y_s + q * COUT + co0, v);
+      const int qr = q / W;
+      store4_ord_in(y_s + (q + 2 * qr + 1) * COUT + co0, v,
+                    static_cast<unsigned>(cr0 + qr) < static_cast<unsigned>(H));
     });
     __syncthreads();
     if (kKeep(xcd, 1))
-    pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
-                    argmax);
+    pool_tile<COUT>(y_s, W, Wo, pb_w, n, Hp, i0, Rpv, pooled, argmax);
   }
 }
 
@@ -1041,8 +1061,8 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
   const int Wp = W + 2;
   bf16_t* w_s = reinterpret_cast<bf16_t*>(smem);        // [3 ky][16 co][16 k]
-  bf16_t* y_s = w_s + 3 * 16 * 16;                        // [(2Rp+1)*W][16]
-  bf16_t* x4 = y_s + (2 * Rp + 1) * W * COUT;             // [(2Rp+3)][W+2][4] + pad
+  bf16_t* y_s = w_s + 3 * 16 * 16;                        // [2Rp+1][W+2][16]
+  bf16_t* x4 = y_s + (2 * Rp + 1) * (W + 2) * COUT;       // [(2Rp+3)][W+2][4] + pad
   for (int e = threadIdx.x; e < 3 * 16 * 16; e += blockDim.x) {
     const int ky = e / 256, co = (e / 16) % 16, k = e % 16;
     const int kx = k / 4, ci = k % 4;
@@ -1062,6 +1082,8 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   float breg[1][4];
   bias_regs<COUT>(bias, reinterpret_cast<float*>(y_s), breg);
   const float b0 = breg[0][0], b1 = breg[0][1], b2 = breg[0][2], b3 = breg[0][3];
+  __syncthreads();  // bias scratch (in y_s) read before the pads overwrite it
+  init_pool_pads<COUT>(y_s, 2 * Rp + 1, W);
   const TileIter it(ntiles, xcd);
   int tile = it.first;
   if (it.valid(tile)) issue(tile);
@@ -1095,13 +1117,13 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
       }
       if (valid) {
         const float v[4] = {acc[0] + b0, acc[1] + b1, acc[2] + b2, acc[3] + b3};
-        store4_ord(y_s + q * COUT + 4 * (lane >> 4), v);
+        store4_ord_in(y_s + (q + 2 * qr + 1) * COUT + 4 * (lane >> 4), v,
+                      static_cast<unsigned>(cr0 + qr) < static_cast<unsigned>(H));
       }
     }
     __syncthreads();
     if (kKeep(xcd, 1))
-    pool_tile<COUT>(y_s, cr0, H, W, Wo, pb_h, pb_w, n, Hp, i0, Rpv, pooled,
-                    argmax);
+    pool_tile<COUT>(y_s, W, Wo, pb_w, n, Hp, i0, Rpv, pooled, argmax);
   }
 }
 
@@ -1730,7 +1752,7 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
               "conv_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
   const size_t smem = (w_lds_elems(CIN, COUT, true) + (2 * Rp + 3) * row_pitch(CIN, W) + CIN +
-                       (2 * Rp + 1) * W * COUT) * sizeof(bf16_t);
+                       (2 * Rp + 1) * (W + 2) * COUT) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto X = static_cast<const bf16_t*>(x);
   auto P = static_cast<bf16_t*>(pooled);
@@ -1758,7 +1780,7 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
   const int Rp = rows_conv1_fwd(H, W, g_tune.px_conv1_fwd);
   require_fit(((2 * Rp + 3) * W + 3) / 4 <= kU8Groups * kThreads, "conv1_pool_fwd");
   const int ntiles = N * ((Hp + Rp - 1) / Rp);
-  const size_t smem = (3 * 16 * 16 + (2 * Rp + 1) * W * 16 +
+  const size_t smem = (3 * 16 * 16 + (2 * Rp + 1) * (W + 2) * 16 +
                        ((2 * Rp + 3) * (W + 2) + 4) * 4) * sizeof(bf16_t);
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto P = static_cast<bf16_t*>(pooled);
