@@ -264,15 +264,22 @@ Status Batcher::GetInputsInto(const std::vector<void*>& dst,
 }
 
 Status Batcher::GetInputsPacked(void* dst, size_t cap, size_t align,
-                                std::vector<TensorMeta>* metas,
+                                bool layout_pow2, std::vector<TensorMeta>* metas,
                                 std::vector<size_t>* offsets, size_t* used,
-                                int64_t* batch_size, int64_t* computation_id) {
+                                int64_t* layout_rows, int64_t* batch_size,
+                                int64_t* computation_id) {
   std::vector<Request*> reqs;
   int64_t id = -1;
   Status st = TakeBatch(&reqs, &id);
   if (!st.ok()) return st;
   const auto& first = *reqs[0]->inputs;
   const int64_t n = static_cast<int64_t>(reqs.size());
+  int64_t rows = n;
+  if (layout_pow2) {
+    rows = 1;
+    while (rows < n) rows <<= 1;
+    if (rows > max_) rows = max_;
+  }
   if (align == 0) align = 1;
   metas->clear();
   offsets->clear();
@@ -282,7 +289,7 @@ Status Batcher::GetInputsPacked(void* dst, size_t cap, size_t align,
     m.shape[0] = n;
     off = (off + align - 1) / align * align;
     offsets->push_back(off);
-    off += m.nbytes();
+    off += m.row_bytes() * static_cast<size_t>(rows);
     metas->push_back(m);
   }
   if (off > cap) {
@@ -303,6 +310,7 @@ Status Batcher::GetInputsPacked(void* dst, size_t cap, size_t align,
   EndCopy(id, &st);
   if (!st.ok()) return st;
   *used = off;
+  *layout_rows = rows;
   *batch_size = n;
   *computation_id = id;
   return Status::OK();

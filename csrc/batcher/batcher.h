@@ -100,11 +100,14 @@ class Batcher {
   // segments back to back (each start aligned to `align` bytes), so the
   // whole batched input is ONE contiguous range [0, *used) of the slab and
   // reaches the GPU with a single host->device copy.
-  Status GetInputsPacked(void* dst, size_t cap, size_t align,
+  // layout_pow2: segments are laid out for `*layout_rows` = the batch size
+  // rounded up to a power of two (capped at the maximum batch size), so a
+  // consumer can keep one fixed layout (and one captured graph) per bucket.
+  Status GetInputsPacked(void* dst, size_t cap, size_t align, bool layout_pow2,
                          std::vector<TensorMeta>* metas,
                          std::vector<size_t>* offsets, size_t* used,
-                         int64_t* batch_size, int64_t* computation_id)
-      SA_EXCLUDES(mu_);
+                         int64_t* layout_rows, int64_t* batch_size,
+                         int64_t* computation_id) SA_EXCLUDES(mu_);
 
   Status SetOutputs(const std::vector<TensorView>& outputs,
                     int64_t computation_id) SA_EXCLUDES(mu_);

@@ -132,23 +132,24 @@ class PyBatcher {
   }
 
   // Packed variant: one slab (address, capacity); returns (batch_size, id,
-  // used_bytes, [(dtype, shape, offset)]).
-  py::tuple GetInputsPacked(uintptr_t addr, size_t cap, size_t align) {
+  // used_bytes, layout_rows, [(dtype, shape, offset)]).
+  py::tuple GetInputsPacked(uintptr_t addr, size_t cap, size_t align,
+                            bool layout_pow2) {
     std::vector<TensorMeta> metas;
     std::vector<size_t> offs;
     size_t used = 0;
-    int64_t n = 0, id = -1;
+    int64_t n = 0, id = -1, rows = 0;
     Status s;
     {
       py::gil_scoped_release nogil;
-      s = b_.GetInputsPacked(reinterpret_cast<void*>(addr), cap, align, &metas,
-                             &offs, &used, &n, &id);
+      s = b_.GetInputsPacked(reinterpret_cast<void*>(addr), cap, align, layout_pow2,
+                             &metas, &offs, &used, &rows, &n, &id);
     }
     if (!s.ok()) Raise(s);
     py::list m;
     for (size_t k = 0; k < metas.size(); ++k)
       m.append(py::make_tuple(metas[k].dtype, py::cast(metas[k].shape), offs[k]));
-    return py::make_tuple(n, id, used, m);
+    return py::make_tuple(n, id, used, rows, m);
   }
 
   void SetOutputs(const py::list& outputs, int64_t id) {
@@ -206,7 +207,8 @@ PYBIND11_MODULE(_native, m) {
       .def("get_inputs", &PyBatcher::GetInputs)
       .def("get_inputs_into", &PyBatcher::GetInputsInto)
       .def("get_inputs_packed", &PyBatcher::GetInputsPacked, py::arg("address"),
-           py::arg("capacity"), py::arg("align") = 256)
+           py::arg("capacity"), py::arg("align") = 256,
+           py::arg("layout_pow2") = false)
       .def("set_outputs", &PyBatcher::SetOutputs)
       .def("close", &PyBatcher::Close)
       .def("cancel", &PyBatcher::Cancel)

@@ -10,6 +10,8 @@
 // argmax_a (logit_a - log(-log u_a)), reduced across the wave with the lower
 // index winning ties - an exact sample from softmax(logits), reproducible for
 // a given (seed, offset) whatever the batch composition of the other rows.
+// With offset_ptr the offset is read from device memory, so a captured
+// inference graph draws fresh samples on every replay (the graph bumps it).
 #include "launchers.h"
 
 namespace sa {
@@ -34,8 +36,10 @@ __global__ __launch_bounds__(256) void actor_head_sample_kernel(
     const float* __restrict__ bp, const float* __restrict__ wb,
     const float* __restrict__ bb, float* __restrict__ logits,
     float* __restrict__ baseline, int64_t* __restrict__ action, int B, int A,
-    unsigned long long seed, unsigned long long offset) {
+    unsigned long long seed, unsigned long long offset,
+    const unsigned long long* __restrict__ offset_ptr) {
   const int lane = threadIdx.x & 63;
+  if (offset_ptr != nullptr) offset = *offset_ptr;  // graph-replayed stream
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;  // whole wave exits together
   const float4 x = reinterpret_cast<const float4*>(h + (int64_t)row * 256)[lane];
@@ -93,11 +97,12 @@ void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
                               const float* wb, const float* bb, float* logits,
                               float* baseline, int64_t* action, int B, int A,
                               unsigned long long seed, unsigned long long offset,
+                              const unsigned long long* offset_ptr,
                               hipStream_t stream) {
   if (B <= 0) return;
   hipLaunchKernelGGL(actor_head_sample_kernel, dim3((B + 3) / 4), dim3(256), 0,
                      stream, h, wp, bp, wb, bb, logits, baseline, action, B, A,
-                     seed, offset);
+                     seed, offset, offset_ptr);
 }
 
 }  // namespace sa

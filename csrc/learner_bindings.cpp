@@ -150,7 +150,8 @@ void relu_mask_bf16_(at::Tensor dx, at::Tensor x) {
 // caller advances offset once per call.
 std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tensor bp,
                                           at::Tensor wb, at::Tensor bb, int64_t seed,
-                                          int64_t offset) {
+                                          int64_t offset,
+                                          c10::optional<at::Tensor> offset_dev) {
   LB_CHECK(h); LB_CHECK(wp); LB_CHECK(bp); LB_CHECK(wb); LB_CHECK(bb);
   LB_F32(h); LB_F32(wp); LB_F32(bp); LB_F32(wb); LB_F32(bb);
   TORCH_CHECK(h.dim() == 2 && h.size(1) == 256, "h must be [B,256]");
@@ -162,6 +163,13 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
   TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0 &&
               reinterpret_cast<uintptr_t>(wb.data_ptr()) % 16 == 0,
               "h / baseline w must be 16-byte aligned");
+  const unsigned long long* op = nullptr;
+  if (offset_dev.has_value()) {
+    LB_CHECK(*offset_dev);
+    TORCH_CHECK(offset_dev->scalar_type() == at::kLong && offset_dev->numel() == 1,
+                "offset_dev must be one int64");
+    op = reinterpret_cast<const unsigned long long*>(offset_dev->data_ptr());
+  }
   const c10::DeviceGuard guard(h.device());
   auto logits = at::empty({B, A}, h.options());
   auto baseline = at::empty({B}, h.options());
@@ -172,7 +180,7 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
                                baseline.data_ptr<float>(),
                                action.data_ptr<int64_t>(), B, A,
                                static_cast<unsigned long long>(seed),
-                               static_cast<unsigned long long>(offset), stream());
+                               static_cast<unsigned long long>(offset), op, stream());
   return {logits, baseline, action};
 }
 
@@ -186,5 +194,8 @@ void register_learner_ops(pybind11::module& m) {
   m.def("relu_bwd_colsum_", &relu_bwd_colsum_, pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("out") = pybind11::none());
   m.def("relu_mask_bf16_", &relu_mask_bf16_);
-  m.def("actor_head_sample", &actor_head_sample);
+  m.def("actor_head_sample", &actor_head_sample, pybind11::arg("h"),
+        pybind11::arg("wp"), pybind11::arg("bp"), pybind11::arg("wb"),
+        pybind11::arg("bb"), pybind11::arg("seed"), pybind11::arg("offset"),
+        pybind11::arg("offset_dev") = pybind11::none());
 }

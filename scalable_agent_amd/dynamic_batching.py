@@ -52,12 +52,14 @@ class Batcher(object):
     """buffers: list of (address, nbytes). Returns (batch, id, metas)."""
     return self._impl.get_inputs_into(list(buffers))
 
-  def get_inputs_packed(self, address, capacity, align=256):
+  def get_inputs_packed(self, address, capacity, align=256,
+                        layout_pow2=False):
     """Gathers the batch into ONE slab at `address` (capacity bytes), input
-    k at an `align`-aligned offset.  Returns (batch, id, used_bytes,
-    [(dtype, shape, offset)])."""
+    k at an `align`-aligned offset (segments sized for `layout_rows` rows:
+    the batch, or with layout_pow2 the batch rounded up to a power of two).
+    Returns (batch, id, used_bytes, layout_rows, [(dtype, shape, offset)])."""
     return self._impl.get_inputs_packed(int(address), int(capacity),
-                                        int(align))
+                                        int(align), bool(layout_pow2))
 
   def set_outputs(self, flat_result, computation_id):
     self._impl.set_outputs([np.require(r, requirements='C') for r in flat_result],

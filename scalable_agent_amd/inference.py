@@ -20,6 +20,7 @@ pinned slab, and one stream synchronisation ends the batch (SURVEY.md §2.2
 """
 
 import threading
+import time
 
 import numpy as np
 import torch
@@ -43,7 +44,7 @@ class InferenceModel(object):
                     if self.device.type == 'cuda' else None)
     if self.device.type == 'cuda' and getattr(agent, 'backend', '') == 'hip':
       from .ops.heads import PhiloxStream
-      self._gen = PhiloxStream(seed)
+      self._gen = PhiloxStream(seed, device=self.device)
     else:
       self._gen = torch.Generator(device=self.device).manual_seed(seed)
 
@@ -111,6 +112,17 @@ def _torch_dtype(np_dtype):
   return torch.from_numpy(np.empty(0, np.dtype(np_dtype))).dtype
 
 
+class _BucketGraph(object):
+  """One captured inference step for a padded batch of `rows` rows: static
+  input views into the device slab, outputs copied into a device output
+  slab inside the graph."""
+
+  def __init__(self, rows, offsets, graph, out_dev, out_host, layout):
+    self.rows, self.offsets, self.graph = rows, offsets, graph
+    self.out_dev, self.out_host, self.layout = out_dev, out_host, layout
+    self.out_bytes = layout[-1][2] + layout[-1][3]
+
+
 class StagedBatchedInfer(object):
   """GPU inference server over the native batcher with pinned staging slabs.
 
@@ -118,11 +130,25 @@ class StagedBatchedInfer(object):
   `infer(last_action, reward, done, frame, instr_ids, instr_len, c, h)` on
   batch-1 numpy arrays from any number of actor threads, plus
   start/close/cancel/join/stats.
+
+  graphs=True (HIP backend): batches are padded to power-of-two buckets
+  (padding rows zeroed in the host slab) and each bucket's whole inference
+  step - torso, core, heads + sampler - is ONE hipGraph replay between the
+  one H2D and the one D2H copy, so the per-batch host cost no longer scales
+  with the ~40 kernel launches of an agent step.
   """
 
-  def __init__(self, model, min_batch=1, max_batch=1024, timeout_ms=100):
+  def __init__(self, model, min_batch=1, max_batch=1024, timeout_ms=100,
+               graphs=None):
     self.model = model
     self.max_batch = int(max_batch)
+    if graphs is None:
+      graphs = (model.device.type == 'cuda' and
+                getattr(model.agent, 'backend', '') == 'hip')
+    self.graphs = bool(graphs)
+    self._bucket_graphs = {}
+    self._pool = None
+    self.busy_s = 0.0  # server time from batch taken to outputs scattered
     self._batcher = dynamic_batching.Batcher(min_batch, max_batch, timeout_ms)
     self._lock = threading.Lock()
     self._thread = None
@@ -156,10 +182,13 @@ class StagedBatchedInfer(object):
 
   # ---- runner ------------------------------------------------------------
   def _serve_one(self):
+    if self.graphs:
+      return self._serve_one_graph()
     m = self.model
     host = self._in_host
-    n, cid, used, metas = self._batcher.get_inputs_packed(
+    n, cid, used, _, metas = self._batcher.get_inputs_packed(
         host.data_ptr(), host.numel(), _ALIGN)
+    self._t_taken = time.perf_counter()
     hnp = host.numpy()
     ctx = torch.cuda.stream(m.stream) if m.stream is not None else _null()
     with m._lock, ctx:
@@ -192,10 +221,75 @@ class StagedBatchedInfer(object):
       result.append(onp[oo:oo + nb].view(npdt).reshape(shape))
     self._batcher.set_outputs(result, cid)
 
+  # ---- graph path ----------------------------------------------------------
+  def _capture(self, rows, metas, has_instr):
+    m = self.model
+    views, layout = [], []
+    for dt, shape, off in metas:
+      nb = rows * int(np.prod(shape[1:], dtype=np.int64)) * np.dtype(dt).itemsize
+      views.append(self._in_dev[off:off + nb].view(_torch_dtype(dt)).view(
+          rows, *shape[1:]))
+    s = m.stream
+    with m._lock, torch.cuda.stream(s):
+      for _ in range(2):  # warm-up: lazy library init outside the capture
+        m.step_device(*views, has_instr=has_instr)
+      s.synchronize()
+      if self._pool is None:
+        self._pool = torch.cuda.graph_pool_handle()
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, pool=self._pool, stream=s,
+                            capture_error_mode='thread_local'):
+        outs = [o.contiguous() for o in m.step_device(*views,
+                                                      has_instr=has_instr)]
+        off = 0
+        for o in outs:
+          nb = o.numel() * o.element_size()
+          layout.append((o.dtype, tuple(o.shape), off, nb))
+          off += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
+        out_dev = torch.empty(off, dtype=torch.uint8, device=m.device)
+        for o, (_, _, oo, nb) in zip(outs, layout):
+          out_dev[oo:oo + nb].copy_(o.view(-1).view(torch.uint8))
+    out_host = self._pinned(off)
+    return _BucketGraph(rows, [x[2] for x in metas], g, out_dev, out_host,
+                        layout)
+
+  def _serve_one_graph(self):
+    m = self.model
+    host = self._in_host
+    n, cid, used, rows, metas = self._batcher.get_inputs_packed(
+        host.data_ptr(), host.numel(), _ALIGN, True)
+    self._t_taken = time.perf_counter()
+    hnp = host.numpy()
+    len_dt, len_shape, len_off = metas[5]
+    has_instr = int(np.max(hnp[len_off:len_off + n * 8].view(np.int64),
+                           initial=0)) > 0
+    for dt, shape, off in metas:  # zero the padding rows
+      rb = int(np.prod(shape[1:], dtype=np.int64)) * np.dtype(dt).itemsize
+      if rows > n:
+        hnp[off + n * rb:off + rows * rb] = 0
+    key = (rows, has_instr)
+    bg = self._bucket_graphs.get(key)
+    if bg is None or bg.offsets != [x[2] for x in metas]:
+      self._in_dev[:used].copy_(host[:used])
+      bg = self._capture(rows, metas, has_instr)
+      self._bucket_graphs[key] = bg
+    with m._lock, torch.cuda.stream(m.stream):
+      self._in_dev[:used].copy_(host[:used], non_blocking=True)
+      bg.graph.replay()
+      bg.out_host.copy_(bg.out_dev, non_blocking=True)
+      m.stream.synchronize()
+    onp = bg.out_host.numpy()
+    result = []
+    for dt, shape, oo, nb in bg.layout:
+      npdt = torch.empty(0, dtype=dt).numpy().dtype
+      result.append(onp[oo:oo + nb].view(npdt).reshape(shape)[:n])
+    self._batcher.set_outputs(result, cid)
+
   def _run(self):
     try:
       while True:
         self._serve_one()
+        self.busy_s += time.perf_counter() - self._t_taken
     except dynamic_batching.CancelledError as e:
       if not self._stop_requested and 'Batcher is closed' not in str(e):
         self._error = e
@@ -237,16 +331,19 @@ class StagedBatchedInfer(object):
 
   def stats(self):
     return {'batches': int(self._batcher.num_batches),
-            'requests': int(self._batcher.num_requests)}
+            'requests': int(self._batcher.num_requests),
+            'busy_s': self.busy_s}
 
 
 def make_batched_infer(model, min_batch=1, max_batch=1024, timeout_ms=100,
-                       staged=None):
-  """staged: None = pinned-slab server on a GPU, batch_fn runner on CPU."""
+                       staged=None, graphs=None):
+  """staged: None = pinned-slab server on a GPU, batch_fn runner on CPU;
+  graphs: None = per-bucket hipGraph replay on the HIP backend."""
   if staged is None:
     staged = model.device.type == 'cuda'
   if staged:
-    return StagedBatchedInfer(model, min_batch, max_batch, timeout_ms)
+    return StagedBatchedInfer(model, min_batch, max_batch, timeout_ms,
+                              graphs=graphs)
   return dynamic_batching.batch_fn_with_options(
       minimum_batch_size=min_batch, maximum_batch_size=max_batch,
       timeout_ms=timeout_ms)(model.infer)

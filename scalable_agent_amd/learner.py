@@ -208,7 +208,9 @@ class Learner:
     torch.cuda.current_stream(self.device).wait_stream(s)
     self.flat.rebind_grads()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread_local: actor-inference threads keep using the GPU (and the
+    # caching allocator) while the learner captures
+    with torch.cuda.graph(g, capture_error_mode='thread_local'):
       # detached: holding the autograd graph would keep its AccumulateGrad
       # nodes (and the streams they were created on) alive into later
       # captures and eager steps

@@ -215,7 +215,8 @@ class Agent(nn.Module):
     ids, lengths = instr
     ids = ids.reshape(n, -1).to(device)
     lengths = lengths.reshape(n).to(device)
-    if lengths.numel() == 0 or int(lengths.max()) == 0:
+    capturing = lengths.is_cuda and torch.cuda.is_current_stream_capturing()
+    if lengths.numel() == 0 or (not capturing and int(lengths.max()) == 0):
       return torch.zeros(n, INSTR_LSTM, device=device)
     emb = F.embedding(ids, self.embed)  # [N, L, 20]
     if self.backend == 'hip' and emb.is_cuda:

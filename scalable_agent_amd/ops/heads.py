@@ -75,15 +75,21 @@ class PhiloxStream(object):
   """(seed, offset) counter for the actor sampler: every call draws from a
   fresh Philox4x32-10 counter block, so samples never repeat and a run is
   reproducible from its seed (the device-side analogue of a torch
-  Generator)."""
+  Generator).  With `device`, the offset lives in device memory and the
+  sampler advances it on the device, so a captured inference graph draws new
+  samples on every replay."""
 
-  def __init__(self, seed):
+  def __init__(self, seed, device=None):
     self.seed = int(seed) & ((1 << 63) - 1)
     self.offset = 0
+    self.counter = (None if device is None else
+                    torch.zeros(1, dtype=torch.int64, device=device))
 
   def manual_seed(self, seed):
     self.seed = int(seed) & ((1 << 63) - 1)
     self.offset = 0
+    if self.counter is not None:
+      self.counter.zero_()
     return self
 
   def next_offset(self):
@@ -97,8 +103,14 @@ def actor_heads_sample(core_out, policy_w, policy_b, baseline_w, baseline_b,
   """Actor inference heads + sampling in one kernel (actor_io.hip):
   core_out [B,256] f32 -> (action [B] int64, logits [B,A], baseline [B]).
   `stream`: a PhiloxStream (advanced by one)."""
-  logits, baseline, action = ext().actor_head_sample(
-      core_out.float().contiguous(), policy_w.contiguous(),
-      policy_b.contiguous(), baseline_w.reshape(-1).contiguous(),
-      baseline_b.reshape(-1).contiguous(), stream.seed, stream.next_offset())
+  args = (core_out.float().contiguous(), policy_w.contiguous(),
+          policy_b.contiguous(), baseline_w.reshape(-1).contiguous(),
+          baseline_b.reshape(-1).contiguous(), stream.seed)
+  if stream.counter is not None and stream.counter.device == core_out.device:
+    logits, baseline, action = ext().actor_head_sample(*args, 0,
+                                                       stream.counter)
+    stream.counter.add_(1)
+  else:
+    logits, baseline, action = ext().actor_head_sample(*args,
+                                                       stream.next_offset())
   return action, logits, baseline

@@ -125,22 +125,46 @@ def test_agent_step_fused_sampler(cuda):
   assert out_f.action.shape == (B,) and out_f.action.dtype == torch.int64
 
 
-def test_staged_server_gpu(cuda):
+def test_device_counter_stream(cuda):
+  ops = _ops()
+  h = torch.randn(64, 256, device=cuda)
+  wp = torch.randn(256, 9, device=cuda)
+  bp, wb, bb = (torch.zeros(9, device=cuda), torch.zeros(256, 1, device=cuda),
+                torch.zeros(1, device=cuda))
+  s = ops.PhiloxStream(5, device=cuda)
+  a1, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, s)
+  a2, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, s)
+  assert int(s.counter.item()) == 2 and s.offset == 0
+  host = ops.PhiloxStream(5)
+  b1, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, host)
+  b2, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, host)
+  assert torch.equal(a1, b1) and torch.equal(a2, b2)
+  assert not torch.equal(a1, a2)
+
+
+@pytest.mark.parametrize('graphs', [True, False])
+def test_staged_server_gpu(cuda, graphs):
   torch.manual_seed(0)
   agent = Agent(9, torso='deep', backend='hip', compute_dtype=torch.bfloat16)
   model = inference.InferenceModel(agent, cuda, True, seed=3)
-  srv = inference.make_batched_infer(model, 1, 16, 5)
+  srv = inference.make_batched_infer(model, 1, 16, 5, graphs=graphs)
   assert isinstance(srv, inference.StagedBatchedInfer)
+  assert srv.graphs == graphs
   errors = []
 
   def actor(i):
     rng = np.random.RandomState(i)
     try:
       for k in range(6):
+        ids = np.zeros((1, 16), np.int64)
+        n = np.zeros(1, np.int64)
+        if i % 3 == 0 and k % 2 == 1:  # some batches carry instructions
+          n[0] = 1 + k % 4
+          ids[0, :n[0]] = rng.randint(0, 1000, n[0])
         a = (np.array([k % 9], np.int64), np.array([0.5], np.float32),
              np.array([k == 3]),
              rng.randint(0, 255, (1, 72, 96, 3)).astype(np.uint8),
-             np.zeros((1, 16), np.int64), np.zeros(1, np.int64),
+             ids, n,
              rng.rand(1, 256).astype(np.float32),
              rng.rand(1, 256).astype(np.float32))
         o = srv(*a)

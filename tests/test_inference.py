@@ -35,8 +35,9 @@ def test_get_inputs_packed_layout():
   for t in ts:
     t.start()
   slab = np.zeros(4096, np.uint8)
-  n, cid, used, metas = b.get_inputs_packed(slab.ctypes.data, slab.nbytes, 256)
-  assert n == 3
+  n, cid, used, rows, metas = b.get_inputs_packed(slab.ctypes.data,
+                                                  slab.nbytes, 256)
+  assert n == 3 and rows == 3
   assert [m[2] for m in metas] == [0, 256, 512]
   assert used == 512 + 3
   x = slab[0:60].view(np.float32).reshape(3, 5)
@@ -97,3 +98,28 @@ def test_staged_server_matches_direct_inference():
   srv.join()
   assert not errors, errors[0]
   assert st['requests'] == 24 and 1 <= st['batches'] <= 24
+
+
+def test_get_inputs_packed_pow2_layout():
+  b = dynamic_batching.Batcher(3, 8, None)
+  outs = {}
+
+  def client(i):
+    outs[i] = b.compute([np.full((1, 5), i, np.float32),
+                         np.full((1, 6), i, np.int64)])
+
+  ts = [threading.Thread(target=client, args=(i,)) for i in range(3)]
+  for t in ts:
+    t.start()
+  slab = np.zeros(4096, np.uint8)
+  n, cid, used, rows, metas = b.get_inputs_packed(
+      slab.ctypes.data, slab.nbytes, 256, True)
+  assert (n, rows) == (3, 4)
+  assert [m[2] for m in metas] == [0, 256] and used == 256 + 4 * 48
+  assert metas[0][1] == [3, 5]
+  x = slab[0:60].view(np.float32).reshape(3, 5)
+  b.set_outputs([x + 1], cid)
+  for t in ts:
+    t.join()
+  for i in range(3):
+    assert np.all(outs[i][0] == i + 1)
