@@ -210,7 +210,7 @@ def train(flags):
   from . import inference as inference_lib
   from . import parallel
   from .actor import Actor, stack_unrolls
-  from .learner import Learner, batch_to_device
+  from .learner import FlatStaging, Learner, batch_to_device
   from .runtime.faults import FaultSpec
   from .summary import SummaryWriter
   from .utils.timing import StepTimer
@@ -322,6 +322,7 @@ def train(flags):
   last_log_frames = int(learner.frames.item())
   steps = 0
   use_graph = flags.use_hip_graph and device.type == 'cuda'
+  staging = dev_stage = copied = None
   try:
     frames = int(learner.frames.item())
     while frames < flags.total_environment_frames:
@@ -341,8 +342,7 @@ def train(flags):
       if flags.deterministic:
         # batch order independent of actor timing: sort by actor identity
         unrolls.sort(key=lambda u: (u.level_name, float(u.agent_state[0][0])))
-      host = stack_unrolls(unrolls, use_instruction=use_instr,
-                           pin=device.type == 'cuda')
+      host = stack_unrolls(unrolls, use_instruction=use_instr, pin=False)
       if faults.get('learner_nan') == steps + 1:
         host.env_outputs.reward[1:, 0] = float('nan')  # poisoned batch
       dev_batch = host
@@ -351,12 +351,28 @@ def train(flags):
         dev_batch = host._replace(level_name=torch.tensor(
             [task_index[l] for l in host.level_name], dtype=torch.int64))
       with trace('h2d'):
-        data = batch_to_device(dev_batch, device)
+        if device.type == 'cuda':
+          # the batch goes into one of two pinned flat buffers and reaches
+          # the device (the graph's static slot) with ONE async copy
+          if staging is None:
+            staging = [FlatStaging(dev_batch, 'cpu', pin=True)
+                       for _ in range(2)]
+            dev_stage = FlatStaging(dev_batch, device)
+            copied = [None, None]
+          slot = steps % 2
+          if copied[slot] is not None:
+            copied[slot].synchronize()  # its previous H2D copy has landed
+          staging[slot].load(dev_batch)
+          dev_stage.copy_from(staging[slot])
+          copied[slot] = torch.cuda.Event()
+          copied[slot].record()
+          data = dev_stage.views
+        else:
+          data = batch_to_device(dev_batch, device)
       with trace('learner_step'):
         if use_graph:
           if learner._graph is None:
-            learner.capture(data)
-          learner.load_static(data)
+            learner.capture(data, clone=False)
           loss = learner.graph_step()
         else:
           loss = learner.step(data)

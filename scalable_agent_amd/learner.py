@@ -193,12 +193,15 @@ class Learner:
     return self.last_loss
 
   # ------------------------------------------------------------ graph step
-  def capture(self, example, warmup=2):
-    """Captures fwd+bwd into a HIP graph on static input slots."""
+  def capture(self, example, warmup=2, clone=True):
+    """Captures fwd+bwd into a HIP graph on static input slots.
+
+    clone=False: `example` (already on the device) IS the static slot, e.g.
+    the views of a `FlatStaging` device buffer that one H2D copy refills."""
     assert self.device.type == 'cuda'
     self._static_in = batch_to_device(example, self.device)
-    # clone so the static slot owns its memory
-    self._static_in = _map_tensors(self._static_in, lambda t: t.clone())
+    if clone:  # the static slot owns its memory
+      self._static_in = _map_tensors(self._static_in, lambda t: t.clone())
     s = torch.cuda.Stream(self.device)
     s.wait_stream(torch.cuda.current_stream(self.device))
     saved_p = self.flat.params.clone()
@@ -210,7 +213,8 @@ class Learner:
     g = torch.cuda.CUDAGraph()
     # thread_local: actor-inference threads keep using the GPU (and the
     # caching allocator) while the learner captures
-    with torch.cuda.graph(g, capture_error_mode='thread_local'):
+    mode = os.environ.get('SA_CAPTURE_MODE', 'thread_local')
+    with torch.cuda.graph(g, capture_error_mode=mode):
       # detached: holding the autograd graph would keep its AccumulateGrad
       # nodes (and the streams they were created on) alive into later
       # captures and eager steps
@@ -254,6 +258,45 @@ def _gather_targets(targets, tasks):
   dist.all_gather(t_all, targets.contiguous())
   dist.all_gather(k_all, tasks.contiguous())
   return torch.cat(t_all, 1), torch.cat(k_all, 0)
+
+
+class FlatStaging(object):
+  """A learner batch laid out in ONE flat byte buffer (256-B aligned
+  segments, one per tensor), with views nested like the batch.
+
+  A pinned host FlatStaging and a device FlatStaging of the same layout turn
+  the per-step StagingArea put (reference experiment.py:587-597) into ONE
+  hipMemcpyAsync of `nbytes` instead of one copy (and one pinned-pointer
+  query) per tensor; the device views can be the graph's static inputs.
+  """
+
+  def __init__(self, template, device, pin=False):
+    leaves = []
+    _map_tensors(template, lambda t: leaves.append(t) or t)
+    offs, off = [], 0
+    for t in leaves:
+      off = (off + 255) // 256 * 256
+      offs.append(off)
+      off += t.numel() * t.element_size()
+    self.nbytes = off
+    flat = torch.empty(max(off, 1), dtype=torch.uint8, device=device)
+    self.flat = flat.pin_memory() if pin else flat
+    it = iter(range(len(leaves)))
+
+    def view(t):
+      o = offs[next(it)]
+      nb = t.numel() * t.element_size()
+      return self.flat[o:o + nb].view(t.dtype).view(t.shape)
+
+    self.views = _map_tensors(template, view)
+
+  def load(self, batch):
+    _copy_into(self.views, batch, False)
+    return self
+
+  def copy_from(self, other, non_blocking=True):
+    self.flat[:self.nbytes].copy_(other.flat[:other.nbytes],
+                                  non_blocking=non_blocking)
 
 
 def _map_tensors(x, fn):

@@ -178,3 +178,29 @@ def test_learner_popart_step_cpu():
   assert float(learner.popart.mu.abs().sum()) > 0
   sd = learner.state_dict()
   assert 'popart' in sd
+
+
+def test_flat_staging_roundtrip():
+  from scalable_agent_amd.learner import FlatStaging, _map_tensors
+  b1 = make_synthetic_batch(3, 5, (8, 10, 3), 4, seed=1)
+  b2 = make_synthetic_batch(3, 5, (8, 10, 3), 4, seed=2)
+  host = FlatStaging(b1, 'cpu').load(b1)
+  dev = FlatStaging(b1, 'cpu')
+  leaves = []
+  _map_tensors(dev.views, lambda t: leaves.append(t) or t)
+  assert all(t.data_ptr() % 256 == 0 for t in leaves)
+  assert all(t.untyped_storage().data_ptr() == dev.flat.data_ptr()
+             for t in leaves)
+  dev.copy_from(host, non_blocking=False)
+  got, want = [], []
+  _map_tensors(dev.views, lambda t: got.append(t) or t)
+  _map_tensors(b1, lambda t: want.append(t) or t)
+  assert len(got) == len(want) and all(torch.equal(a, b)
+                                       for a, b in zip(got, want))
+  host.load(b2)  # reusing the slab changes every view in place
+  dev.copy_from(host, non_blocking=False)
+  got2, want2 = [], []
+  _map_tensors(dev.views, lambda t: got2.append(t) or t)
+  _map_tensors(b2, lambda t: want2.append(t) or t)
+  assert all(torch.equal(a, b) for a, b in zip(got2, want2))
+  assert got2[0].data_ptr() == got[0].data_ptr()
