@@ -28,7 +28,7 @@ def main():
   start = next(i for i, l in enumerate(lines)
                if re.match(r'^_Z\S*:', l) and sub in l)
   end = next(i for i in range(start, len(lines))
-             if lines[i].strip().startswith('s_endpgm'))
+             if lines[i].startswith('.Lfunc_end'))
   print(lines[start].split(':')[0])
   blocks, cur, order = [], None, {}
   for l in lines[start + 1:end + 1]:
