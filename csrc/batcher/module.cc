@@ -14,6 +14,7 @@ namespace sa {
 
 void register_envpool(py::module& m);  // csrc/envpool/module_part.cc
 void register_image_ops(py::module& m);  // csrc/envpool/image_ops.cc
+void register_crc(py::module& m);        // csrc/envpool/crc32c.cc
 
 namespace {
 
@@ -220,4 +221,5 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("timeout_ms", &PyBatcher::timeout);
   sa::register_envpool(m);
   sa::register_image_ops(m);
+  sa::register_crc(m);
 }

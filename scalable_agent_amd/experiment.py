@@ -258,6 +258,13 @@ def train(flags):
   restored = ckpt_lib.restore(flags.logdir, learner)
   if restored is not None:
     log.info('Restored checkpoint at %d frames', restored)
+  elif flags.import_tf_checkpoint:
+    # a reference (TF) run's model.ckpt-N: weights, RMSProp slots, frames
+    from . import tf_checkpoint
+    frames = tf_checkpoint.import_tf_checkpoint(flags.import_tf_checkpoint,
+                                                learner=learner)
+    log.info('Imported TF checkpoint %s (frames %s)',
+             flags.import_tf_checkpoint, frames)
   if world > 1:
     parallel.broadcast_params(learner.flat.params)
   saver = ckpt_lib.PeriodicSaver(flags.logdir, learner, flags,

@@ -91,6 +91,10 @@ def build_parser() -> argparse.ArgumentParser:
                  help='PopArt value normalisation (north-star config #4).')
   p.add_argument('--popart_beta', type=float, default=3e-4)
   p.add_argument('--save_checkpoint_secs', type=float, default=600)
+  p.add_argument('--import_tf_checkpoint', type=str, default='',
+                 help='TF V2 checkpoint prefix (or a logdir with a '
+                      '`checkpoint` file) of a reference run to start from '
+                      'when --logdir has no checkpoint of its own.')
   p.add_argument('--save_summaries_secs', type=float, default=30)
   p.add_argument('--keep_checkpoints', type=int, default=5)
   p.add_argument('--log_every_frames', type=int, default=50000,

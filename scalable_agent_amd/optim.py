@@ -56,6 +56,14 @@ class FlatParams:
       p.data = self.params[o:o + n].view_as(p)
       p.grad = self.grads[o:o + n].view_as(p)
 
+  def view_of(self, buf, name):
+    """View of parameter `name` in a buffer with the flat layout (e.g. the
+    RMSProp ms / mom slots)."""
+    for (n, p), o in zip(self.named, self.offsets):
+      if n == name:
+        return buf[o:o + p.numel()].view_as(p)
+    raise KeyError(name)
+
   def zero_grad(self):
     self.grads.zero_()
 

@@ -27,11 +27,30 @@ for _i in range(256):
   _CRC_TABLE.append(_c)
 
 
-def crc32c(data):
+def _crc32c_py(data):
   crc = 0xFFFFFFFF
   for b in data:
     crc = _CRC_TABLE[(crc ^ b) & 0xFF] ^ (crc >> 8)
   return crc ^ 0xFFFFFFFF
+
+
+def _native_crc():
+  try:
+    from .runtime import native
+    return getattr(native.load(), 'crc32c', None)
+  except Exception:  # pylint: disable=broad-except
+    return None
+
+
+_CRC_NATIVE = _native_crc()
+
+
+def crc32c(data):
+  """CRC-32C; the native slicing-by-8 version when the runtime is built."""
+  if _CRC_NATIVE is not None:
+    return _CRC_NATIVE(memoryview(bytes(data) if not isinstance(
+        data, (bytes, bytearray, memoryview)) else data).cast('B'))
+  return _crc32c_py(data)
 
 
 def masked_crc32c(data):
