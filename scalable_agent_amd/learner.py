@@ -279,8 +279,12 @@ class FlatStaging(object):
       offs.append(off)
       off += t.numel() * t.element_size()
     self.nbytes = off
-    flat = torch.empty(max(off, 1), dtype=torch.uint8, device=device)
-    self.flat = flat.pin_memory() if pin else flat
+    raw = torch.empty(off + 256, dtype=torch.uint8, device=device)
+    if pin:
+      raw = raw.pin_memory()
+    shift = (-raw.data_ptr()) % 256  # segment offsets are base-relative
+    self._raw = raw
+    self.flat = raw[shift:shift + max(off, 1)]
     it = iter(range(len(leaves)))
 
     def view(t):

@@ -189,8 +189,8 @@ def test_flat_staging_roundtrip():
   leaves = []
   _map_tensors(dev.views, lambda t: leaves.append(t) or t)
   assert all(t.data_ptr() % 256 == 0 for t in leaves)
-  assert all(t.untyped_storage().data_ptr() == dev.flat.data_ptr()
-             for t in leaves)
+  assert all(t.untyped_storage().data_ptr() ==
+             dev.flat.untyped_storage().data_ptr() for t in leaves)
   dev.copy_from(host, non_blocking=False)
   got, want = [], []
   _map_tensors(dev.views, lambda t: got.append(t) or t)
