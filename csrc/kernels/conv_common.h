@@ -28,6 +28,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// Two floats -> packed bf16 pair (lo in bits 0-15): ONE v_cvt_pk_bf16_f32
+// (RNE).  Packing two f2bf results by hand costs two converts plus
+// and/shift/or, the compiler does not merge them.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{lo, hi}, bf2v));
+}
 // ReLU on two packed bf16 (sign bit set -> 0).
 __device__ __forceinline__ uint32_t relu2(uint32_t v) {
   const uint32_t s = (v >> 15) & 0x00010001u;

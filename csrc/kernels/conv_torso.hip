@@ -334,8 +334,8 @@ constexpr uint32_t kOrdMin2 = 0x80008000u;
 __device__ __forceinline__ void store4_ord_in(bf16_t* dst, const float v[4],
                                               bool in_image) {
   uint2 o;
-  o.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-  o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+  o.x = pack_bf16x2(v[0], v[1]);
+  o.y = pack_bf16x2(v[2], v[3]);
   o.x = in_image ? bf2_to_ord(o.x) : kOrdMin2;
   o.y = in_image ? bf2_to_ord(o.y) : kOrdMin2;
   *reinterpret_cast<uint2*>(dst) = o;
@@ -1264,10 +1264,10 @@ __device__ __forceinline__ void gather_pool_grad_blocks(
       const int cc = 2 * jb - pb_w + (cidx & 1);
       if (rr >= 0 && rr < rows && cc >= 0 && cc < W) {
         uint4 o;
-        o.x = f2bf(cell[cidx][0]) | (static_cast<uint32_t>(f2bf(cell[cidx][1])) << 16);
-        o.y = f2bf(cell[cidx][2]) | (static_cast<uint32_t>(f2bf(cell[cidx][3])) << 16);
-        o.z = f2bf(cell[cidx][4]) | (static_cast<uint32_t>(f2bf(cell[cidx][5])) << 16);
-        o.w = f2bf(cell[cidx][6]) | (static_cast<uint32_t>(f2bf(cell[cidx][7])) << 16);
+        o.x = pack_bf16x2(cell[cidx][0], cell[cidx][1]);
+        o.y = pack_bf16x2(cell[cidx][2], cell[cidx][3]);
+        o.z = pack_bf16x2(cell[cidx][4], cell[cidx][5]);
+        o.w = pack_bf16x2(cell[cidx][6], cell[cidx][7]);
         *reinterpret_cast<uint4*>(d_s + rr * RPd + (cc + 1) * COUT + part * 8) = o;
       }
     }
