@@ -36,6 +36,14 @@ typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{lo, hi}, bf2v));
 }
+// Same instruction as an opaque asm statement: used where the vector-convert
+// form changes the compiler's unrolling of the surrounding tile loops (the
+// residual-operand register arrays of res_conv_fwd/bwd then went to scratch).
+__device__ __forceinline__ uint32_t pack_bf16x2_asm(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
 // ReLU on two packed bf16 (sign bit set -> 0).
 __device__ __forceinline__ uint32_t relu2(uint32_t v) {
   const uint32_t s = (v >> 15) & 0x00010001u;

@@ -306,6 +306,16 @@ __device__ __forceinline__ void store4(bf16_t* dst, const float v[4]) {
   o.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
   *reinterpret_cast<uint2*>(dst) = o;
 }
+// store4 with one v_cvt_pk_bf16_f32 per pair (same bits).  Measured per
+// kernel (profiles/experiments.md): it also keeps the residual/skip operand
+// arrays of the 32-channel and backward kernels out of scratch, but slows
+// the 16-channel forward convs, which keep store4.
+__device__ __forceinline__ void store4_pk(bf16_t* dst, const float v[4]) {
+  uint2 o;
+  o.x = pack_bf16x2_asm(v[0], v[1]);
+  o.y = pack_bf16x2_asm(v[2], v[3]);
+  *reinterpret_cast<uint2*>(dst) = o;
+}
 __device__ __forceinline__ void load4(const bf16_t* src, float v[4]) {
   const uint2 o = *reinterpret_cast<const uint2*>(src);
   v[0] = __uint_as_float(o.x << 16);
@@ -903,7 +913,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], 0.f);
       }
-      store4(y + (img0 + q) * C + co0, v);
+      if constexpr (C == 16)
+        store4(y + (img0 + q) * C + co0, v);
+      else
+        store4_pk(y + (img0 + q) * C + co0, v);
     });
     if (kLatePrefetch) prefetch();
   }
@@ -1180,7 +1193,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       if (ADD_SKIP) sop.get(slot, ci0, s);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = s[i] + (m[i] > 0.f ? v[i] : 0.f);
-      store4(dx + (img0 + q) * C + ci0, v);
+      store4_pk(dx + (img0 + q) * C + ci0, v);
     });
     if (kKeep(xcd, 2))
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
@@ -1345,7 +1358,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       const int64_t img0 = (static_cast<int64_t>(n) * H + r0) * W;
     if (kKeep(xcd, 4))
       conv_tile_dgrad<CIN, COUT>(d_s, w_s, W, npix, [&](int q, int ci0, float v[4], int) {
-        store4(dx + (img0 + q) * CIN + ci0, v);
+        store4_pk(dx + (img0 + q) * CIN + ci0, v);
       });
     }
     if (kKeep(xcd, 2))
