@@ -990,8 +990,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       const bool in = r >= 0 && r < H;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = in ? fmaxf(v[i] + bq1[co0 >> 4][i], 0.f) : 0.f;
-      store4(t_s + qr * RP + (qc + 1) * C + co0, v);
-      if (qr >= 1 && qr <= Rv) store4(t_out + (img0 + q - W) * C + co0, v);
+      store4_pk(t_s + qr * RP + (qc + 1) * C + co0, v);
+      if (qr >= 1 && qr <= Rv) store4_pk(t_out + (img0 + q - W) * C + co0, v);
     });
     __syncthreads();
     if (kKeep(xcd, 4))
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         v[i] += r[i];
         if (POST_RELU) v[i] = fmaxf(v[i], 0.f);
       }
-      store4(y + (img0 + q) * C + co0, v);
+      store4_pk(y + (img0 + q) * C + co0, v);
     });
   }
 }
