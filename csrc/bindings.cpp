@@ -107,6 +107,16 @@ bool g_lstm_persistent = [] {
 
 bool use_persistent(int H, int B) { return g_lstm_persistent && H == 256 && B <= 32; }
 
+// Gang kernels (lstm_gang.hip: 8 workgroups, bf16 recurrent product) for
+// H == 256, B <= 32 (SA_LSTM_GANG=1 or lstm_set_gang(True)); they take
+// precedence over the fp32 persistent kernels.
+bool g_lstm_gang = [] {
+  const char* e = std::getenv("SA_LSTM_GANG");
+  return e && e[0] == '1';
+}();
+
+bool use_gang(int H, int B) { return g_lstm_gang && H == 256 && B <= 32; }
+
 // Sticky per-device timeout word of the persistent kernels (0 = healthy).
 at::Tensor lstm_err_word(const at::Device& dev) {
   static std::map<int, at::Tensor> words;
@@ -144,9 +154,21 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   const int64_t RT = (B + 31) / 32;
   auto hpk = at::empty({2, RT * 32 * H}, xw.options());
   auto s = cur_stream();
+  const uint8_t* dn = u8ptr(done);
+  if (use_gang(H, B)) {
+    // w4 / wt carry the bf16 gang fragments instead (512 KB of their 1 MB)
+    sa::lstm_gang_pack_launch(w_h.data_ptr<float>(), w4.data_ptr(), wt.data_ptr(), s);
+    auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(false)},
+                          xw.options().dtype(at::kLong));
+    sa::lstm_fwd_gang_launch(
+        xw.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), dn,
+        w4.data_ptr(), hs.data_ptr<float>(), cs.data_ptr<float>(),
+        acts.data_ptr<float>(), hpm.data_ptr<float>(), xbuf.data_ptr(),
+        reinterpret_cast<unsigned*>(lstm_err_word(xw.device()).data_ptr<int>()), T, B, s);
+    return {hs, cs, acts, hpm, wt};
+  }
   sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
                                wt.data_ptr<float>(), H, s);
-  const uint8_t* dn = u8ptr(done);
   if (use_persistent(H, B)) {
     auto xbuf = lstm_xbuf(false, xw.options());
     sa::lstm_fwd_persistent_launch(
@@ -196,6 +218,20 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
   auto dgpk = at::empty({2, RT * 32 * H4}, acts.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
+  if (use_gang(H, B)) {
+    auto dc0 = at::empty({B, H}, acts.options());
+    auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(true)},
+                          acts.options().dtype(at::kLong));
+    sa::lstm_bwd_gang_launch(
+        dh_out.data_ptr<float>(), dn, wt.data_ptr(), acts.data_ptr<float>(),
+        cs.data_ptr<float>(), c0.data_ptr<float>(),
+        dc_last.has_value() ? dc_last->data_ptr<float>() : nullptr,
+        dg.data_ptr<float>(), want_bf16 ? dg16.data_ptr() : nullptr,
+        dc0.data_ptr<float>(), xbuf.data_ptr(),
+        reinterpret_cast<unsigned*>(lstm_err_word(acts.device()).data_ptr<int>()), T, B, s);
+    if (!want_bf16) dg16 = at::empty({0}, acts.options());
+    return {dg, dc0, dg16};
+  }
   if (use_persistent(H, B)) {
     auto dc0 = at::empty({B, H}, acts.options());
     auto xbuf = lstm_xbuf(true, acts.options());
@@ -229,6 +265,8 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
 
 void lstm_set_persistent(bool on) { g_lstm_persistent = on; }
 bool lstm_get_persistent() { return g_lstm_persistent; }
+void lstm_set_gang(bool on) { g_lstm_gang = on; }
+bool lstm_get_gang() { return g_lstm_gang; }
 at::Tensor lstm_error(at::Tensor like) { return lstm_err_word(like.device()); }
 
 void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
@@ -255,6 +293,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("want_bf16") = false);
   m.def("lstm_set_persistent", &lstm_set_persistent);
   m.def("lstm_get_persistent", &lstm_get_persistent);
+  m.def("lstm_set_gang", &lstm_set_gang);
+  m.def("lstm_get_gang", &lstm_get_gang);
   m.def("lstm_error_word", &lstm_error);
   m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);

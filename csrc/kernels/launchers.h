@@ -81,6 +81,22 @@ void lstm_bwd_persistent_launch(const float* dh_out, const uint8_t* done,
                                 void* dg16, float* dc0, void* xbuf, unsigned* err,
                                 int T, int B, hipStream_t stream);
 
+// ---- lstm_gang.hip ---------------------------------------------------------
+// Whole-unroll LSTM-256 recurrence on a gang of 8 workgroups with bf16 MFMA
+// (B <= 32).  lstm_gang_pack_launch writes the bf16 fwd / bwd fragments (512
+// KB each) of W_h [256,1024]; xbuf: lstm_gang_xbuf_granules(bwd) zeroed
+// granules (zero before EVERY launch); err: the sticky timeout word.
+size_t lstm_gang_xbuf_granules(bool bwd);
+void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stream);
+void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
+                          const uint8_t* done, const void* wf, float* hs, float* cs,
+                          float* acts, float* hpm, void* xbuf, unsigned* err, int T,
+                          int B, hipStream_t stream);
+void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* wbk,
+                          const float* acts, const float* cs, const float* c0,
+                          const float* dc_last, float* dg, void* dg16, float* dc0,
+                          void* xbuf, unsigned* err, int T, int B, hipStream_t stream);
+
 // ---- learner_io.hip --------------------------------------------------------
 // Fused heads + V-trace + loss (one workgroup per batch column; see the file
 // header).  core [T+1,B,256]; behaviour/actions/rewards/done point at row 1

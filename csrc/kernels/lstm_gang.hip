@@ -1,0 +1,415 @@
+// "Gang" LSTM-256 recurrence: one launch per direction for all T steps, run
+// by a gang of EIGHT workgroups with the recurrent product on bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16, fp32 accumulate).  Same math and outputs as
+// lstm.hip / lstm_persistent.hip (reference experiment.py:228-235).
+//
+// Why eight: lstm_persistent.hip (64 / 16 workgroups, exact fp32 MFMA) lost
+// to the per-step kernels because every consumer workgroup swept the whole
+// 64 KB (fwd) / 256 KB (bwd) exchange per step.  The exchange probe
+// (tools/micro/xcd_sync_bench.hip, profiles/experiments.md) puts an 8-
+// workgroup, 32 KB, all-loads-in-flight hand-off at ~1.9 us per step in any
+// XCD placement, and with bf16 MFMA the whole 32x1024x256 step product is
+// ~16 MFMAs per wave, so eight workgroups are enough and the exchange per
+// consumer shrinks:
+//   fwd: workgroup j owns units [32j, 32j+32) (128 gate columns); it
+//        publishes its h_t as {tag, bf16 pair} granules and every workgroup
+//        sweeps the whole h_t (4096 granules = 32 KB) into an LDS A image.
+//   bwd: workgroup j owns units [32j, 32j+32); its dG_t slice stays in LDS
+//        and its wave w computes the PARTIAL dG_t[:, own] W_h[32w.., own]^T
+//        for destination workgroup w (a reduce-scatter): every workgroup
+//        sweeps 8 sources x 32 x 32 fp32 partials (64 KB) and sums them in
+//        a fixed order (deterministic).
+// Granule hand-off, tags, double-buffered slots, bounded spins and the
+// sticky error word are those of lstm_persistent.hip (file header there).
+// Numerics: the recurrent operand h_{t-1} / dG_{t+1} and W_h are rounded to
+// bf16 for the product only; the cell state, gates, carries and every
+// output stay fp32.  Requires B <= 32 (rows >= B are computed as zeros and
+// never stored).
+#include "launchers.h"
+
+#include <hip/hip_bf16.h>
+
+namespace sa {
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+typedef unsigned short bf16_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+constexpr unsigned kSpinLimit = 1u << 21;
+constexpr int kH = 256;
+constexpr int kGang = 8;              // workgroups
+constexpr int kU = kH / kGang;        // 32 units per workgroup
+constexpr int kThreads = 512;         // 8 waves
+constexpr int kFSlot = 32 * kH / 2;   // fwd granules per slot: [row][unit pair]
+constexpr int kBDest = 8 * 32 * kU;   // bwd granules per destination (8192)
+constexpr int kBSlot = kGang * kBDest;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{lo, hi}, bf2v));
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ f4v mfma(bf8v a, bf8v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void publish(unsigned long long* g, unsigned tag,
+                                        uint32_t bits) {
+  __hip_atomic_store((gu64*)(g), (static_cast<unsigned long long>(tag) << 32) | bits,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sweeps N contiguous granules until every tag == `tag` (all loads of a
+// pass in flight together); v receives the low 32 bits.  false on timeout
+// or when another workgroup already reported one (sticky error word).
+// Granule k is read at g + (k / R) * S + k % R (R contiguous granules per
+// run, runs S granules apart).
+template <int N, int R = N, int S = 0>
+__device__ __forceinline__ bool sweep(const unsigned long long* g, unsigned tag,
+                                      uint32_t (&v)[N], unsigned* err) {
+  const gu64* p = (const gu64*)(g);
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const unsigned long long x = __hip_atomic_load(
+          p + (k / R) * S + k % R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[k] = static_cast<uint32_t>(x);
+      ok &= static_cast<unsigned>(x >> 32) == tag;
+    }
+    if (__all(ok)) return true;
+    if ((spins & 63) == 63 &&
+        __hip_atomic_load((gu32*)(err), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      return false;
+    if (spins >= kSpinLimit) {
+      __hip_atomic_store((gu32*)(err), 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// W_h [256, 1024] (k, n = g*256 + u) -> bf16 MFMA B fragments, 16 bytes per
+// (workgroup j, wave w, step s, lane):
+//   wf  (fwd): k = 32s + 8(l>>4) + e, column c = l&15 of wave w's n-tile:
+//              unit 32j + 4w + (c>>2), gate c&3
+//   wbk (bwd): row k = 32s + 8(l>>4) + e of the local dG image (gate s,
+//              local unit 8(l>>4)+e of source j), column = unit
+//              32w + 16a + (l&15) (a = n-tile), fragment index a*4 + s
+__global__ __launch_bounds__(256) void lstm_gang_pack_kernel(
+    const float* __restrict__ w, bf16_t* __restrict__ wf, bf16_t* __restrict__ wbk) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= kH * 4 * kH) return;
+  const int k = idx >> 10, n = idx & 1023;
+  const bf16_t v = f2bf(w[idx]);
+  {
+    const int g = n >> 8, u = n & 255;
+    const int j = u >> 5, wv = (u & 31) >> 2, c = 4 * (u & 3) + g;
+    const int s = k >> 5, lane = 16 * ((k & 31) >> 3) + c, e = k & 7;
+    wf[((((j * 8 + wv) * 8 + s) * 64) + lane) * 8 + e] = v;
+  }
+  {
+    const int g = n >> 8, rest = n & 255, j = rest >> 5, ul = rest & 31;
+    const int wv = k >> 5, a = (k >> 4) & 1, lane = 16 * (ul >> 3) + (k & 15),
+              e = ul & 7;
+    wbk[((((j * 8 + wv) * 8 + a * 4 + g) * 64) + lane) * 8 + e] = v;
+  }
+}
+
+// ---------------------------------------------------------------- forward
+// Epilogue thread tid: row er = tid>>4, units 32j + 2q + {0,1} (q = tid&15);
+// it publishes granule [er][16j + q] = {tag, bf16(h_u0), bf16(h_u1)}.  The
+// sweep gives thread tid granules [8 tid, 8 tid + 8): row tid>>4, units
+// 16(tid&15) .. +16, written keep-masked into the LDS A image.
+__global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
+    const float* __restrict__ xw, const float* __restrict__ h0,
+    const float* __restrict__ c0, const uint8_t* __restrict__ done,
+    const bf16_t* __restrict__ wf, float* __restrict__ hs, float* __restrict__ cs,
+    float* __restrict__ acts, float* __restrict__ hpm,
+    unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
+    int B) {
+  constexpr int H = kH;
+  __shared__ __attribute__((aligned(16))) bf16_t h_s[32][H + 8];
+  __shared__ __attribute__((aligned(16))) float g_s[32][128 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x;
+  bf8v wb[8];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wf) + (j * 8 + wave) * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wb[s] = __builtin_bit_cast(bf8v, src[s * 64]);
+  }
+  const int er = tid >> 4, q = tid & 15;
+  const int ej = j * kU + 2 * q;  // first of the thread's two units
+  const bool live = er < B;
+  float c[2] = {0.f, 0.f}, h[2] = {0.f, 0.f};
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      c[e] = c0[er * H + ej + e];
+      h[e] = h0[er * H + ej + e];
+    }
+  }
+  float xv[2][4] = {}, ekeep = 0.f;
+  auto fetch = [&](int t) {
+    if (live) {
+      const int64_t g0 = (static_cast<int64_t>(t) * B + er) * 4 * H + ej;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float2 x2 = *reinterpret_cast<const float2*>(xw + g0 + g * H);
+        xv[0][g] = x2.x;
+        xv[1][g] = x2.y;
+      }
+      ekeep = done[t * B + er] ? 0.f : 1.f;
+    }
+  };
+  fetch(0);
+  const int arow = lane & 15, ak = 8 * (lane >> 4);
+  for (int t = 0; t < T; ++t) {
+    // ---- LDS A image: keep_t * h_{t-1}, bf16
+    bool fail = false;
+    {
+      const int sr = tid >> 4, u0 = 16 * (tid & 15);
+      const bool keep = sr < B && !done[t * B + (sr < B ? sr : 0)];
+      uint32_t v[8];
+      if (t == 0) {
+        const float* hr = h0 + (sr < B ? sr : 0) * H + u0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+          v[p] = keep ? pack2(hr[2 * p], hr[2 * p + 1]) : 0u;
+      } else {
+        fail = !sweep<8>(xbuf + ((t - 1) & 1) * kFSlot + 8 * tid,
+                         static_cast<unsigned>(t), v, err);
+        if (!keep) {
+#pragma unroll
+          for (int p = 0; p < 8; ++p) v[p] = 0u;
+        }
+      }
+      uint4* dst = reinterpret_cast<uint4*>(&h_s[sr][u0]);
+      dst[0] = uint4{v[0], v[1], v[2], v[3]};
+      dst[1] = uint4{v[4], v[5], v[6], v[7]};
+    }
+    if (__syncthreads_or(fail)) break;  // a timed-out sweep anywhere: leave
+    {
+      f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const bf8v a = __builtin_bit_cast(
+              bf8v, *reinterpret_cast<const uint4*>(&h_s[16 * mt + arow][32 * s + ak]));
+          acc[mt] = mfma(a, wb[s], acc[mt]);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          g_s[16 * mt + 4 * (lane >> 4) + i][16 * wave + (lane & 15)] = acc[mt][i];
+    }
+    __syncthreads();
+    {
+      const float4 ga = *reinterpret_cast<const float4*>(&g_s[er][8 * q]);
+      const float4 gb = *reinterpret_cast<const float4*>(&g_s[er][8 * q + 4]);
+      const float gv[2][4] = {{ga.x, ga.y, ga.z, ga.w}, {gb.x, gb.y, gb.z, gb.w}};
+      float hn[2], gi[2], gg[2], gf[2], go[2], hprev[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        gi[e] = sigm(gv[e][0] + xv[e][0]);
+        gg[e] = tanhf(gv[e][1] + xv[e][1]);
+        gf[e] = sigm(gv[e][2] + xv[e][2] + 1.0f);
+        go[e] = sigm(gv[e][3] + xv[e][3]);
+        hprev[e] = h[e];
+        c[e] = gf[e] * ekeep * c[e] + gi[e] * gg[e];
+        hn[e] = live ? go[e] * tanhf(c[e]) : 0.f;
+        h[e] = hn[e];
+      }
+      publish(xbuf + (t & 1) * kFSlot + er * (H / 2) + j * (kU / 2) + q,
+              static_cast<unsigned>(t + 1), pack2(hn[0], hn[1]));
+      if (live) {
+        const int64_t hj = (static_cast<int64_t>(t) * B + er) * H + ej;
+        const int64_t g0 = (static_cast<int64_t>(t) * B + er) * 4 * H + ej;
+        *reinterpret_cast<float2*>(hs + hj) = float2{hn[0], hn[1]};
+        *reinterpret_cast<float2*>(cs + hj) = float2{c[0], c[1]};
+        *reinterpret_cast<float2*>(hpm + hj) = float2{ekeep * hprev[0], ekeep * hprev[1]};
+        *reinterpret_cast<float2*>(acts + g0) = float2{gi[0], gi[1]};
+        *reinterpret_cast<float2*>(acts + g0 + H) = float2{gg[0], gg[1]};
+        *reinterpret_cast<float2*>(acts + g0 + 2 * H) = float2{gf[0], gf[1]};
+        *reinterpret_cast<float2*>(acts + g0 + 3 * H) = float2{go[0], go[1]};
+      }
+    }
+    if (t + 1 < T) fetch(t + 1);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// Thread tid owns pairs idx = 2 tid + e (e = 0, 1) of the destination
+// numbering idx = ((mt*2 + a)*64 + l)*4 + i4 (the MFMA D map of the
+// producing wave): rows 16mt + 4(l>>4) + i4, local unit 16a + (l&15).  The
+// producer of source j stores pair idx at granule j*1024 + idx of the
+// destination slot, so every 128-B line has ONE writer (a layout whose lines
+// mixed 8 sources' granules timed out sporadically on MI355X), and each
+// consumer thread sweeps 8 runs of 2 granules, 1024 granules apart.
+__global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
+    const float* __restrict__ dh_out, const uint8_t* __restrict__ done,
+    const bf16_t* __restrict__ wbk, const float* __restrict__ acts,
+    const float* __restrict__ cs, const float* __restrict__ c0,
+    const float* __restrict__ dc_last, float* __restrict__ dg,
+    __hip_bfloat16* __restrict__ dg16, float* __restrict__ dc0,
+    unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
+    int B) {
+  constexpr int H = kH;
+  __shared__ __attribute__((aligned(16))) bf16_t d_s[2][32][4 * kU + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x;
+  bf8v wb[8];  // [a*4 + s]
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wbk) + (j * 8 + wave) * 8 * 64 + lane;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) wb[f] = __builtin_bit_cast(bf8v, src[f * 64]);
+  }
+  // this thread's two (row, unit) pairs
+  const int pl = (tid >> 1) & 63, pa = (tid >> 7) & 1, pmt = tid >> 8;
+  const int r0 = 16 * pmt + 4 * (pl >> 4) + 2 * (tid & 1);
+  const int ul = 16 * pa + (pl & 15), ej = j * kU + ul;
+  bool live[2];
+  float carry[2] = {0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    live[e] = r0 + e < B;
+    if (live[e] && dc_last) carry[e] = dc_last[(r0 + e) * H + ej];
+  }
+  float dho[2] = {}, ai[2] = {}, ag[2] = {}, af[2] = {}, ao[2] = {}, cc[2] = {},
+        cpv[2] = {}, kf[2] = {}, knext[2] = {1.f, 1.f};
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (!live[e]) continue;
+      const int r = r0 + e;
+      const int64_t hj = (static_cast<int64_t>(t) * B + r) * H + ej;
+      const int64_t g0 = (static_cast<int64_t>(t) * B + r) * 4 * H + ej;
+      dho[e] = dh_out[hj];
+      ai[e] = acts[g0];
+      ag[e] = acts[g0 + H];
+      af[e] = acts[g0 + 2 * H];
+      ao[e] = acts[g0 + 3 * H];
+      cc[e] = cs[hj];
+      cpv[e] = t > 0 ? cs[hj - static_cast<int64_t>(B) * H] : c0[r * H + ej];
+      kf[e] = done[t * B + r] ? 0.f : 1.f;
+      knext[e] = t + 1 < T ? (done[(t + 1) * B + r] ? 0.f : 1.f) : 1.f;
+    }
+  };
+  fetch(T - 1);
+  const int arow = lane & 15, ak = 8 * (lane >> 4);
+  for (int t = T - 1; t >= 0; --t) {
+    const int p = T - 1 - t;  // processing step
+    float rec[2] = {0.f, 0.f};
+    bool fail = false;
+    if (t < T - 1) {
+      uint32_t v[16];
+      fail = !sweep<16, 2, 32 * kU>(xbuf + ((t + 1) & 1) * kBSlot + j * kBDest + 2 * tid,
+                                    static_cast<unsigned>(p), v, err);
+#pragma unroll
+      for (int src = 0; src < kGang; ++src) {
+        rec[0] += __uint_as_float(v[2 * src]);
+        rec[1] += __uint_as_float(v[2 * src + 1]);
+      }
+    }
+    const int par = t & 1;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float dgv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (live[e]) {
+        const float dh = dho[e] + knext[e] * rec[e];
+        const float tc = tanhf(cc[e]);
+        const float dc = carry[e] + dh * ao[e] * (1.f - tc * tc);
+        dgv[0] = dc * ag[e] * ai[e] * (1.f - ai[e]);
+        dgv[1] = dc * ai[e] * (1.f - ag[e] * ag[e]);
+        dgv[2] = dc * kf[e] * cpv[e] * af[e] * (1.f - af[e]);
+        dgv[3] = dh * tc * ao[e] * (1.f - ao[e]);
+        const int64_t g0 = (static_cast<int64_t>(t) * B + r0 + e) * 4 * H + ej;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          dg[g0 + g * H] = dgv[g];
+          if (dg16) dg16[g0 + g * H] = __float2bfloat16(dgv[g]);
+        }
+        carry[e] = dc * af[e] * kf[e];
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) d_s[par][r0 + e][g * kU + ul] = f2bf(dgv[g]);
+    }
+    if (__syncthreads_or(fail)) break;
+    if (t > 0) {
+      f4v acc[2][2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) acc[mt][a] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const bf8v av = __builtin_bit_cast(
+              bf8v, *reinterpret_cast<const uint4*>(&d_s[par][16 * mt + arow][32 * s + ak]));
+#pragma unroll
+          for (int a = 0; a < 2; ++a) acc[mt][a] = mfma(av, wb[a * 4 + s], acc[mt][a]);
+        }
+      }
+      // wave w's partial goes to destination workgroup w
+      unsigned long long* dst = xbuf + par * kBSlot + wave * kBDest + j * 32 * kU;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            publish(dst + ((mt * 2 + a) * 64 + lane) * 4 + i, static_cast<unsigned>(p + 1),
+                    __float_as_uint(acc[mt][a][i]));
+    }
+    if (t > 0) fetch(t - 1);
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+    if (live[e] && dc0) dc0[(r0 + e) * H + ej] = carry[e];
+}
+
+}  // namespace
+
+size_t lstm_gang_xbuf_granules(bool bwd) {
+  return 2 * static_cast<size_t>(bwd ? kBSlot : kFSlot);
+}
+
+void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stream) {
+  hipLaunchKernelGGL(lstm_gang_pack_kernel, dim3(kH * 4 * kH / 256), dim3(256), 0,
+                     stream, w, static_cast<bf16_t*>(wf), static_cast<bf16_t*>(wbk));
+}
+
+void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
+                          const uint8_t* done, const void* wf, float* hs, float* cs,
+                          float* acts, float* hpm, void* xbuf, unsigned* err, int T,
+                          int B, hipStream_t stream) {
+  hipLaunchKernelGGL(lstm_fwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream, xw,
+                     h0, c0, done, static_cast<const bf16_t*>(wf), hs, cs, acts, hpm,
+                     static_cast<unsigned long long*>(xbuf), err, T, B);
+}
+
+void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* wbk,
+                          const float* acts, const float* cs, const float* c0,
+                          const float* dc_last, float* dg, void* dg16, float* dc0,
+                          void* xbuf, unsigned* err, int T, int B, hipStream_t stream) {
+  hipLaunchKernelGGL(lstm_bwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream,
+                     dh_out, done, static_cast<const bf16_t*>(wbk), acts, cs, c0,
+                     dc_last, dg, static_cast<__hip_bfloat16*>(dg16), dc0,
+                     static_cast<unsigned long long*>(xbuf), err, T, B);
+}
+
+}  // namespace sa

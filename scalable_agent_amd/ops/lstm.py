@@ -79,6 +79,15 @@ def set_persistent(on):
   return prev
 
 
+def set_gang(on):
+  """Selects the 8-workgroup bf16-MFMA whole-unroll kernels (lstm_gang.hip;
+  B <= 32, H == 256); they take precedence over set_persistent.  Returns the
+  previous setting."""
+  prev = bool(ext().lstm_get_gang())
+  ext().lstm_set_gang(bool(on))
+  return prev
+
+
 def persistent_error(device):
   """Sticky timeout word of the persistent kernels on `device` (0 = healthy;
   nonzero means a workgroup could not co-reside and the unroll was

@@ -233,6 +233,51 @@ def test_lstm_persistent_matches_per_step(cuda, T, B):
                                msg='output %d' % i)
 
 
+@pytest.mark.parametrize('T,B', [(101, 32), (37, 7), (1, 32), (2, 5)])
+def test_lstm_gang_matches_per_step(cuda, T, B):
+  """The 8-workgroup gang kernels (bf16 recurrent product, granule
+  all-gather fwd / reduce-scatter bwd) track the fp32 per-step kernels to
+  bf16-operand accuracy, are bitwise repeatable over launches (stale-tag /
+  race check) and leave the error word clear."""
+  ops = _ops()
+  from scalable_agent_amd.ops import lstm as lstm_ops
+  C = ops.ext()
+  torch.manual_seed(11)
+  H = 256
+  xw = torch.randn(T, B, 4 * H, device=cuda)
+  done = (torch.rand(T, B, device=cuda) < 0.1).to(torch.uint8)
+  c0 = torch.randn(B, H, device=cuda) * 0.5
+  h0 = torch.randn(B, H, device=cuda) * 0.5
+  w_h = torch.randn(H, 4 * H, device=cuda) * 0.05
+  dh = torch.randn(T, B, H, device=cuda)
+  dcl = torch.randn(B, H, device=cuda)
+  outs = {}
+  prev_p = lstm_ops.set_persistent(False)
+  prev_g = lstm_ops.set_gang(False)
+  try:
+    for mode in (False, True):
+      lstm_ops.set_gang(mode)
+      runs = []
+      for _ in range(3 if mode else 1):
+        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
+        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True)
+        runs.append([hs, cs, acts, hpm, dg, dc0, dg16.float()])
+      for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+          assert torch.equal(a, b)
+      outs[mode] = runs[0]
+  finally:
+    lstm_ops.set_gang(prev_g)
+    lstm_ops.set_persistent(prev_p)
+  torch.cuda.synchronize()
+  assert lstm_ops.persistent_error(cuda) == 0
+  names = ['hs', 'cs', 'acts', 'hpm', 'dg', 'dc0', 'dg16']
+  for name, a, b in zip(names, outs[False], outs[True]):
+    rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+    assert rel < 1e-2, (name, rel)
+    torch.testing.assert_close(b, a, rtol=0.1, atol=0.05, msg=name)
+
+
 def test_instruction_encoder_hip_matches_torch(cuda):
   """Language LSTM (K7) on the H=64 fused step kernels vs the per-word
   PyTorch loop: outputs and gradients."""

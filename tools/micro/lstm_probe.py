@@ -1,4 +1,5 @@
-"""Times the LSTM recurrence kernels (persistent vs per-step) in a hipGraph."""
+"""Times the LSTM recurrence kernels (per-step, persistent fp32, 8-workgroup
+bf16 gang) in a hipGraph."""
 import os
 import sys
 import torch
@@ -40,13 +41,15 @@ def main():
   h0 = torch.randn(B, H, device=d) * 0.5
   w_h = torch.randn(H, 4 * H, device=d) * 0.05
   dh = torch.randn(T, B, H, device=d)
-  for mode, xp in ((False, 1), (False, 2), (False, 4), (False, 8), (True, 1)):
-    lstm_ops.set_persistent(mode)
+  for mode, xp in (('step', 4), ('persistent', 1), ('gang', 1), ('step', 4),
+                   ('gang', 1)):
+    lstm_ops.set_persistent(mode == 'persistent')
+    lstm_ops.set_gang(mode == 'gang')
     C.lstm_xpack(xp)
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
     f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h)
     b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True)
-    print('persistent=%d xpack=%d fwd %8.1f us  bwd %8.1f us' % (mode, xp, t_us(f), t_us(b)),
+    print('%-10s xpack=%d fwd %8.1f us  bwd %8.1f us' % (mode, xp, t_us(f), t_us(b)),
           flush=True)
   print('error word', lstm_ops.persistent_error(d))
 
