@@ -108,11 +108,13 @@ bool g_lstm_persistent = [] {
 bool use_persistent(int H, int B) { return g_lstm_persistent && H == 256 && B <= 32; }
 
 // Gang kernels (lstm_gang.hip: 8 workgroups, bf16 recurrent product) for
-// H == 256, B <= 32 (SA_LSTM_GANG=1 or lstm_set_gang(True)); they take
-// precedence over the fp32 persistent kernels.
+// H == 256, B <= 32: the DEFAULT (SA_LSTM_GANG=0 or lstm_set_gang(False)
+// selects the exact-fp32 per-step kernels); they take precedence over the
+// fp32 persistent kernels.  Measured at T=101, B=32 (tools/micro/
+// lstm_probe.py): fwd 446 vs 446-460 us, bwd 448 vs 724 us per unroll.
 bool g_lstm_gang = [] {
   const char* e = std::getenv("SA_LSTM_GANG");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }();
 
 bool use_gang(int H, int B) { return g_lstm_gang && H == 256 && B <= 32; }

@@ -17,13 +17,13 @@
 //   bwd: workgroup j owns units [32j, 32j+32); its dG_t slice stays in LDS
 //        and its wave w computes the PARTIAL dG_t[:, own] W_h[32w.., own]^T
 //        for destination workgroup w (a reduce-scatter): every workgroup
-//        sweeps 8 sources x 32 x 32 fp32 partials (64 KB) and sums them in
-//        a fixed order (deterministic).
+//        sweeps 8 sources x 32 x 32 partials as {tag, bf16 pair} granules
+//        (32 KB) and sums them in fp32 in a fixed order (deterministic).
 // Granule hand-off, tags, double-buffered slots, bounded spins and the
 // sticky error word are those of lstm_persistent.hip (file header there).
 // Numerics: the recurrent operand h_{t-1} / dG_{t+1} and W_h are rounded to
-// bf16 for the product only; the cell state, gates, carries and every
-// output stay fp32.  Requires B <= 32 (rows >= B are computed as zeros and
+// bf16 for the product only (and the bwd partial sums for the exchange);
+// the cell state, gates, carries and every output stay fp32.  Requires B <= 32 (rows >= B are computed as zeros and
 // never stored).
 #include "launchers.h"
 
@@ -46,7 +46,7 @@ constexpr int kGang = 8;              // workgroups
 constexpr int kU = kH / kGang;        // 32 units per workgroup
 constexpr int kThreads = 512;         // 8 waves
 constexpr int kFSlot = 32 * kH / 2;   // fwd granules per slot: [row][unit pair]
-constexpr int kBDest = 8 * 32 * kU;   // bwd granules per destination (8192)
+constexpr int kBDest = 8 * 16 * kU;   // bwd granules per destination (4096)
 constexpr int kBSlot = kGang * kBDest;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
@@ -255,10 +255,11 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
 // Thread tid owns pairs idx = 2 tid + e (e = 0, 1) of the destination
 // numbering idx = ((mt*2 + a)*64 + l)*4 + i4 (the MFMA D map of the
 // producing wave): rows 16mt + 4(l>>4) + i4, local unit 16a + (l&15).  The
-// producer of source j stores pair idx at granule j*1024 + idx of the
-// destination slot, so every 128-B line has ONE writer (a layout whose lines
-// mixed 8 sources' granules timed out sporadically on MI355X), and each
-// consumer thread sweeps 8 runs of 2 granules, 1024 granules apart.
+// producer of source j packs the partials of pairs 2 tid, 2 tid + 1 (rows
+// i4 = 2(tid&1) + {0,1} of one D register quad) into granule j*512 + tid of
+// the destination slot, so every 128-B line has ONE writer (a layout whose
+// lines mixed 8 sources' granules timed out sporadically on MI355X), and
+// consumer thread tid sweeps 8 granules, 512 apart.
 __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     const float* __restrict__ dh_out, const uint8_t* __restrict__ done,
     const bf16_t* __restrict__ wbk, const float* __restrict__ acts,
@@ -315,13 +316,13 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     float rec[2] = {0.f, 0.f};
     bool fail = false;
     if (t < T - 1) {
-      uint32_t v[16];
-      fail = !sweep<16, 2, 32 * kU>(xbuf + ((t + 1) & 1) * kBSlot + j * kBDest + 2 * tid,
-                                    static_cast<unsigned>(p), v, err);
+      uint32_t v[8];
+      fail = !sweep<8, 1, 16 * kU>(xbuf + ((t + 1) & 1) * kBSlot + j * kBDest + tid,
+                                   static_cast<unsigned>(p), v, err);
 #pragma unroll
       for (int src = 0; src < kGang; ++src) {
-        rec[0] += __uint_as_float(v[2 * src]);
-        rec[1] += __uint_as_float(v[2 * src + 1]);
+        rec[0] += __uint_as_float(v[src] << 16);
+        rec[1] += __uint_as_float(v[src] & 0xffff0000u);
       }
     }
     const int par = t & 1;
@@ -365,15 +366,15 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
         }
       }
       // wave w's partial goes to destination workgroup w
-      unsigned long long* dst = xbuf + par * kBSlot + wave * kBDest + j * 32 * kU;
+      unsigned long long* dst = xbuf + par * kBSlot + wave * kBDest + j * 16 * kU;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            publish(dst + ((mt * 2 + a) * 64 + lane) * 4 + i, static_cast<unsigned>(p + 1),
-                    __float_as_uint(acc[mt][a][i]));
+          for (int ip = 0; ip < 2; ++ip)
+            publish(dst + ((mt * 2 + a) * 64 + lane) * 2 + ip, static_cast<unsigned>(p + 1),
+                    pack2(acc[mt][a][2 * ip], acc[mt][a][2 * ip + 1]));
     }
     if (t > 0) fetch(t - 1);
   }
