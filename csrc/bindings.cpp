@@ -297,6 +297,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_get_persistent", &lstm_get_persistent);
   m.def("lstm_set_gang", &lstm_set_gang);
   m.def("lstm_get_gang", &lstm_get_gang);
+  m.def("lstm_gang_ws", [](int v) { return sa::lstm_gang_ws(v); });
+  m.def("lstm_gang_nap", [](int v) { return sa::lstm_gang_nap(v); });
   m.def("lstm_error_word", &lstm_error);
   m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);

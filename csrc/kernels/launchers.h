@@ -87,6 +87,11 @@ void lstm_bwd_persistent_launch(const float* dh_out, const uint8_t* done,
 // KB each) of W_h [256,1024]; xbuf: lstm_gang_xbuf_granules(bwd) zeroed
 // granules (zero before EVERY launch); err: the sticky timeout word.
 size_t lstm_gang_xbuf_granules(bool bwd);
+// 1 = wave-specialised kernels, 0 = uniform roles (default); other values
+// only query.  Returns the previous value.
+int lstm_gang_ws(int v);
+// s_sleep(1) count between sweep passes (0..64; other values only query).
+int lstm_gang_nap(int v);
 void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stream);
 void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
                           const uint8_t* done, const void* wf, float* hs, float* cs,

@@ -29,6 +29,8 @@
 
 #include <hip/hip_bf16.h>
 
+#include <cstdlib>
+
 namespace sa {
 namespace {
 
@@ -73,7 +75,7 @@ __device__ __forceinline__ void publish(unsigned long long* g, unsigned tag,
 // run, runs S granules apart).
 template <int N, int R = N, int S = 0>
 __device__ __forceinline__ bool sweep(const unsigned long long* g, unsigned tag,
-                                      uint32_t (&v)[N], unsigned* err) {
+                                      uint32_t (&v)[N], unsigned* err, int nap = 1) {
   const gu64* p = (const gu64*)(g);
   for (unsigned spins = 0;; ++spins) {
     bool ok = true;
@@ -94,7 +96,7 @@ __device__ __forceinline__ bool sweep(const unsigned long long* g, unsigned tag,
                          __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    for (int i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(1);
   }
 }
 
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
     const bf16_t* __restrict__ wf, float* __restrict__ hs, float* __restrict__ cs,
     float* __restrict__ acts, float* __restrict__ hpm,
     unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
-    int B) {
+    int B, int nap) {
   constexpr int H = kH;
   __shared__ __attribute__((aligned(16))) bf16_t h_s[32][H + 8];
   __shared__ __attribute__((aligned(16))) float g_s[32][128 + 4];
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
           v[p] = keep ? pack2(hr[2 * p], hr[2 * p + 1]) : 0u;
       } else {
         fail = !sweep<8>(xbuf + ((t - 1) & 1) * kFSlot + 8 * tid,
-                         static_cast<unsigned>(t), v, err);
+                         static_cast<unsigned>(t), v, err, nap);
         if (!keep) {
 #pragma unroll
           for (int p = 0; p < 8; ++p) v[p] = 0u;
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     const float* __restrict__ dc_last, float* __restrict__ dg,
     __hip_bfloat16* __restrict__ dg16, float* __restrict__ dc0,
     unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
-    int B) {
+    int B, int nap) {
   constexpr int H = kH;
   __shared__ __attribute__((aligned(16))) bf16_t d_s[2][32][4 * kU + 8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     if (t < T - 1) {
       uint32_t v[8];
       fail = !sweep<8, 1, 16 * kU>(xbuf + ((t + 1) & 1) * kBSlot + j * kBDest + tid,
-                                   static_cast<unsigned>(p), v, err);
+                                   static_cast<unsigned>(p), v, err, nap);
 #pragma unroll
       for (int src = 0; src < kGang; ++src) {
         rec[0] += __uint_as_float(v[src] << 16);
@@ -383,6 +385,296 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     if (live[e] && dc0) dc0[(r0 + e) * H + ej] = carry[e];
 }
 
+// ------------------------------------------------- wave-specialised variants
+// Same protocol, layouts and outputs as the kernels above, but the waves that
+// POLL never have global stores in flight: on gfx950 one vmcnt counter covers
+// loads and stores, so a sweep issued behind the epilogue's output stores and
+// its own sc1 publish store could not retire a pass before those writes were
+// acknowledged by memory.
+//   fwd: waves 4-7 sweep h_{t-1} into the LDS A image; all 8 waves run the
+//        MFMAs; waves 0-3 run the epilogue (thread: row tid>>3, units
+//        32j + 4(tid&7) .. +4), publish and store the outputs.
+//   bwd: waves 0-3 sweep the partials and run the epilogue (thread: unit
+//        16a + (l&15), rows 16mt + 4(l>>4) + 0..3 for st = tid: l = st&63,
+//        a = (st>>6)&1, mt = st>>7) and stage dG (bf16 A image + fp32 copy)
+//        in LDS; waves 4-7 run the MFMAs for destinations 2w', 2w'+1,
+//        publish, and store dg / dg16 from the fp32 LDS copy.
+__global__ __launch_bounds__(kThreads) void lstm_fwd_gang_ws_kernel(
+    const float* __restrict__ xw, const float* __restrict__ h0,
+    const float* __restrict__ c0, const uint8_t* __restrict__ done,
+    const bf16_t* __restrict__ wf, float* __restrict__ hs, float* __restrict__ cs,
+    float* __restrict__ acts, float* __restrict__ hpm,
+    unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
+    int B, int nap) {
+  constexpr int H = kH;
+  __shared__ __attribute__((aligned(16))) bf16_t h_s[32][H + 8];
+  __shared__ __attribute__((aligned(16))) float g_s[32][128 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x;
+  const bool epi_wave = wave < 4;
+  bf8v wb[8];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wf) + (j * 8 + wave) * 8 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) wb[s] = __builtin_bit_cast(bf8v, src[s * 64]);
+  }
+  // epilogue role
+  const int er = (tid & 255) >> 3, uq = tid & 7;
+  const int ej = j * kU + 4 * uq;
+  const bool live = epi_wave && er < B;
+  float c[4] = {0.f, 0.f, 0.f, 0.f}, h[4] = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    const float4 c4 = *reinterpret_cast<const float4*>(c0 + er * H + ej);
+    const float4 h4 = *reinterpret_cast<const float4*>(h0 + er * H + ej);
+    c[0] = c4.x; c[1] = c4.y; c[2] = c4.z; c[3] = c4.w;
+    h[0] = h4.x; h[1] = h4.y; h[2] = h4.z; h[3] = h4.w;
+  }
+  float4 xv[4] = {};
+  float ekeep = 0.f;
+  auto fetch = [&](int t) {
+    if (live) {
+      const int64_t g0 = (static_cast<int64_t>(t) * B + er) * 4 * H + ej;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) xv[g] = *reinterpret_cast<const float4*>(xw + g0 + g * H);
+      ekeep = done[t * B + er] ? 0.f : 1.f;
+    }
+  };
+  fetch(0);
+  // sweep role: granules [16 st, 16 st + 16) = row st>>3, units 32(st&7) .. +32
+  const int st = tid & 255, sr = st >> 3, su0 = 32 * (st & 7);
+  const int arow = lane & 15, ak = 8 * (lane >> 4);
+  for (int t = 0; t < T; ++t) {
+    bool fail = false;
+    if (!epi_wave) {
+      const bool keep = sr < B && !done[t * B + (sr < B ? sr : 0)];
+      uint32_t v[16];
+      if (t == 0) {
+        const float* hr = h0 + (sr < B ? sr : 0) * H + su0;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) v[p] = keep ? pack2(hr[2 * p], hr[2 * p + 1]) : 0u;
+      } else {
+        fail = !sweep<16>(xbuf + ((t - 1) & 1) * kFSlot + 16 * st,
+                          static_cast<unsigned>(t), v, err, nap);
+        if (!keep) {
+#pragma unroll
+          for (int p = 0; p < 16; ++p) v[p] = 0u;
+        }
+      }
+      uint4* dst = reinterpret_cast<uint4*>(&h_s[sr][su0]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = uint4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    }
+    if (__syncthreads_or(fail)) break;
+    {
+      f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const bf8v a = __builtin_bit_cast(
+              bf8v, *reinterpret_cast<const uint4*>(&h_s[16 * mt + arow][32 * s + ak]));
+          acc[mt] = mfma(a, wb[s], acc[mt]);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          g_s[16 * mt + 4 * (lane >> 4) + i][16 * wave + (lane & 15)] = acc[mt][i];
+    }
+    __syncthreads();
+    if (epi_wave) {
+      float hn[4], gi[4], gg[4], gf[4], go[4], hp[4];
+      const float* xg[4] = {&xv[0].x, &xv[1].x, &xv[2].x, &xv[3].x};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 gv = *reinterpret_cast<const float4*>(&g_s[er][16 * uq + 4 * e]);
+        gi[e] = sigm(gv.x + xg[0][e]);
+        gg[e] = tanhf(gv.y + xg[1][e]);
+        gf[e] = sigm(gv.z + xg[2][e] + 1.0f);
+        go[e] = sigm(gv.w + xg[3][e]);
+        hp[e] = h[e];
+        c[e] = gf[e] * ekeep * c[e] + gi[e] * gg[e];
+        hn[e] = live ? go[e] * tanhf(c[e]) : 0.f;
+        h[e] = hn[e];
+      }
+      unsigned long long* pub = xbuf + (t & 1) * kFSlot + er * (H / 2) + j * (kU / 2) + 2 * uq;
+      publish(pub, static_cast<unsigned>(t + 1), pack2(hn[0], hn[1]));
+      publish(pub + 1, static_cast<unsigned>(t + 1), pack2(hn[2], hn[3]));
+      if (live) {
+        const int64_t hj = (static_cast<int64_t>(t) * B + er) * H + ej;
+        const int64_t g0 = (static_cast<int64_t>(t) * B + er) * 4 * H + ej;
+        *reinterpret_cast<float4*>(hs + hj) = float4{hn[0], hn[1], hn[2], hn[3]};
+        *reinterpret_cast<float4*>(cs + hj) = float4{c[0], c[1], c[2], c[3]};
+        *reinterpret_cast<float4*>(hpm + hj) =
+            float4{ekeep * hp[0], ekeep * hp[1], ekeep * hp[2], ekeep * hp[3]};
+        *reinterpret_cast<float4*>(acts + g0) = float4{gi[0], gi[1], gi[2], gi[3]};
+        *reinterpret_cast<float4*>(acts + g0 + H) = float4{gg[0], gg[1], gg[2], gg[3]};
+        *reinterpret_cast<float4*>(acts + g0 + 2 * H) = float4{gf[0], gf[1], gf[2], gf[3]};
+        *reinterpret_cast<float4*>(acts + g0 + 3 * H) = float4{go[0], go[1], go[2], go[3]};
+      }
+      if (t + 1 < T) fetch(t + 1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void lstm_bwd_gang_ws_kernel(
+    const float* __restrict__ dh_out, const uint8_t* __restrict__ done,
+    const bf16_t* __restrict__ wbk, const float* __restrict__ acts,
+    const float* __restrict__ cs, const float* __restrict__ c0,
+    const float* __restrict__ dc_last, float* __restrict__ dg,
+    __hip_bfloat16* __restrict__ dg16, float* __restrict__ dc0,
+    unsigned long long* __restrict__ xbuf, unsigned* __restrict__ err, int T,
+    int B, int nap) {
+  constexpr int H = kH;
+  __shared__ __attribute__((aligned(16))) bf16_t d_s[2][32][4 * kU + 8];
+  __shared__ __attribute__((aligned(16))) float f_s[2][32][4 * kU + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x;
+  const bool epi_wave = wave < 4;
+  const int mw = wave & 3;  // MFMA role: destinations 2mw, 2mw + 1
+  bf8v wb[2][8];
+  if (!epi_wave) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const uint4* src =
+          reinterpret_cast<const uint4*>(wbk) + (j * 8 + 2 * mw + d) * 8 * 64 + lane;
+#pragma unroll
+      for (int f = 0; f < 8; ++f) wb[d][f] = __builtin_bit_cast(bf8v, src[f * 64]);
+    }
+  }
+  // epilogue role: unit ul, rows r0 .. r0+3
+  const int st = tid & 255, pl = st & 63, pa = (st >> 6) & 1, pmt = st >> 7;
+  const int r0 = 16 * pmt + 4 * (pl >> 4);
+  const int ul = 16 * pa + (pl & 15), ej = j * kU + ul;
+  bool live[4];
+  float carry[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    live[e] = epi_wave && r0 + e < B;
+    if (live[e] && dc_last) carry[e] = dc_last[(r0 + e) * H + ej];
+  }
+  float dho[4] = {}, ai[4] = {}, ag[4] = {}, af[4] = {}, ao[4] = {}, cc[4] = {},
+        cpv[4] = {}, kf[4] = {}, knext[4] = {1.f, 1.f, 1.f, 1.f};
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!live[e]) continue;
+      const int r = r0 + e;
+      const int64_t hj = (static_cast<int64_t>(t) * B + r) * H + ej;
+      const int64_t g0 = (static_cast<int64_t>(t) * B + r) * 4 * H + ej;
+      dho[e] = dh_out[hj];
+      ai[e] = acts[g0];
+      ag[e] = acts[g0 + H];
+      af[e] = acts[g0 + 2 * H];
+      ao[e] = acts[g0 + 3 * H];
+      cc[e] = cs[hj];
+      cpv[e] = t > 0 ? cs[hj - static_cast<int64_t>(B) * H] : c0[r * H + ej];
+      kf[e] = done[t * B + r] ? 0.f : 1.f;
+      knext[e] = t + 1 < T ? (done[(t + 1) * B + r] ? 0.f : 1.f) : 1.f;
+    }
+  };
+  if (epi_wave) fetch(T - 1);
+  const int arow = lane & 15, ak = 8 * (lane >> 4);
+  for (int t = T - 1; t >= 0; --t) {
+    const int p = T - 1 - t;
+    const int par = t & 1;
+    bool fail = false;
+    if (epi_wave) {
+      float rec[4] = {0.f, 0.f, 0.f, 0.f};
+      if (t < T - 1) {
+        uint32_t v[16];
+        fail = !sweep<16, 2, 16 * kU>(xbuf + ((t + 1) & 1) * kBSlot + j * kBDest + 2 * st,
+                                      static_cast<unsigned>(p), v, err, nap);
+#pragma unroll
+        for (int src = 0; src < kGang; ++src) {
+          rec[0] += __uint_as_float(v[2 * src] << 16);
+          rec[1] += __uint_as_float(v[2 * src] & 0xffff0000u);
+          rec[2] += __uint_as_float(v[2 * src + 1] << 16);
+          rec[3] += __uint_as_float(v[2 * src + 1] & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float dgv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (live[e]) {
+          const float dh = dho[e] + knext[e] * rec[e];
+          const float tc = tanhf(cc[e]);
+          const float dc = carry[e] + dh * ao[e] * (1.f - tc * tc);
+          dgv[0] = dc * ag[e] * ai[e] * (1.f - ai[e]);
+          dgv[1] = dc * ai[e] * (1.f - ag[e] * ag[e]);
+          dgv[2] = dc * kf[e] * cpv[e] * af[e] * (1.f - af[e]);
+          dgv[3] = dh * tc * ao[e] * (1.f - ao[e]);
+          carry[e] = dc * af[e] * kf[e];
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          d_s[par][r0 + e][g * kU + ul] = f2bf(dgv[g]);
+          f_s[par][r0 + e][g * kU + ul] = dgv[g];
+        }
+      }
+      if (t > 0) fetch(t - 1);
+    }
+    if (__syncthreads_or(fail)) break;
+    if (!epi_wave) {
+      if (t > 0) {
+        f4v acc[2][2][2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) acc[d][mt][a] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt) {
+            const bf8v av = __builtin_bit_cast(
+                bf8v, *reinterpret_cast<const uint4*>(&d_s[par][16 * mt + arow][32 * s + ak]));
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+#pragma unroll
+              for (int a = 0; a < 2; ++a)
+                acc[d][mt][a] = mfma(av, wb[d][a * 4 + s], acc[d][mt][a]);
+          }
+        }
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          unsigned long long* dst =
+              xbuf + par * kBSlot + (2 * mw + d) * kBDest + j * 16 * kU;
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+              for (int ip = 0; ip < 2; ++ip)
+                publish(dst + ((mt * 2 + a) * 64 + lane) * 2 + ip,
+                        static_cast<unsigned>(p + 1),
+                        pack2(acc[d][mt][a][2 * ip], acc[d][mt][a][2 * ip + 1]));
+        }
+      }
+      // outputs: 32 rows x 128 local columns, float4 per (row, gate, unit quad)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int q = st + 256 * k;  // 0..1023
+        const int r = q >> 5, g = (q >> 3) & 3, u4 = (q & 7) * 4;
+        if (r < B) {
+          const float4 v = *reinterpret_cast<const float4*>(&f_s[par][r][g * kU + u4]);
+          const int64_t g0 = (static_cast<int64_t>(t) * B + r) * 4 * H + g * H + j * kU + u4;
+          *reinterpret_cast<float4*>(dg + g0) = v;
+          if (dg16) {
+            uint2 pk{pack2(v.x, v.y), pack2(v.z, v.w)};
+            *reinterpret_cast<uint2*>(dg16 + g0) = pk;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (live[e] && dc0) dc0[(r0 + e) * H + ej] = carry[e];
+}
+
 }  // namespace
 
 size_t lstm_gang_xbuf_granules(bool bwd) {
@@ -394,23 +686,48 @@ void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stre
                      stream, w, static_cast<bf16_t*>(wf), static_cast<bf16_t*>(wbk));
 }
 
+// Uniform-role kernels by default; SA_LSTM_GANG_WS=1 selects the wave-
+// specialised ones, measured slower (T=101, B=32: fwd 676-678 vs 446-448 us,
+// bwd 823-839 vs 448-449 us; tools/micro/lstm_probe.py).
+static int g_gang_ws = [] {
+  const char* e = std::getenv("SA_LSTM_GANG_WS");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
+// s_sleep(1) count between sweep passes (SA_LSTM_GANG_NAP, default 1).
+static int g_gang_nap = [] {
+  const char* e = std::getenv("SA_LSTM_GANG_NAP");
+  const int v = e ? std::atoi(e) : 1;
+  return v >= 0 && v <= 64 ? v : 1;
+}();
+int lstm_gang_nap(int v) {
+  const int old = g_gang_nap;
+  if (v >= 0 && v <= 64) g_gang_nap = v;
+  return old;
+}
+
+int lstm_gang_ws(int v) {
+  const int old = g_gang_ws;
+  if (v == 0 || v == 1) g_gang_ws = v;
+  return old;
+}
+
 void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
                           const uint8_t* done, const void* wf, float* hs, float* cs,
                           float* acts, float* hpm, void* xbuf, unsigned* err, int T,
                           int B, hipStream_t stream) {
-  hipLaunchKernelGGL(lstm_fwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream, xw,
+  hipLaunchKernelGGL(g_gang_ws ? lstm_fwd_gang_ws_kernel : lstm_fwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream, xw,
                      h0, c0, done, static_cast<const bf16_t*>(wf), hs, cs, acts, hpm,
-                     static_cast<unsigned long long*>(xbuf), err, T, B);
+                     static_cast<unsigned long long*>(xbuf), err, T, B, g_gang_nap);
 }
 
 void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* wbk,
                           const float* acts, const float* cs, const float* c0,
                           const float* dc_last, float* dg, void* dg16, float* dc0,
                           void* xbuf, unsigned* err, int T, int B, hipStream_t stream) {
-  hipLaunchKernelGGL(lstm_bwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream,
+  hipLaunchKernelGGL(g_gang_ws ? lstm_bwd_gang_ws_kernel : lstm_bwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream,
                      dh_out, done, static_cast<const bf16_t*>(wbk), acts, cs, c0,
                      dc_last, dg, static_cast<__hip_bfloat16*>(dg16), dc0,
-                     static_cast<unsigned long long*>(xbuf), err, T, B);
+                     static_cast<unsigned long long*>(xbuf), err, T, B, g_gang_nap);
 }
 
 }  // namespace sa

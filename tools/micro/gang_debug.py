@@ -20,7 +20,9 @@ def main():
   C = ops.load()
   d = torch.device('cuda')
   H = 256
-  for T, B in [(37, 7), (37, 8), (37, 32), (101, 7), (4, 7), (2, 1)]:
+  ws = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+  C.lstm_gang_ws(ws)
+  for T, B in [(37, 7), (37, 8), (37, 32), (101, 7), (101, 32), (4, 7), (2, 1)]:
     torch.manual_seed(11)
     xw = torch.randn(T, B, 4 * H, device=d)
     done = (torch.rand(T, B, device=d) < 0.1).to(torch.uint8)

@@ -41,15 +41,18 @@ def main():
   h0 = torch.randn(B, H, device=d) * 0.5
   w_h = torch.randn(H, 4 * H, device=d) * 0.05
   dh = torch.randn(T, B, H, device=d)
-  for mode, xp in (('step', 4), ('persistent', 1), ('gang', 1), ('step', 4),
-                   ('gang', 1)):
+  modes = [('step', 4, 1), ('persistent', 1, 1), ('gang_ws', 1, 1)]
+  modes += [('gang', 1, nap) for nap in (0, 1, 2, 4, 8, 16, 1, 0)]
+  for mode, xp, nap in modes:
     lstm_ops.set_persistent(mode == 'persistent')
-    lstm_ops.set_gang(mode == 'gang')
+    lstm_ops.set_gang(mode.startswith('gang'))
+    C.lstm_gang_ws(1 if mode == 'gang_ws' else 0)
+    C.lstm_gang_nap(nap)
     C.lstm_xpack(xp)
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
     f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h)
     b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True)
-    print('%-10s xpack=%d fwd %8.1f us  bwd %8.1f us' % (mode, xp, t_us(f), t_us(b)),
+    print('%-10s xpack=%d nap=%2d fwd %8.1f us  bwd %8.1f us' % (mode, xp, nap, t_us(f), t_us(b)),
           flush=True)
   print('error word', lstm_ops.persistent_error(d))
 
