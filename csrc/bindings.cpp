@@ -8,6 +8,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <mutex>
 
 #include "kernels/launchers.h"
 #include "kernels/conv_launchers.h"
@@ -117,10 +118,15 @@ bool g_lstm_gang = [] {
   return !(e && e[0] == '0');
 }();
 
-bool use_gang(int H, int B) { return g_lstm_gang && H == 256 && B <= 32; }
+// T == 1 (actor inference steps) stays on the per-step kernels: one step
+// gains nothing from the gang and the inference graphs keep their layout.
+bool use_gang(int H, int B, int T) { return g_lstm_gang && H == 256 && B <= 32 && T >= 2; }
 
 // Sticky per-device timeout word of the persistent kernels (0 = healthy).
 at::Tensor lstm_err_word(const at::Device& dev) {
+  // called from the learner and from actor-inference threads
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
   static std::map<int, at::Tensor> words;
   auto it = words.find(dev.index());
   if (it != words.end()) return it->second;
@@ -157,7 +163,7 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   auto hpk = at::empty({2, RT * 32 * H}, xw.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
-  if (use_gang(H, B)) {
+  if (use_gang(H, B, T)) {
     // w4 / wt carry the bf16 gang fragments instead (512 KB of their 1 MB)
     sa::lstm_gang_pack_launch(w_h.data_ptr<float>(), w4.data_ptr(), wt.data_ptr(), s);
     auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(false)},
@@ -220,7 +226,7 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
   auto dgpk = at::empty({2, RT * 32 * H4}, acts.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
-  if (use_gang(H, B)) {
+  if (use_gang(H, B, T)) {
     auto dc0 = at::empty({B, H}, acts.options());
     auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(true)},
                           acts.options().dtype(at::kLong));

@@ -257,8 +257,9 @@ def test_lstm_persistent_matches_per_step(cuda, T, B):
                                msg='output %d' % i)
 
 
+@pytest.mark.parametrize('ws', [0, 1])
 @pytest.mark.parametrize('T,B', [(101, 32), (37, 7), (1, 32), (2, 5)])
-def test_lstm_gang_matches_per_step(cuda, T, B):
+def test_lstm_gang_matches_per_step(cuda, T, B, ws):
   """The 8-workgroup gang kernels (bf16 recurrent product, granule
   all-gather fwd / reduce-scatter bwd) track the fp32 per-step kernels to
   bf16-operand accuracy, are bitwise repeatable over launches (stale-tag /
@@ -278,6 +279,7 @@ def test_lstm_gang_matches_per_step(cuda, T, B):
   outs = {}
   prev_p = lstm_ops.set_persistent(False)
   prev_g = lstm_ops.set_gang(False)
+  prev_ws = C.lstm_gang_ws(ws)  # 1: the opt-in wave-specialised kernels
   try:
     for mode in (False, True):
       lstm_ops.set_gang(mode)
@@ -291,6 +293,7 @@ def test_lstm_gang_matches_per_step(cuda, T, B):
           assert torch.equal(a, b)
       outs[mode] = runs[0]
   finally:
+    C.lstm_gang_ws(prev_ws)
     lstm_ops.set_gang(prev_g)
     lstm_ops.set_persistent(prev_p)
   torch.cuda.synchronize()
