@@ -59,6 +59,9 @@ def main():
 
   rank, world, local = parallel.init_distributed()
   if args.device == 'auto':
+    # SA_DIST_BACKEND (one-card rehearsal): ranks share the visible GPUs
+    if os.environ.get('SA_DIST_BACKEND') and torch.cuda.is_available():
+      local = local % torch.cuda.device_count()
     device = torch.device('cuda', local) if torch.cuda.is_available() else \
         torch.device('cpu')
   else:
