@@ -3,21 +3,28 @@
 
 Config (BASELINE.json): B=32 per learner, unroll T=100 (T+1=101 frames per
 sequence), 4 action repeats -> 12 800 env frames per learner step, synthetic
-72x96x3 uint8 frames, 9 actions, random-init weights, bf16 convs/GEMMs with
-fp32 V-trace/loss/optimizer state.  One process per GPU; N>1 is weak scaling
-(each learner consumes its own B=32 batch, gradients summed with one RCCL
-all-reduce).
+72x96x3 uint8 frames, 9 actions, random-init weights.
 
-Every timed step does the full learner work of experiment.py:346-427: H2D of
-the next batch from pinned host memory (StagingArea equivalent, overlapped on
-a copy stream), T+1-step re-unroll, V-trace, loss, backward, gradient
-all-reduce, RMSProp with on-device LR decay, frame-counter increment.
+Precision: the reported `value` is measured at the REFERENCE's precision,
+fp32 (reference experiment.py:153-189, 118, 413-415 all run fp32): exact-fp32
+MFMA conv kernels (v_mfma_f32_16x16x4_f32), fp32 LSTM recurrence, fp32
+V-trace / loss / RMSProp.  The bf16 learner (bf16 conv/GEMM operands, fp32
+accumulation and state) is measured in the same run as a second field
+(`config.bf16`), unless --dtype bf16 makes it the headline.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+One process per GPU; N>1 is weak scaling (each learner consumes its own B=32
+batch, gradients summed with one RCCL all-reduce).  Every timed step does the
+full learner work of experiment.py:346-427: H2D of the next batch from pinned
+host memory (StagingArea equivalent, overlapped on a copy stream), T+1-step
+re-unroll, V-trace, loss, backward, gradient all-reduce, RMSProp with
+on-device LR decay, frame-counter increment.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
 (multi-GPU: launched by torch.distributed.run, one rank per GPU).
 """
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -31,6 +38,7 @@ from scalable_agent_amd import flags as flags_lib  # noqa: E402
 from scalable_agent_amd.envs.synthetic import make_synthetic_batch  # noqa
 from scalable_agent_amd.learner import FlatStaging, Learner  # noqa
 from scalable_agent_amd.models import Agent  # noqa: E402
+from scalable_agent_amd.models.agent import torso_precision  # noqa: E402
 from scalable_agent_amd import parallel  # noqa: E402
 
 METRIC = ('learner env-frames/sec, IMPALA deep-ResNet+LSTM, batch=32 '
@@ -38,50 +46,15 @@ METRIC = ('learner env-frames/sec, IMPALA deep-ResNet+LSTM, batch=32 '
 BASELINE_FPS = 250000.0  # BASELINE.md §B best published single-learner figure
 
 
-def main():
-  ap = argparse.ArgumentParser()
-  ap.add_argument('--gpus', type=int, default=1)
-  ap.add_argument('--steps', type=int, default=20)
-  ap.add_argument('--warmup', type=int, default=5)
-  ap.add_argument('--batch_size', type=int, default=32)
-  ap.add_argument('--unroll_length', type=int, default=100)
-  ap.add_argument('--torso', default='deep')
-  ap.add_argument('--height', type=int, default=72)
-  ap.add_argument('--width', type=int, default=96)
-  ap.add_argument('--backend', default='auto', choices=['auto', 'torch', 'hip'])
-  ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-  ap.add_argument('--graph', type=int, default=1)
-  ap.add_argument('--device', default='auto')
-  ap.add_argument('--profile_steps', type=int, default=0)
-  ap.add_argument('--pipeline_chunks', type=int, default=1,
-                  help='time chunks of the torso || LSTM pipeline (1 = off)')
-  args = ap.parse_args()
-
-  rank, world, local = parallel.init_distributed()
-  if args.device == 'auto':
-    # SA_DIST_BACKEND (one-card rehearsal): ranks share the visible GPUs
-    if os.environ.get('SA_DIST_BACKEND') and torch.cuda.is_available():
-      local = local % torch.cuda.device_count()
-    device = torch.device('cuda', local) if torch.cuda.is_available() else \
-        torch.device('cpu')
-  else:
-    device = torch.device(args.device)
-  if device.type == 'cuda':
-    torch.cuda.set_device(device)
-
-  backend = args.backend
-  if backend == 'auto':
-    backend = 'torch'
-    if device.type == 'cuda':
-      from scalable_agent_amd import ops
-      backend = 'hip' if ops.available() else 'torch'
-
+def measure(args, dtype, device, backend, rank, world):
+  """Builds one learner at `dtype` and times K steps after W warmups.
+  Returns a dict of per-rank results (dt is the MAX over ranks)."""
   flags = flags_lib.default_flags(
       batch_size=args.batch_size, unroll_length=args.unroll_length,
-      torso=args.torso, dtype=args.dtype, height=args.height, width=args.width)
+      torso=args.torso, dtype=dtype, height=args.height, width=args.width)
   num_actions = 9
-  frame_shape = (args.height, args.width, 3)
-  cdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+  frame_shape = (args.height, args.width, args.channels)
+  cdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
   agent = Agent(num_actions, torso=args.torso, frame_shape=frame_shape,
                 seed=flags.seed, backend=backend, compute_dtype=cdt,
                 pipeline_chunks=args.pipeline_chunks)
@@ -89,14 +62,14 @@ def main():
   if world > 1:
     parallel.broadcast_params(learner.flat.params)
 
-  pin = device.type == 'cuda'
   host_batches = [
       make_synthetic_batch(args.batch_size, args.unroll_length, frame_shape,
                            num_actions, seed=1000 * rank + i, pin_memory=False)
       for i in range(2)]
-
-  use_graph = bool(args.graph) and device.type == 'cuda'
-  if device.type == 'cuda':
+  cuda = device.type == 'cuda'
+  use_graph = bool(args.graph) and cuda
+  graphs = []
+  if cuda:
     copy_stream = torch.cuda.Stream(device)
     # one flat pinned host buffer per batch and one flat device buffer per
     # staging slot: the per-step prefetch is ONE H2D copy
@@ -106,25 +79,21 @@ def main():
     slots = [d.views for d in dev_flat]
     if use_graph:
       # one captured graph per staging slot (static input addresses)
-      learner.capture(slots[0], clone=False)
-      g0 = (learner._graph, learner._static_in, learner._static_loss)
-      learner.capture(slots[1], clone=False)
-      g1 = (learner._graph, learner._static_in, learner._static_loss)
-      graphs = [g0, g1]
+      for sl in slots:
+        learner.capture(sl, clone=False)
+        graphs.append((learner._graph, learner._static_in, learner._static_loss))
     slot_free = [torch.cuda.Event(), torch.cuda.Event()]
     slot_ready = [torch.cuda.Event(), torch.cuda.Event()]
-    for e in slot_ready:
+    for e in slot_ready + slot_free:
       e.record()
-    for e in slot_free:
-      e.record()
-  comp = torch.cuda.current_stream(device) if device.type == 'cuda' else None
+    comp = torch.cuda.current_stream(device)
   # diagnostic only (never the reported benchmark): SA_BENCH_SKIP_H2D=1 drops
   # the per-step host->device prefetch of the next batch
   skip_h2d = os.environ.get('SA_BENCH_SKIP_H2D') == '1'
 
   def run_step(k):
     i = k % 2
-    if device.type != 'cuda':
+    if not cuda:
       return learner.step(host_batches[i])
     # prefetch batch k+1 into the other slot while computing on slot i
     j = (k + 1) % 2
@@ -143,11 +112,11 @@ def main():
     return loss
 
   def sync():
-    if device.type == 'cuda':
+    if cuda:
       torch.cuda.synchronize(device)
     if world > 1:
       torch.distributed.barrier()
-    if device.type == 'cuda':
+    if cuda:
       torch.cuda.synchronize(device)
 
   for k in range(args.warmup):
@@ -163,31 +132,111 @@ def main():
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     dt = float(t.item())
-  frames = learner.frames_per_step * args.steps
-  value = frames / dt
-  ok = bool(torch.isfinite(loss).item())
+  res = {
+      'dt': dt, 'loss_finite': bool(torch.isfinite(loss).item()),
+      'enqueue_s': t_enq, 'frames_per_step': learner.frames_per_step,
+      'health': learner.health(), 'torso': torso_precision(agent),
+      'hip_graph': use_graph, 'h2d_prefetch': not skip_h2d,
+  }
+  del learner, agent, graphs
+  gc.collect()
+  if cuda:
+    torch.cuda.synchronize(device)
+    torch.cuda.empty_cache()
+  return res
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=20)
+  ap.add_argument('--warmup', type=int, default=5)
+  ap.add_argument('--batch_size', type=int, default=32)
+  ap.add_argument('--unroll_length', type=int, default=100)
+  ap.add_argument('--torso', default='deep')
+  ap.add_argument('--height', type=int, default=72)
+  ap.add_argument('--width', type=int, default=96)
+  ap.add_argument('--channels', type=int, default=3)
+  ap.add_argument('--backend', default='auto', choices=['auto', 'torch', 'hip'])
+  ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                  help='precision of the reported value (fp32 = reference)')
+  ap.add_argument('--also_bf16', type=int, default=1,
+                  help='with --dtype fp32: also time the bf16 learner')
+  ap.add_argument('--graph', type=int, default=1)
+  ap.add_argument('--device', default='auto')
+  ap.add_argument('--pipeline_chunks', type=int, default=1,
+                  help='time chunks of the torso || LSTM pipeline (1 = off)')
+  args = ap.parse_args()
+
+  rank, world, local = parallel.init_distributed()
+  if args.gpus != world:
+    raise SystemExit(
+        'bench.py: --gpus %d but WORLD_SIZE=%d; launch N>1 GPUs with '
+        '`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`'
+        % (args.gpus, world))
+  if args.device == 'auto':
+    # one-card rehearsal (SA_DIST_BACKEND): ranks share the visible GPUs
+    if torch.cuda.is_available():
+      local = local % torch.cuda.device_count()
+    device = torch.device('cuda', local) if torch.cuda.is_available() else \
+        torch.device('cpu')
+  else:
+    device = torch.device(args.device)
+  if device.type == 'cuda':
+    torch.cuda.set_device(device)
+
+  backend = args.backend
+  if backend == 'auto':
+    backend = 'torch'
+    if device.type == 'cuda':
+      from scalable_agent_amd import ops
+      backend = 'hip' if ops.available() else 'torch'
+
+  main_res = measure(args, args.dtype, device, backend, rank, world)
+  extra = None
+  if args.dtype == 'fp32' and args.also_bf16 and backend == 'hip':
+    extra = measure(args, 'bf16', device, backend, rank, world)
+
+  def fps(r):
+    return r['frames_per_step'] * args.steps / r['dt']
+
+  value = fps(main_res)
   if rank == 0:
+    dist_info = parallel.backend_info()
+    cfg = {'model': 'IMPALA %s-ResNet+LSTM-256' % args.torso
+                    if args.torso == 'deep' else 'IMPALA shallow+LSTM',
+           'global_batch': args.batch_size * world,
+           'seq_len': args.unroll_length,
+           'frame': '%dx%dx%d' % (args.height, args.width, args.channels),
+           'parallelism': 'dp%d' % world, 'backend': backend,
+           'torso_kernels': main_res['torso'],
+           'hip_graph': main_res['hip_graph'],
+           'loss_finite': main_res['loss_finite'],
+           'learner_health': main_res['health'],
+           'pipeline_chunks': args.pipeline_chunks,
+           'host_enqueue_ms_per_step': round(
+               1000 * main_res['enqueue_s'] / args.steps, 3),
+           'h2d_prefetch': main_res['h2d_prefetch'],
+           'dist': dist_info,
+           'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
+                           'frames/s (BASELINE.md B), fp32 P100'}
+    if extra is not None:
+      cfg['bf16'] = {'value': round(fps(extra), 1),
+                     'ms_per_step': round(1000 * extra['dt'] / args.steps, 3),
+                     'vs_baseline': round(fps(extra) / BASELINE_FPS, 3),
+                     'torso_kernels': extra['torso'],
+                     'loss_finite': extra['loss_finite'],
+                     'learner_health': extra['health']}
     rec = {
         'metric': METRIC, 'value': round(value, 1), 'unit': 'env-frames/s',
         'n_gpus': world if device.type == 'cuda' else 0,
         'steps': args.steps, 'warmup': args.warmup,
-        'ms_per_step': round(1000 * dt / args.steps, 3),
+        'ms_per_step': round(1000 * main_res['dt'] / args.steps, 3),
         'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': round(value / BASELINE_FPS, 3),
-        'dtype': args.dtype, 'data': 'synthetic (random uint8 frames, '
-                                     'random-init weights)',
-        'config': {'model': 'IMPALA %s-ResNet+LSTM-256' % args.torso
-                            if args.torso == 'deep' else 'IMPALA shallow+LSTM',
-                   'global_batch': args.batch_size * world,
-                   'seq_len': args.unroll_length,
-                   'frame': '%dx%dx3' % (args.height, args.width),
-                   'parallelism': 'dp%d' % world, 'backend': backend,
-                   'hip_graph': use_graph, 'loss_finite': ok,
-                   'pipeline_chunks': args.pipeline_chunks,
-                   'host_enqueue_ms_per_step': round(1000 * t_enq / args.steps, 3),
-                   'h2d_prefetch': not skip_h2d,
-                   'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
-                                   'frames/s (BASELINE.md B)'},
+        'dtype': args.dtype,
+        'data': 'synthetic (random uint8 frames, random-init weights)',
+        'config': cfg,
     }
     print(json.dumps(rec), flush=True)
   parallel.cleanup()

@@ -30,7 +30,8 @@ const uint8_t* u8ptr(const at::Tensor& t) {
 
 void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
              at::Tensor frames, double lr0, double total_frames, double decay,
-             double momentum, double eps, c10::optional<at::Tensor> guard) {
+             double momentum, double eps, c10::optional<at::Tensor> guard,
+             c10::optional<at::Tensor> lstm_err) {
   SA_CHECK(w); SA_CHECK(g); SA_CHECK(ms); SA_CHECK(mom); SA_CHECK_CUDA(frames);
   SA_CHECK_F32(w); SA_CHECK_F32(g); SA_CHECK_F32(ms); SA_CHECK_F32(mom);
   TORCH_CHECK(frames.scalar_type() == at::kLong, "frames must be int64");
@@ -40,16 +41,23 @@ void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
   int* gp = nullptr;
   if (guard.has_value()) {
     SA_CHECK_CUDA(*guard);
-    TORCH_CHECK(guard->scalar_type() == at::kInt && guard->numel() >= 2,
-                "guard must be int32[2] (flag, skipped)");
+    TORCH_CHECK(guard->scalar_type() == at::kInt && guard->numel() >= 4,
+                "guard must be int32[4] (flag, skipped, lstm_timeouts, -)");
     gp = guard->data_ptr<int>();
+  }
+  unsigned* ep = nullptr;
+  if (lstm_err.has_value() && lstm_err->defined()) {
+    TORCH_CHECK(gp != nullptr, "lstm_err needs a guard");
+    SA_CHECK_CUDA(*lstm_err);
+    TORCH_CHECK(lstm_err->scalar_type() == at::kInt, "lstm_err must be int32");
+    ep = reinterpret_cast<unsigned*>(lstm_err->data_ptr<int>());
   }
   const c10::DeviceGuard dguard(w.device());
   sa::rmsprop_launch(w.data_ptr<float>(), g.data_ptr<float>(),
                      ms.data_ptr<float>(), mom.data_ptr<float>(),
                      frames.data_ptr<int64_t>(), w.numel(), (float)lr0,
                      total_frames, (float)decay, (float)momentum, (float)eps,
-                     gp, cur_stream());
+                     gp, ep, cur_stream());
 }
 
 std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
@@ -122,6 +130,18 @@ bool g_lstm_gang = [] {
 // gains nothing from the gang and the inference graphs keep their layout.
 bool use_gang(int H, int B, int T) { return g_lstm_gang && H == 256 && B <= 32 && T >= 2; }
 
+// Recurrence implementation, resolved ONCE per unroll by the caller and
+// passed to both lstm_fwd and lstm_bwd (the packed weights differ between
+// them): 2 = gang (bf16 recurrent product), 1 = persistent (fp32),
+// 0 = per-step kernels (fp32).  exact: the caller needs fp32 (reference
+// precision), so the bf16 gang is never chosen.
+enum LstmMode { kStep = 0, kPersistent = 1, kGang = 2 };
+int64_t lstm_mode(int64_t H, int64_t B, int64_t T, bool exact) {
+  if (!exact && use_gang(H, B, T)) return kGang;
+  if (use_persistent(H, B)) return kPersistent;
+  return kStep;
+}
+
 // Sticky per-device timeout word of the persistent kernels (0 = healthy).
 at::Tensor lstm_err_word(const at::Device& dev) {
   // called from the learner and from actor-inference threads
@@ -144,7 +164,7 @@ at::Tensor lstm_xbuf(bool bwd, const at::TensorOptions& o) {
 // Returns {hs, cs, acts, hpm, wt}: hpm[t] = keep_t * h_{t-1} (A operand of
 // the dW_h GEMM), wt = W_h^T packed for lstm_bwd.
 std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
-                                 at::Tensor h0, at::Tensor w_h) {
+                                 at::Tensor h0, at::Tensor w_h, int64_t mode) {
   SA_CHECK(xw); SA_CHECK(done); SA_CHECK(c0); SA_CHECK(h0); SA_CHECK(w_h);
   SA_CHECK_F32(xw); SA_CHECK_F32(c0); SA_CHECK_F32(h0); SA_CHECK_F32(w_h);
   const int T = xw.size(0), B = xw.size(1), H4 = xw.size(2), H = H4 / 4;
@@ -163,7 +183,10 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   auto hpk = at::empty({2, RT * 32 * H}, xw.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
-  if (use_gang(H, B, T)) {
+  TORCH_CHECK(mode >= kStep && mode <= kGang, "lstm mode");
+  TORCH_CHECK(mode == kStep || (H == 256 && B <= 32 && (mode != kGang || T >= 2)),
+              "lstm mode ", mode, " does not cover H=", H, " B=", B, " T=", T);
+  if (mode == kGang) {
     // w4 / wt carry the bf16 gang fragments instead (512 KB of their 1 MB)
     sa::lstm_gang_pack_launch(w_h.data_ptr<float>(), w4.data_ptr(), wt.data_ptr(), s);
     auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(false)},
@@ -177,7 +200,7 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   }
   sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
                                wt.data_ptr<float>(), H, s);
-  if (use_persistent(H, B)) {
+  if (mode == kPersistent) {
     auto xbuf = lstm_xbuf(false, xw.options());
     sa::lstm_fwd_persistent_launch(
         xw.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), dn,
@@ -205,7 +228,8 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
 // w.r.t. the initial cell state (already masked by keep_0).
 std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor wt,
                                  at::Tensor acts, at::Tensor cs, at::Tensor c0,
-                                 c10::optional<at::Tensor> dc_last, bool want_bf16) {
+                                 c10::optional<at::Tensor> dc_last, bool want_bf16,
+                                 int64_t mode) {
   SA_CHECK(dh_out); SA_CHECK(done); SA_CHECK(wt); SA_CHECK(acts);
   SA_CHECK(cs); SA_CHECK(c0);
   SA_CHECK_F32(dh_out);
@@ -226,7 +250,10 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
   auto dgpk = at::empty({2, RT * 32 * H4}, acts.options());
   auto s = cur_stream();
   const uint8_t* dn = u8ptr(done);
-  if (use_gang(H, B, T)) {
+  TORCH_CHECK(mode >= kStep && mode <= kGang, "lstm mode");
+  TORCH_CHECK(mode == kStep || (H == 256 && B <= 32), "lstm mode ", mode,
+              " does not cover H=", H, " B=", B);
+  if (mode == kGang) {
     auto dc0 = at::empty({B, H}, acts.options());
     auto xbuf = at::zeros({(int64_t)sa::lstm_gang_xbuf_granules(true)},
                           acts.options().dtype(at::kLong));
@@ -240,7 +267,7 @@ std::vector<at::Tensor> lstm_bwd(at::Tensor dh_out, at::Tensor done, at::Tensor 
     if (!want_bf16) dg16 = at::empty({0}, acts.options());
     return {dg, dc0, dg16};
   }
-  if (use_persistent(H, B)) {
+  if (mode == kPersistent) {
     auto dc0 = at::empty({B, H}, acts.options());
     auto xbuf = lstm_xbuf(true, acts.options());
     sa::lstm_bwd_persistent_launch(
@@ -285,6 +312,7 @@ void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
 
 void register_conv_ops(pybind11::module& m);     // conv_bindings.cpp
 void register_learner_ops(pybind11::module& m);  // learner_bindings.cpp
+void register_conv_f32_ops(pybind11::module& m); // conv_f32_bindings.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "scalable_agent_amd gfx950 HIP kernels";
@@ -292,22 +320,28 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("ms"), pybind11::arg("mom"), pybind11::arg("frames"),
         pybind11::arg("lr0"), pybind11::arg("total_frames"),
         pybind11::arg("decay"), pybind11::arg("momentum"), pybind11::arg("eps"),
-        pybind11::arg("guard") = pybind11::none());
+        pybind11::arg("guard") = pybind11::none(),
+        pybind11::arg("lstm_err") = pybind11::none());
   m.def("vtrace_loss", &vtrace_loss);
-  m.def("lstm_fwd", &lstm_fwd);
+  m.def("lstm_fwd", &lstm_fwd, pybind11::arg("xw"), pybind11::arg("done"),
+        pybind11::arg("c0"), pybind11::arg("h0"), pybind11::arg("w_h"),
+        pybind11::arg("mode"));
   m.def("lstm_bwd", &lstm_bwd, pybind11::arg("dh_out"), pybind11::arg("done"),
         pybind11::arg("wt"), pybind11::arg("acts"), pybind11::arg("cs"),
         pybind11::arg("c0"), pybind11::arg("dc_last") = pybind11::none(),
-        pybind11::arg("want_bf16") = false);
+        pybind11::arg("want_bf16") = false, pybind11::arg("mode"));
   m.def("lstm_set_persistent", &lstm_set_persistent);
   m.def("lstm_get_persistent", &lstm_get_persistent);
   m.def("lstm_set_gang", &lstm_set_gang);
   m.def("lstm_get_gang", &lstm_get_gang);
   m.def("lstm_gang_ws", [](int v) { return sa::lstm_gang_ws(v); });
   m.def("lstm_gang_nap", [](int v) { return sa::lstm_gang_nap(v); });
+  m.def("lstm_gang_fault", [](int v) { return sa::lstm_gang_fault(v); });
+  m.def("lstm_mode", &lstm_mode);
   m.def("lstm_error_word", &lstm_error);
   m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);
   register_conv_ops(m);
   register_learner_ops(m);
+  register_conv_f32_ops(m);
 }

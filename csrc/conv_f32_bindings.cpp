@@ -1,0 +1,181 @@
+// Torch bindings for the exact-fp32 conv kernels (kernels/conv_f32.hip).
+// Every op validates shapes on the host, allocates through the caching
+// allocator and launches on the current stream (graph-capturable); a shape
+// with no compiled instance raises instead of falling back.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/conv_f32.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int src_kind(const at::Tensor& x) {
+  if (x.scalar_type() == at::kByte) return sa::cf32::kSrcU8;
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "conv source must be uint8 frames or float32");
+  return sa::cf32::kSrcF32;
+}
+
+void check_nhwc(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, name,
+              " must be a contiguous NHWC GPU tensor");
+}
+
+const float* opt_f32(const c10::optional<at::Tensor>& t, const at::Tensor& like,
+                     const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->sizes() == like.sizes(),
+              name, " must be a contiguous float32 tensor shaped like the output");
+  return t->data_ptr<float>();
+}
+
+void check_w(const at::Tensor& w) {
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat && w.dim() == 4 &&
+                  w.size(0) == w.size(1),
+              "weights must be contiguous float32 HWIO [K,K,Cin,Cout]");
+}
+
+// y = conv(relu_in ? relu(x) : x, w, stride, pads) [+ b] [* (mask > 0)] [+ add] [relu]
+at::Tensor conv_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, int64_t stride,
+                    int64_t pt, int64_t pl, int64_t Ho, int64_t Wo, bool relu_in,
+                    c10::optional<at::Tensor> add, bool relu_out) {
+  check_nhwc(x, "x");
+  check_w(w);
+  const int kind = src_kind(x);
+  TORCH_CHECK(w.size(2) == x.size(3), "weights Cin ", w.size(2), " != input channels ", x.size(3));
+  const int64_t Cout = w.size(3);
+  const c10::DeviceGuard g(x.device());
+  auto y = at::empty({x.size(0), Ho, Wo, Cout}, x.options().dtype(at::kFloat));
+  sa::cf32::ConvArgs a{};
+  a.src = x.data_ptr();
+  a.w = w.data_ptr<float>();
+  if (b.has_value() && b->defined()) {
+    TORCH_CHECK(b->numel() == Cout && b->scalar_type() == at::kFloat && b->is_contiguous(), "bias");
+    a.bias = b->data_ptr<float>();
+  }
+  a.add = opt_f32(add, y, "add");
+  a.out = y.data_ptr<float>();
+  a.N = x.size(0); a.Hs = x.size(1); a.Ws = x.size(2); a.Cs = x.size(3);
+  a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.pt = pt; a.pl = pl; a.D = 1;
+  a.wcin = w.size(2); a.wcout = Cout;
+  a.relu_in = relu_in; a.relu_out = relu_out;
+  TORCH_CHECK(sa::cf32::conv_launch(a, w.size(0), stride, kind, false, stream()),
+              "conv_f32: no kernel instance for K=", w.size(0), " stride=", stride, " Cin=",
+              x.size(3), " Cout=", Cout, " src=", kind == sa::cf32::kSrcU8 ? "uint8" : "f32");
+  return y;
+}
+
+// dx [N,H,W,Cin] of y = conv(x, w, stride, pads): correlation of the
+// stride-dilated dy with the flipped, transposed weights; then
+// [* (mask > 0)] [+ add].
+at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, int64_t pl,
+                      int64_t H, int64_t W, c10::optional<at::Tensor> mask,
+                      c10::optional<at::Tensor> add) {
+  check_nhwc(dy, "dy");
+  check_w(w);
+  TORCH_CHECK(dy.scalar_type() == at::kFloat, "dy must be float32");
+  TORCH_CHECK(w.size(3) == dy.size(3), "weights Cout != dy channels");
+  const int64_t K = w.size(0), Cin = w.size(2);
+  const c10::DeviceGuard g(dy.device());
+  auto dx = at::empty({dy.size(0), H, W, Cin}, dy.options());
+  sa::cf32::ConvArgs a{};
+  a.src = dy.data_ptr();
+  a.w = w.data_ptr<float>();
+  a.mask = opt_f32(mask, dx, "mask");
+  a.add = opt_f32(add, dx, "add");
+  a.out = dx.data_ptr<float>();
+  a.N = dy.size(0); a.Hs = dy.size(1); a.Ws = dy.size(2); a.Cs = dy.size(3);
+  a.Ho = H; a.Wo = W; a.Cout = Cin;
+  a.pt = K - 1 - pt; a.pl = K - 1 - pl; a.D = stride;
+  a.wcin = Cin; a.wcout = w.size(3);
+  TORCH_CHECK(sa::cf32::conv_launch(a, K, 1, sa::cf32::kSrcF32, true, stream()),
+              "conv_f32 dgrad: no kernel instance for K=", K, " dy channels=", dy.size(3),
+              " dx channels=", Cin);
+  return dx;
+}
+
+// dw += sum x^T dy (HWIO), db += sum dy; x: the layer input (uint8 frames
+// or float32, optionally ReLU'd on load).  Deterministic (no atomics).
+void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t pl,
+                bool relu_in, at::Tensor dw, c10::optional<at::Tensor> db) {
+  check_nhwc(x, "x");
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat, "dy must be float32");
+  check_w(dw);
+  const int kind = src_kind(x);
+  const int64_t K = dw.size(0);
+  TORCH_CHECK(dw.size(2) == x.size(3) && dw.size(3) == dy.size(3), "dw shape");
+  const c10::DeviceGuard g(x.device());
+  auto ws = at::empty({sa::cf32::wgrad_workspace_floats(K, x.size(3), dy.size(3))},
+                      dy.options());
+  sa::cf32::WgradArgs a{};
+  a.src = x.data_ptr();
+  a.dy = dy.data_ptr<float>();
+  a.dw = dw.data_ptr<float>();
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->numel() == dy.size(3) && db->scalar_type() == at::kFloat &&
+                    db->is_contiguous(), "db");
+    a.db = db->data_ptr<float>();
+  }
+  a.N = x.size(0); a.H = x.size(1); a.W = x.size(2); a.Cin = x.size(3);
+  a.Ho = dy.size(1); a.Wo = dy.size(2); a.Cout = dy.size(3);
+  a.pt = pt; a.pl = pl; a.relu_in = relu_in;
+  TORCH_CHECK(sa::cf32::wgrad_launch(a, K, stride, kind, ws.data_ptr<float>(), stream()),
+              "conv_f32 wgrad: no kernel instance for K=", K, " stride=", stride, " Cin=",
+              x.size(3), " Cout=", dy.size(3));
+}
+
+std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t pb_h, int64_t pb_w) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.size(3) % 4 == 0, "maxpool: float32, C % 4 == 0");
+  const c10::DeviceGuard g(x.device());
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t Hp = (H + 1) / 2, Wp = (W + 1) / 2;
+  auto y = at::empty({N, Hp, Wp, C}, x.options());
+  auto arg = at::empty({N, Hp, Wp, C}, x.options().dtype(at::kByte));
+  sa::cf32::maxpool_fwd_launch(x.data_ptr<float>(), y.data_ptr<float>(), arg.data_ptr<uint8_t>(),
+                               N, H, W, C, Hp, Wp, pb_h, pb_w, stream());
+  return {y, arg};
+}
+
+at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int64_t pb_h,
+                       int64_t pb_w) {
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.size(3) % 4 == 0, "dy float32, C % 4 == 0");
+  TORCH_CHECK(arg.sizes() == dy.sizes() && arg.scalar_type() == at::kByte && arg.is_contiguous(),
+              "argmax");
+  TORCH_CHECK(dy.size(1) == (H + 1) / 2 && dy.size(2) == (W + 1) / 2, "pooled shape");
+  const c10::DeviceGuard g(dy.device());
+  auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  sa::cf32::maxpool_bwd_launch(dy.data_ptr<float>(), arg.data_ptr<uint8_t>(), dx.data_ptr<float>(),
+                               dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2), pb_h, pb_w,
+                               stream());
+  return dx;
+}
+
+void relu_mask_(at::Tensor dy, at::Tensor ref) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.scalar_type() == at::kFloat, "dy");
+  TORCH_CHECK(ref.is_contiguous() && ref.scalar_type() == at::kFloat &&
+                  ref.numel() == dy.numel() && dy.numel() % 4 == 0, "ref");
+  const c10::DeviceGuard g(dy.device());
+  sa::cf32::relu_mask_launch(dy.data_ptr<float>(), ref.data_ptr<float>(), dy.numel(), stream());
+}
+
+}  // namespace
+
+void register_conv_f32_ops(pybind11::module& m) {
+  using pybind11::arg;
+  m.def("cf32_conv_fwd", &conv_fwd, arg("x"), arg("w"), arg("b"), arg("stride"), arg("pt"),
+        arg("pl"), arg("Ho"), arg("Wo"), arg("relu_in") = false, arg("add") = pybind11::none(),
+        arg("relu_out") = false);
+  m.def("cf32_conv_dgrad", &conv_dgrad, arg("dy"), arg("w"), arg("stride"), arg("pt"), arg("pl"),
+        arg("H"), arg("W"), arg("mask") = pybind11::none(), arg("add") = pybind11::none());
+  m.def("cf32_conv_wgrad", &conv_wgrad, arg("x"), arg("dy"), arg("stride"), arg("pt"), arg("pl"),
+        arg("relu_in"), arg("dw"), arg("db") = pybind11::none());
+  m.def("cf32_maxpool_fwd", &maxpool_fwd);
+  m.def("cf32_maxpool_bwd", &maxpool_bwd);
+  m.def("cf32_relu_mask_", &relu_mask_);
+}

@@ -1,0 +1,83 @@
+// Reference-precision (exact fp32) conv kernels for gfx950: NHWC fp32
+// implicit GEMM on v_mfma_f32_16x16x4_f32 (f32 inputs, f32 accumulate, one
+// rounding per product - bit-for-bit an fmaf chain, no xf32/TF32 shortcut).
+//
+// One templated forward kernel covers every conv the agent needs
+// (reference experiment.py:153-189): the shallow torso's 8x8/4, 4x4/2, 3x3/2
+// (TF-SAME, incl. the asymmetric W pad 0/1 of the third layer), the deep
+// ResNet's 3x3/1 convs, uint8 frames (x/255 on load, any C <= 4 so RGB and
+// Atari-style 4-frame stacks share the path) and, with flipped/transposed
+// weights over a zero-dilated source, the data gradient.  Weight gradients
+// are a pixel-reduction GEMM with a fixed-order two-stage reduction
+// (deterministic: per-workgroup partials, then one summing pass).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace sa {
+namespace cf32 {
+
+enum SrcKind { kSrcF32 = 0, kSrcU8 = 1 };
+
+// Forward conv / data gradient.  The kernel computes
+//   out[n, oy, ox, co] = sum_{ky,kx,i} L[n, oy*S + ky, ox*S + kx, i] * Wk[ky,kx,i,co]
+// over the LDS image L of the source: source pixel (j, i) sits at image
+// position (j*D + pt, i*D + pl), zeros elsewhere (padding and dilation).
+//   forward : D = 1, S = stride, Wk = W (HWIO), pads = TF-SAME pad_before
+//   dgrad   : D = stride, S = 1, Wk = W flipped in (ky, kx) and transposed in
+//             (ci, co) (flip = true), pads = K - 1 - pad_before
+// Epilogue: v = acc [+ bias]; [v = mask > 0 ? v : 0]; [v += add]; [relu].
+struct ConvArgs {
+  const void* src;     // [N, Hs, Ws, Cs] fp32 (or uint8 frames, Cs <= 4)
+  const float* w;      // HWIO [K, K, wcin, wcout]
+  const float* bias;   // [Cout] or null
+  const float* mask;   // [N, Ho, Wo, Cout] or null (ReLU derivative source)
+  const float* add;    // [N, Ho, Wo, Cout] or null (residual / skip)
+  float* out;          // [N, Ho, Wo, Cout]
+  int N, Hs, Ws, Cs;   // source dims
+  int Ho, Wo, Cout;    // output dims
+  int pt, pl, D;       // image placement of the source
+  int wcin, wcout;
+  int relu_in, relu_out;
+};
+
+// Weight gradient of the FORWARD conv (stride S, pads pt/pl):
+//   dW[ky,kx,ci,co] += sum_{n,oy,ox} X[n, oy*S+ky-pt, ox*S+kx-pl, ci] * dY[n,oy,ox,co]
+//   db[co]          += sum dY[n,oy,ox,co]          (when db != null)
+// X is the layer input (optionally ReLU'd on load, or uint8 frames / 255).
+struct WgradArgs {
+  const void* src;     // [N, H, W, Cin]
+  const float* dy;     // [N, Ho, Wo, Cout]
+  float* dw;           // [K, K, Cin, Cout], accumulated
+  float* db;           // [Cout] or null, accumulated
+  int N, H, W, Cin;
+  int Ho, Wo, Cout;
+  int pt, pl;
+  int relu_in;
+};
+
+// Returns false (and launches nothing) when no instance matches the shape;
+// the bindings turn that into an error naming the shape.
+bool conv_launch(const ConvArgs& a, int K, int S, int src_kind, bool flip,
+                 hipStream_t s);
+// Workgroup slots of one wgrad launch (partial-sum rows in the workspace).
+int64_t wgrad_slots(int K, int cinp, int cout);
+// `ws` must hold wgrad_workspace_floats(K, Cin, Cout) floats.
+int64_t wgrad_workspace_floats(int K, int Cin, int Cout);
+bool wgrad_launch(const WgradArgs& a, int K, int S, int src_kind, float* ws,
+                  hipStream_t s);
+
+// 3x3/2 max-pool, TF SAME (pads pb_h/pb_w before, -inf padding):
+// y [N, Hp, Wp, C] and the first maximal tap dy*3+dx per element.
+void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H,
+                        int W, int C, int Hp, int Wp, int pb_h, int pb_w,
+                        hipStream_t s);
+// dx[n, y, x, c] = sum of dy over the windows whose argmax is (y, x).
+void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N,
+                        int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w,
+                        hipStream_t s);
+// dy *= (ref > 0), fp32, n % 4 == 0
+void relu_mask_launch(float* dy, const float* ref, int64_t n, hipStream_t s);
+
+}  // namespace cf32
+}  // namespace sa

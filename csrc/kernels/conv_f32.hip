@@ -1,0 +1,636 @@
+// Exact-fp32 NHWC conv kernels on v_mfma_f32_16x16x4_f32 (see conv_f32.h).
+//
+// MFMA operand maps (cdna_hip_programming.md §3, 16x16x4 f32):
+//   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], D[i = 4(l>>4)+r][j = l&15].
+// Forward / dgrad compute D^T = Wk^T X^T: i = output channel, j = pixel, so a
+// lane ends with 4 consecutive channels of one pixel (one 16-B NHWC store).
+// The k index of MFMA v in a 16-channel block b is channel 16b + 4g + v for
+// lane group g = l>>4, on BOTH operands, so each lane fetches its 4 channels
+// of a tap with one ds_read_b128 and feeds 4 consecutive MFMAs.
+//
+// Tiling (forward): a workgroup (4 waves) owns R full-width output rows of
+// one image and an output-channel slice; the source rows it needs are staged
+// into LDS once (zero padding / dilation / uint8 -> x/255 / ReLU applied on
+// the way in), its weight slice as [tap][co][ci].  Pixels are linearised in
+// 16-pixel MFMA groups, dealt round-robin to the waves, two at a time.
+// LDS pixel pitches keep every ds_read_b128 group (4 x 16 lanes,
+// MI355X_MICROARCH.md §LDS) conflict-free: pitch/4 = 2 mod 4 in 16-B units.
+//
+// Weight gradient: the reduction runs over pixels (k = 4 pixels per MFMA);
+// rows i = (tap, ci) [+ one ones-row for the bias], columns j = co.  Waves
+// split the rows (WSM groups) and/or the pixels (4/WSM groups, combined in
+// LDS in a fixed order); each workgroup walks a fixed tile list and writes
+// its partial sums, and one reduce kernel sums the partials in slot order:
+// bitwise reproducible run to run (no float atomics).
+#include "conv_f32.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace sa {
+namespace cf32 {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int kThreads = 256;
+constexpr size_t kLdsSoft = 80 * 1024;   // two workgroups per CU
+constexpr size_t kLdsHard = 156 * 1024;  // one workgroup per CU
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// pixel pitch (floats) of the forward LDS images: 16-B units = 2 mod 4
+__host__ __device__ constexpr int fwd_pitch(int c) { return c >= 16 ? c + 8 : c; }
+// pixel pitch of the wgrad input image: the A operand is read with
+// ds_read_b32 (lane halves of 2 pixels x 16 consecutive channels), so the
+// pitch is 16 mod 32 dwords
+__host__ __device__ constexpr int wg_pitch(int c) { return c >= 16 ? c + 16 : c; }
+
+template <int VPL>
+__device__ __forceinline__ void lds_get(const float* p, float (&v)[VPL]) {
+  if constexpr (VPL == 4) {
+    const f4 t = *reinterpret_cast<const f4*>(p);
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  } else if constexpr (VPL == 2) {
+    const f2 t = *reinterpret_cast<const f2*>(p);
+    v[0] = t[0]; v[1] = t[1];
+  } else {
+    v[0] = *p;
+  }
+}
+
+// Stages image rows [0, rows) x cols [0, Wl) (CINP channels, `pitch` floats
+// per pixel) of the zero-padded, D-dilated source into LDS: image position
+// (j0 + r, c - pl) holds source pixel ((j0 + r) / D, (c - pl) / D) when both
+// are non-negative multiples of D inside the source, else zeros.
+template <int CINP, int SRC>
+__device__ __forceinline__ void stage_image(const void* __restrict__ src, int n, int Hs,
+                                            int Ws, int Cs, int j0, int pl, int D,
+                                            int rows, int Wl, int pitch, bool relu,
+                                            float* __restrict__ x_s) {
+  constexpr int CH = CINP / 4;
+  const int total = rows * Wl * CH;
+  for (int e = threadIdx.x; e < total; e += kThreads) {
+    const int ch = e % CH;
+    const int pix = e / CH;
+    const int r = pix / Wl;
+    const int c = pix - r * Wl;
+    int j = j0 + r, i = c - pl;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    bool ok = j >= 0 && i >= 0;
+    if (D > 1) {
+      ok = ok && (j % D) == 0 && (i % D) == 0;
+      j /= D;
+      i /= D;
+    }
+    ok = ok && j < Hs && i < Ws;
+    if (ok) {
+      const int64_t pixel = (static_cast<int64_t>(n) * Hs + j) * Ws + i;
+      if constexpr (SRC == kSrcU8) {
+        // tf.to_float(frame) / 255 (reference experiment.py:153-155)
+        const uint8_t* p = static_cast<const uint8_t*>(src) + pixel * Cs;
+        v[0] = static_cast<float>(p[0]) / 255.f;
+        if (Cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
+        if (Cs > 2) v[2] = static_cast<float>(p[2]) / 255.f;
+        if (Cs > 3) v[3] = static_cast<float>(p[3]) / 255.f;
+      } else {
+        if (4 * ch < Cs) {
+          v = *reinterpret_cast<const f4*>(static_cast<const float*>(src) + pixel * Cs +
+                                           4 * ch);
+          if (relu) {
+            v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f);
+            v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
+          }
+        }
+      }
+    }
+    *reinterpret_cast<f4*>(x_s + pix * pitch + 4 * ch) = v;
+  }
+}
+
+// ------------------------------------------------------------------ forward
+template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
+__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a, int R,
+                                                            int tiles_per_img) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int PP = fwd_pitch(CINP);
+  constexpr int NH = COUT_T / 16;
+  constexpr int VPL = CINP >= 16 ? 4 : CINP / 4;
+  constexpr int NB = CINP >= 16 ? CINP / 16 : 1;
+  constexpr int KK = K * K;
+  static_assert(CINP == 4 || CINP == 8 || CINP % 16 == 0, "CINP");
+  const int Wl = (a.Wo - 1) * S + K;
+  const int rows = (R - 1) * S + K;
+  float* w_s = smem;                      // [KK][COUT_T][PP]
+  float* x_s = smem + KK * COUT_T * PP;   // [rows][Wl][PP]
+  const int n = blockIdx.x / tiles_per_img;
+  const int oy0 = (blockIdx.x - n * tiles_per_img) * R;
+  const int co0 = blockIdx.y * COUT_T;
+  if (!FLIP) {
+    // W[tap][i][o] (o fastest: coalesced) -> w_s[tap][o][i]
+    for (int e = threadIdx.x; e < KK * COUT_T * CINP; e += kThreads) {
+      const int o = e % COUT_T, i = (e / COUT_T) % CINP, tap = e / (COUT_T * CINP);
+      float v = 0.f;
+      if (i < a.wcin)
+        v = a.w[(static_cast<int64_t>(tap) * a.wcin + i) * a.wcout + co0 + o];
+      w_s[(tap * COUT_T + o) * PP + i] = v;
+    }
+  } else {
+    // w_s[tap][o][i] = W[KK-1-tap][o][i]: o = input channel of the forward
+    // conv (= dgrad output), i = its output channel (= dY channel)
+    for (int e = threadIdx.x; e < KK * COUT_T * CINP; e += kThreads) {
+      const int i = e % CINP, o = (e / CINP) % COUT_T, tap = e / (CINP * COUT_T);
+      float v = 0.f;
+      if (i < a.wcout)
+        v = a.w[(static_cast<int64_t>(KK - 1 - tap) * a.wcin + co0 + o) * a.wcout + i];
+      w_s[(tap * COUT_T + o) * PP + i] = v;
+    }
+  }
+  stage_image<CINP, SRC>(a.src, n, a.Hs, a.Ws, a.Cs, oy0 * S - a.pt, a.pl, a.D, rows,
+                         Wl, PP, a.relu_in != 0, x_s);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int Rv = min(R, a.Ho - oy0);
+  const int P = Rv * a.Wo;
+  const int ngroups = (P + 15) >> 4;
+  float bias[NH][4];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bias[h][r] = a.bias != nullptr ? a.bias[co0 + 16 * h + 4 * g + r] : 0.f;
+  const float* wl = w_s + c16 * PP + VPL * g;
+
+  auto run = [&](auto NGc, int grp0) {
+    constexpr int NG = decltype(NGc)::value;
+    f4 acc[NG][NH];
+    int xb[NG], q[NG];
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      const int p = (grp0 + 4 * gi) * 16 + c16;
+      q[gi] = p < P ? p : -1;
+      const int pp = p < P ? p : 0;
+      const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
+      xb[gi] = (oy * S * Wl + ox * S) * PP + VPL * g;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int tap = 0; tap < KK; ++tap) {
+      const int ky = tap / K, kx = tap - (tap / K) * K;
+      const int toff = (ky * Wl + kx) * PP;
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float av[NH][VPL], bv[NG][VPL];
+#pragma unroll
+        for (int h = 0; h < NH; ++h) lds_get<VPL>(wl + (tap * COUT_T + 16 * h) * PP + 16 * b, av[h]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[gi]);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v)
+#pragma unroll
+          for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma4(av[h][v], bv[gi][v], acc[gi][h]);
+      }
+    }
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      if (q[gi] < 0) continue;
+      const int oy = q[gi] / a.Wo, ox = q[gi] - (q[gi] / a.Wo) * a.Wo;
+      const int64_t pix = (static_cast<int64_t>(n) * a.Ho + oy0 + oy) * a.Wo + ox;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int64_t o = pix * a.Cout + co0 + 16 * h + 4 * g;
+        f4 v = acc[gi][h];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bias[h][r];
+        if (a.mask != nullptr) {
+          const f4 m = *reinterpret_cast<const f4*>(a.mask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+        }
+        if (a.add != nullptr) {
+          const f4 s = *reinterpret_cast<const f4*>(a.add + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += s[r];
+        }
+        if (a.relu_out) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        *reinterpret_cast<f4*>(a.out + o) = v;
+      }
+    }
+  };
+  // wave w owns groups w, w+4, w+8, ...; two per pass (independent MFMA
+  // chains), a single one for an odd remainder
+  int grp = wave;
+  for (; grp + 4 < ngroups; grp += 8) run(std::integral_constant<int, 2>{}, grp);
+  if (grp < ngroups) run(std::integral_constant<int, 1>{}, grp);
+}
+
+// ------------------------------------------------------------ weight grads
+template <int CINP, int K, int S, int SRC, int NTT, int WSM>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R,
+                                                              int tiles_per_img,
+                                                              int ntiles,
+                                                              float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int M = K * K * CINP;
+  constexpr int MTc = (M + 15) / 16;
+  constexpr int MT = MTc + 1;  // + the bias ones-row tile
+  constexpr int MTW = (MT + WSM - 1) / WSM;
+  constexpr int PG = 4 / WSM;
+  constexpr int XP = wg_pitch(CINP);
+  constexpr int CG = NTT * 16;
+  constexpr int DP = (CG % 32 == 0) ? CG + 16 : CG;
+  const int Wl = (a.Wo - 1) * S + K;
+  const int rows = (R - 1) * S + K;
+  float* x_s = smem;
+  float* d_s = smem + rows * Wl * XP;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int mg = wave % WSM, pg = wave / WSM;
+  const int co0 = blockIdx.y * CG;
+  int moff[MTW];
+  float kconst[MTW];
+  bool kimg[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    const int mb = mg + WSM * i;
+    const int m = 16 * mb + c16;
+    moff[i] = 0;
+    kimg[i] = false;
+    kconst[i] = 0.f;
+    if (mb < MTc && m < M) {
+      const int tap = m / CINP, ci = m - (m / CINP) * CINP;
+      const int ky = tap / K, kx = tap - (tap / K) * K;
+      moff[i] = (ky * Wl + kx) * XP + ci;
+      kimg[i] = true;
+    } else if (mb == MT - 1) {
+      kconst[i] = c16 == 0 ? 1.f : 0.f;  // row 16*(MT-1): sum of dY
+    }
+  }
+  f4 acc[MTW][NTT];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tiles_per_img;
+    const int oy0 = (tile - n * tiles_per_img) * R;
+    const int Rv = min(R, a.Ho - oy0);
+    const int P = Rv * a.Wo;
+    __syncthreads();  // the previous tile's reads are done
+    stage_image<CINP, SRC>(a.src, n, a.H, a.W, a.Cin, oy0 * S - a.pt, a.pl, 1, rows, Wl,
+                           XP, a.relu_in != 0, x_s);
+    {
+      constexpr int CH = CG / 4;
+      const float* dsrc =
+          a.dy + (static_cast<int64_t>(n) * a.Ho + oy0) * a.Wo * a.Cout + co0;
+      for (int e = threadIdx.x; e < P * CH; e += kThreads) {
+        const int ch = e % CH, p = e / CH;
+        *reinterpret_cast<f4*>(d_s + p * DP + 4 * ch) =
+            *reinterpret_cast<const f4*>(dsrc + static_cast<int64_t>(p) * a.Cout + 4 * ch);
+      }
+    }
+    __syncthreads();
+    const int nq = (P + 3) >> 2;
+    for (int qd = pg; qd < nq; qd += PG) {
+      const int p = 4 * qd + g;
+      const bool valid = p < P;
+      const int pp = valid ? p : 0;
+      const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
+      const int xb = (oy * S * Wl + ox * S) * XP;
+      float bv[NTT];
+#pragma unroll
+      for (int nb = 0; nb < NTT; ++nb) bv[nb] = valid ? d_s[pp * DP + 16 * nb + c16] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        const float av = kimg[i] ? x_s[xb + moff[i]] : kconst[i];
+#pragma unroll
+        for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = mfma4(av, bv[nb], acc[i][nb]);
+      }
+    }
+  }
+
+  float* dst = part + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * (MT * 16 * CG);
+  if constexpr (PG == 1) {
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int mb = mg + WSM * i;
+      if (mb >= MT) continue;
+#pragma unroll
+      for (int nb = 0; nb < NTT; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(16 * mb + 4 * g + r) * CG + 16 * nb + c16] = acc[i][nb][r];
+    }
+  } else {
+    // the PG pixel groups' partial sums, added in a fixed order in LDS
+    float* red = smem;  // [MT*16][CG]
+    __syncthreads();
+    for (int k = 0; k < PG; ++k) {
+      if (pg == k) {
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+          const int mb = mg + WSM * i;
+          if (mb >= MT) continue;
+#pragma unroll
+          for (int nb = 0; nb < NTT; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int idx = (16 * mb + 4 * g + r) * CG + 16 * nb + c16;
+              red[idx] = (k == 0 ? 0.f : red[idx]) + acc[i][nb][r];
+            }
+        }
+      }
+      __syncthreads();
+    }
+    for (int e = threadIdx.x; e < MT * 16 * CG; e += kThreads) dst[e] = red[e];
+  }
+}
+
+// Sums the G per-workgroup partials of every (row, co) in slot order and
+// accumulates into dW (HWIO) / db.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+    const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
+    int bias_row, int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int per = MT16 * CG;
+  if (idx >= ngrp * per) return;
+  const int ng = idx / per, rem = idx - ng * per;
+  const int m = rem / CG, c = rem - (rem / CG) * CG;
+  if (!(m < M && (m % CINP) < Cin) && !(db != nullptr && m == bias_row)) return;
+  const float* p = part + static_cast<int64_t>(ng) * G * per + rem;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= G; k += 4) {
+    s0 += p[static_cast<int64_t>(k) * per];
+    s1 += p[static_cast<int64_t>(k + 1) * per];
+    s2 += p[static_cast<int64_t>(k + 2) * per];
+    s3 += p[static_cast<int64_t>(k + 3) * per];
+  }
+  for (; k < G; ++k) s0 += p[static_cast<int64_t>(k) * per];
+  const float s = (s0 + s1) + (s2 + s3);
+  const int co = ng * CG + c;
+  if (m < M) {
+    const int tap = m / CINP, ci = m - (m / CINP) * CINP;
+    dw[(static_cast<int64_t>(tap) * Cin + ci) * Cout + co] += s;
+  } else {
+    db[co] += s;
+  }
+}
+
+// ------------------------------------------------------------------ pooling
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(
+    const float* __restrict__ x, float* __restrict__ y, uint8_t* __restrict__ arg, int N,
+    int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w) {
+  const int C4 = C / 4;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= static_cast<int64_t>(N) * Hp * Wp * C4) return;
+  const int c4 = static_cast<int>(idx % C4);
+  int64_t t = idx / C4;
+  const int px = static_cast<int>(t % Wp);
+  t /= Wp;
+  const int py = static_cast<int>(t % Hp);
+  const int n = static_cast<int>(t / Hp);
+  float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int code[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = 2 * py - pb_h + dy;
+    if (yy < 0 || yy >= H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int xx = 2 * px - pb_w + dx;
+      if (xx < 0 || xx >= W) continue;
+      const f4 v = *reinterpret_cast<const f4*>(
+          x + ((static_cast<int64_t>(n) * H + yy) * W + xx) * C + 4 * c4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (v[r] > best[r]) {  // strict: the first maximal tap wins
+          best[r] = v[r];
+          code[r] = dy * 3 + dx;
+        }
+      }
+    }
+  }
+  *reinterpret_cast<f4*>(y + idx * 4) = f4{best[0], best[1], best[2], best[3]};
+  *reinterpret_cast<uint32_t*>(arg + idx * 4) =
+      static_cast<uint32_t>(code[0]) | (static_cast<uint32_t>(code[1]) << 8) |
+      (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(
+    const float* __restrict__ dy, const uint8_t* __restrict__ arg, float* __restrict__ dx,
+    int N, int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w) {
+  const int C4 = C / 4;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= static_cast<int64_t>(N) * H * W * C4) return;
+  const int c4 = static_cast<int>(idx % C4);
+  int64_t t = idx / C4;
+  const int x = static_cast<int>(t % W);
+  t /= W;
+  const int y = static_cast<int>(t % H);
+  const int n = static_cast<int>(t / H);
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int py_hi = (y + pb_h) >> 1, px_hi = (x + pb_w) >> 1;
+#pragma unroll
+  for (int a = 1; a >= 0; --a) {
+    const int py = py_hi - a;
+    const int oy = y - (2 * py - pb_h);
+    if (py < 0 || py >= Hp || oy < 0 || oy > 2) continue;
+#pragma unroll
+    for (int b = 1; b >= 0; --b) {
+      const int px = px_hi - b;
+      const int ox = x - (2 * px - pb_w);
+      if (px < 0 || px >= Wp || ox < 0 || ox > 2) continue;
+      const int64_t o = ((static_cast<int64_t>(n) * Hp + py) * Wp + px) * C + 4 * c4;
+      const uint32_t codes = *reinterpret_cast<const uint32_t*>(arg + o);
+      const f4 g = *reinterpret_cast<const f4*>(dy + o);
+      const uint32_t want = static_cast<uint32_t>(oy * 3 + ox);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (((codes >> (8 * r)) & 0xFFu) == want) acc[r] += g[r];
+    }
+  }
+  *reinterpret_cast<f4*>(dx + idx * 4) = acc;
+}
+
+__global__ __launch_bounds__(256) void relu_mask_kernel(f4* __restrict__ dy,
+                                                        const f4* __restrict__ ref,
+                                                        int64_t n4) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n4; i += stride) {
+    f4 v = dy[i];
+    const f4 r = ref[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = r[k] > 0.f ? v[k] : 0.f;
+    dy[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ launch
+template <typename Kern>
+void allow_lds(Kern k, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(bytes));
+}
+
+template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
+bool run_conv(const ConvArgs& a, hipStream_t s) {
+  constexpr int PP = fwd_pitch(CINP);
+  const int Wl = (a.Wo - 1) * S + K;
+  const size_t wbytes = static_cast<size_t>(4) * K * K * COUT_T * PP;
+  auto bytes = [&](int R) {
+    return wbytes + static_cast<size_t>(4) * ((R - 1) * S + K) * Wl * PP;
+  };
+  const size_t budget = bytes(1) <= kLdsSoft ? kLdsSoft : kLdsHard;
+  int Rmax = a.Ho;
+  while (Rmax > 1 && bytes(Rmax) > budget) --Rmax;
+  if (bytes(Rmax) > kLdsHard) return false;
+  const int nt = (a.Ho + Rmax - 1) / Rmax;
+  const int R = (a.Ho + nt - 1) / nt;
+  auto kern = conv_fwd_kernel<CINP, COUT_T, K, S, SRC, FLIP>;
+  allow_lds(kern, bytes(R));
+  hipLaunchKernelGGL(kern, dim3(a.N * nt, a.Cout / COUT_T), dim3(kThreads), bytes(R), s, a,
+                     R, nt);
+  return true;
+}
+
+// output-channel tile: 32 when the weight slice stays small, else 16
+int cout_tile(int cinp, int cout, int K) {
+  if (cout % 32 == 0 && 4ll * K * K * 32 * fwd_pitch(cinp) <= 48 * 1024) return 32;
+  return 16;
+}
+
+template <int CINP, int K, int S, int SRC, int NTT, int WSM>
+bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
+  constexpr int M = K * K * CINP;
+  constexpr int MT = (M + 15) / 16 + 1;
+  constexpr int XP = wg_pitch(CINP);
+  constexpr int CG = NTT * 16;
+  constexpr int DP = (CG % 32 == 0) ? CG + 16 : CG;
+  constexpr int PG = 4 / WSM;
+  const int Wl = (a.Wo - 1) * S + K;
+  const size_t red = PG > 1 ? static_cast<size_t>(4) * MT * 16 * CG : 0;
+  auto bytes = [&](int R) {
+    return std::max(red, static_cast<size_t>(4) * (((R - 1) * S + K) * Wl * XP + R * a.Wo * DP));
+  };
+  const size_t budget = bytes(1) <= kLdsSoft ? kLdsSoft : kLdsHard;
+  int Rmax = a.Ho;
+  while (Rmax > 1 && bytes(Rmax) > budget) --Rmax;
+  if (bytes(Rmax) > kLdsHard) return false;
+  const int nt = (a.Ho + Rmax - 1) / Rmax;
+  const int R = (a.Ho + nt - 1) / nt;
+  const int ntiles = a.N * nt;
+  const int ngrp = a.Cout / CG;
+  const int G = static_cast<int>(
+      std::min<int64_t>(ntiles, wgrad_slots(K, CINP, a.Cout)));
+  auto kern = conv_wgrad_kernel<CINP, K, S, SRC, NTT, WSM>;
+  allow_lds(kern, bytes(R));
+  hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
+  const int total = ngrp * MT * 16 * CG;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ws, G,
+                     ngrp, MT * 16, CG, CINP, M, (MT - 1) * 16, a.Cin, a.Cout, a.dw, a.db);
+  return true;
+}
+
+}  // namespace
+
+// Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
+// least 128 slots (before the tile-count cap) so the reduction fills the GPU.
+int64_t wgrad_slots(int K, int cinp, int cout) {
+  const int64_t rows = ((K * K * cinp + 15) / 16 + 1) * 16;
+  return std::max<int64_t>(128, std::min<int64_t>(512, (8ll << 20) / (rows * cout)));
+}
+
+int64_t wgrad_workspace_floats(int K, int Cin, int Cout) {
+  const int cinp = Cin <= 4 ? 4 : Cin;
+  const int64_t rows = ((K * K * cinp + 15) / 16 + 1) * 16;
+  return wgrad_slots(K, cinp, Cout) * rows * Cout;
+}
+
+bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_t s) {
+  const int cinp = src == kSrcU8 ? 4 : a.Cs;
+  if (src == kSrcU8 && (a.Cs < 1 || a.Cs > 4)) return false;
+  if (src == kSrcF32 && a.Cs % 4 != 0) return false;
+  const int ct = cout_tile(cinp, a.Cout, K);
+  if (a.Cout % ct != 0) return false;
+#define SA_CONV_CASE(CINP, CT, KK, SS, SRC, FL)                                          \
+  if (cinp == CINP && ct == CT && K == KK && S == SS && src == SRC && flip == FL)        \
+    return run_conv<CINP, CT, KK, SS, SRC, FL>(a, s);
+  // forward: deep ResNet (3x3/1; uint8 stage-1 input), shallow torso
+  SA_CONV_CASE(4, 16, 3, 1, kSrcU8, false)
+  SA_CONV_CASE(16, 16, 3, 1, kSrcF32, false)
+  SA_CONV_CASE(16, 32, 3, 1, kSrcF32, false)
+  SA_CONV_CASE(32, 32, 3, 1, kSrcF32, false)
+  SA_CONV_CASE(4, 32, 8, 4, kSrcU8, false)
+  SA_CONV_CASE(32, 32, 4, 2, kSrcF32, false)
+  SA_CONV_CASE(32, 16, 4, 2, kSrcF32, false)
+  SA_CONV_CASE(64, 16, 3, 2, kSrcF32, false)
+  SA_CONV_CASE(64, 32, 3, 2, kSrcF32, false)
+  // data gradients (stride-1 correlation over the dilated dY)
+  SA_CONV_CASE(16, 16, 3, 1, kSrcF32, true)
+  SA_CONV_CASE(32, 16, 3, 1, kSrcF32, true)
+  SA_CONV_CASE(32, 32, 3, 1, kSrcF32, true)
+  SA_CONV_CASE(64, 16, 4, 1, kSrcF32, true)
+  SA_CONV_CASE(128, 16, 3, 1, kSrcF32, true)
+#undef SA_CONV_CASE
+  return false;
+}
+
+bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStream_t s) {
+  const int cinp = src == kSrcU8 ? 4 : a.Cin;
+  if (src == kSrcU8 && (a.Cin < 1 || a.Cin > 4)) return false;
+  if (src == kSrcF32 && a.Cin % 4 != 0) return false;
+#define SA_WG_CASE(CINP, KK, SS, SRC, COUT, NTT, WSM)                                     \
+  if (cinp == CINP && K == KK && S == SS && src == SRC && a.Cout == COUT)                 \
+    return run_wgrad<CINP, KK, SS, SRC, NTT, WSM>(a, ws, s);
+  SA_WG_CASE(4, 3, 1, kSrcU8, 16, 1, 1)
+  SA_WG_CASE(4, 3, 1, kSrcU8, 32, 2, 1)
+  SA_WG_CASE(16, 3, 1, kSrcF32, 16, 1, 1)
+  SA_WG_CASE(16, 3, 1, kSrcF32, 32, 2, 1)
+  SA_WG_CASE(32, 3, 1, kSrcF32, 32, 2, 2)
+  SA_WG_CASE(4, 8, 4, kSrcU8, 32, 2, 2)
+  SA_WG_CASE(32, 4, 2, kSrcF32, 64, 4, 4)
+  SA_WG_CASE(64, 3, 2, kSrcF32, 128, 4, 4)
+#undef SA_WG_CASE
+  return false;
+}
+
+void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H, int W, int C,
+                        int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
+  const int64_t total = static_cast<int64_t>(N) * Hp * Wp * (C / 4);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, x, y,
+                     arg, N, H, W, C, Hp, Wp, pb_h, pb_w);
+}
+
+void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, int H, int W,
+                        int C, int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
+  const int64_t total = static_cast<int64_t>(N) * H * W * (C / 4);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, dy, arg,
+                     dx, N, H, W, C, Hp, Wp, pb_h, pb_w);
+}
+
+void relu_mask_launch(float* dy, const float* ref, int64_t n, hipStream_t s) {
+  const int64_t n4 = n / 4;
+  int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(blocks), dim3(256), 0, s,
+                     reinterpret_cast<f4*>(dy), reinterpret_cast<const f4*>(ref), n4);
+}
+
+}  // namespace cf32
+}  // namespace sa

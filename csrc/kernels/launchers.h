@@ -14,7 +14,8 @@ namespace sa {
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, int* guard, hipStream_t stream);
+                    float eps, int* guard, unsigned* lstm_err,
+                    hipStream_t stream);
 
 // ---- vtrace_loss.hip -------------------------------------------------------
 // Fused V-trace (from logits) + IMPALA loss + analytic gradients.
@@ -92,6 +93,8 @@ size_t lstm_gang_xbuf_granules(bool bwd);
 int lstm_gang_ws(int v);
 // s_sleep(1) count between sweep passes (0..64; other values only query).
 int lstm_gang_nap(int v);
+// 1: every gang sweep reports a timeout (tests); v < 0 queries only.
+int lstm_gang_fault(int v);
 void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stream);
 void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
                           const uint8_t* done, const void* wf, float* hs, float* cs,

@@ -77,6 +77,10 @@ template <int N, int R = N, int S = 0>
 __device__ __forceinline__ bool sweep(const unsigned long long* g, unsigned tag,
                                       uint32_t (&v)[N], unsigned* err, int nap = 1) {
   const gu64* p = (const gu64*)(g);
+  if (nap < 0) {  // fault injection (lstm_gang_fault): behave as a timeout
+    __hip_atomic_store((gu32*)(err), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
   for (unsigned spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
@@ -705,6 +709,15 @@ int lstm_gang_nap(int v) {
   return old;
 }
 
+// Fault injection for tests: every sweep reports a timeout (sticky error
+// word set, unroll abandoned) so the learner-side guard can be exercised.
+static int g_gang_fault = 0;
+int lstm_gang_fault(int v) {
+  const int old = g_gang_fault;
+  if (v == 0 || v == 1) g_gang_fault = v;
+  return old;
+}
+
 int lstm_gang_ws(int v) {
   const int old = g_gang_ws;
   if (v == 0 || v == 1) g_gang_ws = v;
@@ -717,7 +730,8 @@ void lstm_fwd_gang_launch(const float* xw, const float* h0, const float* c0,
                           int B, hipStream_t stream) {
   hipLaunchKernelGGL(g_gang_ws ? lstm_fwd_gang_ws_kernel : lstm_fwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream, xw,
                      h0, c0, done, static_cast<const bf16_t*>(wf), hs, cs, acts, hpm,
-                     static_cast<unsigned long long*>(xbuf), err, T, B, g_gang_nap);
+                     static_cast<unsigned long long*>(xbuf), err, T, B,
+                     g_gang_fault ? -1 : g_gang_nap);
 }
 
 void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* wbk,
@@ -727,7 +741,8 @@ void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* 
   hipLaunchKernelGGL(g_gang_ws ? lstm_bwd_gang_ws_kernel : lstm_bwd_gang_kernel, dim3(kGang), dim3(kThreads), 0, stream,
                      dh_out, done, static_cast<const bf16_t*>(wbk), acts, cs, c0,
                      dc_last, dg, static_cast<__hip_bfloat16*>(dg16), dc0,
-                     static_cast<unsigned long long*>(xbuf), err, T, B, g_gang_nap);
+                     static_cast<unsigned long long*>(xbuf), err, T, B,
+                     g_gang_fault ? -1 : g_gang_nap);
 }
 
 }  // namespace sa

@@ -5,10 +5,15 @@
 //   mom = momentum * mom + lr * g / sqrt(ms + eps)
 //   w  -= mom
 //
-// Non-finite guard (optional): a check kernel ORs "some gradient is NaN/inf"
-// into guard[0] (zeroed by a memset node each step); the update kernel then
-// leaves every parameter and slot untouched and counts the skipped step in
-// guard[1].  One extra 8-MB read per step, no host synchronisation.
+// Step guard (optional), int32[4] = {flag, skipped, lstm_timeouts, -}: a
+// check kernel ORs "some gradient is NaN/inf" (bit 0) into guard[0] (zeroed
+// by a memset node each step) and, when given the recurrence's sticky
+// timeout word (lstm_gang.hip / lstm_persistent.hip: a workgroup of the
+// cooperative unroll could not co-reside and the unroll was abandoned, so
+// its activations/gradients are stale), consumes it: bit 1, guard[2] += 1,
+// word reset.  The update kernel then leaves every parameter and slot
+// untouched and counts the skipped step in guard[1].  One extra 8-MB read
+// per step, no host synchronisation; the host reads the counters lazily.
 //
 // Memory-bound: 5 streams of 4 B (w, g, ms, mom read; w, ms, mom written) per
 // element, float4 vectorised, grid-stride with a grid sized for 256 CUs.  The
@@ -20,7 +25,17 @@ namespace sa {
 namespace {
 
 __global__ __launch_bounds__(256) void finite_check_kernel(
-    const float4* __restrict__ g, int64_t n4, int* __restrict__ guard) {
+    const float4* __restrict__ g, int64_t n4, int* __restrict__ guard,
+    unsigned* __restrict__ lstm_err) {
+  if (lstm_err != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned e = __hip_atomic_load(lstm_err, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0u) {
+      atomicOr(guard, 2);
+      atomicAdd(guard + 2, 1);
+      __hip_atomic_store(lstm_err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   bool bad = false;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -67,7 +82,8 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, int* guard, hipStream_t stream) {
+                    float eps, int* guard, unsigned* lstm_err,
+                    hipStream_t stream) {
   const int64_t n4 = n / 4;  // FlatParams pads every tensor to 64 elements
   const int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
@@ -76,7 +92,8 @@ void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
   if (guard != nullptr) {
     (void)hipMemsetAsync(guard, 0, sizeof(int), stream);
     hipLaunchKernelGGL(finite_check_kernel, dim3(blocks), dim3(threads), 0,
-                       stream, reinterpret_cast<const float4*>(g), n4, guard);
+                       stream, reinterpret_cast<const float4*>(g), n4, guard,
+                       lstm_err);
   }
   hipLaunchKernelGGL(rmsprop_kernel, dim3(blocks), dim3(threads), 0, stream,
                      reinterpret_cast<float4*>(w),

@@ -327,6 +327,7 @@ def train(flags):
   timer = StepTimer(learner.frames_per_step)
   last_summary = time.time()
   last_log_frames = int(learner.frames.item())
+  reported_skips = 0
   steps = 0
   use_graph = flags.use_hip_graph and device.type == 'cuda'
   staging = dev_stage = copied = None
@@ -409,8 +410,8 @@ def train(flags):
                    'frames_per_sec': timer.frames_per_sec(),
                    'learner_steps_per_sec': timer.steps_per_sec(),
                    'queue_wait_frac': timer.wait_fraction(),
-                   'skipped_updates': learner.opt.skipped_steps,
                    'env_restarts': sum(a.env_restarts for a in actors)}
+        scalars.update(learner.health())
         if infer is not None and infer.stats()['batches']:
           st = infer.stats()
           scalars['inference_batch_size_mean'] = (st['requests'] /
@@ -427,6 +428,13 @@ def train(flags):
                  'queue-wait %.0f%%', frames, timer.frames_per_sec(),
                  timer.steps_per_sec(), float(loss),
                  100 * timer.wait_fraction())
+        health = learner.health()
+        if health['skipped_updates'] > reported_skips:
+          # loud, not fatal: the guard already dropped those updates
+          log.warning('learner dropped %d update(s) so far (%d LSTM unroll '
+                      'timeout(s), rest non-finite gradients)',
+                      health['skipped_updates'], health['lstm_timeouts'])
+          reported_skips = health['skipped_updates']
       if saver is not None:
         saver.maybe_save()
   except _Terminated:

@@ -74,9 +74,11 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
                  help='sum: N learners x B == one learner with N*B (reference '
                       'losses are sums).')
-  p.add_argument('--dtype', default='bf16', choices=['fp32', 'bf16'],
-                 help='Compute dtype of convs/GEMMs (V-trace/loss/optimizer '
-                      'state always fp32).')
+  p.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                 help='Compute dtype of convs/GEMMs: fp32 = the reference\'s '
+                      'precision (exact-fp32 MFMA kernels on HIP); bf16 = '
+                      'bf16 operands, fp32 accumulation (V-trace/loss/'
+                      'optimizer state always fp32).')
   p.add_argument('--device', default='auto',
                  help='auto | cpu | cuda | cuda:N')
   p.add_argument('--inference_min_batch', type=int, default=1)

@@ -126,9 +126,17 @@ class Learner:
     self.flat = FlatParams(self.agent)
     use_hip = getattr(agent, 'backend', 'torch') == 'hip'
     self.use_fused = use_hip
+    lstm_err = None
+    if use_hip and self.device.type == 'cuda':
+      # a cooperative LSTM unroll that timed out skips the update (and is
+      # counted) instead of applying gradients of stale activations
+      from .ops import lstm as lstm_ops
+      lstm_err = lstm_ops.persistent_error_word(self.device)
     self.opt = RMSProp(self.flat, flags.learning_rate, flags.decay,
                        flags.momentum, flags.epsilon,
-                       flags.total_environment_frames, use_hip=use_hip)
+                       flags.total_environment_frames, use_hip=use_hip,
+                       skip_nonfinite=getattr(flags, 'skip_nonfinite', True),
+                       lstm_err=lstm_err)
     self.frames = torch.zeros((), dtype=torch.int64, device=self.device)
     self.world_size = world_size
     self.pg = process_group
@@ -232,6 +240,13 @@ class Learner:
     self._apply()
     self.last_loss = self._static_loss
     return self._static_loss
+
+  def health(self):
+    """{'skipped_updates', 'lstm_timeouts'} since construction (one device
+    read): updates the step guard dropped (non-finite gradients or an
+    abandoned LSTM unroll) and how many of them were LSTM timeouts."""
+    skipped, timeouts = self.opt.health()
+    return {'skipped_updates': skipped, 'lstm_timeouts': timeouts}
 
   # ------------------------------------------------------------ state
   def state_dict(self):

@@ -35,9 +35,26 @@ INSTR_EMBED = 20
 INSTR_LSTM = 64
 
 
-def _hip_torso_ready(agent):
+def _bf16_torso_ready(agent):
+  """The fused bf16 torso kernels (conv_torso.hip) apply: bf16 compute and a
+  shape they cover."""
   from ..ops import conv
-  return conv.TORSO_READY and conv.supports(agent)
+  return (agent.compute_dtype == torch.bfloat16 and conv.TORSO_READY and
+          conv.supports(agent))
+
+
+def _hip_torso_ready(agent):
+  """Some HIP torso covers the agent: the fused bf16 kernels, else the
+  exact-fp32 kernels (any torso, C <= 4 frames)."""
+  from ..ops import conv_f32
+  return _bf16_torso_ready(agent) or conv_f32.supports(agent)
+
+
+def torso_precision(agent):
+  """'bf16' / 'fp32' (HIP kernels) or 'torch' for the torso that runs."""
+  if agent.backend != 'hip':
+    return 'torch'
+  return 'bf16' if _bf16_torso_ready(agent) else 'fp32'
 
 
 def hip_ops_in_use(agent):
@@ -46,7 +63,7 @@ def hip_ops_in_use(agent):
     return []
   ops = ['lstm_recurrence', 'vtrace_loss', 'rmsprop']
   if _hip_torso_ready(agent):
-    ops += ['conv_torso']
+    ops += ['conv_torso_' + torso_precision(agent)]
   return ops
 
 
@@ -175,9 +192,13 @@ class Agent(nn.Module):
 
   def conv_features(self, frames):
     """frames uint8 [N,H,W,C] -> flattened conv features [N, flat]."""
-    if self.backend == 'hip' and _hip_torso_ready(self):
+    if self.backend == 'hip' and frames.is_cuda:
       from .. import ops
-      return ops.torso_forward(self, frames)
+      if _bf16_torso_ready(self):
+        return ops.torso_forward(self, frames)
+      # exact fp32 kernels (also for a bf16 agent whose shape the bf16
+      # kernels do not cover); unsupported shapes raise, never fall back
+      return ops.torso_forward_f32(self, frames)
     x = frames.to(torch.float32) / 255.0
     cdt = self.compute_dtype
     if cdt != torch.float32:
@@ -201,9 +222,11 @@ class Agent(nn.Module):
     return x.reshape(x.shape[0], -1)
 
   def torso_fc(self, feats):
-    if self.backend == 'hip' and _hip_torso_ready(self):
+    if self.backend == 'hip' and feats.is_cuda:
       from .. import ops
-      return ops.linear_relu(feats, self.linear_w, self.linear_b)
+      if feats.dtype == torch.bfloat16:
+        return ops.linear_relu(feats, self.linear_w, self.linear_b)
+      return ops.linear_relu_f32(feats, self.linear_w, self.linear_b)
     w = self.linear_w.to(feats.dtype)
     b = self.linear_b.to(feats.dtype)
     return F.relu(feats @ w + b).to(torch.float32)
@@ -256,7 +279,8 @@ class Agent(nn.Module):
     """x [T,B,F], done [T,B] bool, state (c,h) -> (h_all [T,B,256], state)."""
     if self.backend == 'hip':
       from .. import ops
-      return ops.lstm_unroll(x, done, state, self.lstm_kernel, self.lstm_bias)
+      return ops.lstm_unroll(x, done, state, self.lstm_kernel, self.lstm_bias,
+                             exact=self.compute_dtype == torch.float32)
     c, h = state
     T = x.shape[0]
     kx = self.lstm_kernel[:self.core_input_size]
@@ -317,7 +341,8 @@ class Agent(nn.Module):
       x.record_stream(side)
       with torch.cuda.stream(side):
         hs, state = ops.lstm_unroll(x, done[t0:t1], state, self.lstm_kernel,
-                                    self.lstm_bias, w_x=w_x, w_h=w_h)
+                                    self.lstm_bias, w_x=w_x, w_h=w_h,
+                                    exact=self.compute_dtype == torch.float32)
       outs.append(hs)
     main.wait_stream(side)
     for h in outs:
@@ -343,8 +368,8 @@ class Agent(nn.Module):
     """True when the HIP learner path (fused torso-FC/core-input/LSTM op,
     fused heads+V-trace loss) applies: HIP backend, HIP torso, no
     instruction strings, bf16 compute."""
-    return (self.backend == 'hip' and _hip_torso_ready(self) and
-            instr is None and self.compute_dtype == torch.bfloat16)
+    return (self.backend == 'hip' and _bf16_torso_ready(self) and
+            instr is None)
 
   def unroll_core(self, actions, env_outputs, core_state):
     """Everything of `unroll` up to the LSTM output: -> (core_out [T,B,256],

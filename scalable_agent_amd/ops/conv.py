@@ -28,7 +28,10 @@ FUSED_BLOCK = os.environ.get('SA_FUSED_BLOCK', '0') == '1'
 
 
 def supports(agent):
-  return agent.torso_kind == 'deep'
+  """Shapes the fused bf16 kernels cover: the deep ResNet on uint8 RGB
+  frames (conv1 is specialised for C=3; other inputs take the fp32
+  kernels, ops/conv_f32.py)."""
+  return agent.torso_kind == 'deep' and agent.frame_shape[2] == 3
 
 
 def _pool_pads(h, w):
@@ -149,7 +152,9 @@ class _DeepTorso(torch.autograd.Function):
 def torso_forward(agent, frames):
   """uint8 frames [N,H,W,3] -> relu'd conv features [N, flat] (bf16)."""
   if not supports(agent):
-    raise NotImplementedError('HIP torso implements the deep ResNet only')
+    raise NotImplementedError(
+        'bf16 HIP torso: deep ResNet on uint8 RGB frames only (got %r, %r)' %
+        (agent.torso_kind, agent.frame_shape))
   return _DeepTorso.apply(frames, *deep_param_list(agent))
 
 

@@ -1,0 +1,172 @@
+"""Reference-precision conv torsos on the exact-fp32 MFMA kernels
+(csrc/kernels/conv_f32.hip: v_mfma_f32_16x16x4_f32, f32 in / f32 accumulate).
+
+The reference computes its torso in fp32 (experiment.py:153-189: to_float/255,
+fp32 cuDNN convs); these kernels reproduce that numerically (one rounding
+per product, like an fmaf chain) with every TF-SAME padding, the uint8 /255
+scaling and the ReLUs/residual adds fused into the conv loads and epilogues:
+
+  shallow (experiment.py:178-183): 3 x [conv (8x8/4, 4x4/2, 3x3/2 with the
+      asymmetric W pad 0/1) + bias + ReLU]
+  deep    (experiment.py:156-176): per stage conv3x3 + bias -> maxpool
+      3x3/2 SAME (argmax saved) -> 2 x [t = relu(conv(relu(x)) + b1);
+      y = conv(t) + b2 + x], final ReLU
+
+Backward: data gradients are the same kernel over the stride-dilated dY with
+flipped/transposed weights (ReLU masks and skip adds in the epilogue);
+weight+bias gradients are a deterministic two-stage reduction accumulated
+straight into the learner's flat gradient buffer (grad_sink).  Frames may
+carry any C <= 4 channels (RGB, or Atari-style stacked grayscale).
+"""
+
+import torch
+
+from . import grad_sink
+from ._ext import ext
+from ..models import layers
+
+
+def supports(agent):
+  """Shapes the fp32 kernels cover: both torsos, uint8 frames with C <= 4."""
+  c = agent.frame_shape[2]
+  return agent.torso_kind in ('deep', 'shallow') and 1 <= c <= 4
+
+
+def _conv_geom(H, W, k, s):
+  return (layers.same_pads(H, k, s)[0], layers.same_pads(W, k, s)[0],
+          layers.same_out(H, s), layers.same_out(W, s))
+
+
+class _ShallowTorsoF32(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, frames, *params):
+    C = ext()
+    x = frames.contiguous()
+    acts = [x]
+    geoms = []
+    for i in range(3):
+      w, b = params[2 * i], params[2 * i + 1]
+      k = w.shape[0]
+      s = (4, 2, 2)[i]
+      H, W = x.shape[1], x.shape[2]
+      pt, pl, Ho, Wo = _conv_geom(H, W, k, s)
+      x = C.cf32_conv_fwd(x, w, b, s, pt, pl, Ho, Wo, relu_out=True)
+      acts.append(x)
+      geoms.append((s, pt, pl, H, W))
+    ctx.save_for_backward(*acts, *params)
+    ctx.geoms = geoms
+    return x.reshape(x.shape[0], -1)
+
+  @staticmethod
+  def backward(ctx, grad_out):
+    C = ext()
+    t = ctx.saved_tensors
+    acts, params = t[:4], t[4:]
+    out = acts[3]
+    gv, direct = grad_sink.sinks(params)
+    # the torso's trailing ReLUs (layer-3 ReLU and experiment.py:185)
+    dy = grad_out.reshape(out.shape).to(torch.float32).clone(
+        memory_format=torch.contiguous_format)
+    C.cf32_relu_mask_(dy, out)
+    for i in reversed(range(3)):
+      s, pt, pl, H, W = ctx.geoms[i]
+      C.cf32_conv_wgrad(acts[i], dy, s, pt, pl, False, gv[2 * i], gv[2 * i + 1])
+      if i > 0:
+        # input of layer i is the ReLU'd output of layer i-1
+        dy = C.cf32_conv_dgrad(dy, params[2 * i], s, pt, pl, H, W, mask=acts[i])
+    return (None,) + grad_sink.returned(gv, direct)
+
+
+class _DeepTorsoF32(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, frames, *params):
+    C = ext()
+    x = frames.contiguous()
+    saved, meta = [], []
+    p = 0
+    for s in range(3):
+      w, b = params[p], params[p + 1]
+      p += 2
+      H, W = x.shape[1], x.shape[2]
+      conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
+      pbh = layers.same_pads(H, 3, 2)[0]
+      pbw = layers.same_pads(W, 3, 2)[0]
+      xa, arg = C.cf32_maxpool_fwd(conv, pbh, pbw)
+      del conv
+      h, w_ = xa.shape[1], xa.shape[2]
+      saved += [x, arg]
+      for blk in range(2):
+        w1, b1, w2, b2 = params[p:p + 4]
+        p += 4
+        last = s == 2 and blk == 1
+        # t stored ReLU'd: conv 2 reads it as is, its mask is (t > 0)
+        t = C.cf32_conv_fwd(xa, w1, b1, 1, 1, 1, h, w_, relu_in=True,
+                            relu_out=True)
+        y = C.cf32_conv_fwd(t, w2, b2, 1, 1, 1, h, w_, add=xa, relu_out=last)
+        saved += [xa, t]
+        xa = y
+      meta.append((H, W, h, w_, pbh, pbw))
+      x = xa
+    ctx.save_for_backward(*saved, x, *params)
+    ctx.meta = meta
+    ctx.nparams = len(params)
+    return x.reshape(x.shape[0], -1)
+
+  @staticmethod
+  def backward(ctx, grad_out):
+    C = ext()
+    t = ctx.saved_tensors
+    params = t[-ctx.nparams:]
+    out = t[-ctx.nparams - 1]
+    saved = t[:-ctx.nparams - 1]
+    gv, direct = grad_sink.sinks(params)
+    dy = grad_out.reshape(out.shape).to(torch.float32).clone(
+        memory_format=torch.contiguous_format)
+    C.cf32_relu_mask_(dy, out)  # final ReLU of the torso
+    for s in reversed(range(3)):
+      k = 6 * s
+      stage_in, arg = saved[k], saved[k + 1]
+      H, W, h, w_, pbh, pbw = ctx.meta[s]
+      pb = 10 * s
+      for blk in reversed(range(2)):
+        xa, tt = saved[k + 2 + 2 * blk], saved[k + 3 + 2 * blk]
+        i1 = pb + 2 + 4 * blk
+        w1, w2 = params[i1], params[i1 + 2]
+        C.cf32_conv_wgrad(tt, dy, 1, 1, 1, False, gv[i1 + 2], gv[i1 + 3])
+        dt = C.cf32_conv_dgrad(dy, w2, 1, 1, 1, h, w_, mask=tt)
+        C.cf32_conv_wgrad(xa, dt, 1, 1, 1, True, gv[i1], gv[i1 + 1])
+        dy = C.cf32_conv_dgrad(dt, w1, 1, 1, 1, h, w_, mask=xa, add=dy)
+      dconv = C.cf32_maxpool_bwd(dy, arg, H, W, pbh, pbw)
+      C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gv[pb], gv[pb + 1])
+      if s > 0:
+        dy = C.cf32_conv_dgrad(dconv, params[pb], 1, 1, 1, H, W)
+    return (None,) + grad_sink.returned(gv, direct)
+
+
+def shallow_param_list(agent):
+  out = []
+  for sp in agent.specs:
+    out += list(agent._conv_params(sp['name']))
+  return out
+
+
+def torso_forward_f32(agent, frames):
+  """uint8 frames [N,H,W,C] -> ReLU'd conv features [N, flat] (fp32)."""
+  if not supports(agent):
+    raise NotImplementedError(
+        'fp32 HIP torso: unsupported torso %r / frame shape %r' %
+        (agent.torso_kind, agent.frame_shape))
+  if frames.dtype != torch.uint8:
+    raise TypeError('HIP torso expects uint8 frames, got %s' % frames.dtype)
+  if agent.torso_kind == 'shallow':
+    return _ShallowTorsoF32.apply(frames, *shallow_param_list(agent))
+  from .conv import deep_param_list
+  return _DeepTorsoF32.apply(frames, *deep_param_list(agent))
+
+
+def linear_relu_f32(x, w, b):
+  """Torso FC in fp32: relu(x W + b) (library fp32 GEMM: exact f32 on gfx950,
+  which has no xf32/TF32 mode)."""
+  return torch.relu(torch.addmm(b, x, w))

@@ -62,8 +62,10 @@ class _CoreLSTM(torch.autograd.Function):
     h_aug = C.core_aug_fwd(h, rewards, actions, K, 0)
     del h
     xw = torch.addmm(bias, h_aug, wx16, out_dtype=torch.float32)
+    mode = C.lstm_mode(CORE, B, T, False)  # bf16 path: the gang may run
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
-                                       kernel[f_in:])
+                                       kernel[f_in:], mode)
+    ctx.mode = mode
     ctx.save_for_backward(feats, w_fc, b_fc, kernel, bias, w16_fc, wx16, h_aug,
                           wt, acts, cs, c0, hpm, done_u8)
     ctx.f_in = f_in
@@ -83,7 +85,7 @@ class _CoreLSTM(torch.autograd.Function):
     if dc_last is not None:
       dc_last = dc_last.contiguous()
     dg, dc0, dg16 = C.lstm_bwd(dhs.contiguous(), done_u8, wt, acts, cs, c0,
-                               dc_last, True)
+                               dc_last, True, ctx.mode)
     (gwfc, gbfc, gk, gb), direct = grad_sink.sinks([w_fc, b_fc, kernel, bias])
     dg2 = dg.view(N, G)
     dg16_2 = dg16.view(N, G)

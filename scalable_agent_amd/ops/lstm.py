@@ -20,13 +20,17 @@ from ._ext import ext, check_cuda
 class _LSTMRecurrence(torch.autograd.Function):
 
   @staticmethod
-  def forward(ctx, xw, w_h, c0, h0, done_u8):
+  def forward(ctx, xw, w_h, c0, h0, done_u8, exact):
     xw = xw.contiguous()
     w_h_c = w_h.contiguous()
     c0 = c0.contiguous()
     h0 = h0.contiguous()
-    hs, cs, acts, hpm, wt = ext().lstm_fwd(xw, done_u8, c0, h0, w_h_c)
+    T, B, H4 = xw.shape
+    # resolved once: forward and backward must agree on the packed weights
+    mode = ext().lstm_mode(H4 // 4, B, T, bool(exact))
+    hs, cs, acts, hpm, wt = ext().lstm_fwd(xw, done_u8, c0, h0, w_h_c, mode)
     ctx.save_for_backward(w_h_c, wt, acts, cs, c0, hpm, done_u8)
+    ctx.mode = mode
     return hs, cs[-1]
 
   @staticmethod
@@ -39,7 +43,7 @@ class _LSTMRecurrence(torch.autograd.Function):
     if dc_last is not None:
       dc_last = dc_last.contiguous()
     dg, dc0, _ = ext().lstm_bwd(dhs.contiguous(), done_u8, wt, acts, cs, c0,
-                                dc_last, False)
+                                dc_last, False, ctx.mode)
     # dW_h = sum_t (keep_t h_{t-1})^T dG_t; hpm is saved by the fwd kernel
     dw_h = hpm.reshape(T * B, H).t() @ dg.reshape(T * B, 4 * H)
     dh0 = None
@@ -48,15 +52,16 @@ class _LSTMRecurrence(torch.autograd.Function):
       dh0 = (dg[0] @ w_h.t()) * keep0
     if not ctx.needs_input_grad[2]:
       dc0 = None
-    return dg, dw_h, dc0, dh0, None
+    return dg, dw_h, dc0, dh0, None, None
 
 
-def lstm_unroll(x, done, state, kernel, bias, w_x=None, w_h=None):
+def lstm_unroll(x, done, state, kernel, bias, w_x=None, w_h=None, exact=False):
   """x [T,B,F] f32, done [T,B] bool, state (c,h) -> (h_all, (c_T, h_T)).
 
   w_x / w_h: optional pre-sliced views of `kernel` (rows [:F] and [F:]); a
   chunked unroll passes the same views to every chunk so the slice backward
-  runs once instead of once per chunk.
+  runs once instead of once per chunk.  exact: reference (fp32) precision -
+  the bf16-operand gang recurrence is never used.
   """
   c0, h0 = state
   check_cuda(x, kernel)
@@ -67,7 +72,8 @@ def lstm_unroll(x, done, state, kernel, bias, w_x=None, w_h=None):
     w_h = kernel[F_in:]
   xw = torch.matmul(x.float(), w_x) + bias
   hs, c_last = _LSTMRecurrence.apply(xw, w_h, c0.float(), h0.float(),
-                                     done.to(torch.uint8).contiguous())
+                                     done.to(torch.uint8).contiguous(),
+                                     bool(exact))
   return hs, (c_last, hs[-1])
 
 
@@ -86,6 +92,17 @@ def set_gang(on):
   prev = bool(ext().lstm_get_gang())
   ext().lstm_set_gang(bool(on))
   return prev
+
+
+def persistent_error_word(device):
+  """The device-resident sticky timeout word itself (int32[4], element 0)."""
+  return ext().lstm_error_word(torch.empty(0, device=device))
+
+
+def set_gang_fault(on):
+  """Test hook: every gang sweep reports a timeout.  Returns the previous
+  setting."""
+  return bool(ext().lstm_gang_fault(1 if on else 0))
 
 
 def persistent_error(device):

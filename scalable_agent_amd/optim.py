@@ -90,7 +90,7 @@ class RMSProp:
 
   def __init__(self, flat: FlatParams, learning_rate, decay=0.99, momentum=0.,
                epsilon=0.1, total_frames=int(1e9), use_hip=None,
-               skip_nonfinite=True):
+               skip_nonfinite=True, lstm_err=None):
     self.flat = flat
     self.lr0 = float(learning_rate)
     self.decay = float(decay)
@@ -103,14 +103,26 @@ class RMSProp:
     if use_hip is None:
       use_hip = dev.type == 'cuda'
     self.use_hip = use_hip
-    # (flag, skipped steps): a step with NaN/inf gradients leaves the
-    # parameters and slots untouched (SURVEY §5.3 failure detection).
+    # (flag, skipped steps, lstm timeouts, -): a step with NaN/inf gradients
+    # or an abandoned cooperative LSTM unroll (lstm_err: the recurrence's
+    # sticky timeout word) leaves the parameters and slots untouched
+    # (SURVEY §5.3 failure detection).
     self.skip_nonfinite = skip_nonfinite
-    self.guard = torch.zeros(2, dtype=torch.int32, device=dev)
+    self.lstm_err = lstm_err if skip_nonfinite else None
+    self.guard = torch.zeros(4, dtype=torch.int32, device=dev)
 
   @property
   def skipped_steps(self):
     return int(self.guard[1].item())
+
+  @property
+  def lstm_timeouts(self):
+    return int(self.guard[2].item())
+
+  def health(self):
+    """(skipped steps, lstm timeouts) with one device read."""
+    g = self.guard.tolist()
+    return int(g[1]), int(g[2])
 
   def step(self, frames):
     """frames: int64 0-d tensor on the param device (read-only here)."""
@@ -119,7 +131,8 @@ class RMSProp:
       ops.rmsprop_step(self.flat.params, self.flat.grads, self.ms, self.mom,
                        frames, self.lr0, self.total_frames, self.decay,
                        self.momentum, self.epsilon,
-                       self.guard if self.skip_nonfinite else None)
+                       self.guard if self.skip_nonfinite else None,
+                       self.lstm_err)
       return
     g = self.flat.grads
     if self.skip_nonfinite and not bool(torch.isfinite(g).all()):

@@ -9,4 +9,5 @@ under the reference's sum losses.
 """
 
 from .dist import (init_distributed, GradientSynchronizer, broadcast_params,
-                   param_checksum_consistent, world_info, cleanup)
+                   param_checksum_consistent, world_info, cleanup,
+                   backend_info)

@@ -48,10 +48,29 @@ def init_distributed(backend=None, timeout_s=600):
       # a collective that times out aborts the process (instead of hanging
       # the job); torchrun --max-restarts + checkpoint auto-restore resume it
       os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
+      # more ranks than visible GPUs (a one-card rehearsal): share the cards
+      local = local % max(1, torch.cuda.device_count())
       torch.cuda.set_device(local)
       kwargs['device_id'] = torch.device('cuda', local)
     dist.init_process_group(**kwargs)
   return rank, world, local
+
+
+def backend_info():
+  """{'world_size', 'backend', 'rccl_version'} of the default group (for
+  logs and the bench JSON: proves how many ranks the collective saw)."""
+  info = {'world_size': 1, 'backend': None, 'rccl_version': None}
+  if dist.is_initialized():
+    info['world_size'] = dist.get_world_size()
+    info['backend'] = dist.get_backend()
+  try:
+    if torch.cuda.is_available():
+      v = torch.cuda.nccl.version()
+      info['rccl_version'] = '.'.join(str(x) for x in v) if isinstance(
+          v, tuple) else str(v)
+  except Exception:  # pragma: no cover - build without RCCL
+    pass
+  return info
 
 
 def cleanup():

@@ -1,0 +1,222 @@
+"""Exact-fp32 conv kernels (csrc/kernels/conv_f32.hip) vs float64 PyTorch.
+
+Every layer shape of both torsos (reference experiment.py:156-189: shallow
+8x8/4, 4x4/2, 3x3/2 with the asymmetric W pad; deep 3x3/1 stages, 3x3/2
+max-pool) plus the Atari-shaped 84x84x4 and Doom-shaped 72x128x3 inputs:
+forward (with the fused ReLU-in / residual / ReLU-out), data gradient (fused
+mask + skip add), weight + bias gradient (deterministic reduction) and the
+pool.  The oracle is the float64 TF-SAME reference of models/layers.py on
+the CPU; the fp32 kernels must agree to <= 1e-5 of the output scale.
+"""
+
+import pytest
+import torch
+
+from scalable_agent_amd.models import layers
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _C():
+  from scalable_agent_amd import ops
+  return ops.ext()
+
+
+def rel_err(a, ref):
+  a = a.detach().double().cpu()
+  ref = ref.detach().double().cpu()
+  return (a - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+# (N, H, W, Cin, Cout, K, S, uint8 source)
+SHAPES = {
+    'shallow1': (3, 72, 96, 3, 32, 8, 4, True),
+    'shallow2': (3, 18, 24, 32, 64, 4, 2, False),
+    'shallow3': (3, 9, 12, 64, 128, 3, 2, False),   # W pad 0/1
+    'deep_conv1': (3, 72, 96, 3, 16, 3, 1, True),
+    'deep_conv2': (3, 36, 48, 16, 32, 3, 1, False),
+    'deep_res16': (3, 36, 48, 16, 16, 3, 1, False),
+    'deep_res32': (3, 18, 24, 32, 32, 3, 1, False),
+    'deep_res32_s3': (3, 9, 12, 32, 32, 3, 1, False),
+    'atari_deep_conv1': (2, 84, 84, 4, 16, 3, 1, True),
+    'atari_deep_res32': (2, 11, 11, 32, 32, 3, 1, False),
+    'atari_shallow1': (2, 84, 84, 4, 32, 8, 4, True),
+    'atari_shallow2': (2, 21, 21, 32, 64, 4, 2, False),
+    'atari_shallow3': (2, 11, 11, 64, 128, 3, 2, False),
+    'doom_deep_conv1': (2, 72, 128, 3, 16, 3, 1, True),
+}
+
+
+def _make(name, cuda, seed=0):
+  N, H, W, Cin, Cout, K, S, u8 = SHAPES[name]
+  g = torch.Generator().manual_seed(seed)
+  if u8:
+    x = torch.randint(0, 256, (N, H, W, Cin), generator=g, dtype=torch.uint8)
+    x64 = x.double() / 255.0
+  else:
+    x = torch.randn(N, H, W, Cin, generator=g)
+    x64 = x.double()
+  w = torch.randn(K, K, Cin, Cout, generator=g) / (K * K * Cin) ** 0.5
+  b = torch.randn(Cout, generator=g) * 0.1
+  pt, pl = layers.same_pads(H, K, S)[0], layers.same_pads(W, K, S)[0]
+  Ho, Wo = layers.same_out(H, S), layers.same_out(W, S)
+  return dict(x=x, x64=x64, w=w, b=b, K=K, S=S, pt=pt, pl=pl, Ho=Ho, Wo=Wo,
+              H=H, W=W, u8=u8, g=g, dev=cuda)
+
+
+@pytest.mark.parametrize('name', sorted(SHAPES))
+@pytest.mark.parametrize('relu_in,resid,relu_out', [
+    (False, False, False), (True, False, True), (False, True, True)])
+def test_conv_f32_forward(cuda, name, relu_in, resid, relu_out):
+  d = _make(name, cuda)
+  if d['u8'] and relu_in:
+    pytest.skip('frames are never ReLU\'d')
+  C = _C()
+  N = d['x'].shape[0]
+  Cout = d['w'].shape[3]
+  add = torch.randn(N, d['Ho'], d['Wo'], Cout, generator=d['g']) if resid else None
+  xin = d['x64'].clamp(min=0) if relu_in else d['x64']
+  ref = layers.conv2d_same_nhwc(xin, d['w'].double(), d['b'].double(), d['S'])
+  if resid:
+    ref = ref + add.double()
+  if relu_out:
+    ref = ref.clamp(min=0)
+  y = C.cf32_conv_fwd(d['x'].to(cuda), d['w'].to(cuda), d['b'].to(cuda), d['S'],
+                      d['pt'], d['pl'], d['Ho'], d['Wo'], relu_in=relu_in,
+                      add=None if add is None else add.to(cuda), relu_out=relu_out)
+  assert y.dtype == torch.float32 and y.shape == ref.shape
+  assert rel_err(y, ref) <= TOL
+
+
+@pytest.mark.parametrize('name', sorted(k for k, v in SHAPES.items() if not v[7]))
+@pytest.mark.parametrize('masked', [False, True])
+def test_conv_f32_dgrad(cuda, name, masked):
+  d = _make(name, cuda, seed=1)
+  C = _C()
+  N = d['x'].shape[0]
+  Cout = d['w'].shape[3]
+  dy = torch.randn(N, d['Ho'], d['Wo'], Cout, generator=d['g'])
+  x64 = d['x64'].clone().requires_grad_(True)
+  y = layers.conv2d_same_nhwc(x64, d['w'].double(), None, d['S'])
+  (ref,) = torch.autograd.grad(y, x64, dy.double())
+  mask = add = None
+  if masked:
+    mask = torch.randn(d['x'].shape, generator=d['g'])
+    add = torch.randn(d['x'].shape, generator=d['g'])
+    ref = torch.where(mask.double() > 0, ref, torch.zeros_like(ref)) + add.double()
+  dx = C.cf32_conv_dgrad(dy.to(cuda), d['w'].to(cuda), d['S'], d['pt'], d['pl'],
+                         d['H'], d['W'],
+                         mask=None if mask is None else mask.to(cuda),
+                         add=None if add is None else add.to(cuda))
+  assert dx.shape == ref.shape
+  assert rel_err(dx, ref) <= TOL
+
+
+@pytest.mark.parametrize('name', sorted(SHAPES))
+@pytest.mark.parametrize('relu_in', [False, True])
+def test_conv_f32_wgrad(cuda, name, relu_in):
+  d = _make(name, cuda, seed=2)
+  if d['u8'] and relu_in:
+    pytest.skip('frames are never ReLU\'d')
+  C = _C()
+  N = d['x'].shape[0]
+  Cout = d['w'].shape[3]
+  dy = torch.randn(N, d['Ho'], d['Wo'], Cout, generator=d['g'])
+  w64 = d['w'].double().requires_grad_(True)
+  b64 = d['b'].double().requires_grad_(True)
+  xin = d['x64'].clamp(min=0) if relu_in else d['x64']
+  y = layers.conv2d_same_nhwc(xin, w64, b64, d['S'])
+  rw, rb = torch.autograd.grad(y, (w64, b64), dy.double())
+  # the kernels ACCUMULATE: start from a known non-zero gradient
+  dw0 = torch.randn(d['w'].shape, generator=d['g'])
+  db0 = torch.randn(Cout, generator=d['g'])
+  dw, db = dw0.to(cuda), db0.to(cuda)
+  x, dyc = d['x'].to(cuda), dy.to(cuda)
+  C.cf32_conv_wgrad(x, dyc, d['S'], d['pt'], d['pl'], relu_in, dw, db)
+  assert rel_err(dw - dw0.to(cuda), rw) <= TOL
+  assert rel_err(db - db0.to(cuda), rb) <= TOL
+  # deterministic: a second accumulation adds bitwise the same amount
+  dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
+  dw3, db3 = torch.zeros_like(dw), torch.zeros_like(db)
+  C.cf32_conv_wgrad(x, dyc, d['S'], d['pt'], d['pl'], relu_in, dw2, db2)
+  C.cf32_conv_wgrad(x, dyc, d['S'], d['pt'], d['pl'], relu_in, dw3, db3)
+  assert torch.equal(dw2, dw3) and torch.equal(db2, db3)
+
+
+@pytest.mark.parametrize('N,H,W,C', [(3, 72, 96, 16), (3, 36, 48, 32),
+                                     (3, 18, 24, 32), (2, 84, 84, 16),
+                                     (2, 21, 21, 32)])
+def test_maxpool_f32(cuda, N, H, W, C):
+  g = torch.Generator().manual_seed(3)
+  x = torch.randn(N, H, W, C, generator=g)
+  dy = torch.randn(N, (H + 1) // 2, (W + 1) // 2, C, generator=g)
+  x64 = x.double().requires_grad_(True)
+  ref = layers.maxpool_same_nhwc(x64, 3, 2)
+  (rdx,) = torch.autograd.grad(ref, x64, dy.double())
+  pbh, pbw = layers.same_pads(H, 3, 2)[0], layers.same_pads(W, 3, 2)[0]
+  C_ = _C()
+  y, arg = C_.cf32_maxpool_fwd(x.to(cuda), pbh, pbw)
+  assert torch.equal(y.cpu().double(), ref.detach())  # max is exact
+  dx = C_.cf32_maxpool_bwd(dy.to(cuda), arg, H, W, pbh, pbw)
+  assert rel_err(dx, rdx) <= 1e-6
+
+
+def _ref_features(agent, frames):
+  """float64 replica of Agent.conv_features (the torch oracle)."""
+  x = frames.double() / 255.0
+  P = {k: v.detach().double().requires_grad_(True) for k, v in agent.convnet.items()}
+  for sp in agent.specs:
+    if sp['kind'] == 'conv':
+      x = layers.conv2d_same_nhwc(x, P[sp['name'] + '__w'], P[sp['name'] + '__b'], sp['s'])
+      if sp['relu_out']:
+        x = x.clamp(min=0)
+    elif sp['kind'] == 'pool':
+      x = layers.maxpool_same_nhwc(x, 3, 2)
+    else:
+      block_in = x
+      for sub in ('conv_2d', 'conv_2d_1'):
+        x = x.clamp(min=0)
+        x = layers.conv2d_same_nhwc(x, P[sp['name'] + '__' + sub + '__w'],
+                                    P[sp['name'] + '__' + sub + '__b'], 1)
+      x = x + block_in
+  x = x.clamp(min=0)
+  return x.reshape(x.shape[0], -1), P
+
+
+@pytest.mark.parametrize('torso,shape', [('deep', (72, 96, 3)), ('shallow', (72, 96, 3)),
+                                         ('deep', (84, 84, 4)), ('shallow', (84, 84, 4)),
+                                         ('deep', (72, 128, 3))])
+def test_torso_f32_matches_float64(cuda, torso, shape):
+  """Whole fp32 HIP torso (features and every conv weight/bias gradient)
+  against the float64 oracle; the bf16 kernels are not involved."""
+  from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.models.agent import torso_precision
+  agent = Agent(9, torso=torso, frame_shape=shape, seed=5, backend='hip',
+                compute_dtype=torch.float32).to(cuda)
+  assert torso_precision(agent) == 'fp32'
+  g = torch.Generator().manual_seed(6)
+  frames = torch.randint(0, 256, (6,) + shape, generator=g, dtype=torch.uint8)
+  feats = agent.conv_features(frames.to(cuda))
+  assert feats.dtype == torch.float32
+  ref, P = _ref_features(agent, frames)
+  assert rel_err(feats, ref) <= TOL
+  r = torch.randn(ref.shape, generator=g)
+  (feats * r.to(cuda)).sum().backward()
+  (ref * r.double()).sum().backward()
+  for k, p in agent.convnet.items():
+    assert rel_err(p.grad, P[k].grad) <= 5 * TOL, k
+
+
+def test_bf16_agent_non_rgb_takes_fp32_kernels(cuda):
+  """Shapes the fused bf16 kernels do not cover (Atari 4-channel stack)
+  run the exact-fp32 kernels instead of failing or leaving the GPU path."""
+  from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.models.agent import torso_precision
+  agent = Agent(6, torso='deep', frame_shape=(84, 84, 4), seed=1, backend='hip',
+                compute_dtype=torch.bfloat16).to(cuda)
+  assert torso_precision(agent) == 'fp32'
+  frames = torch.randint(0, 256, (4, 84, 84, 4), dtype=torch.uint8, device=cuda)
+  feats = agent.conv_features(frames)
+  assert feats.shape == (4, 11 * 11 * 32) and torch.isfinite(feats).all()

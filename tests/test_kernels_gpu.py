@@ -49,17 +49,17 @@ def test_rmsprop_nonfinite_guard(cuda):
   ms = torch.ones(n, device=cuda)
   mom = torch.zeros(n, device=cuda)
   frames = torch.zeros((), device=cuda, dtype=torch.int64)
-  guard = torch.zeros(2, dtype=torch.int32, device=cuda)
+  guard = torch.zeros(4, dtype=torch.int32, device=cuda)
   g = torch.randn(n, device=cuda)
   g[n - 7] = float('inf')
   w0, ms0 = w.clone(), ms.clone()
   ops.rmsprop_step(w, g, ms, mom, frames, 1e-3, 1e6, 0.99, 0., 0.1, guard)
   assert torch.equal(w, w0) and torch.equal(ms, ms0)
-  assert guard.tolist() == [1, 1]
+  assert guard.tolist() == [1, 1, 0, 0]
   g[n - 7] = 0.5
   ops.rmsprop_step(w, g, ms, mom, frames, 1e-3, 1e6, 0.99, 0., 0.1, guard)
   assert not torch.equal(w, w0)
-  assert guard.tolist() == [0, 1]
+  assert guard.tolist() == [0, 1, 0, 0]
 
 
 def _ref_loss(bl, tl, a, r, done, v, boot, clip, bc, ec):
@@ -238,10 +238,11 @@ def test_lstm_persistent_matches_per_step(cuda, T, B):
   try:
     for mode in (False, True):
       lstm_ops.set_persistent(mode)
+      m = 1 if mode else 0  # explicit recurrence mode (persistent / step)
       runs = []
       for _ in range(3 if mode else 1):
-        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
-        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True)
+        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h, m)
+        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True, m)
         runs.append([hs, cs, acts, hpm, dg, dc0, dg16.float()])
       for r in runs[1:]:
         for a, b in zip(runs[0], r):
@@ -258,7 +259,7 @@ def test_lstm_persistent_matches_per_step(cuda, T, B):
 
 
 @pytest.mark.parametrize('ws', [0, 1])
-@pytest.mark.parametrize('T,B', [(101, 32), (37, 7), (1, 32), (2, 5)])
+@pytest.mark.parametrize('T,B', [(101, 32), (37, 7), (2, 32), (2, 5)])
 def test_lstm_gang_matches_per_step(cuda, T, B, ws):
   """The 8-workgroup gang kernels (bf16 recurrent product, granule
   all-gather fwd / reduce-scatter bwd) track the fp32 per-step kernels to
@@ -283,10 +284,11 @@ def test_lstm_gang_matches_per_step(cuda, T, B, ws):
   try:
     for mode in (False, True):
       lstm_ops.set_gang(mode)
+      m = 2 if mode else 0  # explicit recurrence mode (gang / step)
       runs = []
       for _ in range(3 if mode else 1):
-        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
-        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True)
+        hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h, m)
+        dg, dc0, dg16 = C.lstm_bwd(dh, done, wt, acts, cs, c0, dcl, True, m)
         runs.append([hs, cs, acts, hpm, dg, dc0, dg16.float()])
       for r in runs[1:]:
         for a, b in zip(runs[0], r):

@@ -49,9 +49,10 @@ def main():
     C.lstm_gang_ws(1 if mode == 'gang_ws' else 0)
     C.lstm_gang_nap(nap)
     C.lstm_xpack(xp)
-    hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h)
-    f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h)
-    b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True)
+    m = C.lstm_mode(H, B, T, False)
+    hs, cs, acts, hpm, wt = C.lstm_fwd(xw, done, c0, h0, w_h, m)
+    f = lambda: C.lstm_fwd(xw, done, c0, h0, w_h, m)
+    b = lambda: C.lstm_bwd(dh, done, wt, acts, cs, c0, None, True, m)
     print('%-10s xpack=%d nap=%2d fwd %8.1f us  bwd %8.1f us' % (mode, xp, nap, t_us(f), t_us(b)),
           flush=True)
   print('error word', lstm_ops.persistent_error(d))
