@@ -12,6 +12,13 @@ namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// A launch that fails (e.g. an LDS request the device refuses) must not
+// leave its output uninitialised silently.
+void check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, what, ": kernel launch failed: ", hipGetErrorString(e));
+}
+
 int src_kind(const at::Tensor& x) {
   if (x.scalar_type() == at::kByte) return sa::cf32::kSrcU8;
   TORCH_CHECK(x.scalar_type() == at::kFloat, "conv source must be uint8 frames or float32");
@@ -65,6 +72,7 @@ at::Tensor conv_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, int
   TORCH_CHECK(sa::cf32::conv_launch(a, w.size(0), stride, kind, false, stream()),
               "conv_f32: no kernel instance for K=", w.size(0), " stride=", stride, " Cin=",
               x.size(3), " Cout=", Cout, " src=", kind == sa::cf32::kSrcU8 ? "uint8" : "f32");
+  check_launch("cf32_conv_fwd");
   return y;
 }
 
@@ -94,6 +102,7 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
   TORCH_CHECK(sa::cf32::conv_launch(a, K, 1, sa::cf32::kSrcF32, true, stream()),
               "conv_f32 dgrad: no kernel instance for K=", K, " dy channels=", dy.size(3),
               " dx channels=", Cin);
+  check_launch("cf32_conv_dgrad");
   return dx;
 }
 
@@ -126,6 +135,7 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
   TORCH_CHECK(sa::cf32::wgrad_launch(a, K, stride, kind, ws.data_ptr<float>(), stream()),
               "conv_f32 wgrad: no kernel instance for K=", K, " stride=", stride, " Cin=",
               x.size(3), " Cout=", dy.size(3));
+  check_launch("cf32_conv_wgrad");
 }
 
 std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t pb_h, int64_t pb_w) {
@@ -138,6 +148,7 @@ std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t pb_h, int64_t pb_w) {
   auto arg = at::empty({N, Hp, Wp, C}, x.options().dtype(at::kByte));
   sa::cf32::maxpool_fwd_launch(x.data_ptr<float>(), y.data_ptr<float>(), arg.data_ptr<uint8_t>(),
                                N, H, W, C, Hp, Wp, pb_h, pb_w, stream());
+  check_launch("cf32_maxpool_fwd");
   return {y, arg};
 }
 
@@ -153,6 +164,7 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int6
   sa::cf32::maxpool_bwd_launch(dy.data_ptr<float>(), arg.data_ptr<uint8_t>(), dx.data_ptr<float>(),
                                dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2), pb_h, pb_w,
                                stream());
+  check_launch("cf32_maxpool_bwd");
   return dx;
 }
 

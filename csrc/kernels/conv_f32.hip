@@ -482,10 +482,12 @@ __global__ __launch_bounds__(256) void relu_mask_kernel(f4* __restrict__ dy,
 // ------------------------------------------------------------------ launch
 template <typename Kern>
 void allow_lds(Kern k, size_t bytes) {
-  if (bytes > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(bytes));
+  if (bytes > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(bytes));
+    if (e != hipSuccess) (void)hipGetLastError();  // the launch reports it
+  }
 }
 
 template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>

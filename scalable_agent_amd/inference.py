@@ -53,14 +53,24 @@ class InferenceModel(object):
     return self._stream
 
   def publish(self, flat_params, version=None):
-    """Copies the learner's flat parameter buffer into the snapshot."""
+    """Copies the learner's flat parameter buffer into the snapshot.
+
+    The copy runs on the inference stream (behind any queued inference
+    replay, which still reads the previous snapshot) and the caller's stream
+    then waits for it, so the learner's next RMSProp cannot overwrite
+    `flat_params` while the copy is still queued: a snapshot never mixes
+    two weight versions."""
     with self._lock:
       if self._stream is not None:
+        cur = torch.cuda.current_stream(self.device)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        ev.record(cur)
         self._stream.wait_event(ev)
         with torch.cuda.stream(self._stream):
           self.flat.params.copy_(flat_params, non_blocking=True)
+          done = torch.cuda.Event()
+          done.record(self._stream)
+        cur.wait_event(done)
       else:
         self.flat.params.copy_(flat_params)
       self.version = self.version + 1 if version is None else version

@@ -81,7 +81,7 @@ def compute_loss(agent, data, flags, use_fused=False, popart=None,
     bootstrap_value = bootstrap_value * sigma + mu
 
   clipped_rewards = losses_lib.clip_rewards(rewards, flags.reward_clipping)
-  discounts = (~done.to(torch.bool)).to(torch.float32) * flags.discounting
+  discounts = (~done.to(torch.bool)).to(values.dtype) * flags.discounting
   vt = vtrace_lib.from_logits(
       behaviour_policy_logits=behaviour_logits,
       target_policy_logits=target_logits, actions=actions,

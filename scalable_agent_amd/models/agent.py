@@ -183,7 +183,8 @@ class Agent(nn.Module):
 
   def initial_state(self, batch_size, device=None):
     device = device or self.lstm_bias.device
-    z = torch.zeros(batch_size, CORE_SIZE, device=device)
+    z = torch.zeros(batch_size, CORE_SIZE, device=device,
+                    dtype=self.lstm_bias.dtype)
     return (z, z.clone())
 
   # ------------------------------------------------------------------ torso
@@ -199,9 +200,11 @@ class Agent(nn.Module):
       # exact fp32 kernels (also for a bf16 agent whose shape the bf16
       # kernels do not cover); unsupported shapes raise, never fall back
       return ops.torso_forward_f32(self, frames)
-    x = frames.to(torch.float32) / 255.0
     cdt = self.compute_dtype
-    if cdt != torch.float32:
+    # float64: the learner-parity oracle (tests); else x/255 in fp32
+    wide = torch.float64 if cdt == torch.float64 else torch.float32
+    x = frames.to(wide) / 255.0
+    if cdt != wide:
       x = x.to(cdt)
     for sp in self.specs:
       if sp['kind'] == 'conv':
@@ -229,18 +232,19 @@ class Agent(nn.Module):
       return ops.linear_relu_f32(feats, self.linear_w, self.linear_b)
     w = self.linear_w.to(feats.dtype)
     b = self.linear_b.to(feats.dtype)
-    return F.relu(feats @ w + b).to(torch.float32)
+    out = F.relu(feats @ w + b)
+    return out.float() if out.dtype == torch.bfloat16 else out
 
   def instruction_encoding(self, instr, n, device):
     """instr: None or (ids [N,L] int64, lengths [N] int64) -> [N, 64]."""
     if instr is None:
-      return torch.zeros(n, INSTR_LSTM, device=device)
+      return torch.zeros(n, INSTR_LSTM, device=device, dtype=self.embed.dtype)
     ids, lengths = instr
     ids = ids.reshape(n, -1).to(device)
     lengths = lengths.reshape(n).to(device)
     capturing = lengths.is_cuda and torch.cuda.is_current_stream_capturing()
     if lengths.numel() == 0 or (not capturing and int(lengths.max()) == 0):
-      return torch.zeros(n, INSTR_LSTM, device=device)
+      return torch.zeros(n, INSTR_LSTM, device=device, dtype=self.embed.dtype)
     emb = F.embedding(ids, self.embed)  # [N, L, 20]
     if self.backend == 'hip' and emb.is_cuda:
       # words are the time axis of the fused H=64 LSTM step kernels (K7
@@ -254,7 +258,7 @@ class Agent(nn.Module):
       last = (lengths - 1).clamp(min=0).view(1, n, 1).expand(1, n, INSTR_LSTM)
       out = hs.gather(0, last).squeeze(0)
       return out * (lengths > 0).unsqueeze(-1).to(out.dtype)
-    c = torch.zeros(n, INSTR_LSTM, device=device)
+    c = torch.zeros(n, INSTR_LSTM, device=device, dtype=self.embed.dtype)
     h = torch.zeros_like(c)
     out = torch.zeros_like(c)
     for t in range(ids.shape[1]):
@@ -268,9 +272,10 @@ class Agent(nn.Module):
     n = frames.shape[0]
     feats = self.conv_features(frames)
     torso_out = self.torso_fc(feats)
-    clipped_reward = torch.clamp(rewards.reshape(n, 1).to(torch.float32), -1, 1)
+    dt = torso_out.dtype
+    clipped_reward = torch.clamp(rewards.reshape(n, 1).to(dt), -1, 1)
     one_hot = F.one_hot(last_actions.reshape(n).long(),
-                        self.num_actions).to(torch.float32)
+                        self.num_actions).to(dt)
     instr_out = self.instruction_encoding(instr, n, frames.device)
     return torch.cat([torso_out, clipped_reward, one_hot, instr_out], dim=1)
 
@@ -288,7 +293,7 @@ class Agent(nn.Module):
     xw = torch.matmul(x, kx) + self.lstm_bias  # one GEMM for all steps
     outs = []
     for t in range(T):
-      keep = (~done[t]).to(torch.float32).unsqueeze(-1)
+      keep = (~done[t]).to(c.dtype).unsqueeze(-1)
       c = c * keep
       h = h * keep
       gates = xw[t] + h @ kh

@@ -25,6 +25,10 @@ from . import grad_sink
 from ._ext import ext
 from ..models import layers
 
+# debug hook (tools/debug): when a dict, the deep torso backward records its
+# intermediate gradients in it
+DEBUG_TAPE = None
+
 
 def supports(agent):
   """Shapes the fp32 kernels cover: both torsos, uint8 frames with C <= 4."""
@@ -112,6 +116,8 @@ class _DeepTorsoF32(torch.autograd.Function):
     ctx.save_for_backward(*saved, x, *params)
     ctx.meta = meta
     ctx.nparams = len(params)
+    if DEBUG_TAPE is not None:
+      DEBUG_TAPE['saved'] = [t.clone() for t in saved]
     return x.reshape(x.shape[0], -1)
 
   @staticmethod
@@ -127,6 +133,9 @@ class _DeepTorsoF32(torch.autograd.Function):
     C.cf32_relu_mask_(dy, out)  # final ReLU of the torso
     for s in reversed(range(3)):
       k = 6 * s
+      if DEBUG_TAPE is not None:
+        DEBUG_TAPE[('intact', s)] = [bool(torch.equal(a, b)) for a, b in
+                                     zip(saved, DEBUG_TAPE['saved'])]
       stage_in, arg = saved[k], saved[k + 1]
       H, W, h, w_, pbh, pbw = ctx.meta[s]
       pb = 10 * s
@@ -137,8 +146,14 @@ class _DeepTorsoF32(torch.autograd.Function):
         C.cf32_conv_wgrad(tt, dy, 1, 1, 1, False, gv[i1 + 2], gv[i1 + 3])
         dt = C.cf32_conv_dgrad(dy, w2, 1, 1, 1, h, w_, mask=tt)
         C.cf32_conv_wgrad(xa, dt, 1, 1, 1, True, gv[i1], gv[i1 + 1])
+        if DEBUG_TAPE is not None:
+          DEBUG_TAPE[('dy', s, blk)] = dy.clone()
+          DEBUG_TAPE[('dt', s, blk)] = dt.clone()
         dy = C.cf32_conv_dgrad(dt, w1, 1, 1, 1, h, w_, mask=xa, add=dy)
       dconv = C.cf32_maxpool_bwd(dy, arg, H, W, pbh, pbw)
+      if DEBUG_TAPE is not None:
+        DEBUG_TAPE[('dpool', s)] = dy.clone()
+        DEBUG_TAPE[('dconv', s)] = dconv.clone()
       C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gv[pb], gv[pb + 1])
       if s > 0:
         dy = C.cf32_conv_dgrad(dconv, params[pb], 1, 1, 1, H, W)

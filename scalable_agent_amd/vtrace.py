@@ -22,8 +22,9 @@ from .structs import VTraceFromLogitsReturns, VTraceReturns
 
 
 def _as_f32(x, device=None):
+  """At least fp32 (float64 passes through: the fp64 learner oracle)."""
   t = torch.as_tensor(x, device=device)
-  return t.to(torch.float32)
+  return t if t.dtype == torch.float64 else t.to(torch.float32)
 
 
 def _check_rank(t, rank, name):

@@ -166,7 +166,7 @@ def test_maxpool_f32(cuda, N, H, W, C):
 def _ref_features(agent, frames):
   """float64 replica of Agent.conv_features (the torch oracle)."""
   x = frames.double() / 255.0
-  P = {k: v.detach().double().requires_grad_(True) for k, v in agent.convnet.items()}
+  P = {k: v.detach().double().cpu().requires_grad_(True) for k, v in agent.convnet.items()}
   for sp in agent.specs:
     if sp['kind'] == 'conv':
       x = layers.conv2d_same_nhwc(x, P[sp['name'] + '__w'], P[sp['name'] + '__b'], sp['s'])
@@ -185,19 +185,27 @@ def _ref_features(agent, frames):
   return x.reshape(x.shape[0], -1), P
 
 
-@pytest.mark.parametrize('torso,shape', [('deep', (72, 96, 3)), ('shallow', (72, 96, 3)),
-                                         ('deep', (84, 84, 4)), ('shallow', (84, 84, 4)),
-                                         ('deep', (72, 128, 3))])
-def test_torso_f32_matches_float64(cuda, torso, shape):
+# frame seeds whose float64 forward has no pool near-tie / ReLU near-zero
+# (tests/_discontinuity.py): there fp32 and float64 may branch differently
+# and a single flip moves a whole local gradient
+@pytest.mark.parametrize('torso,shape,fseed', [('deep', (72, 96, 3), 2),
+                                               ('shallow', (72, 96, 3), 0),
+                                               ('deep', (84, 84, 4), 8),
+                                               ('shallow', (84, 84, 4), 0),
+                                               ('deep', (72, 128, 3), 3)])
+def test_torso_f32_matches_float64(cuda, torso, shape, fseed):
   """Whole fp32 HIP torso (features and every conv weight/bias gradient)
   against the float64 oracle; the bf16 kernels are not involved."""
   from scalable_agent_amd.models import Agent
   from scalable_agent_amd.models.agent import torso_precision
+  from tests import _discontinuity
   agent = Agent(9, torso=torso, frame_shape=shape, seed=5, backend='hip',
-                compute_dtype=torch.float32).to(cuda)
+                compute_dtype=torch.float32)
+  g = torch.Generator().manual_seed(fseed)
+  frames = torch.randint(0, 256, (2,) + shape, generator=g, dtype=torch.uint8)
+  assert _discontinuity.count(agent, frames) == 0
+  agent = agent.to(cuda)
   assert torso_precision(agent) == 'fp32'
-  g = torch.Generator().manual_seed(6)
-  frames = torch.randint(0, 256, (6,) + shape, generator=g, dtype=torch.uint8)
   feats = agent.conv_features(frames.to(cuda))
   assert feats.dtype == torch.float32
   ref, P = _ref_features(agent, frames)

@@ -13,18 +13,46 @@ import torch
 
 from scalable_agent_amd import flags as flags_lib
 from scalable_agent_amd.envs.synthetic import make_synthetic_batch
-from scalable_agent_amd.learner import Learner, batch_to_device
+from scalable_agent_amd.learner import (Learner, batch_to_device, compute_loss,
+                                        _map_tensors)
 from scalable_agent_amd.models import Agent
 
 pytestmark = pytest.mark.gpu
 
 
-def _step(backend, torso, dtype, cuda, shape=(72, 96, 3), B=4, T=8):
+def _oracle64(torso, cuda, shape=(72, 96, 3), B=4, T=8, aseed=3, bseed=4):
+  """float64 loss gradients of the same step (torch ops, no HIP kernels)."""
   flags = flags_lib.default_flags(batch_size=B, unroll_length=T, torso=torso)
-  agent = Agent(9, torso=torso, frame_shape=shape, seed=3, backend=backend,
+  agent = Agent(9, torso=torso, frame_shape=shape, seed=aseed, backend='torch',
+                compute_dtype=torch.float64).to(cuda).double()
+  batch = batch_to_device(make_synthetic_batch(B, T, shape, 9, seed=bseed), cuda)
+  batch = _map_tensors(batch, lambda t: t.double() if t.is_floating_point() else t)
+  names, params = zip(*agent.named_parameters())
+  loss = compute_loss(agent, batch, flags, use_fused=False)
+  grads = torch.autograd.grad(loss, params, allow_unused=True)
+  return float(loss), {n: (torch.zeros_like(p) if g is None else g)
+                       for n, p, g in zip(names, params, grads)}
+
+
+def _vs_oracle(res, oracle, name_filter=None):
+  """-> {param: relative L2 error of res's gradient vs the fp64 oracle}."""
+  out = {}
+  for name, _ in res['flat'].named:
+    g64 = oracle[1][name]
+    g = res['flat'].view_of(res['grads'], name).double()
+    if g64.abs().max() == 0:
+      continue
+    out[name] = ((g - g64).norm() / g64.norm()).item()
+  return out
+
+
+def _step(backend, torso, dtype, cuda, shape=(72, 96, 3), B=4, T=8, aseed=3,
+          bseed=4):
+  flags = flags_lib.default_flags(batch_size=B, unroll_length=T, torso=torso)
+  agent = Agent(9, torso=torso, frame_shape=shape, seed=aseed, backend=backend,
                 compute_dtype=dtype)
   learner = Learner(agent, flags, cuda)
-  batch = batch_to_device(make_synthetic_batch(B, T, shape, 9, seed=4), cuda)
+  batch = batch_to_device(make_synthetic_batch(B, T, shape, 9, seed=bseed), cuda)
   p0 = learner.flat.params.clone()
   loss = learner.step(batch)
   torch.cuda.synchronize()
@@ -65,18 +93,49 @@ def test_fp32_hip_learner_step_matches_torch(cuda, torso):
   assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
 
 
-def test_fp32_hip_learner_step_atari_shape(cuda):
-  """Atari-shaped 84x84x4 frames (BASELINE config #2) on the HIP learner."""
-  ref = _step('torch', 'deep', torch.float32, cuda, shape=(84, 84, 4))
-  hip = _step('hip', 'deep', torch.float32, cuda, shape=(84, 84, 4))
-  _compare(ref, hip, cos_min=0.999999, rel_max=1e-4)
+# (agent seed, batch seed) whose float64 forward has no pool near-tie /
+# ReLU near-zero (tests/_discontinuity.py): fp32 and float64 may branch
+# differently there, and one flip moves a whole local gradient
+@pytest.mark.parametrize('torso,shape,aseed,bseed', [
+    ('deep', (72, 96, 3), 7, 35), ('shallow', (72, 96, 3), 3, 2),
+    ('deep', (84, 84, 4), 3, 30), ('shallow', (84, 84, 4), 3, 0)])
+def test_fp32_hip_learner_matches_fp64(cuda, torso, shape, aseed, bseed):
+  """One fp32 HIP learner step against the float64 oracle of the same step:
+  loss and every parameter gradient to fp32 accuracy (<= 2e-5 relative L2),
+  next to the torch fp32 learner's own error for comparison."""
+  from tests import _discontinuity
+  kw = dict(shape=shape, B=2, T=3, aseed=aseed, bseed=bseed)
+  probe = Agent(9, torso=torso, frame_shape=shape, seed=aseed)
+  frames = make_synthetic_batch(2, 3, shape, 9, seed=bseed).env_outputs.observation[0]
+  assert _discontinuity.count(probe, frames.reshape((-1,) + shape)) == 0
+  oracle = _oracle64(torso, cuda, **kw)
+  ref = _step('torch', torso, torch.float32, cuda, **kw)
+  hip = _step('hip', torso, torch.float32, cuda, **kw)
+  assert abs(hip['loss'] - oracle[0]) <= 1e-5 * max(1.0, abs(oracle[0]))
+  e_hip, e_ref = _vs_oracle(hip, oracle), _vs_oracle(ref, oracle)
+  for name in e_hip:
+    print('%-40s hip %.2e  torch %.2e' % (name, e_hip[name], e_ref[name]))
+  for name in e_hip:
+    assert e_hip[name] <= 2e-5, (name, e_hip[name], e_ref[name])
 
 
-def test_bf16_hip_learner_step_tracks_torch_fp32(cuda):
-  ref = _step('torch', 'deep', torch.float32, cuda)
+def test_bf16_hip_learner_step_tracks_fp64(cuda):
+  """bf16 operands (fp32 accumulation/state): every gradient keeps cosine
+  >= 0.99 to the float64 oracle.  The heavily cancelling early-conv weight
+  gradients are the loosest (that is why the headline runs fp32)."""
+  oracle = _oracle64('deep', cuda)
   hip = _step('hip', 'deep', torch.bfloat16, cuda)
-  worst = _compare(ref, hip, cos_min=0.999, rel_max=0.05)
-  print('bf16 deep worst relative gradient error %.3g (%s)' % (worst[0], worst[1]))
+  worst = 1.0
+  for name, _ in hip['flat'].named:
+    g64 = oracle[1][name]
+    if g64.abs().max() == 0:
+      continue
+    g = hip['flat'].view_of(hip['grads'], name).double()
+    cos = torch.nn.functional.cosine_similarity(g.reshape(1, -1),
+                                                g64.reshape(1, -1)).item()
+    print('%-40s cos %.5f' % (name, cos))
+    worst = min(worst, cos)
+    assert cos >= 0.99, (name, cos)
 
 
 def test_gang_lstm_timeout_skips_update(cuda):
