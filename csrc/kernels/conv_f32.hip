@@ -112,9 +112,111 @@ __device__ __forceinline__ void stage_image(const void* __restrict__ src, int n,
 }
 
 // ------------------------------------------------------------------ forward
+// Persistent: each workgroup loads its weight slice into LDS ONCE and walks
+// tiles blockIdx.x, blockIdx.x + gridDim.x, ...; the next tile's source
+// chunks are loaded into registers (kMaxC 16-B chunks per thread, address
+// math, padding/dilation/uint8 conversion/ReLU applied on load) while the
+// current tile computes, and committed to LDS between two barriers.  Every
+// wave computes all of its groups of the tile (<= kGmax, kept in registers)
+// before the epilogue, so the epilogue's global loads (residual / mask) never
+// force the in-flight prefetch to drain early (vmcnt is in order).
+constexpr int kGmax = 4;   // 16-pixel groups per wave per tile
+constexpr int kMaxC = 8;   // staged 16-B chunks per thread per tile
+
+template <int CINP, int SRC, int MAXC = kMaxC>
+struct Stager {
+  static constexpr int CH = CINP / 4;
+  f4 v[MAXC];
+  // loads tile rows [0, rows) x [0, Wl) of the padded, D-dilated image of
+  // source image n starting at source row j0 (see stage_image)
+  __device__ __forceinline__ void load(const void* __restrict__ src, int n, int Hs, int Ws,
+                                       int Cs, int j0, int pl, int D, int Wl, int total,
+                                       bool relu) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      f4 x = {0.f, 0.f, 0.f, 0.f};
+      if (e < total) {
+        const int ch = e % CH;
+        const int pix = e / CH;
+        const int r = pix / Wl;
+        const int c = pix - r * Wl;
+        int j = j0 + r, i = c - pl;
+        bool ok = j >= 0 && i >= 0;
+        if (D > 1) {
+          ok = ok && (j % D) == 0 && (i % D) == 0;
+          j /= D;
+          i /= D;
+        }
+        ok = ok && j < Hs && i < Ws;
+        if (ok) {
+          const int64_t pixel = (static_cast<int64_t>(n) * Hs + j) * Ws + i;
+          if constexpr (SRC == kSrcU8) {
+            const uint8_t* p = static_cast<const uint8_t*>(src) + pixel * Cs;
+            x[0] = static_cast<float>(p[0]) / 255.f;
+            if (Cs > 1) x[1] = static_cast<float>(p[1]) / 255.f;
+            if (Cs > 2) x[2] = static_cast<float>(p[2]) / 255.f;
+            if (Cs > 3) x[3] = static_cast<float>(p[3]) / 255.f;
+          } else if (4 * ch < Cs) {
+            x = *reinterpret_cast<const f4*>(static_cast<const float*>(src) + pixel * Cs +
+                                             4 * ch);
+            if (relu) {
+              x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f);
+              x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
+            }
+          }
+        }
+      }
+      v[k] = x;
+    }
+  }
+  __device__ __forceinline__ void commit(float* x_s, int pitch, int total) const {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < total) {
+        const int ch = e % CH, pix = e / CH;
+        *reinterpret_cast<f4*>(x_s + pix * pitch + 4 * ch) = v[k];
+      }
+    }
+  }
+};
+
+// Register prefetch of a contiguous [P pixels][CG of Cout channels] slice of
+// dY (a tile of full rows) for the weight-gradient kernel.
+template <int CG, int MAXD>
+struct DyStager {
+  static constexpr int CH = CG / 4;
+  f4 v[MAXD];
+  __device__ __forceinline__ void load(const float* __restrict__ src, int cout, int total) {
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      f4 x = {0.f, 0.f, 0.f, 0.f};
+      if (e < total) {
+        const int ch = e % CH, p = e / CH;
+        x = *reinterpret_cast<const f4*>(src + static_cast<int64_t>(p) * cout + 4 * ch);
+      }
+      v[k] = x;
+    }
+  }
+  __device__ __forceinline__ void commit(float* d_s, int pitch, int total) const {
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+      const int e = threadIdx.x + k * kThreads;
+      if (e < total) {
+        const int ch = e % CH, p = e / CH;
+        *reinterpret_cast<f4*>(d_s + p * pitch + 4 * ch) = v[k];
+      }
+    }
+  }
+};
+constexpr int kMaxD = 4;  // staged dY chunks per thread per tile
+
 template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
-__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a, int R,
-                                                            int tiles_per_img) {
+__global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R,
+                                                               int tiles_per_img,
+                                                               int ntiles) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int PP = fwd_pitch(CINP);
   constexpr int NH = COUT_T / 16;
@@ -124,19 +226,23 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a, int R,
   static_assert(CINP == 4 || CINP == 8 || CINP % 16 == 0, "CINP");
   const int Wl = (a.Wo - 1) * S + K;
   const int rows = (R - 1) * S + K;
-  float* w_s = smem;                      // [KK][COUT_T][PP]
-  float* x_s = smem + KK * COUT_T * PP;   // [rows][Wl][PP]
-  const int n = blockIdx.x / tiles_per_img;
-  const int oy0 = (blockIdx.x - n * tiles_per_img) * R;
+  const int total = rows * Wl * (CINP / 4);
+  // weights as MFMA A fragments: [tap][b][g][co][VPL] (16-B lane reads,
+  // consecutive lanes consecutive: conflict-free without padding)
+  float* w_s = smem;
+  float* x_s = smem + KK * CINP * COUT_T;  // [rows][Wl][PP]
   const int co0 = blockIdx.y * COUT_T;
+  auto wput = [&](int tap, int o, int i, float v) {
+    const int b = i / 16, rem = i - 16 * (i / 16);
+    const int g = rem / VPL, v_ = rem - (rem / VPL) * VPL;
+    w_s[(((tap * NB + b) * 4 + g) * COUT_T + o) * VPL + v_] = v;
+  };
   if (!FLIP) {
-    // W[tap][i][o] (o fastest: coalesced) -> w_s[tap][o][i]
     for (int e = threadIdx.x; e < KK * COUT_T * CINP; e += kThreads) {
       const int o = e % COUT_T, i = (e / COUT_T) % CINP, tap = e / (COUT_T * CINP);
       float v = 0.f;
-      if (i < a.wcin)
-        v = a.w[(static_cast<int64_t>(tap) * a.wcin + i) * a.wcout + co0 + o];
-      w_s[(tap * COUT_T + o) * PP + i] = v;
+      if (i < a.wcin) v = a.w[(static_cast<int64_t>(tap) * a.wcin + i) * a.wcout + co0 + o];
+      wput(tap, o, i, v);
     }
   } else {
     // w_s[tap][o][i] = W[KK-1-tap][o][i]: o = input channel of the forward
@@ -146,69 +252,96 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a, int R,
       float v = 0.f;
       if (i < a.wcout)
         v = a.w[(static_cast<int64_t>(KK - 1 - tap) * a.wcin + co0 + o) * a.wcout + i];
-      w_s[(tap * COUT_T + o) * PP + i] = v;
+      wput(tap, o, i, v);
     }
   }
-  stage_image<CINP, SRC>(a.src, n, a.Hs, a.Ws, a.Cs, oy0 * S - a.pt, a.pl, a.D, rows,
-                         Wl, PP, a.relu_in != 0, x_s);
-  __syncthreads();
-
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int Rv = min(R, a.Ho - oy0);
-  const int P = Rv * a.Wo;
-  const int ngroups = (P + 15) >> 4;
   float bias[NH][4];
 #pragma unroll
   for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       bias[h][r] = a.bias != nullptr ? a.bias[co0 + 16 * h + 4 * g + r] : 0.f;
-  const float* wl = w_s + c16 * PP + VPL * g;
+  const float* wl = w_s + (g * COUT_T + c16) * VPL;
 
-  auto run = [&](auto NGc, int grp0) {
-    constexpr int NG = decltype(NGc)::value;
-    f4 acc[NG][NH];
-    int xb[NG], q[NG];
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  Stager<CINP, SRC> st;
+  auto prefetch = [&](int t) {
+    const int n = t / tiles_per_img;
+    const int oy0 = (t - n * tiles_per_img) * R;
+    st.load(a.src, n, a.Hs, a.Ws, a.Cs, oy0 * S - a.pt, a.pl, a.D, Wl, total,
+            a.relu_in != 0);
+  };
+  prefetch(tile);
+  for (;;) {
+    __syncthreads();  // the previous tile's LDS reads are done
+    st.commit(x_s, PP, total);
+    __syncthreads();
+    const int cur = tile;
+    tile += gridDim.x;
+    if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
+    const int n = cur / tiles_per_img;
+    const int oy0 = (cur - n * tiles_per_img) * R;
+    const int P = min(R, a.Ho - oy0) * a.Wo;
+    const int ngroups = (P + 15) >> 4;
+    f4 acc[kGmax][NH];
+    // groups wave + 4 i, two at a time (independent MFMA chains)
+    auto mma = [&](auto NGc, int i0) {
+      constexpr int NG = decltype(NGc)::value;
+      int xb[NG];
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi) {
-      const int p = (grp0 + 4 * gi) * 16 + c16;
-      q[gi] = p < P ? p : -1;
-      const int pp = p < P ? p : 0;
-      const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
-      xb[gi] = (oy * S * Wl + ox * S) * PP + VPL * g;
+      for (int gi = 0; gi < NG; ++gi) {
+        const int p = (wave + 4 * (i0 + gi)) * 16 + c16;
+        const int pp = p < P ? p : 0;
+        const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
+        xb[gi] = (oy * S * Wl + ox * S) * PP + VPL * g;
 #pragma unroll
-      for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int tap = 0; tap < KK; ++tap) {
-      const int ky = tap / K, kx = tap - (tap / K) * K;
-      const int toff = (ky * Wl + kx) * PP;
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        float av[NH][VPL], bv[NG][VPL];
-#pragma unroll
-        for (int h = 0; h < NH; ++h) lds_get<VPL>(wl + (tap * COUT_T + 16 * h) * PP + 16 * b, av[h]);
-#pragma unroll
-        for (int gi = 0; gi < NG; ++gi) lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[gi]);
-#pragma unroll
-        for (int v = 0; v < VPL; ++v)
-#pragma unroll
-          for (int gi = 0; gi < NG; ++gi)
-#pragma unroll
-            for (int h = 0; h < NH; ++h) acc[gi][h] = mfma4(av[h][v], bv[gi][v], acc[gi][h]);
+        for (int h = 0; h < NH; ++h) acc[i0 + gi][h] = f4{0.f, 0.f, 0.f, 0.f};
       }
-    }
 #pragma unroll
-    for (int gi = 0; gi < NG; ++gi) {
-      if (q[gi] < 0) continue;
-      const int oy = q[gi] / a.Wo, ox = q[gi] - (q[gi] / a.Wo) * a.Wo;
+      for (int tap = 0; tap < KK; ++tap) {
+        const int ky = tap / K, kx = tap - (tap / K) * K;
+        const int toff = (ky * Wl + kx) * PP;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          float av[NH][VPL], bv[NG][VPL];
+#pragma unroll
+          for (int h = 0; h < NH; ++h)
+            lds_get<VPL>(wl + (((tap * NB + b) * 4) * COUT_T + 16 * h) * VPL, av[h]);
+#pragma unroll
+          for (int gi = 0; gi < NG; ++gi) lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[gi]);
+#pragma unroll
+          for (int v = 0; v < VPL; ++v)
+#pragma unroll
+            for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+              for (int h = 0; h < NH; ++h)
+                acc[i0 + gi][h] = mfma4(av[h][v], bv[gi][v], acc[i0 + gi][h]);
+        }
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < kGmax; i += 2) {
+      if (wave + 4 * i >= ngroups) break;
+      if (wave + 4 * (i + 1) < ngroups)
+        mma(std::integral_constant<int, 2>{}, i);
+      else
+        mma(std::integral_constant<int, 1>{}, i);
+    }
+    // epilogue (after all MFMAs of the tile)
+#pragma unroll
+    for (int i = 0; i < kGmax; ++i) {
+      const int p = (wave + 4 * i) * 16 + c16;
+      if (p >= P) continue;
+      const int oy = p / a.Wo, ox = p - (p / a.Wo) * a.Wo;
       const int64_t pix = (static_cast<int64_t>(n) * a.Ho + oy0 + oy) * a.Wo + ox;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int64_t o = pix * a.Cout + co0 + 16 * h + 4 * g;
-        f4 v = acc[gi][h];
+        f4 v = acc[i][h];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bias[h][r];
         if (a.mask != nullptr) {
@@ -228,12 +361,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a, int R,
         *reinterpret_cast<f4*>(a.out + o) = v;
       }
     }
-  };
-  // wave w owns groups w, w+4, w+8, ...; two per pass (independent MFMA
-  // chains), a single one for an odd remainder
-  int grp = wave;
-  for (; grp + 4 < ngroups; grp += 8) run(std::integral_constant<int, 2>{}, grp);
-  if (grp < ngroups) run(std::integral_constant<int, 1>{}, grp);
+    if (tile >= ntiles) break;
+  }
 }
 
 // ------------------------------------------------------------ weight grads
@@ -285,25 +414,31 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
 #pragma unroll
     for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // persistent walk with the next tile's x / dY chunks prefetched into
+  // registers while the current one computes
+  Stager<CINP, SRC> sx;
+  DyStager<CG, kMaxD> sd;
+  const int xtotal = rows * Wl * (CINP / 4);
+  auto prefetch = [&](int t) {
+    const int n = t / tiles_per_img;
+    const int oy0 = (t - n * tiles_per_img) * R;
+    sx.load(a.src, n, a.H, a.W, a.Cin, oy0 * S - a.pt, a.pl, 1, Wl, xtotal, a.relu_in != 0);
+    sd.load(a.dy + (static_cast<int64_t>(n) * a.Ho + oy0) * a.Wo * a.Cout + co0, a.Cout,
+            min(R, a.Ho - oy0) * a.Wo * (CG / 4));
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) prefetch(tile);
+  while (tile < ntiles) {
     const int n = tile / tiles_per_img;
     const int oy0 = (tile - n * tiles_per_img) * R;
     const int Rv = min(R, a.Ho - oy0);
     const int P = Rv * a.Wo;
     __syncthreads();  // the previous tile's reads are done
-    stage_image<CINP, SRC>(a.src, n, a.H, a.W, a.Cin, oy0 * S - a.pt, a.pl, 1, rows, Wl,
-                           XP, a.relu_in != 0, x_s);
-    {
-      constexpr int CH = CG / 4;
-      const float* dsrc =
-          a.dy + (static_cast<int64_t>(n) * a.Ho + oy0) * a.Wo * a.Cout + co0;
-      for (int e = threadIdx.x; e < P * CH; e += kThreads) {
-        const int ch = e % CH, p = e / CH;
-        *reinterpret_cast<f4*>(d_s + p * DP + 4 * ch) =
-            *reinterpret_cast<const f4*>(dsrc + static_cast<int64_t>(p) * a.Cout + 4 * ch);
-      }
-    }
+    sx.commit(x_s, XP, xtotal);
+    sd.commit(d_s, DP, P * (CG / 4));
     __syncthreads();
+    tile += gridDim.x;
+    if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
     const int nq = (P + 3) >> 2;
     for (int qd = pg; qd < nq; qd += PG) {
       const int p = 4 * qd + g;
@@ -494,26 +629,48 @@ template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
 bool run_conv(const ConvArgs& a, hipStream_t s) {
   constexpr int PP = fwd_pitch(CINP);
   const int Wl = (a.Wo - 1) * S + K;
-  const size_t wbytes = static_cast<size_t>(4) * K * K * COUT_T * PP;
+  const size_t wbytes = static_cast<size_t>(4) * K * K * COUT_T * CINP;
   auto bytes = [&](int R) {
     return wbytes + static_cast<size_t>(4) * ((R - 1) * S + K) * Wl * PP;
   };
   const size_t budget = bytes(1) <= kLdsSoft ? kLdsSoft : kLdsHard;
-  int Rmax = a.Ho;
-  while (Rmax > 1 && bytes(Rmax) > budget) --Rmax;
-  if (bytes(Rmax) > kLdsHard) return false;
-  const int nt = (a.Ho + Rmax - 1) / Rmax;
-  const int R = (a.Ho + nt - 1) / nt;
+  // tile height: fits LDS, the per-thread staging registers and kGmax groups
+  // per wave; among those the one with the least busiest-wave work summed
+  // over all tiles (+ a per-tile staging overhead)
+  int best = 0;
+  double best_cost = 1e30;
+  for (int R = 1; R <= a.Ho; ++R) {
+    const int rows = (R - 1) * S + K;
+    if (bytes(R) > budget || rows * Wl * (CINP / 4) > kMaxC * kThreads ||
+        (R * a.Wo + 15) / 16 > 4 * kGmax)
+      break;
+    const int nt = (a.Ho + R - 1) / R;
+    double cost = 0;
+    for (int t = 0; t < nt; ++t) {
+      const int rv = std::min(R, a.Ho - t * R);
+      cost += ((rv * a.Wo + 15) / 16 + 3) / 4 + 0.4;
+    }
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = R;
+    }
+  }
+  if (best == 0) return false;
+  const int R = best;
+  const int nt = (a.Ho + R - 1) / R;
+  const int ntiles = a.N * nt;
+  const int gy = a.Cout / COUT_T;
+  const int per_cu = bytes(R) <= kLdsSoft ? 2 : 1;
+  const int G = std::max(1, std::min(ntiles, 256 * per_cu / gy));
   auto kern = conv_fwd_kernel<CINP, COUT_T, K, S, SRC, FLIP>;
   allow_lds(kern, bytes(R));
-  hipLaunchKernelGGL(kern, dim3(a.N * nt, a.Cout / COUT_T), dim3(kThreads), bytes(R), s, a,
-                     R, nt);
+  hipLaunchKernelGGL(kern, dim3(G, gy), dim3(kThreads), bytes(R), s, a, R, nt, ntiles);
   return true;
 }
 
 // output-channel tile: 32 when the weight slice stays small, else 16
 int cout_tile(int cinp, int cout, int K) {
-  if (cout % 32 == 0 && 4ll * K * K * 32 * fwd_pitch(cinp) <= 48 * 1024) return 32;
+  if (cout % 32 == 0 && 4ll * K * K * 32 * cinp <= 48 * 1024) return 32;
   return 16;
 }
 
@@ -531,9 +688,15 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
     return std::max(red, static_cast<size_t>(4) * (((R - 1) * S + K) * Wl * XP + R * a.Wo * DP));
   };
   const size_t budget = bytes(1) <= kLdsSoft ? kLdsSoft : kLdsHard;
-  int Rmax = a.Ho;
-  while (Rmax > 1 && bytes(Rmax) > budget) --Rmax;
-  if (bytes(Rmax) > kLdsHard) return false;
+  // tallest tile that fits LDS and the per-thread prefetch registers
+  int Rmax = 0;
+  for (int R = 1; R <= a.Ho; ++R) {
+    if (bytes(R) > budget || ((R - 1) * S + K) * Wl * (CINP / 4) > kMaxC * kThreads ||
+        R * a.Wo * (CG / 4) > kMaxD * kThreads)
+      break;
+    Rmax = R;
+  }
+  if (Rmax == 0) return false;
   const int nt = (a.Ho + Rmax - 1) / Rmax;
   const int R = (a.Ho + nt - 1) / nt;
   const int ntiles = a.N * nt;

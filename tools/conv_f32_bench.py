@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Per-layer timing of the exact-fp32 conv kernels at learner-batch size.
+
+Deep-ResNet layers at N = (T+1) * B = 3232 frames (72x96x3 input): forward,
+data gradient and weight gradient of every distinct layer shape, with the
+achieved TFLOP/s against the 157 TF fp32 MFMA peak.  Usage:
+  python tools/conv_f32_bench.py [N] [reps]
+"""
+import sys
+import torch
+
+sys.path.insert(0, '.')
+from scalable_agent_amd import ops  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 3232
+REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+C = ops.ext()
+dev = torch.device('cuda')
+# name, H, W, Cin, Cout, K, S, pt, pl, uint8 source, relu_in, resid
+LAYERS = [
+    ('deep conv1 3->16 72x96', 72, 96, 3, 16, 3, 1, 1, 1, True),
+    ('deep res16 36x48', 36, 48, 16, 16, 3, 1, 1, 1, False),
+    ('deep conv2 16->32 36x48', 36, 48, 16, 32, 3, 1, 1, 1, False),
+    ('deep res32 18x24', 18, 24, 32, 32, 3, 1, 1, 1, False),
+    ('deep res32 9x12', 9, 12, 32, 32, 3, 1, 1, 1, False),
+    ('shallow1 8x8/4', 72, 96, 3, 32, 8, 4, 2, 2, True),
+    ('shallow2 4x4/2', 18, 24, 32, 64, 4, 2, 1, 1, False),
+    ('shallow3 3x3/2', 9, 12, 64, 128, 3, 2, 1, 0, False),
+]
+
+
+def timeit(fn):
+  fn()
+  torch.cuda.synchronize()
+  s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+  s.record()
+  for _ in range(REPS):
+    fn()
+  e.record()
+  torch.cuda.synchronize()
+  return s.elapsed_time(e) / REPS * 1e3
+
+
+for name, H, W, Ci, Co, K, S, pt, pl, u8 in LAYERS:
+  Ho, Wo = -(-H // S), -(-W // S)
+  x = (torch.randint(0, 256, (N, H, W, Ci), dtype=torch.uint8, device=dev) if u8
+       else torch.randn(N, H, W, Ci, device=dev))
+  w = torch.randn(K, K, Ci, Co, device=dev) * 0.1
+  b = torch.randn(Co, device=dev)
+  dy = torch.randn(N, Ho, Wo, Co, device=dev)
+  dw = torch.zeros_like(w)
+  db = torch.zeros_like(b)
+  flop = 2.0 * N * Ho * Wo * K * K * Ci * Co
+  tf = timeit(lambda: C.cf32_conv_fwd(x, w, b, S, pt, pl, Ho, Wo))
+  tw = timeit(lambda: C.cf32_conv_wgrad(x, dy, S, pt, pl, False, dw, db))
+  line = '%-26s fwd %8.1f us %6.1f TF | wgrad %8.1f us %6.1f TF' % (
+      name, tf, flop / tf / 1e6, tw, flop / tw / 1e6)
+  if not u8:
+    td = timeit(lambda: C.cf32_conv_dgrad(dy, w, S, pt, pl, H, W))
+    line += ' | dgrad %8.1f us %6.1f TF' % (td, flop / td / 1e6)
+  print(line, flush=True)
+xp = torch.randn(N, 72, 96, 16, device=dev)
+tp = timeit(lambda: C.cf32_maxpool_fwd(xp, 0, 0))
+y, arg = C.cf32_maxpool_fwd(xp, 0, 0)
+tb = timeit(lambda: C.cf32_maxpool_bwd(y, arg, 72, 96, 0, 0))
+print('maxpool 72x96x16 fwd %.1f us bwd %.1f us' % (tp, tb))
