@@ -79,9 +79,23 @@ at::Tensor conv_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, int
 // dx [N,H,W,Cin] of y = conv(x, w, stride, pads): correlation of the
 // stride-dilated dy with the flipped, transposed weights; then
 // [* (mask > 0)] [+ add].
+sa::cf32::PoolGeom pool_geom(const c10::optional<at::Tensor>& arg, const at::Tensor& dP,
+                             int64_t Hc, int64_t Wc, int64_t pbh, int64_t pbw) {
+  sa::cf32::PoolGeom pg{};
+  if (!arg.has_value() || !arg->defined()) return pg;
+  TORCH_CHECK(arg->sizes() == dP.sizes() && arg->scalar_type() == at::kByte &&
+                  arg->is_contiguous(), "pool argmax must be uint8 shaped like dP");
+  TORCH_CHECK(dP.size(1) == (Hc + 1) / 2 && dP.size(2) == (Wc + 1) / 2 && dP.size(3) % 4 == 0,
+              "dP must be the 3x3/2 pool of a ", Hc, "x", Wc, " map");
+  pg.arg = arg->data_ptr<uint8_t>();
+  pg.Hp = dP.size(1); pg.Wp = dP.size(2); pg.pbh = pbh; pg.pbw = pbw;
+  return pg;
+}
+
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, int64_t pl,
                       int64_t H, int64_t W, c10::optional<at::Tensor> mask,
-                      c10::optional<at::Tensor> add) {
+                      c10::optional<at::Tensor> add, c10::optional<at::Tensor> pool_arg,
+                      int64_t pool_pbh, int64_t pool_pbw) {
   check_nhwc(dy, "dy");
   check_w(w);
   TORCH_CHECK(dy.scalar_type() == at::kFloat, "dy must be float32");
@@ -89,17 +103,24 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
   const int64_t K = w.size(0), Cin = w.size(2);
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, Cin}, dy.options());
+  // dy is the conv output's gradient, or (pool_arg) the gradient of its
+  // 3x3/2 max-pool, gathered on load
+  const int64_t Hc = (H + stride - 1) / stride, Wc = (W + stride - 1) / stride;
+  const auto pg = pool_geom(pool_arg, dy, Hc, Wc, pool_pbh, pool_pbw);
   sa::cf32::ConvArgs a{};
+  a.pool = pg;
   a.src = dy.data_ptr();
   a.w = w.data_ptr<float>();
   a.mask = opt_f32(mask, dx, "mask");
   a.add = opt_f32(add, dx, "add");
   a.out = dx.data_ptr<float>();
-  a.N = dy.size(0); a.Hs = dy.size(1); a.Ws = dy.size(2); a.Cs = dy.size(3);
+  a.N = dy.size(0); a.Hs = pg.arg ? Hc : dy.size(1); a.Ws = pg.arg ? Wc : dy.size(2);
+  a.Cs = dy.size(3);
   a.Ho = H; a.Wo = W; a.Cout = Cin;
   a.pt = K - 1 - pt; a.pl = K - 1 - pl; a.D = stride;
   a.wcin = Cin; a.wcout = w.size(3);
-  TORCH_CHECK(sa::cf32::conv_launch(a, K, 1, sa::cf32::kSrcF32, true, stream()),
+  const int kind = pg.arg ? sa::cf32::kSrcPoolGrad : sa::cf32::kSrcF32;
+  TORCH_CHECK(sa::cf32::conv_launch(a, K, 1, kind, true, stream()),
               "conv_f32 dgrad: no kernel instance for K=", K, " dy channels=", dy.size(3),
               " dx channels=", Cin);
   check_launch("cf32_conv_dgrad");
@@ -109,7 +130,8 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
 // dw += sum x^T dy (HWIO), db += sum dy; x: the layer input (uint8 frames
 // or float32, optionally ReLU'd on load).  Deterministic (no atomics).
 void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t pl,
-                bool relu_in, at::Tensor dw, c10::optional<at::Tensor> db) {
+                bool relu_in, at::Tensor dw, c10::optional<at::Tensor> db,
+                c10::optional<at::Tensor> pool_arg, int64_t pool_pbh, int64_t pool_pbw) {
   check_nhwc(x, "x");
   check_nhwc(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == at::kFloat, "dy must be float32");
@@ -131,11 +153,44 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
   }
   a.N = x.size(0); a.H = x.size(1); a.W = x.size(2); a.Cin = x.size(3);
   a.Ho = dy.size(1); a.Wo = dy.size(2); a.Cout = dy.size(3);
+  if (pool_arg.has_value() && pool_arg->defined()) {
+    // dy is the gradient of the conv output's 3x3/2 max-pool
+    a.Ho = (x.size(1) + stride - 1) / stride;
+    a.Wo = (x.size(2) + stride - 1) / stride;
+    a.pool = pool_geom(pool_arg, dy, a.Ho, a.Wo, pool_pbh, pool_pbw);
+  }
   a.pt = pt; a.pl = pl; a.relu_in = relu_in;
   TORCH_CHECK(sa::cf32::wgrad_launch(a, K, stride, kind, ws.data_ptr<float>(), stream()),
               "conv_f32 wgrad: no kernel instance for K=", K, " stride=", stride, " Cin=",
               x.size(3), " Cout=", dy.size(3));
   check_launch("cf32_conv_wgrad");
+}
+
+// Fused stage head: maxpool3x3/2(conv3x3/1(x) + b) -> {pooled, argmax}
+std::vector<at::Tensor> conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b, int64_t pbh,
+                                      int64_t pbw) {
+  check_nhwc(x, "x");
+  check_w(w);
+  const int kind = src_kind(x);
+  TORCH_CHECK(w.size(0) == 3 && w.size(2) == x.size(3), "conv_pool_fwd: 3x3 weights");
+  TORCH_CHECK(b.numel() == w.size(3) && b.scalar_type() == at::kFloat && b.is_contiguous(), "bias");
+  const c10::DeviceGuard g(x.device());
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), Cout = w.size(3);
+  auto y = at::empty({N, (H + 1) / 2, (W + 1) / 2, Cout}, x.options().dtype(at::kFloat));
+  auto arg = at::empty(y.sizes(), x.options().dtype(at::kByte));
+  sa::cf32::ConvArgs a{};
+  a.src = x.data_ptr();
+  a.w = w.data_ptr<float>();
+  a.bias = b.data_ptr<float>();
+  a.N = N; a.Hs = H; a.Ws = W; a.Cs = x.size(3);
+  a.Ho = H; a.Wo = W; a.Cout = Cout;
+  a.pt = 1; a.pl = 1; a.D = 1;
+  a.wcin = w.size(2); a.wcout = Cout;
+  TORCH_CHECK(sa::cf32::conv_pool_fwd_launch(a, kind, pbh, pbw, y.data_ptr<float>(),
+                                             arg.data_ptr<uint8_t>(), stream()),
+              "conv_pool_fwd: no kernel instance for Cin=", x.size(3), " Cout=", Cout);
+  check_launch("cf32_conv_pool_fwd");
+  return {y, arg};
 }
 
 std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t pb_h, int64_t pb_w) {
@@ -168,6 +223,18 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int6
   return dx;
 }
 
+at::Tensor frames_f32(at::Tensor x) {
+  check_nhwc(x, "frames");
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.size(3) >= 1 && x.size(3) <= 4,
+              "frames must be uint8 NHWC with 1..4 channels");
+  const c10::DeviceGuard g(x.device());
+  auto y = at::empty({x.size(0), x.size(1), x.size(2), 4}, x.options().dtype(at::kFloat));
+  sa::cf32::frames_f32_launch(x.data_ptr<uint8_t>(), y.data_ptr<float>(),
+                              x.size(0) * x.size(1) * x.size(2), x.size(3), stream());
+  check_launch("cf32_frames_f32");
+  return y;
+}
+
 void relu_mask_(at::Tensor dy, at::Tensor ref) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.scalar_type() == at::kFloat, "dy");
   TORCH_CHECK(ref.is_contiguous() && ref.scalar_type() == at::kFloat &&
@@ -184,10 +251,14 @@ void register_conv_f32_ops(pybind11::module& m) {
         arg("pl"), arg("Ho"), arg("Wo"), arg("relu_in") = false, arg("add") = pybind11::none(),
         arg("relu_out") = false);
   m.def("cf32_conv_dgrad", &conv_dgrad, arg("dy"), arg("w"), arg("stride"), arg("pt"), arg("pl"),
-        arg("H"), arg("W"), arg("mask") = pybind11::none(), arg("add") = pybind11::none());
+        arg("H"), arg("W"), arg("mask") = pybind11::none(), arg("add") = pybind11::none(),
+        arg("pool_arg") = pybind11::none(), arg("pool_pbh") = 0, arg("pool_pbw") = 0);
   m.def("cf32_conv_wgrad", &conv_wgrad, arg("x"), arg("dy"), arg("stride"), arg("pt"), arg("pl"),
-        arg("relu_in"), arg("dw"), arg("db") = pybind11::none());
+        arg("relu_in"), arg("dw"), arg("db") = pybind11::none(),
+        arg("pool_arg") = pybind11::none(), arg("pool_pbh") = 0, arg("pool_pbw") = 0);
+  m.def("cf32_conv_pool_fwd", &conv_pool_fwd);
   m.def("cf32_maxpool_fwd", &maxpool_fwd);
   m.def("cf32_maxpool_bwd", &maxpool_bwd);
   m.def("cf32_relu_mask_", &relu_mask_);
+  m.def("cf32_frames_f32", &frames_f32);
 }

@@ -17,7 +17,18 @@
 namespace sa {
 namespace cf32 {
 
-enum SrcKind { kSrcF32 = 0, kSrcU8 = 1 };
+// kSrcPoolGrad: the source is the gradient of a 3x3/2 SAME max-pool's
+// OUTPUT (dP [N, Hp, Wp, C] + its argmax codes); the kernel gathers the
+// pre-pool gradient on load (sum of dP over the windows whose argmax is the
+// position, windows in ascending order: bitwise the maxpool_bwd result), so
+// the pre-pool gradient is never materialised.
+enum SrcKind { kSrcF32 = 0, kSrcU8 = 1, kSrcPoolGrad = 2 };
+
+// Max-pool geometry for the gather (pre-pool dims come from the caller).
+struct PoolGeom {
+  const uint8_t* arg;  // [N, Hp, Wp, C] first-max tap codes dy*3+dx
+  int Hp, Wp, pbh, pbw;
+};
 
 // Forward conv / data gradient.  The kernel computes
 //   out[n, oy, ox, co] = sum_{ky,kx,i} L[n, oy*S + ky, ox*S + kx, i] * Wk[ky,kx,i,co]
@@ -39,6 +50,7 @@ struct ConvArgs {
   int pt, pl, D;       // image placement of the source
   int wcin, wcout;
   int relu_in, relu_out;
+  PoolGeom pool;       // src_kind == kSrcPoolGrad: src is dP, (Hs, Ws) pre-pool
 };
 
 // Weight gradient of the FORWARD conv (stride S, pads pt/pl):
@@ -54,6 +66,7 @@ struct WgradArgs {
   int Ho, Wo, Cout;
   int pt, pl;
   int relu_in;
+  PoolGeom pool;       // pool.arg != null: dy is dP, (Ho, Wo) pre-pool dims
 };
 
 // Returns false (and launches nothing) when no instance matches the shape;
@@ -67,6 +80,11 @@ int64_t wgrad_workspace_floats(int K, int Cin, int Cout);
 bool wgrad_launch(const WgradArgs& a, int K, int S, int src_kind, float* ws,
                   hipStream_t s);
 
+// Fused conv3x3/1 (SAME) + bias + 3x3/2 SAME max-pool: y [N, Hp, Wp, Cout]
+// and argmax codes; the pre-pool conv output only ever lives in LDS.
+bool conv_pool_fwd_launch(const ConvArgs& a, int src_kind, int pbh, int pbw,
+                          float* pooled, uint8_t* arg, hipStream_t s);
+
 // 3x3/2 max-pool, TF SAME (pads pb_h/pb_w before, -inf padding):
 // y [N, Hp, Wp, C] and the first maximal tap dy*3+dx per element.
 void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H,
@@ -76,6 +94,8 @@ void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H,
 void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N,
                         int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w,
                         hipStream_t s);
+// uint8 frames [P pixels][Cs <= 4] -> fp32 [P][4] (x / 255, zero-padded)
+void frames_f32_launch(const uint8_t* x, float* y, int64_t P, int Cs, hipStream_t s);
 // dy *= (ref > 0), fp32, n % 4 == 0
 void relu_mask_launch(float* dy, const float* ref, int64_t n, hipStream_t s);
 

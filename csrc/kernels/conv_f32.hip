@@ -123,6 +123,36 @@ __device__ __forceinline__ void stage_image(const void* __restrict__ src, int n,
 constexpr int kGmax = 4;   // 16-pixel groups per wave per tile
 constexpr int kMaxC = 8;   // staged 16-B chunks per thread per tile
 
+// Pre-pool gradient at (n, y, x), channels 4ch..4ch+3, gathered from the
+// pooled gradient dP [N, Hp, Wp, C] through the argmax codes: windows in
+// ascending (py, px) order, as maxpool_bwd_kernel (bitwise the same sums).
+__device__ __forceinline__ f4 pool_grad_gather(const float* __restrict__ dP,
+                                               const PoolGeom& pg, int n, int y, int x,
+                                               int C, int ch) {
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int py_hi = (y + pg.pbh) >> 1, px_hi = (x + pg.pbw) >> 1;
+#pragma unroll
+  for (int a = 1; a >= 0; --a) {
+    const int py = py_hi - a;
+    const int oy = y - (2 * py - pg.pbh);
+    if (py < 0 || py >= pg.Hp || oy > 2) continue;
+#pragma unroll
+    for (int b = 1; b >= 0; --b) {
+      const int px = px_hi - b;
+      const int ox = x - (2 * px - pg.pbw);
+      if (px < 0 || px >= pg.Wp || ox > 2) continue;
+      const int64_t o = ((static_cast<int64_t>(n) * pg.Hp + py) * pg.Wp + px) * C + 4 * ch;
+      const uint32_t codes = *reinterpret_cast<const uint32_t*>(pg.arg + o);
+      const f4 gv = *reinterpret_cast<const f4*>(dP + o);
+      const uint32_t want = static_cast<uint32_t>(oy * 3 + ox);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (((codes >> (8 * r)) & 0xFFu) == want) acc[r] += gv[r];
+    }
+  }
+  return acc;
+}
+
 template <int CINP, int SRC, int MAXC = kMaxC>
 struct Stager {
   static constexpr int CH = CINP / 4;
@@ -131,7 +161,7 @@ struct Stager {
   // source image n starting at source row j0 (see stage_image)
   __device__ __forceinline__ void load(const void* __restrict__ src, int n, int Hs, int Ws,
                                        int Cs, int j0, int pl, int D, int Wl, int total,
-                                       bool relu) {
+                                       bool relu, const PoolGeom& pg) {
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
       const int e = threadIdx.x + k * kThreads;
@@ -157,6 +187,8 @@ struct Stager {
             if (Cs > 1) x[1] = static_cast<float>(p[1]) / 255.f;
             if (Cs > 2) x[2] = static_cast<float>(p[2]) / 255.f;
             if (Cs > 3) x[3] = static_cast<float>(p[3]) / 255.f;
+          } else if constexpr (SRC == kSrcPoolGrad) {
+            if (4 * ch < Cs) x = pool_grad_gather(static_cast<const float*>(src), pg, n, j, i, Cs, ch);
           } else if (4 * ch < Cs) {
             x = *reinterpret_cast<const f4*>(static_cast<const float*>(src) + pixel * Cs +
                                              4 * ch);
@@ -184,18 +216,28 @@ struct Stager {
 
 // Register prefetch of a contiguous [P pixels][CG of Cout channels] slice of
 // dY (a tile of full rows) for the weight-gradient kernel.
-template <int CG, int MAXD>
+template <int CG, int MAXD, bool GATHER>
 struct DyStager {
   static constexpr int CH = CG / 4;
   f4 v[MAXD];
-  __device__ __forceinline__ void load(const float* __restrict__ src, int cout, int total) {
+  // rows [oy0, oy0 + total / (Wo * CH)) of image n, channels co0 .. co0+CG;
+  // GATHER: dy is the pooled gradient dP (see pool_grad_gather)
+  __device__ __forceinline__ void load(const float* __restrict__ dy, int n, int oy0, int Ho,
+                                       int Wo, int cout, int co0, int total,
+                                       const PoolGeom& pg) {
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
       const int e = threadIdx.x + k * kThreads;
       f4 x = {0.f, 0.f, 0.f, 0.f};
       if (e < total) {
         const int ch = e % CH, p = e / CH;
-        x = *reinterpret_cast<const f4*>(src + static_cast<int64_t>(p) * cout + 4 * ch);
+        if constexpr (GATHER) {
+          const int y = oy0 + p / Wo, xx = p - (p / Wo) * Wo;
+          x = pool_grad_gather(dy, pg, n, y, xx, cout, co0 / 4 + ch);
+        } else {
+          x = *reinterpret_cast<const f4*>(
+              dy + ((static_cast<int64_t>(n) * Ho + oy0) * Wo + p) * cout + co0 + 4 * ch);
+        }
       }
       v[k] = x;
     }
@@ -273,7 +315,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
     const int n = t / tiles_per_img;
     const int oy0 = (t - n * tiles_per_img) * R;
     st.load(a.src, n, a.Hs, a.Ws, a.Cs, oy0 * S - a.pt, a.pl, a.D, Wl, total,
-            a.relu_in != 0);
+            a.relu_in != 0, a.pool);
   };
   prefetch(tile);
   for (;;) {
@@ -301,26 +343,34 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[i0 + gi][h] = f4{0.f, 0.f, 0.f, 0.f};
       }
-#pragma unroll
-      for (int tap = 0; tap < KK; ++tap) {
+      // software-pipelined over the KK * NB (tap, channel-block) steps: the
+      // next step's operand reads are issued ahead of this step's MFMAs
+      constexpr int STEPS = KK * NB;
+      float av[2][NH][VPL], bv[2][NG][VPL];
+      auto load_step = [&](int st, int buf) {
+        const int tap = st / NB, b = st - (st / NB) * NB;
         const int ky = tap / K, kx = tap - (tap / K) * K;
         const int toff = (ky * Wl + kx) * PP;
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          float av[NH][VPL], bv[NG][VPL];
+        for (int h = 0; h < NH; ++h)
+          lds_get<VPL>(wl + (((tap * NB + b) * 4) * COUT_T + 16 * h) * VPL, av[buf][h]);
 #pragma unroll
-          for (int h = 0; h < NH; ++h)
-            lds_get<VPL>(wl + (((tap * NB + b) * 4) * COUT_T + 16 * h) * VPL, av[h]);
+        for (int gi = 0; gi < NG; ++gi)
+          lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[buf][gi]);
+      };
+      load_step(0, 0);
 #pragma unroll
-          for (int gi = 0; gi < NG; ++gi) lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[gi]);
+      for (int st = 0; st < STEPS; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < STEPS) load_step(st + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int v = 0; v < VPL; ++v)
+        for (int v = 0; v < VPL; ++v)
 #pragma unroll
-            for (int gi = 0; gi < NG; ++gi)
+          for (int gi = 0; gi < NG; ++gi)
 #pragma unroll
-              for (int h = 0; h < NH; ++h)
-                acc[i0 + gi][h] = mfma4(av[h][v], bv[gi][v], acc[i0 + gi][h]);
-        }
+            for (int h = 0; h < NH; ++h)
+              acc[i0 + gi][h] = mfma4(av[cur][h][v], bv[cur][gi][v], acc[i0 + gi][h]);
       }
     };
 #pragma unroll
@@ -365,8 +415,166 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
   }
 }
 
+// ------------------------------------------------------- fused conv + pool
+// Stage head of the deep torso: conv3x3/1 SAME + bias, then the 3x3/2 SAME
+// max-pool, in one persistent kernel.  A tile is R pooled rows of one image:
+// its 2R+1 conv rows are computed into LDS (one row recomputed per tile
+// boundary) and pooled from there, so the pre-pool map (4x the pooled size)
+// never touches HBM.  Argmax codes as maxpool_fwd_kernel (first maximal tap).
+template <int CINP, int COUT, int SRC>
+__global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
+    ConvArgs a, int R, int tiles_per_img, int ntiles, int pbh, int pbw, int Hp, int Wp,
+    float* __restrict__ pooled, uint8_t* __restrict__ parg) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int K = 3, KK = 9;
+  constexpr int PP = fwd_pitch(CINP);
+  constexpr int NH = COUT / 16;
+  constexpr int VPL = CINP >= 16 ? 4 : CINP / 4;
+  constexpr int NB = CINP >= 16 ? CINP / 16 : 1;
+  constexpr int YP = COUT + 4;
+  constexpr int C4 = COUT / 4;
+  const int H = a.Ho, W = a.Wo;
+  const int Wl = W + 2;
+  const int CR = 2 * R + 1;
+  const int rows = CR + 2;
+  const int total = rows * Wl * (CINP / 4);
+  float* w_s = smem;
+  float* x_s = w_s + KK * CINP * COUT;
+  float* y_s = x_s + rows * Wl * PP;
+  for (int e = threadIdx.x; e < KK * COUT * CINP; e += kThreads) {
+    const int o = e % COUT, i = (e / COUT) % CINP, tap = e / (COUT * CINP);
+    float v = 0.f;
+    if (i < a.wcin) v = a.w[(static_cast<int64_t>(tap) * a.wcin + i) * a.wcout + o];
+    const int b = i / 16, rem = i - 16 * (i / 16);
+    const int g = rem / VPL, v_ = rem - (rem / VPL) * VPL;
+    w_s[(((tap * NB + b) * 4 + g) * COUT + o) * VPL + v_] = v;
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  float bias[NH][4];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[h][r] = a.bias[16 * h + 4 * g + r];
+  const float* wl = w_s + (g * COUT + c16) * VPL;
+
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  Stager<CINP, SRC> st;
+  auto prefetch = [&](int t) {
+    const int n = t / tiles_per_img;
+    const int pi0 = (t - n * tiles_per_img) * R;
+    st.load(a.src, n, a.Hs, a.Ws, a.Cs, 2 * pi0 - pbh - 1, 1, 1, Wl, total, false, a.pool);
+  };
+  prefetch(tile);
+  const int P = CR * W;
+  const int ngroups = (P + 15) >> 4;
+  for (;;) {
+    __syncthreads();  // previous tile: conv reads of x_s and pool reads of y_s done
+    st.commit(x_s, PP, total);
+    __syncthreads();
+    const int cur = tile;
+    tile += gridDim.x;
+    if (tile < ntiles) prefetch(tile);
+    const int n = cur / tiles_per_img;
+    const int pi0 = (cur - n * tiles_per_img) * R;
+    const int cr0 = 2 * pi0 - pbh;
+    auto mma = [&](auto NGc, int g0) {
+      constexpr int NG = decltype(NGc)::value;
+      f4 acc[NG][NH];
+      int xb[NG], q[NG];
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        const int p = (g0 + 4 * gi) * 16 + c16;
+        q[gi] = p < P ? p : -1;
+        const int pp = p < P ? p : 0;
+        const int oy = pp / W, ox = pp - oy * W;
+        xb[gi] = (oy * Wl + ox) * PP + VPL * g;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      constexpr int STEPS = KK * NB;
+      float av[2][NH][VPL], bv[2][NG][VPL];
+      auto load_step = [&](int st, int buf) {
+        const int tap = st / NB, b = st - (st / NB) * NB;
+        const int ky = tap / K, kx = tap - (tap / K) * K;
+        const int toff = (ky * Wl + kx) * PP;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+          lds_get<VPL>(wl + (((tap * NB + b) * 4) * COUT + 16 * h) * VPL, av[buf][h]);
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi)
+          lds_get<VPL>(x_s + xb[gi] + toff + 16 * b, bv[buf][gi]);
+      };
+      load_step(0, 0);
+#pragma unroll
+      for (int st = 0; st < STEPS; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < STEPS) load_step(st + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int v = 0; v < VPL; ++v)
+#pragma unroll
+          for (int gi = 0; gi < NG; ++gi)
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+              acc[gi][h] = mfma4(av[cur][h][v], bv[cur][gi][v], acc[gi][h]);
+      }
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        if (q[gi] < 0) continue;
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+          f4 v = acc[gi][h];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bias[h][r];
+          *reinterpret_cast<f4*>(y_s + q[gi] * YP + 16 * h + 4 * g) = v;
+        }
+      }
+    };
+    int grp = wave;
+    for (; grp + 4 < ngroups; grp += 8) mma(std::integral_constant<int, 2>{}, grp);
+    if (grp < ngroups) mma(std::integral_constant<int, 1>{}, grp);
+    __syncthreads();
+    // pool the tile's conv rows (rows outside the image are never a max)
+    const int Rv = min(R, Hp - pi0);
+    for (int e = threadIdx.x; e < Rv * Wp * C4; e += kThreads) {
+      const int c4 = e % C4;
+      const int t = e / C4;
+      const int pc = t % Wp, pr = t / Wp;
+      float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      int code[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int cr = 2 * (pi0 + pr) - pbh + dy;
+        if (cr < 0 || cr >= H) continue;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int cc = 2 * pc - pbw + dx;
+          if (cc < 0 || cc >= W) continue;
+          const f4 v = *reinterpret_cast<const f4*>(y_s + ((cr - cr0) * W + cc) * YP + 4 * c4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (v[r] > best[r]) {
+              best[r] = v[r];
+              code[r] = dy * 3 + dx;
+            }
+          }
+        }
+      }
+      const int64_t o = ((static_cast<int64_t>(n) * Hp + pi0 + pr) * Wp + pc) * COUT + 4 * c4;
+      *reinterpret_cast<f4*>(pooled + o) = f4{best[0], best[1], best[2], best[3]};
+      *reinterpret_cast<uint32_t*>(parg + o) =
+          static_cast<uint32_t>(code[0]) | (static_cast<uint32_t>(code[1]) << 8) |
+          (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
+    }
+    if (tile >= ntiles) break;
+  }
+}
+
 // ------------------------------------------------------------ weight grads
-template <int CINP, int K, int S, int SRC, int NTT, int WSM>
+template <int CINP, int K, int S, int SRC, int NTT, int WSM, bool GATHER>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R,
                                                               int tiles_per_img,
                                                               int ntiles,
@@ -417,14 +625,15 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
   // persistent walk with the next tile's x / dY chunks prefetched into
   // registers while the current one computes
   Stager<CINP, SRC> sx;
-  DyStager<CG, kMaxD> sd;
+  DyStager<CG, kMaxD, GATHER> sd;
   const int xtotal = rows * Wl * (CINP / 4);
   auto prefetch = [&](int t) {
     const int n = t / tiles_per_img;
     const int oy0 = (t - n * tiles_per_img) * R;
-    sx.load(a.src, n, a.H, a.W, a.Cin, oy0 * S - a.pt, a.pl, 1, Wl, xtotal, a.relu_in != 0);
-    sd.load(a.dy + (static_cast<int64_t>(n) * a.Ho + oy0) * a.Wo * a.Cout + co0, a.Cout,
-            min(R, a.Ho - oy0) * a.Wo * (CG / 4));
+    sx.load(a.src, n, a.H, a.W, a.Cin, oy0 * S - a.pt, a.pl, 1, Wl, xtotal, a.relu_in != 0,
+            a.pool);
+    sd.load(a.dy, n, oy0, a.Ho, a.Wo, a.Cout, co0, min(R, a.Ho - oy0) * a.Wo * (CG / 4),
+            a.pool);
   };
   int tile = blockIdx.x;
   if (tile < ntiles) prefetch(tile);
@@ -440,21 +649,39 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
     tile += gridDim.x;
     if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
     const int nq = (P + 3) >> 2;
-    for (int qd = pg; qd < nq; qd += PG) {
+    // software-pipelined: quad qd+PG's operand reads are issued ahead of
+    // quad qd's MFMAs
+    float av[MTW], bv[NTT];
+    auto load_quad = [&](int qd) {
       const int p = 4 * qd + g;
       const bool valid = p < P;
       const int pp = valid ? p : 0;
       const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
       const int xb = (oy * S * Wl + ox * S) * XP;
-      float bv[NTT];
 #pragma unroll
-      for (int nb = 0; nb < NTT; ++nb) bv[nb] = valid ? d_s[pp * DP + 16 * nb + c16] : 0.f;
+      for (int nb = 0; nb < NTT; ++nb) {
+        const float d = d_s[pp * DP + 16 * nb + c16];
+        bv[nb] = valid ? d : 0.f;
+      }
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
-        const float av = kimg[i] ? x_s[xb + moff[i]] : kconst[i];
-#pragma unroll
-        for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = mfma4(av, bv[nb], acc[i][nb]);
+        const float x = x_s[xb + moff[i]];
+        av[i] = kimg[i] ? x : kconst[i];
       }
+    };
+    if (pg < nq) load_quad(pg);
+    for (int qd = pg; qd < nq; qd += PG) {
+      float ac[MTW], bc[NTT];
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) ac[i] = av[i];
+#pragma unroll
+      for (int nb = 0; nb < NTT; ++nb) bc[nb] = bv[nb];
+      if (qd + PG < nq) load_quad(qd + PG);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = mfma4(ac[i], bc[nb], acc[i][nb]);
     }
   }
 
@@ -601,6 +828,25 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(
   *reinterpret_cast<f4*>(dx + idx * 4) = acc;
 }
 
+// uint8 frames [P, Cs<=4] -> [P, 4] fp32 x / 255 (tf.to_float(frame) / 255,
+// reference experiment.py:153-155), zero-padded to 4 channels: the torso's
+// first conv then stages one 16-B load per pixel instead of byte loads and
+// divisions in every tile (and its weight gradient reuses the same image).
+__global__ __launch_bounds__(256) void frames_f32_kernel(const uint8_t* __restrict__ x,
+                                                         f4* __restrict__ y, int64_t P,
+                                                         int Cs) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < P; i += stride) {
+    const uint8_t* p = x + i * Cs;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    v[0] = static_cast<float>(p[0]) / 255.f;
+    if (Cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
+    if (Cs > 2) v[2] = static_cast<float>(p[2]) / 255.f;
+    if (Cs > 3) v[3] = static_cast<float>(p[3]) / 255.f;
+    y[i] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void relu_mask_kernel(f4* __restrict__ dy,
                                                         const f4* __restrict__ ref,
                                                         int64_t n4) {
@@ -668,13 +914,42 @@ bool run_conv(const ConvArgs& a, hipStream_t s) {
   return true;
 }
 
+template <int CINP, int COUT, int SRC>
+bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* arg,
+                   hipStream_t s) {
+  constexpr int PP = fwd_pitch(CINP);
+  const int W = a.Wo, Wl = W + 2;
+  const int Hp = (a.Ho + 1) / 2, Wp = (a.Wo + 1) / 2;
+  auto bytes = [&](int R) {
+    return static_cast<size_t>(4) *
+           (9 * CINP * COUT + (2 * R + 3) * Wl * PP + (2 * R + 1) * W * (COUT + 4));
+  };
+  const size_t budget = bytes(2) <= kLdsSoft ? kLdsSoft : kLdsHard;
+  int R = 0;
+  for (int r = 1; r <= Hp; ++r) {
+    if (bytes(r) > budget || (2 * r + 3) * Wl * (CINP / 4) > kMaxC * kThreads) break;
+    R = r;
+  }
+  if (R == 0) return false;
+  const int nt = (Hp + R - 1) / R;
+  R = (Hp + nt - 1) / nt;
+  const int ntiles = a.N * nt;
+  const int per_cu = bytes(R) <= kLdsSoft ? 2 : 1;
+  const int G = std::max(1, std::min(ntiles, 256 * per_cu));
+  auto kern = conv_pool_fwd_kernel<CINP, COUT, SRC>;
+  allow_lds(kern, bytes(R));
+  hipLaunchKernelGGL(kern, dim3(G), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, pbh, pbw,
+                     Hp, Wp, pooled, arg);
+  return true;
+}
+
 // output-channel tile: 32 when the weight slice stays small, else 16
 int cout_tile(int cinp, int cout, int K) {
   if (cout % 32 == 0 && 4ll * K * K * 32 * cinp <= 48 * 1024) return 32;
   return 16;
 }
 
-template <int CINP, int K, int S, int SRC, int NTT, int WSM>
+template <int CINP, int K, int S, int SRC, int NTT, int WSM, bool GATHER>
 bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   constexpr int M = K * K * CINP;
   constexpr int MT = (M + 15) / 16 + 1;
@@ -703,7 +978,7 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   const int ngrp = a.Cout / CG;
   const int G = static_cast<int>(
       std::min<int64_t>(ntiles, wgrad_slots(K, CINP, a.Cout)));
-  auto kern = conv_wgrad_kernel<CINP, K, S, SRC, NTT, WSM>;
+  auto kern = conv_wgrad_kernel<CINP, K, S, SRC, NTT, WSM, GATHER>;
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
   const int total = ngrp * MT * 16 * CG;
@@ -730,7 +1005,8 @@ int64_t wgrad_workspace_floats(int K, int Cin, int Cout) {
 bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_t s) {
   const int cinp = src == kSrcU8 ? 4 : a.Cs;
   if (src == kSrcU8 && (a.Cs < 1 || a.Cs > 4)) return false;
-  if (src == kSrcF32 && a.Cs % 4 != 0) return false;
+  if (src != kSrcU8 && a.Cs % 4 != 0) return false;
+  if (src == kSrcPoolGrad && (a.pool.arg == nullptr || a.D != 1)) return false;
   const int ct = cout_tile(cinp, a.Cout, K);
   if (a.Cout % ct != 0) return false;
 #define SA_CONV_CASE(CINP, CT, KK, SS, SRC, FL)                                          \
@@ -738,6 +1014,8 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
     return run_conv<CINP, CT, KK, SS, SRC, FL>(a, s);
   // forward: deep ResNet (3x3/1; uint8 stage-1 input), shallow torso
   SA_CONV_CASE(4, 16, 3, 1, kSrcU8, false)
+  SA_CONV_CASE(4, 16, 3, 1, kSrcF32, false)
+  SA_CONV_CASE(4, 32, 8, 4, kSrcF32, false)
   SA_CONV_CASE(16, 16, 3, 1, kSrcF32, false)
   SA_CONV_CASE(16, 32, 3, 1, kSrcF32, false)
   SA_CONV_CASE(32, 32, 3, 1, kSrcF32, false)
@@ -752,6 +1030,9 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   SA_CONV_CASE(32, 32, 3, 1, kSrcF32, true)
   SA_CONV_CASE(64, 16, 4, 1, kSrcF32, true)
   SA_CONV_CASE(128, 16, 3, 1, kSrcF32, true)
+  // data gradient of a stage-head conv straight from the pooled gradient
+  SA_CONV_CASE(32, 16, 3, 1, kSrcPoolGrad, true)
+  SA_CONV_CASE(32, 32, 3, 1, kSrcPoolGrad, true)
 #undef SA_CONV_CASE
   return false;
 }
@@ -760,10 +1041,15 @@ bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStrea
   const int cinp = src == kSrcU8 ? 4 : a.Cin;
   if (src == kSrcU8 && (a.Cin < 1 || a.Cin > 4)) return false;
   if (src == kSrcF32 && a.Cin % 4 != 0) return false;
+  const bool gather = a.pool.arg != nullptr;
 #define SA_WG_CASE(CINP, KK, SS, SRC, COUT, NTT, WSM)                                     \
-  if (cinp == CINP && K == KK && S == SS && src == SRC && a.Cout == COUT)                 \
-    return run_wgrad<CINP, KK, SS, SRC, NTT, WSM>(a, ws, s);
+  if (cinp == CINP && K == KK && S == SS && src == SRC && a.Cout == COUT) {               \
+    if (gather) return run_wgrad<CINP, KK, SS, SRC, NTT, WSM, true>(a, ws, s);            \
+    return run_wgrad<CINP, KK, SS, SRC, NTT, WSM, false>(a, ws, s);                       \
+  }
   SA_WG_CASE(4, 3, 1, kSrcU8, 16, 1, 1)
+  SA_WG_CASE(4, 3, 1, kSrcF32, 16, 1, 1)
+  SA_WG_CASE(4, 8, 4, kSrcF32, 32, 2, 2)
   SA_WG_CASE(4, 3, 1, kSrcU8, 32, 2, 1)
   SA_WG_CASE(16, 3, 1, kSrcF32, 16, 1, 1)
   SA_WG_CASE(16, 3, 1, kSrcF32, 32, 2, 1)
@@ -772,6 +1058,15 @@ bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStrea
   SA_WG_CASE(32, 4, 2, kSrcF32, 64, 4, 4)
   SA_WG_CASE(64, 3, 2, kSrcF32, 128, 4, 4)
 #undef SA_WG_CASE
+  return false;
+}
+
+bool conv_pool_fwd_launch(const ConvArgs& a, int src, int pbh, int pbw, float* pooled,
+                          uint8_t* arg, hipStream_t s) {
+  if (src == kSrcU8 && a.Cs <= 4 && a.Cout == 16) return run_conv_pool<4, 16, kSrcU8>(a, pbh, pbw, pooled, arg, s);
+  if (src == kSrcF32 && a.Cs == 4 && a.Cout == 16) return run_conv_pool<4, 16, kSrcF32>(a, pbh, pbw, pooled, arg, s);
+  if (src == kSrcF32 && a.Cs == 16 && a.Cout == 32) return run_conv_pool<16, 32, kSrcF32>(a, pbh, pbw, pooled, arg, s);
+  if (src == kSrcF32 && a.Cs == 32 && a.Cout == 32) return run_conv_pool<32, 32, kSrcF32>(a, pbh, pbw, pooled, arg, s);
   return false;
 }
 
@@ -787,6 +1082,13 @@ void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, i
   const int64_t total = static_cast<int64_t>(N) * H * W * (C / 4);
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, dy, arg,
                      dx, N, H, W, C, Hp, Wp, pb_h, pb_w);
+}
+
+void frames_f32_launch(const uint8_t* x, float* y, int64_t P, int Cs, hipStream_t s) {
+  int64_t blocks = std::min<int64_t>((P + 255) / 256, 8192);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(frames_f32_kernel, dim3(blocks), dim3(256), 0, s, x,
+                     reinterpret_cast<f4*>(y), P, Cs);
 }
 
 void relu_mask_launch(float* dy, const float* ref, int64_t n, hipStream_t s) {

@@ -25,9 +25,18 @@ from . import grad_sink
 from ._ext import ext
 from ..models import layers
 
+import os
+
 # debug hook (tools/debug): when a dict, the deep torso backward records its
 # intermediate gradients in it
 DEBUG_TAPE = None
+# Deep-torso stage heads (conv -> max-pool): stages (0-based) whose forward
+# runs the fused conv+pool kernel (pre-pool map only in LDS), and whether the
+# backward gathers the pre-pool gradient from (dP, argmax) inside the conv
+# kernels' loads instead of materialising it with maxpool_bwd.
+FUSED_POOL_STAGES = tuple(int(c) for c in os.environ.get('SA_F32_FUSED_POOL', '0')
+                          if c.isdigit())
+POOL_GATHER = os.environ.get('SA_F32_POOL_GATHER', '0') == '1'
 
 
 def supports(agent):
@@ -46,11 +55,15 @@ class _ShallowTorsoF32(torch.autograd.Function):
   @staticmethod
   def forward(ctx, frames, *params):
     C = ext()
-    x = frames.contiguous()
+    # x / 255 once, as a 4-channel fp32 image (one 16-B load per pixel in
+    # the conv kernels); layer 1 weights see zero rows for the pad channel
+    x = C.cf32_frames_f32(frames.contiguous())
     acts = [x]
     geoms = []
     for i in range(3):
       w, b = params[2 * i], params[2 * i + 1]
+      if i == 0 and w.shape[2] != 4:
+        w = _pad_cin(w, 4)
       k = w.shape[0]
       s = (4, 2, 2)[i]
       H, W = x.shape[1], x.shape[2]
@@ -75,6 +88,12 @@ class _ShallowTorsoF32(torch.autograd.Function):
     C.cf32_relu_mask_(dy, out)
     for i in reversed(range(3)):
       s, pt, pl, H, W = ctx.geoms[i]
+      if i == 0 and gv[0].shape[2] != 4:
+        dw4 = torch.zeros(gv[0].shape[:2] + (4,) + gv[0].shape[3:],
+                          dtype=torch.float32, device=dy.device)
+        C.cf32_conv_wgrad(acts[0], dy, s, pt, pl, False, dw4, gv[1])
+        gv[0].add_(dw4[:, :, :gv[0].shape[2]])
+        continue
       C.cf32_conv_wgrad(acts[i], dy, s, pt, pl, False, gv[2 * i], gv[2 * i + 1])
       if i > 0:
         # input of layer i is the ReLU'd output of layer i-1
@@ -87,18 +106,23 @@ class _DeepTorsoF32(torch.autograd.Function):
   @staticmethod
   def forward(ctx, frames, *params):
     C = ext()
-    x = frames.contiguous()
+    x = C.cf32_frames_f32(frames.contiguous())  # x / 255, 4 channels
     saved, meta = [], []
     p = 0
     for s in range(3):
       w, b = params[p], params[p + 1]
       p += 2
+      if s == 0 and w.shape[2] != 4:
+        w = _pad_cin(w, 4)
       H, W = x.shape[1], x.shape[2]
-      conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
       pbh = layers.same_pads(H, 3, 2)[0]
       pbw = layers.same_pads(W, 3, 2)[0]
-      xa, arg = C.cf32_maxpool_fwd(conv, pbh, pbw)
-      del conv
+      if s in FUSED_POOL_STAGES:
+        xa, arg = C.cf32_conv_pool_fwd(x, w, b, pbh, pbw)
+      else:
+        conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
+        xa, arg = C.cf32_maxpool_fwd(conv, pbh, pbw)
+        del conv
       h, w_ = xa.shape[1], xa.shape[2]
       saved += [x, arg]
       for blk in range(2):
@@ -150,14 +174,37 @@ class _DeepTorsoF32(torch.autograd.Function):
           DEBUG_TAPE[('dy', s, blk)] = dy.clone()
           DEBUG_TAPE[('dt', s, blk)] = dt.clone()
         dy = C.cf32_conv_dgrad(dt, w1, 1, 1, 1, h, w_, mask=xa, add=dy)
+      gw = gv[pb]
+      if s == 0 and gw.shape[2] != 4:
+        gw = torch.zeros(gw.shape[:2] + (4,) + gw.shape[3:], dtype=torch.float32,
+                         device=dy.device)
+      if POOL_GATHER:
+        # the conv kernels gather the pre-pool gradient from (dP, argmax)
+        C.cf32_conv_wgrad(stage_in, dy, 1, 1, 1, False, gw, gv[pb + 1],
+                          pool_arg=arg, pool_pbh=pbh, pool_pbw=pbw)
+        if gw is not gv[pb]:
+          gv[pb].add_(gw[:, :, :gv[pb].shape[2]])
+        if s > 0:
+          dy = C.cf32_conv_dgrad(dy, params[pb], 1, 1, 1, H, W, pool_arg=arg,
+                                 pool_pbh=pbh, pool_pbw=pbw)
+        continue
       dconv = C.cf32_maxpool_bwd(dy, arg, H, W, pbh, pbw)
       if DEBUG_TAPE is not None:
         DEBUG_TAPE[('dpool', s)] = dy.clone()
         DEBUG_TAPE[('dconv', s)] = dconv.clone()
-      C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gv[pb], gv[pb + 1])
+      C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gw, gv[pb + 1])
+      if gw is not gv[pb]:
+        gv[pb].add_(gw[:, :, :gv[pb].shape[2]])
       if s > 0:
         dy = C.cf32_conv_dgrad(dconv, params[pb], 1, 1, 1, H, W)
     return (None,) + grad_sink.returned(gv, direct)
+
+
+def _pad_cin(w, c):
+  """HWIO weights zero-padded on the input-channel axis to c channels."""
+  out = w.new_zeros(w.shape[:2] + (c,) + w.shape[3:])
+  out[:, :, :w.shape[2]] = w
+  return out
 
 
 def shallow_param_list(agent):

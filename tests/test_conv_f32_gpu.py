@@ -228,3 +228,36 @@ def test_bf16_agent_non_rgb_takes_fp32_kernels(cuda):
   frames = torch.randint(0, 256, (4, 84, 84, 4), dtype=torch.uint8, device=cuda)
   feats = agent.conv_features(frames)
   assert feats.shape == (4, 11 * 11 * 32) and torch.isfinite(feats).all()
+
+
+@pytest.mark.parametrize('N,H,W,Cin,Cout,u8', [
+    (3, 72, 96, 3, 16, True), (3, 36, 48, 16, 32, False), (3, 18, 24, 32, 32, False),
+    (2, 84, 84, 4, 16, True), (2, 42, 42, 16, 32, False), (2, 21, 21, 32, 32, False)])
+def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
+  """Fused conv+pool forward == conv then maxpool (bitwise: same MFMA order);
+  the backward that gathers the pre-pool gradient from (dP, argmax) inside
+  the conv kernels == maxpool_bwd then the plain conv kernels."""
+  C = _C()
+  g = torch.Generator().manual_seed(7)
+  if u8:
+    x = torch.randint(0, 256, (N, H, W, Cin), generator=g, dtype=torch.uint8).to(cuda)
+  else:
+    x = torch.randn(N, H, W, Cin, generator=g).to(cuda)
+  w = (torch.randn(3, 3, Cin, Cout, generator=g) / (9 * Cin) ** 0.5).to(cuda)
+  b = (torch.randn(Cout, generator=g) * 0.1).to(cuda)
+  pbh, pbw = layers.same_pads(H, 3, 2)[0], layers.same_pads(W, 3, 2)[0]
+  conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
+  ref_p, ref_a = C.cf32_maxpool_fwd(conv, pbh, pbw)
+  p, a = C.cf32_conv_pool_fwd(x, w, b, pbh, pbw)
+  assert torch.equal(p, ref_p) and torch.equal(a, ref_a)
+  dP = torch.randn(p.shape, generator=g).to(cuda)
+  dconv = C.cf32_maxpool_bwd(dP, a, H, W, pbh, pbw)
+  dw1, db1 = torch.zeros_like(w), torch.zeros_like(b)
+  dw2, db2 = torch.zeros_like(w), torch.zeros_like(b)
+  C.cf32_conv_wgrad(x, dconv, 1, 1, 1, False, dw1, db1)
+  C.cf32_conv_wgrad(x, dP, 1, 1, 1, False, dw2, db2, pool_arg=a, pool_pbh=pbh, pool_pbw=pbw)
+  assert rel_err(dw2, dw1) <= 1e-6 and rel_err(db2, db1) <= 1e-6
+  if not u8:
+    dx1 = C.cf32_conv_dgrad(dconv, w, 1, 1, 1, H, W)
+    dx2 = C.cf32_conv_dgrad(dP, w, 1, 1, 1, H, W, pool_arg=a, pool_pbh=pbh, pool_pbw=pbw)
+    assert torch.equal(dx1, dx2)

@@ -14,6 +14,7 @@ from scalable_agent_amd import ops  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 3232
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+ONLY = sys.argv[3] if len(sys.argv) > 3 else ''  # substring filter on layer names
 C = ops.ext()
 dev = torch.device('cuda')
 # name, H, W, Cin, Cout, K, S, pt, pl, uint8 source, relu_in, resid
@@ -42,6 +43,8 @@ def timeit(fn):
 
 
 for name, H, W, Ci, Co, K, S, pt, pl, u8 in LAYERS:
+  if ONLY and ONLY not in name:
+    continue
   Ho, Wo = -(-H // S), -(-W // S)
   x = (torch.randint(0, 256, (N, H, W, Ci), dtype=torch.uint8, device=dev) if u8
        else torch.randn(N, H, W, Ci, device=dev))
@@ -59,6 +62,8 @@ for name, H, W, Ci, Co, K, S, pt, pl, u8 in LAYERS:
     td = timeit(lambda: C.cf32_conv_dgrad(dy, w, S, pt, pl, H, W))
     line += ' | dgrad %8.1f us %6.1f TF' % (td, flop / td / 1e6)
   print(line, flush=True)
+if ONLY:
+  sys.exit(0)
 xp = torch.randn(N, 72, 96, 16, device=dev)
 tp = timeit(lambda: C.cf32_maxpool_fwd(xp, 0, 0))
 y, arg = C.cf32_maxpool_fwd(xp, 0, 0)
