@@ -581,8 +581,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
                                                               float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int M = K * K * CINP;
-  constexpr int MTc = (M + 15) / 16;
-  constexpr int MT = MTc + 1;  // + the bias ones-row tile
+  // rows m < M: (tap, ci) of the image; row M: the bias ones-row (in the
+  // last image tile's padding when M % 16 != 0, else one extra tile)
+  constexpr int MT = (M + 16) / 16;
   constexpr int MTW = (MT + WSM - 1) / WSM;
   constexpr int PG = 4 / WSM;
   constexpr int XP = wg_pitch(CINP);
@@ -607,13 +608,13 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
     moff[i] = 0;
     kimg[i] = false;
     kconst[i] = 0.f;
-    if (mb < MTc && m < M) {
+    if (m < M) {
       const int tap = m / CINP, ci = m - (m / CINP) * CINP;
       const int ky = tap / K, kx = tap - (tap / K) * K;
       moff[i] = (ky * Wl + kx) * XP + ci;
       kimg[i] = true;
-    } else if (mb == MT - 1) {
-      kconst[i] = c16 == 0 ? 1.f : 0.f;  // row 16*(MT-1): sum of dY
+    } else if (m == M) {
+      kconst[i] = 1.f;  // row M: sum of dY (bias gradient)
     }
   }
   f4 acc[MTW][NTT];
@@ -721,28 +722,38 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
   }
 }
 
-// Sums the G per-workgroup partials of every (row, co) in slot order and
-// accumulates into dW (HWIO) / db.
+// Sums the G per-workgroup partials of every (row, co) in a fixed order and
+// accumulates into dW (HWIO) / db.  64 elements per block, the slots split
+// over the block's 4 waves (8 loads in flight per thread), the 4 wave sums
+// combined in LDS in wave order: deterministic.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
     const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
-    int bias_row, int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[4][64];
   const int per = MT16 * CG;
-  if (idx >= ngrp * per) return;
-  const int ng = idx / per, rem = idx - ng * per;
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sg = threadIdx.x >> 6;
+  const bool live = e < ngrp * per;
+  const int ng = live ? e / per : 0, rem = live ? e - ng * per : 0;
   const int m = rem / CG, c = rem - (rem / CG) * CG;
-  if (!(m < M && (m % CINP) < Cin) && !(db != nullptr && m == bias_row)) return;
-  const float* p = part + static_cast<int64_t>(ng) * G * per + rem;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int k = 0;
-  for (; k + 4 <= G; k += 4) {
-    s0 += p[static_cast<int64_t>(k) * per];
-    s1 += p[static_cast<int64_t>(k + 1) * per];
-    s2 += p[static_cast<int64_t>(k + 2) * per];
-    s3 += p[static_cast<int64_t>(k + 3) * per];
+  const bool want = live && ((m < M && (m % CINP) < Cin) || (db != nullptr && m == M));
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (want) {
+    const float* p = part + static_cast<int64_t>(ng) * G * per + rem;
+    for (int k = sg; k < G; k += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int kk = k + 4 * u;
+        if (kk < G) acc[u] += p[static_cast<int64_t>(kk) * per];
+      }
+    }
   }
-  for (; k < G; ++k) s0 += p[static_cast<int64_t>(k) * per];
-  const float s = (s0 + s1) + (s2 + s3);
+  red[sg][threadIdx.x & 63] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                               ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (sg != 0 || !want) return;
+  const int l = threadIdx.x;
+  const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
   const int co = ng * CG + c;
   if (m < M) {
     const int tap = m / CINP, ci = m - (m / CINP) * CINP;
@@ -952,7 +963,7 @@ int cout_tile(int cinp, int cout, int K) {
 template <int CINP, int K, int S, int SRC, int NTT, int WSM, bool GATHER>
 bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   constexpr int M = K * K * CINP;
-  constexpr int MT = (M + 15) / 16 + 1;
+  constexpr int MT = (M + 16) / 16;
   constexpr int XP = wg_pitch(CINP);
   constexpr int CG = NTT * 16;
   constexpr int DP = (CG % 32 == 0) ? CG + 16 : CG;
@@ -982,8 +993,8 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
   const int total = ngrp * MT * 16 * CG;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ws, G,
-                     ngrp, MT * 16, CG, CINP, M, (MT - 1) * 16, a.Cin, a.Cout, a.dw, a.db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, ws, G,
+                     ngrp, MT * 16, CG, CINP, M, a.Cin, a.Cout, a.dw, a.db);
   return true;
 }
 
@@ -992,13 +1003,13 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
 // Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
 // least 128 slots (before the tile-count cap) so the reduction fills the GPU.
 int64_t wgrad_slots(int K, int cinp, int cout) {
-  const int64_t rows = ((K * K * cinp + 15) / 16 + 1) * 16;
+  const int64_t rows = ((K * K * cinp + 16) / 16) * 16;
   return std::max<int64_t>(128, std::min<int64_t>(512, (8ll << 20) / (rows * cout)));
 }
 
 int64_t wgrad_workspace_floats(int K, int Cin, int Cout) {
   const int cinp = Cin <= 4 ? 4 : Cin;
-  const int64_t rows = ((K * K * cinp + 15) / 16 + 1) * 16;
+  const int64_t rows = ((K * K * cinp + 16) / 16) * 16;
   return wgrad_slots(K, cinp, Cout) * rows * Cout;
 }
 

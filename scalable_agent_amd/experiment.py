@@ -135,10 +135,12 @@ def _make_agent(flags, num_actions, frame_shape, device, seed):
   import torch
   from .models import Agent
   backend = 'torch'
-  if device.type == 'cuda':
+  if device.type == 'cuda' and getattr(flags, 'backend', 'auto') != 'torch':
     from . import ops
     ops.load()  # fail loudly on a GPU box without the kernels
     backend = 'hip'
+  elif getattr(flags, 'backend', 'auto') == 'hip':
+    raise ValueError('--backend=hip needs a GPU device')
   cdt = torch.bfloat16 if flags.dtype == 'bf16' else torch.float32
   return Agent(num_actions, torso=flags.torso, frame_shape=frame_shape,
                seed=seed, backend=backend, compute_dtype=cdt,

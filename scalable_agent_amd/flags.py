@@ -81,6 +81,9 @@ def build_parser() -> argparse.ArgumentParser:
                       'optimizer state always fp32).')
   p.add_argument('--device', default='auto',
                  help='auto | cpu | cuda | cuda:N')
+  p.add_argument('--backend', default='auto', choices=['auto', 'hip', 'torch'],
+                 help='Model backend: hip = the hand-written gfx950 kernels '
+                      '(default on a GPU), torch = the pure-PyTorch oracle.')
   p.add_argument('--inference_min_batch', type=int, default=1)
   p.add_argument('--inference_max_batch', type=int, default=1024)
   p.add_argument('--inference_timeout_ms', type=int, default=100)

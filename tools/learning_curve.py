@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Learning evidence on the learnable synthetic levels (envs/synthetic.py).
+
+Runs `experiment.train` in-process on 'synthetic_cue' (reactive: act with the
+index of the bright band in the current frame) or 'synthetic_memory' (the
+band is shown only on the first frame of an episode) and reports the mean
+episode return per window of episodes, against the random-policy return
+(episode_length / num_actions).  Usage:
+  python tools/learning_curve.py [--level synthetic_cue] [--backend hip|torch]
+      [--frames 400000] [--dtype fp32|bf16] [--out file.json]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from scalable_agent_amd import experiment  # noqa: E402
+from scalable_agent_amd import flags as flags_lib  # noqa: E402
+
+
+def run(level, backend, frames, dtype, torso='shallow', episode_length=20,
+        num_actors=16, batch_size=8, unroll_length=20, height=36, width=48,
+        learning_rate=0.0006, seed=1, logdir=None):
+  logdir = logdir or tempfile.mkdtemp(prefix='sa_learn_')
+  fl = flags_lib.default_flags(
+      level_name=level, env='synthetic', backend=backend, dtype=dtype,
+      torso=torso, total_environment_frames=frames, num_actors=num_actors,
+      batch_size=batch_size, unroll_length=unroll_length, height=height,
+      width=width, synthetic_episode_length=episode_length,
+      num_action_repeats=1, learning_rate=learning_rate, seed=seed,
+      entropy_cost=0.003, logdir=logdir, save_summaries_secs=0,
+      save_checkpoint_secs=1e9, log_every_frames=10 ** 9)
+  t0 = time.time()
+  experiment.train(fl)
+  wall = time.time() - t0
+  returns = []
+  with open(os.path.join(logdir, 'summaries.jsonl')) as f:
+    for line in f:
+      rec = json.loads(line)
+      for k, v in rec.get('values', rec).items():
+        if k.endswith('/episode_return'):
+          returns.append((rec['step'], v))
+  returns.sort()
+  n = len(returns)
+  win = max(1, n // 10)
+  curve = [(returns[min(n - 1, i + win - 1)][0],
+            sum(r for _, r in returns[i:i + win]) / len(returns[i:i + win]))
+           for i in range(0, n, win)]
+  return {'level': level, 'backend': backend, 'dtype': dtype, 'torso': torso,
+          'frames': frames, 'episodes': n, 'wall_s': round(wall, 1),
+          'random_return': episode_length / 9.0,
+          'perfect_return': float(episode_length),
+          'first_window_mean': curve[0][1] if curve else None,
+          'last_window_mean': curve[-1][1] if curve else None,
+          'curve': curve}
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument('--level', default='synthetic_cue')
+  ap.add_argument('--backend', default='hip')
+  ap.add_argument('--frames', type=int, default=400000)
+  ap.add_argument('--dtype', default='fp32')
+  ap.add_argument('--torso', default='shallow')
+  ap.add_argument('--out', default='')
+  args = ap.parse_args()
+  res = run(args.level, args.backend, args.frames, args.dtype, torso=args.torso)
+  line = json.dumps(res)
+  print(line, flush=True)
+  if args.out:
+    with open(args.out, 'a') as f:
+      f.write(line + '\n')
+
+
+if __name__ == '__main__':
+  main()
