@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "envpool/shm_ring.h"
+#include "envpool/traj_queue.h"
 
 namespace py = pybind11;
 
@@ -49,6 +50,36 @@ void register_envpool(py::module& m) {
              return py::memoryview::from_memory(r.slot_data(s), r.slot_bytes(), false);
            }, py::keep_alive<0, 1>())
       .def_static("unlink", &ShmRing::Unlink);
+
+  py::class_<TrajQueue>(m, "TrajQueue")
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, bool>(),
+           py::arg("name"), py::arg("num_slabs") = 0, py::arg("slab_bytes") = 0,
+           py::arg("batch") = 0, py::arg("create") = false)
+      .def("claim", [](TrajQueue& q, int64_t t) {
+             py::gil_scoped_release nogil;
+             return q.Claim(t);
+           }, py::arg("timeout_ms") = -1)
+      .def("commit", &TrajQueue::Commit)
+      .def("acquire", [](TrajQueue& q, int64_t t) {
+             py::gil_scoped_release nogil;
+             return q.Acquire(t);
+           }, py::arg("timeout_ms") = -1)
+      .def("release", &TrajQueue::Release)
+      .def("close", &TrajQueue::Close)
+      .def_property_readonly("closed", &TrajQueue::closed)
+      .def_property_readonly("num_slabs", &TrajQueue::num_slabs)
+      .def_property_readonly("slab_bytes", &TrajQueue::slab_bytes)
+      .def_property_readonly("batch", &TrajQueue::batch)
+      .def_property_readonly("num_ready", &TrajQueue::num_ready)
+      .def_property_readonly("name", &TrajQueue::name)
+      .def_property_readonly("payload_address", [](TrajQueue& q) {
+             return reinterpret_cast<uintptr_t>(q.payload_base());
+           })
+      .def_property_readonly("payload_bytes", &TrajQueue::payload_bytes)
+      .def("slab_view", [](TrajQueue& q, int64_t s) {
+             return py::memoryview::from_memory(q.slab_data(s), q.slab_bytes(), false);
+           }, py::keep_alive<0, 1>())
+      .def_static("unlink", &TrajQueue::Unlink);
 }
 
 }  // namespace sa

@@ -142,6 +142,69 @@ class Actor(object):
         agent_outputs=AgentOutput(action, logits, baseline))
 
 
+  # ---------------------------------------------------- trajectory queue
+  def unroll_into(self, tq, level_index, stop=None):
+    """Runs one unroll straight into a claimed column of a
+    runtime.traj_queue.TrajectoryQueue slab: every step's fields land in
+    their time-major [t, column] position (no per-unroll arrays, no stacking
+    or transposing on the learner side).  Returns False when the queue is
+    closed / `stop` is set before a column was claimed.  An env restart
+    mid-unroll rewrites the same column from a fresh episode."""
+    while True:
+      s, col, v = tq.claim(timeout_ms=200)
+      if s >= 0:
+        break
+      if s == -2 or (stop is not None and stop.is_set()):
+        return False
+    while True:
+      try:
+        self._unroll_to(v, col, level_index)
+        break
+      except EnvRestartedError as e:
+        self.env_restarts += 1
+        logging.getLogger('scalable_agent_amd').warning(
+            'actor %s: %s; dropping the in-flight unroll (its column is '
+            'rewritten from a fresh episode)', self.level_name, e)
+        self._env_output = None
+    tq.commit(s)
+    return True
+
+  def _unroll_to(self, v, col, level_index):
+    if self._stall_s:
+      time.sleep(self._stall_s)
+    if self._env_output is None:
+      self._reset()
+    v['level'][col] = level_index
+    v['c'][col] = self._agent_state[0]
+    v['h'][col] = self._agent_state[1]
+    frame, reward, done = v['frame'], v['reward'], v['done']
+    ep_ret, ep_step = v['episode_return'], v['episode_step']
+    action, logits, baseline = v['action'], v['policy_logits'], v['baseline']
+    use_instr = self._use_instr and 'instr_ids' in v
+
+    def record(t):
+      eo, ao = self._env_output, self._agent_output
+      frame[t, col] = eo.observation[0]
+      reward[t, col] = eo.reward
+      done[t, col] = eo.done
+      ep_ret[t, col] = eo.info.episode_return
+      ep_step[t, col] = eo.info.episode_step
+      if use_instr:
+        v['instr_ids'][t, col], v['instr_len'][t, col] = encode_instruction(
+            eo.observation[1])
+      action[t, col] = ao.action
+      logits[t, col] = ao.policy_logits
+      baseline[t, col] = ao.baseline
+
+    record(0)
+    for t in range(1, self._T + 1):
+      self._step_agent()
+      raw_action = self._action_set[int(self._agent_output.action)]
+      self._env_output, self._env_state = self._env.step(raw_action,
+                                                         self._env_state)
+      record(t)
+
+
 def stack_unrolls(unrolls, use_instruction=False, pin=False):
   """B unrolls -> one time-major batch (torch tensors [T+1, B, ...])."""
   import torch  # local: actors may run without torch on the hot path

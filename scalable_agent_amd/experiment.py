@@ -188,6 +188,108 @@ class EpisodeLogger(object):
       self.level_returns = {l: [] for l in self.level_names}
 
 
+# --------------------------------------------------------------- feeder
+class _TrajFeeder(object):
+  """Learner side of the trajectory queue (runtime/traj_queue.py).
+
+  Per step: acquire a full slab (one [T+1, B] batch the actors wrote in
+  place), ONE async H2D copy of it into the idle device slot on a copy
+  stream, the compute stream waits on that copy's event and replays the
+  slot's captured learner graph.  While step k computes on slot k % 2 the
+  copy of step k+1 lands in the other slot (StagingArea, experiment.py:
+  587-597).  A slab is released as soon as its copy event has completed
+  (polled: the host never waits on compute)."""
+
+  def __init__(self, tq, learner, device, use_graph):
+    import collections
+    import torch
+    self.torch = torch
+    self.tq = tq
+    self.learner = learner
+    self.device = device
+    self.cuda = device.type == 'cuda'
+    self.use_graph = use_graph and self.cuda
+    n = 2 if self.cuda else 1
+    self.slots = [torch.empty(tq.layout.nbytes, dtype=torch.uint8, device=device)
+                  for _ in range(n)]
+    self.views = [tq.layout.torch_views(s) for s in self.slots]
+    self.graphs = [None] * n
+    self.pending = collections.deque()
+    self.k = 0
+    if self.cuda:
+      self.copy_stream = torch.cuda.Stream(device)
+      self.free = [torch.cuda.Event() for _ in range(n)]
+      for e in self.free:
+        e.record()
+
+  def _reap(self, block):
+    while self.pending:
+      slab, ev = self.pending[0]
+      if not ev.query():
+        if not block:
+          return
+        ev.synchronize()
+      self.pending.popleft()
+      self.tq.release(slab)
+      block = False
+
+  def step(self, timeout_s, poison=False):
+    """-> (loss, host info dict, seconds waited for a full slab)."""
+    torch = self.torch
+    t0 = time.time()
+    while True:
+      self._reap(block=False)
+      slab = self.tq.acquire(timeout_ms=200)
+      if slab >= 0:
+        break
+      if slab == -2:
+        raise RuntimeError('trajectory queue closed')
+      if time.time() - t0 > timeout_s:
+        raise RuntimeError('learner starved: no full batch for %.0fs' %
+                           timeout_s)
+    wait = time.time() - t0
+    hv = self.tq.host_views(slab)
+    info = {'level': hv['level'].copy(), 'done': hv['done'][1:].copy(),
+            'episode_return': hv['episode_return'][1:].copy(),
+            'episode_step': hv['episode_step'][1:].copy(),
+            'action': hv['action'][1:].copy()}
+    if poison:
+      hv['reward'][1:, 0] = float('nan')  # fault injection: poisoned batch
+    learner = self.learner
+    if not self.cuda:
+      self.slots[0].copy_(self.tq.host_tensor(slab))
+      self.tq.release(slab)
+      loss = learner.step(self.views[0])
+      self.k += 1
+      return loss, info, wait
+    j = self.k % 2
+    with torch.cuda.stream(self.copy_stream):
+      self.copy_stream.wait_event(self.free[j])  # slot j's last graph is done
+      self.slots[j].copy_(self.tq.host_tensor(slab), non_blocking=True)
+      copied = torch.cuda.Event()
+      copied.record(self.copy_stream)
+    comp = torch.cuda.current_stream(self.device)
+    comp.wait_event(copied)
+    self.pending.append((slab, copied))
+    if self.use_graph:
+      if self.graphs[j] is None:
+        copied.synchronize()  # capture runs on the data in place
+        learner.capture(self.views[j], clone=False)
+        self.graphs[j] = (learner._graph, learner._static_in,
+                          learner._static_loss)
+      learner._graph, learner._static_in, learner._static_loss = self.graphs[j]
+      loss = learner.graph_step()
+    else:
+      loss = learner.step(self.views[j])
+    self.free[j].record(comp)
+    self.k += 1
+    self._reap(block=len(self.pending) > 2)
+    return loss, info, wait
+
+  def close(self):
+    self._reap(block=True)
+
+
 # --------------------------------------------------------------- train
 class _Terminated(BaseException):
   """Raised in the main thread by SIGTERM: stop cleanly and checkpoint."""
@@ -245,6 +347,11 @@ def train(flags):
 
   rank, world, local_rank = parallel.init_distributed(
       timeout_s=flags.collective_timeout_secs)
+  if flags.num_learners and flags.num_learners != world:
+    raise ValueError(
+        '--num_learners=%d but WORLD_SIZE=%d: launch one process per learner '
+        '(python -m torch.distributed.run --nproc-per-node %d ...)' %
+        (flags.num_learners, world, flags.num_learners))
   device = _device(flags, local_rank)
   _install_sigterm_handler()
   if device.type == 'cuda':
@@ -287,15 +394,41 @@ def train(flags):
     threading.Thread(target=transport.pump, args=(unroll_queue, stop),
                      daemon=True).start()
   else:
-    inf_agent = _make_agent(flags, num_actions, frame_shape, device,
+    inf_device = (device if flags.inference_device == 'auto' else
+                  torch.device(flags.inference_device))
+    inf_agent = _make_agent(flags, num_actions, frame_shape, inf_device,
                             flags.seed)
-    model = inference_lib.InferenceModel(inf_agent, device, use_instr,
+    model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
                                          seed=flags.seed + 17 * rank)
     model.publish(learner.flat.params)
     infer = inference_lib.make_batched_infer(
         model, flags.inference_min_batch, flags.inference_max_batch,
         flags.inference_timeout_ms)
     actor_errors = []
+    # time-major trajectory queue: actors write batches in place (no
+    # stacking / transposing / staging memcpy on the learner); the
+    # deterministic mode keeps the sorted unroll queue (column order would
+    # follow actor timing)
+    use_traj = not flags.deterministic and flags.trajectory_queue
+    if use_traj:
+      from .runtime.traj_queue import BatchLayout, TrajectoryQueue
+      layout = BatchLayout(flags.unroll_length + 1, flags.batch_size,
+                           frame_shape, num_actions, use_instruction=use_instr)
+      num_slabs = max(3, -(-flags.num_actors // flags.batch_size) + 2)
+      tq = TrajectoryQueue(layout, num_slabs,
+                           pin_device=device if device.type == 'cuda' else None)
+      feeder = _TrajFeeder(tq, learner, device,
+                           flags.use_hip_graph and device.type == 'cuda')
+
+    def actor_loop_traj(actor, level_index):
+      try:
+        while not stop.is_set():
+          if not actor.unroll_into(tq, level_index, stop):
+            break
+      except Exception as e:  # pylint: disable=broad-except
+        if not stop.is_set():
+          actor_errors.append(e)
+          log.exception('actor failed')
 
     def actor_loop(actor):
       try:
@@ -318,11 +451,18 @@ def train(flags):
                     num_actions, use_instruction=use_instr,
                     stall_ms=faults.get('actor_stall'))
       actors.append(actor)
-      t = threading.Thread(target=actor_loop, args=(actor,), daemon=True,
-                           name='actor-%d' % i)
+      if use_traj:
+        t = threading.Thread(target=actor_loop_traj,
+                             args=(actor, task_index[actors_levels[i]]),
+                             daemon=True, name='actor-%d' % i)
+      else:
+        t = threading.Thread(target=actor_loop, args=(actor,), daemon=True,
+                             name='actor-%d' % i)
       t.start()
       threads.append(t)
 
+  if distributed_actors:
+    use_traj = False
   episode_logger = EpisodeLogger(flags, level_names, writer)
   if flags.deterministic:
     torch.use_deterministic_algorithms(True, warn_only=True)
@@ -333,76 +473,104 @@ def train(flags):
   steps = 0
   use_graph = flags.use_hip_graph and device.type == 'cuda'
   staging = dev_stage = copied = None
+  host_ms = []
   try:
     frames = int(learner.frames.item())
     while frames < flags.total_environment_frames:
       if flags.max_learner_steps and steps >= flags.max_learner_steps:
         break
-      t_wait = time.time()
-      unrolls = []
-      while len(unrolls) < flags.batch_size:
-        try:
-          unrolls.append(unroll_queue.get(timeout=flags.queue_timeout_secs))
-        except queue.Empty:
-          raise RuntimeError(
-              'learner starved: no unroll for %.0fs (actors alive: %s)' %
-              (flags.queue_timeout_secs,
-               [t.is_alive() for t in threads] or 'remote'))
-      timer.add_wait(time.time() - t_wait)
-      if flags.deterministic:
-        # batch order independent of actor timing: sort by actor identity
-        unrolls.sort(key=lambda u: (u.level_name, float(u.agent_state[0][0])))
-      host = stack_unrolls(unrolls, use_instruction=use_instr, pin=False)
-      if faults.get('learner_nan') == steps + 1:
-        host.env_outputs.reward[1:, 0] = float('nan')  # poisoned batch
-      dev_batch = host
-      if learner.popart is not None:
-        # PopArt: the device batch carries task indices instead of names
-        dev_batch = host._replace(level_name=torch.tensor(
-            [task_index[l] for l in host.level_name], dtype=torch.int64))
-      with trace('h2d'):
-        if device.type == 'cuda':
-          # the batch goes into one of two pinned flat buffers and reaches
-          # the device (the graph's static slot) with ONE async copy
-          if staging is None:
-            staging = [FlatStaging(dev_batch, 'cpu', pin=True)
-                       for _ in range(2)]
-            dev_stage = FlatStaging(dev_batch, device)
-            copied = [None, None]
-          slot = steps % 2
-          if copied[slot] is not None:
-            copied[slot].synchronize()  # its previous H2D copy has landed
-          staging[slot].load(dev_batch)
-          dev_stage.copy_from(staging[slot])
-          copied[slot] = torch.cuda.Event()
-          copied[slot].record()
-          data = dev_stage.views
-        else:
-          data = batch_to_device(dev_batch, device)
-      with trace('learner_step'):
-        if use_graph:
-          if learner._graph is None:
-            learner.capture(data, clone=False)
-          loss = learner.graph_step()
-        else:
-          loss = learner.step(data)
-      steps += 1
-      if (world > 1 and flags.consistency_check_steps and
-          steps % flags.consistency_check_steps == 0 and
-          not parallel.param_checksum_consistent(learner.flat.params)):
-        raise RuntimeError('data-parallel replicas diverged at step %d' %
-                           steps)
-      if infer is not None:
-        model.publish(learner.flat.params)
-      elif transport is not None:
-        transport.publish_weights()
-      frames = int(learner.frames.item())
-      timer.step()
-      # episode logging on env_outputs[1:] (experiment.py:372-375, 632-647)
-      eo = host.env_outputs
-      episode_logger.log_batch(host.level_name, eo.done[1:].numpy(),
-                               eo.info.episode_return[1:].numpy(),
-                               eo.info.episode_step[1:].numpy(), frames)
+      if use_traj:
+        t_step = time.time()
+        with trace('learner_step'):
+          loss, info, wait = feeder.step(
+              flags.queue_timeout_secs,
+              poison=faults.get('learner_nan') == steps + 1)
+        timer.add_wait(wait)
+        steps += 1
+        if (world > 1 and flags.consistency_check_steps and
+            steps % flags.consistency_check_steps == 0 and
+            not parallel.param_checksum_consistent(learner.flat.params)):
+          raise RuntimeError('data-parallel replicas diverged at step %d' %
+                             steps)
+        if infer is not None:
+          model.publish(learner.flat.params)
+        # host frame counter (the device counter drives the LR schedule;
+        # reading it every step would sync the host with the GPU)
+        frames += learner.frames_per_step
+        timer.step()
+        batch_levels = [level_names[i] for i in info['level']]
+        episode_logger.log_batch(batch_levels, info['done'],
+                                 info['episode_return'], info['episode_step'],
+                                 frames)
+        host_ms.append(1e3 * (time.time() - t_step - wait))
+        host_actions = info['action']
+      if not use_traj:
+        t_wait = time.time()
+        unrolls = []
+        while len(unrolls) < flags.batch_size:
+          try:
+            unrolls.append(unroll_queue.get(timeout=flags.queue_timeout_secs))
+          except queue.Empty:
+            raise RuntimeError(
+                'learner starved: no unroll for %.0fs (actors alive: %s)' %
+                (flags.queue_timeout_secs,
+                 [t.is_alive() for t in threads] or 'remote'))
+        timer.add_wait(time.time() - t_wait)
+        if flags.deterministic:
+          # batch order independent of actor timing: sort by actor identity
+          unrolls.sort(key=lambda u: (u.level_name, float(u.agent_state[0][0])))
+        host = stack_unrolls(unrolls, use_instruction=use_instr, pin=False)
+        if faults.get('learner_nan') == steps + 1:
+          host.env_outputs.reward[1:, 0] = float('nan')  # poisoned batch
+        dev_batch = host
+        if learner.popart is not None:
+          # PopArt: the device batch carries task indices instead of names
+          dev_batch = host._replace(level_name=torch.tensor(
+              [task_index[l] for l in host.level_name], dtype=torch.int64))
+        with trace('h2d'):
+          if device.type == 'cuda':
+            # the batch goes into one of two pinned flat buffers and reaches
+            # the device (the graph's static slot) with ONE async copy
+            if staging is None:
+              staging = [FlatStaging(dev_batch, 'cpu', pin=True)
+                         for _ in range(2)]
+              dev_stage = FlatStaging(dev_batch, device)
+              copied = [None, None]
+            slot = steps % 2
+            if copied[slot] is not None:
+              copied[slot].synchronize()  # its previous H2D copy has landed
+            staging[slot].load(dev_batch)
+            dev_stage.copy_from(staging[slot])
+            copied[slot] = torch.cuda.Event()
+            copied[slot].record()
+            data = dev_stage.views
+          else:
+            data = batch_to_device(dev_batch, device)
+        with trace('learner_step'):
+          if use_graph:
+            if learner._graph is None:
+              learner.capture(data, clone=False)
+            loss = learner.graph_step()
+          else:
+            loss = learner.step(data)
+        steps += 1
+        if (world > 1 and flags.consistency_check_steps and
+            steps % flags.consistency_check_steps == 0 and
+            not parallel.param_checksum_consistent(learner.flat.params)):
+          raise RuntimeError('data-parallel replicas diverged at step %d' %
+                             steps)
+        if infer is not None:
+          model.publish(learner.flat.params)
+        elif transport is not None:
+          transport.publish_weights()
+        frames = int(learner.frames.item())
+        timer.step()
+        # episode logging on env_outputs[1:] (experiment.py:372-375, 632-647)
+        eo = host.env_outputs
+        episode_logger.log_batch(host.level_name, eo.done[1:].numpy(),
+                                 eo.info.episode_return[1:].numpy(),
+                                 eo.info.episode_step[1:].numpy(), frames)
+        host_actions = host.agent_outputs.action[1:].numpy()
       if writer is not None and (time.time() - last_summary >=
                                  flags.save_summaries_secs):
         last_summary = time.time()
@@ -421,15 +589,17 @@ def train(flags):
         if learner.grad_sync is not None:
           scalars['allreduce_ms'] = 1e3 * learner.grad_sync.last_time_s
         writer.add_scalars(scalars, frames)
-        writer.add_histogram('action',
-                             host.agent_outputs.action[1:].numpy(), frames)
+        if host_ms:
+          scalars['learner_host_ms'] = float(np.mean(host_ms[-100:]))
+        writer.add_histogram('action', host_actions, frames)
         writer.flush()
       if frames - last_log_frames >= flags.log_every_frames:
         last_log_frames = frames
         log.info('frames %d  %.0f frames/s  %.2f steps/s  loss %.3f  '
-                 'queue-wait %.0f%%', frames, timer.frames_per_sec(),
-                 timer.steps_per_sec(), float(loss),
-                 100 * timer.wait_fraction())
+                 'queue-wait %.0f%%  learner host %.2f ms/step', frames,
+                 timer.frames_per_sec(), timer.steps_per_sec(), float(loss),
+                 100 * timer.wait_fraction(),
+                 float(np.mean(host_ms[-100:])) if host_ms else 0.0)
         health = learner.health()
         if health['skipped_updates'] > reported_skips:
           # loud, not fatal: the guard already dropped those updates
@@ -444,6 +614,9 @@ def train(flags):
                 int(learner.frames.item()))
   finally:
     stop.set()
+    if use_traj:
+      tq.close()
+      feeder.close()
     if infer is not None:
       infer.close()
     for t in threads:

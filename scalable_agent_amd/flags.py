@@ -69,8 +69,10 @@ def build_parser() -> argparse.ArgumentParser:
                  help='Synthetic env frame shape HxWxC (default height x width x 3).')
   p.add_argument('--synthetic_episode_length', type=int, default=200,
                  help='Mean (geometric) episode length of the synthetic env.')
-  p.add_argument('--num_learners', type=int, default=1,
-                 help='Data-parallel learners (one per GPU, RCCL all-reduce).')
+  p.add_argument('--num_learners', type=int, default=0,
+                 help='Data-parallel learners (one process per GPU, RCCL '
+                      'all-reduce), launched with torch.distributed.run; '
+                      '0 = WORLD_SIZE decides, else it must equal WORLD_SIZE.')
   p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
                  help='sum: N learners x B == one learner with N*B (reference '
                       'losses are sums).')
@@ -88,10 +90,12 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--inference_max_batch', type=int, default=1024)
   p.add_argument('--inference_timeout_ms', type=int, default=100)
   p.add_argument('--inference_device', default='auto',
-                 help='Device for actor inference (auto = learner device).')
-  p.add_argument('--actor_processes', type=int, default=0,
-                 help='0: envs run in py_process workers driven by actor '
-                      'threads (reference single-machine mode).')
+                 help='Device of the actor-inference model: auto = the '
+                      'learner device; e.g. cuda:1 or cpu.')
+  p.add_argument('--trajectory_queue', type=_str2bool, default=True,
+                 help='Local actors write time-major batches in place into '
+                      'a pinned shared-memory slab queue (one H2D copy per '
+                      'learner step); false: per-unroll queue + stacking.')
   p.add_argument('--popart', type=_str2bool, default=False,
                  help='PopArt value normalisation (north-star config #4).')
   p.add_argument('--popart_beta', type=float, default=3e-4)

@@ -62,15 +62,20 @@ class InferenceModel(object):
     two weight versions."""
     with self._lock:
       if self._stream is not None:
-        cur = torch.cuda.current_stream(self.device)
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        self._stream.wait_event(ev)
+        # the learner's stream (its params may live on another device:
+        # --inference_device)
+        cur = (torch.cuda.current_stream(flat_params.device)
+               if flat_params.is_cuda else None)
+        if cur is not None:
+          ev = torch.cuda.Event()
+          ev.record(cur)
+          self._stream.wait_event(ev)
         with torch.cuda.stream(self._stream):
           self.flat.params.copy_(flat_params, non_blocking=True)
           done = torch.cuda.Event()
           done.record(self._stream)
-        cur.wait_event(done)
+        if cur is not None:
+          cur.wait_event(done)
       else:
         self.flat.params.copy_(flat_params)
       self.version = self.version + 1 if version is None else version

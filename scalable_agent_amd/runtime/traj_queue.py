@@ -1,0 +1,176 @@
+"""Time-major trajectory batch queue (native csrc/envpool/traj_queue.cc).
+
+Replaces the reference's actor -> learner path (experiment.py:530-531
+FIFOQueue(1) + enqueue, :576 dequeue_many, :579-585 time-major transposes,
+:587-597 StagingArea put/get) with:
+
+  actors ──(write [t, b] in place)──> pinned shm slab = ONE learner batch
+  learner ──(ONE hipMemcpyAsync per step, copy stream)──> device slot
+                 ──(event)──> captured learner graph
+
+No unroll is ever stacked, transposed or memcpy'd on the host: each actor
+claims a column b of the slab being filled and writes every step's fields
+straight into their time-major position; the B-th commit publishes the slab.
+The slab memory is registered with HIP (hipHostRegister) so the learner's
+copy is a DMA from the actors' pages, overlapped with the previous step's
+compute.
+
+`BatchLayout` is the flat byte layout of one batch (256-B aligned segments,
+fields in ActorOutput order); the learner's device slots use the same layout,
+so host slab -> device slot is one contiguous copy.
+"""
+
+import ctypes
+import logging
+
+import numpy as np
+import torch
+
+from ..structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
+
+log = logging.getLogger('scalable_agent_amd')
+
+ALIGN = 256
+
+
+class BatchLayout(object):
+  """Offsets of every field of one [T+1, B] learner batch in a flat buffer."""
+
+  def __init__(self, T1, B, frame_shape, num_actions, use_instruction=False,
+               instr_len=16, core_size=256):
+    self.T1, self.B = T1, B
+    self.use_instruction = use_instruction
+    fields = [('level', (B,), np.int64),
+              ('c', (B, core_size), np.float32),
+              ('h', (B, core_size), np.float32),
+              ('reward', (T1, B), np.float32),
+              ('episode_return', (T1, B), np.float32),
+              ('episode_step', (T1, B), np.int32),
+              ('done', (T1, B), np.bool_),
+              ('frame', (T1, B) + tuple(frame_shape), np.uint8)]
+    if use_instruction:
+      fields += [('instr_ids', (T1, B, instr_len), np.int64),
+                 ('instr_len', (T1, B), np.int64)]
+    fields += [('action', (T1, B), np.int64),
+               ('policy_logits', (T1, B, num_actions), np.float32),
+               ('baseline', (T1, B), np.float32)]
+    self.fields = []
+    off = 0
+    for name, shape, dt in fields:
+      off = (off + ALIGN - 1) // ALIGN * ALIGN
+      nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
+      self.fields.append((name, shape, np.dtype(dt), off, nbytes))
+      off += nbytes
+    self.nbytes = (off + ALIGN - 1) // ALIGN * ALIGN
+
+  def numpy_views(self, buf):
+    """buf: a writable buffer of >= nbytes -> {field: ndarray view}."""
+    base = np.frombuffer(buf, dtype=np.uint8, count=self.nbytes)
+    return {name: base[off:off + nb].view(dt).reshape(shape)
+            for name, shape, dt, off, nb in self.fields}
+
+  def torch_views(self, flat):
+    """flat: a uint8 tensor (host or device) of >= nbytes -> ActorOutput of
+    tensor views (level_name = the [B] level-index tensor)."""
+    tdt = {np.dtype(np.int64): torch.int64, np.dtype(np.float32): torch.float32,
+           np.dtype(np.int32): torch.int32, np.dtype(np.bool_): torch.bool,
+           np.dtype(np.uint8): torch.uint8}
+    v = {name: flat[off:off + nb].view(tdt[dt]).view(shape)
+         for name, shape, dt, off, nb in self.fields}
+    instr = ((v['instr_ids'], v['instr_len']) if self.use_instruction
+             else None)
+    return ActorOutput(
+        level_name=v['level'], agent_state=(v['c'], v['h']),
+        env_outputs=StepOutput(v['reward'],
+                               StepOutputInfo(v['episode_return'],
+                                              v['episode_step']),
+                               v['done'], (v['frame'], instr)),
+        agent_outputs=AgentOutput(v['action'], v['policy_logits'],
+                                  v['baseline']))
+
+
+def _hip_host_register(address, nbytes):
+  """Pins an existing host mapping for async DMA; False if unavailable."""
+  try:
+    lib = ctypes.CDLL('libamdhip64.so')
+  except OSError:
+    return False
+  fn = lib.hipHostRegister
+  fn.restype = ctypes.c_int
+  fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+  return fn(ctypes.c_void_p(address), ctypes.c_size_t(nbytes), 0) == 0
+
+
+def _hip_host_unregister(address):
+  try:
+    lib = ctypes.CDLL('libamdhip64.so')
+    lib.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    lib.hipHostUnregister(ctypes.c_void_p(address))
+  except OSError:
+    pass
+
+
+class TrajectoryQueue(object):
+  """K slabs of one learner batch each; see the module docstring.
+
+  name='' : anonymous shared mapping (actor threads / forked processes);
+  '/name': a named POSIX shm object other processes can attach to.
+  """
+
+  def __init__(self, layout, num_slabs, name='', pin_device=None):
+    from . import native
+    self.layout = layout
+    self.q = native.TrajQueue(name, int(num_slabs), layout.nbytes, layout.B,
+                              True)
+    self.slab_bytes = self.q.slab_bytes
+    self._views = [layout.numpy_views(self.q.slab_view(s))
+                   for s in range(self.q.num_slabs)]
+    self.pinned = False
+    self._pin_addr = None
+    if pin_device is not None and torch.cuda.is_available():
+      # hipHostRegister the whole payload once: each slab is then a valid
+      # async-DMA source (torch sees a pinned pointer)
+      torch.cuda.init()
+      self.pinned = _hip_host_register(self.q.payload_address,
+                                       self.q.payload_bytes)
+      if self.pinned:
+        self._pin_addr = self.q.payload_address
+      else:
+        log.warning('hipHostRegister of the trajectory queue failed; the '
+                    'H2D copy will be a staged (pageable) copy')
+    self._tensors = [torch.frombuffer(self.q.slab_view(s),
+                                      dtype=torch.uint8)[:layout.nbytes]
+                     for s in range(self.q.num_slabs)]
+
+  # ---------------------------------------------------------- producers
+  def claim(self, timeout_ms=-1):
+    """-> (slab, column, numpy views of the slab); slab < 0: timeout/closed."""
+    s, col = self.q.claim(int(timeout_ms))
+    return s, col, (self._views[s] if s >= 0 else None)
+
+  def commit(self, slab):
+    self.q.commit(int(slab))
+
+  # ---------------------------------------------------------- consumer
+  def acquire(self, timeout_ms=-1):
+    return self.q.acquire(int(timeout_ms))
+
+  def release(self, slab):
+    self.q.release(int(slab))
+
+  def host_tensor(self, slab):
+    """uint8 tensor over the slab's bytes (pinned when registered)."""
+    return self._tensors[slab]
+
+  def host_views(self, slab):
+    return self._views[slab]
+
+  @property
+  def num_ready(self):
+    return self.q.num_ready
+
+  def close(self):
+    self.q.close()
+    if self._pin_addr is not None:
+      _hip_host_unregister(self._pin_addr)
+      self._pin_addr = None
