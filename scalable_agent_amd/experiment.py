@@ -222,6 +222,20 @@ class _TrajFeeder(object):
       for e in self.free:
         e.record()
 
+  def prepare(self):
+    """Captures both slots' learner graphs up front, on zero-filled slots
+    (the graph does not depend on the values), BEFORE the actor threads
+    start: no other thread touches the GPU during the captures."""
+    if not self.use_graph:
+      return
+    learner = self.learner
+    for j in range(len(self.slots)):
+      self.slots[j].zero_()
+      self.torch.cuda.synchronize(self.device)
+      learner.capture(self.views[j], clone=False)
+      self.graphs[j] = (learner._graph, learner._static_in,
+                        learner._static_loss)
+
   def _reap(self, block):
     while self.pending:
       slab, ev = self.pending[0]
@@ -419,6 +433,7 @@ def train(flags):
                            pin_device=device if device.type == 'cuda' else None)
       feeder = _TrajFeeder(tq, learner, device,
                            flags.use_hip_graph and device.type == 'cuda')
+      feeder.prepare()
 
     def actor_loop_traj(actor, level_index):
       try:
@@ -502,7 +517,8 @@ def train(flags):
         episode_logger.log_batch(batch_levels, info['done'],
                                  info['episode_return'], info['episode_step'],
                                  frames)
-        host_ms.append(1e3 * (time.time() - t_step - wait))
+        if steps > 2:  # the first steps include graph warmup
+          host_ms.append(1e3 * (time.time() - t_step - wait))
         host_actions = info['action']
       if not use_traj:
         t_wait = time.time()
@@ -590,7 +606,7 @@ def train(flags):
           scalars['allreduce_ms'] = 1e3 * learner.grad_sync.last_time_s
         writer.add_scalars(scalars, frames)
         if host_ms:
-          scalars['learner_host_ms'] = float(np.mean(host_ms[-100:]))
+          scalars['learner_host_ms'] = float(np.median(host_ms[-100:]))
         writer.add_histogram('action', host_actions, frames)
         writer.flush()
       if frames - last_log_frames >= flags.log_every_frames:
@@ -599,7 +615,7 @@ def train(flags):
                  'queue-wait %.0f%%  learner host %.2f ms/step', frames,
                  timer.frames_per_sec(), timer.steps_per_sec(), float(loss),
                  100 * timer.wait_fraction(),
-                 float(np.mean(host_ms[-100:])) if host_ms else 0.0)
+                 float(np.median(host_ms[-100:])) if host_ms else 0.0)
         health = learner.health()
         if health['skipped_updates'] > reported_skips:
           # loud, not fatal: the guard already dropped those updates
