@@ -131,7 +131,7 @@ def num_value_heads(flags):
   return len(level_names_for(flags)) if flags.popart else 1
 
 
-def _make_agent(flags, num_actions, frame_shape, device, seed):
+def _make_agent(flags, num_actions, frame_shape, device, seed, dtype=None):
   import torch
   from .models import Agent
   backend = 'torch'
@@ -141,7 +141,8 @@ def _make_agent(flags, num_actions, frame_shape, device, seed):
     backend = 'hip'
   elif getattr(flags, 'backend', 'auto') == 'hip':
     raise ValueError('--backend=hip needs a GPU device')
-  cdt = torch.bfloat16 if flags.dtype == 'bf16' else torch.float32
+  dtype = dtype or flags.dtype
+  cdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
   return Agent(num_actions, torso=flags.torso, frame_shape=frame_shape,
                seed=seed, backend=backend, compute_dtype=cdt,
                num_value_heads=num_value_heads(flags),
@@ -348,6 +349,9 @@ def train(flags):
                                            frame_shape, use_instr)
 
   rank, world, local_rank = parallel.world_info()
+  # many actor threads share the GIL with the learner thread: a short switch
+  # interval bounds how long the learner waits for it between GPU launches
+  sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
   # Env processes are forked BEFORE the GPU is initialised.
   distributed_actors = flags.task >= 0 and flags.job_name == 'learner'
   envs, actors_levels = [], []
@@ -410,8 +414,10 @@ def train(flags):
   else:
     inf_device = (device if flags.inference_device == 'auto' else
                   torch.device(flags.inference_device))
+    inf_dtype = (flags.dtype if flags.inference_dtype == 'auto' else
+                 flags.inference_dtype)
     inf_agent = _make_agent(flags, num_actions, frame_shape, inf_device,
-                            flags.seed)
+                            flags.seed, dtype=inf_dtype)
     model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
                                          seed=flags.seed + 17 * rank)
     model.publish(learner.flat.params)

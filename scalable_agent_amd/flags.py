@@ -89,6 +89,11 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--inference_min_batch', type=int, default=1)
   p.add_argument('--inference_max_batch', type=int, default=1024)
   p.add_argument('--inference_timeout_ms', type=int, default=100)
+  p.add_argument('--inference_dtype', default='auto',
+                 choices=['auto', 'fp32', 'bf16'],
+                 help='Actor-inference compute dtype (auto = --dtype); bf16 '
+                      'trades behaviour-policy precision (V-trace corrects '
+                      'for the policy lag either way) for actor throughput.')
   p.add_argument('--inference_device', default='auto',
                  help='Device of the actor-inference model: auto = the '
                       'learner device; e.g. cuda:1 or cpu.')
