@@ -248,8 +248,10 @@ class _TrajFeeder(object):
       self.tq.release(slab)
       block = False
 
-  def step(self, timeout_s, poison=False):
-    """-> (loss, host info dict, seconds waited for a full slab)."""
+  def step(self, timeout_s, poison=False, check=None):
+    """-> (loss, host info dict, seconds waited for a full slab).
+    self.last_host_s: host time of the step's data path (slab hand-off,
+    H2D enqueue, graph launch, slab release) excluding the wait."""
     torch = self.torch
     t0 = time.time()
     while True:
@@ -259,10 +261,13 @@ class _TrajFeeder(object):
         break
       if slab == -2:
         raise RuntimeError('trajectory queue closed')
+      if check is not None:
+        check()  # e.g. an actor-group process died
       if time.time() - t0 > timeout_s:
         raise RuntimeError('learner starved: no full batch for %.0fs' %
                            timeout_s)
-    wait = time.time() - t0
+    t1 = time.time()
+    wait = t1 - t0
     hv = self.tq.host_views(slab)
     info = {'level': hv['level'].copy(), 'done': hv['done'][1:].copy(),
             'episode_return': hv['episode_return'][1:].copy(),
@@ -276,6 +281,7 @@ class _TrajFeeder(object):
       self.tq.release(slab)
       loss = learner.step(self.views[0])
       self.k += 1
+      self.last_host_s = time.time() - t1
       return loss, info, wait
     j = self.k % 2
     with torch.cuda.stream(self.copy_stream):
@@ -299,6 +305,7 @@ class _TrajFeeder(object):
     self.free[j].record(comp)
     self.k += 1
     self._reap(block=len(self.pending) > 2)
+    self.last_host_s = time.time() - t1
     return loss, info, wait
 
   def close(self):
@@ -352,15 +359,43 @@ def train(flags):
   # many actor threads share the GIL with the learner thread: a short switch
   # interval bounds how long the learner waits for it between GPU launches
   sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
-  # Env processes are forked BEFORE the GPU is initialised.
+  # Env processes (and actor-group processes) are forked BEFORE the GPU is
+  # initialised.
   distributed_actors = flags.task >= 0 and flags.job_name == 'learner'
-  envs, actors_levels = [], []
+  use_groups = (flags.actor_groups > 0 and not distributed_actors and
+                flags.trajectory_queue and not flags.deterministic)
+  envs, actors_levels, actor_seeds = [], [], []
+  groups = shared_w = None
   if not distributed_actors:
     for i in range(flags.num_actors):
-      level = level_names[i % len(level_names)]
-      seed = flags.seed * 1000003 * (rank + 1) + i + 1
+      actors_levels.append(level_names[i % len(level_names)])
+      actor_seeds.append(flags.seed * 1000003 * (rank + 1) + i + 1)
+  if use_groups:
+    from .runtime.actor_group import ActorGroups, SharedWeights
+    from .runtime.traj_queue import BatchLayout, TrajectoryQueue
+    layout = BatchLayout(flags.unroll_length + 1, flags.batch_size,
+                         frame_shape, num_actions, use_instruction=use_instr)
+    tq = TrajectoryQueue(layout, max(3, -(-flags.num_actors //
+                                          flags.batch_size) + 2))
+    # created (sized) once the learner exists; the groups attach by name
+    shared_w_name = '/sa_w_%d_%d' % (os.getpid(), rank)
+    if flags.inference_device != 'auto':
+      group_dev = flags.inference_device
+    elif flags.device != 'auto':
+      group_dev = flags.device
+    else:  # device_count() does not initialise the GPU in this process
+      ndev = torch.cuda.device_count()
+      group_dev = 'cuda:%d' % (local_rank % ndev) if ndev else 'cpu'
+    groups = ActorGroups(
+        flags, level_names, actors_levels, actor_seeds, tq, shared_w_name,
+        frame_shape, action_set, use_instr, group_dev,
+        flags.dtype if flags.inference_dtype == 'auto' else
+        flags.inference_dtype)
+    log.info('%d actor group(s) over %d envs, inference on %s',
+             len(groups.procs), flags.num_actors, group_dev)
+  elif not distributed_actors:
+    for level, seed in zip(actors_levels, actor_seeds):
       envs.append(create_environment(flags, level, seed))
-      actors_levels.append(level)
     py_process.start_all(envs)
 
   rank, world, local_rank = parallel.init_distributed(
@@ -411,6 +446,16 @@ def train(flags):
                                                num_actions, learner)
     threading.Thread(target=transport.pump, args=(unroll_queue, stop),
                      daemon=True).start()
+  elif use_groups:
+    use_traj = True
+    actor_errors = []
+    tq.pin()
+    feeder = _TrajFeeder(tq, learner, device,
+                         flags.use_hip_graph and device.type == 'cuda')
+    feeder.prepare()
+    shared_w = SharedWeights(shared_w_name, learner.flat.numel, create=True)
+    shared_w.publish(learner.flat.params)  # groups start on these weights
+    shared_w.flush()
   else:
     inf_device = (device if flags.inference_device == 'auto' else
                   torch.device(flags.inference_device))
@@ -494,7 +539,7 @@ def train(flags):
   steps = 0
   use_graph = flags.use_hip_graph and device.type == 'cuda'
   staging = dev_stage = copied = None
-  host_ms = []
+  host_ms, loop_ms = [], []
   try:
     frames = int(learner.frames.item())
     while frames < flags.total_environment_frames:
@@ -505,7 +550,8 @@ def train(flags):
         with trace('learner_step'):
           loss, info, wait = feeder.step(
               flags.queue_timeout_secs,
-              poison=faults.get('learner_nan') == steps + 1)
+              poison=faults.get('learner_nan') == steps + 1,
+              check=groups.check if groups is not None else None)
         timer.add_wait(wait)
         steps += 1
         if (world > 1 and flags.consistency_check_steps and
@@ -515,6 +561,8 @@ def train(flags):
                              steps)
         if infer is not None:
           model.publish(learner.flat.params)
+        elif shared_w is not None:
+          shared_w.publish(learner.flat.params)
         # host frame counter (the device counter drives the LR schedule;
         # reading it every step would sync the host with the GPU)
         frames += learner.frames_per_step
@@ -524,7 +572,8 @@ def train(flags):
                                  info['episode_return'], info['episode_step'],
                                  frames)
         if steps > 2:  # the first steps include graph warmup
-          host_ms.append(1e3 * (time.time() - t_step - wait))
+          host_ms.append(1e3 * feeder.last_host_s)
+          loop_ms.append(1e3 * (time.time() - t_step - wait))
         host_actions = info['action']
       if not use_traj:
         t_wait = time.time()
@@ -602,7 +651,8 @@ def train(flags):
                    'frames_per_sec': timer.frames_per_sec(),
                    'learner_steps_per_sec': timer.steps_per_sec(),
                    'queue_wait_frac': timer.wait_fraction(),
-                   'env_restarts': sum(a.env_restarts for a in actors)}
+                   'env_restarts': (sum(a.env_restarts for a in actors) +
+                                    (groups.env_restarts if groups else 0))}
         scalars.update(learner.health())
         if infer is not None and infer.stats()['batches']:
           st = infer.stats()
@@ -613,15 +663,18 @@ def train(flags):
         writer.add_scalars(scalars, frames)
         if host_ms:
           scalars['learner_host_ms'] = float(np.median(host_ms[-100:]))
+          scalars['learner_loop_host_ms'] = float(np.median(loop_ms[-100:]))
         writer.add_histogram('action', host_actions, frames)
         writer.flush()
       if frames - last_log_frames >= flags.log_every_frames:
         last_log_frames = frames
         log.info('frames %d  %.0f frames/s  %.2f steps/s  loss %.3f  '
-                 'queue-wait %.0f%%  learner host %.2f ms/step', frames,
+                 'queue-wait %.0f%%  learner host %.2f ms/step (data path) '
+                 '%.2f ms/step (loop incl. logging)', frames,
                  timer.frames_per_sec(), timer.steps_per_sec(), float(loss),
                  100 * timer.wait_fraction(),
-                 float(np.median(host_ms[-100:])) if host_ms else 0.0)
+                 float(np.median(host_ms[-100:])) if host_ms else 0.0,
+                 float(np.median(loop_ms[-100:])) if loop_ms else 0.0)
         health = learner.health()
         if health['skipped_updates'] > reported_skips:
           # loud, not fatal: the guard already dropped those updates
@@ -641,6 +694,10 @@ def train(flags):
       feeder.close()
     if infer is not None:
       infer.close()
+    if groups is not None:
+      groups.close()
+      if shared_w is not None:
+        shared_w.close()
     for t in threads:
       t.join(timeout=5)
     py_process.close_all(envs)

@@ -101,6 +101,12 @@ def build_parser() -> argparse.ArgumentParser:
                  help='Local actors write time-major batches in place into '
                       'a pinned shared-memory slab queue (one H2D copy per '
                       'learner step); false: per-unroll queue + stacking.')
+  p.add_argument('--actor_groups', type=int, default=0,
+                 help='Run the num_actors envs as G vectorised actor-group '
+                      'processes (each: its envs stepped in parallel, one '
+                      'captured inference graph per step, writes into the '
+                      'trajectory queue); 0 = actor threads in the learner '
+                      'process.')
   p.add_argument('--popart', type=_str2bool, default=False,
                  help='PopArt value normalisation (north-star config #4).')
   p.add_argument('--popart_beta', type=float, default=3e-4)

@@ -362,3 +362,122 @@ def make_batched_infer(model, min_batch=1, max_batch=1024, timeout_ms=100,
   return dynamic_batching.batch_fn_with_options(
       minimum_batch_size=min_batch, maximum_batch_size=max_batch,
       timeout_ms=timeout_ms)(model.infer)
+
+
+class VectorInfer(object):
+  """Fixed-batch inference for one vectorised actor group
+  (runtime/actor_group.py): `rows` envs step in lockstep, so there is no
+  dynamic batcher - the group fills ONE pinned input slab, and one H2D copy,
+  one captured hipGraph (torso, core, heads + sampler; the LSTM state stays
+  on the device between steps) and one D2H copy of the packed outputs make
+  an inference step.  Without a GPU (tests) the same calls run eagerly.
+
+  Inputs (host numpy views, fill before `run()`): last_action [M] int64,
+  reward [M] f32, done [M] bool, frame [M, H, W, C] u8, instr_ids [M, L]
+  int64, instr_len [M] int64.  `run()` -> (action [M], logits [M, A],
+  baseline [M], c [M, core], h [M, core]) host numpy views of the state
+  AFTER the step (valid until the next run)."""
+
+  _IN = (('last_action', (), np.int64), ('reward', (), np.float32),
+         ('done', (), np.bool_), ('frame', None, np.uint8),
+         ('instr_ids', ('L',), np.int64), ('instr_len', (), np.int64))
+
+  def __init__(self, model, rows, frame_shape, num_actions, instr_len=16,
+               core_size=256, use_graph=None):
+    self.model = model
+    self.rows = M = int(rows)
+    dev = model.device
+    self.cuda = dev.type == 'cuda'
+    if use_graph is None:
+      use_graph = self.cuda and getattr(model.agent, 'backend', '') == 'hip'
+    self.use_graph = bool(use_graph) and self.cuda
+    shapes = {'frame': tuple(frame_shape), 'instr_ids': (int(instr_len),)}
+    layout, off = [], 0
+    for name, shape, dt in self._IN:
+      shape = shapes.get(name, shape)
+      nb = M * int(np.prod(shape, dtype=np.int64)) * np.dtype(dt).itemsize
+      layout.append((name, (M,) + tuple(shape), np.dtype(dt), off, nb))
+      off += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
+    self._in_bytes = off
+    self._in_host = self._host(off)
+    self._in_dev = (torch.empty(off, dtype=torch.uint8, device=dev)
+                    if self.cuda else self._in_host)
+    hnp = self._in_host.numpy()
+    self.inputs = {n: hnp[o:o + nb].view(dt).reshape(s)
+                   for n, s, dt, o, nb in layout}
+    self._dev_in = [self._in_dev[o:o + nb].view(_torch_dtype(dt)).view(*s)
+                    for n, s, dt, o, nb in layout]
+    # device-resident recurrent state
+    self.c = torch.zeros(M, core_size, device=dev)
+    self.h = torch.zeros(M, core_size, device=dev)
+    outs = [('action', (M,), torch.int64), ('logits', (M, num_actions),
+                                             torch.float32),
+            ('baseline', (M,), torch.float32), ('c', (M, core_size),
+                                                 torch.float32),
+            ('h', (M, core_size), torch.float32)]
+    self._out_layout, off = [], 0
+    for n, s, dt in outs:
+      nb = int(np.prod(s)) * torch.empty(0, dtype=dt).element_size()
+      self._out_layout.append((n, s, dt, off, nb))
+      off += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
+    self._out_host = self._host(off)
+    self._out_dev = (torch.empty(off, dtype=torch.uint8, device=dev)
+                     if self.cuda else self._out_host)
+    onp = self._out_host.numpy()
+    npdt = lambda dt: torch.empty(0, dtype=dt).numpy().dtype
+    self._outs = [onp[o:o + nb].view(npdt(dt)).reshape(s)
+                  for n, s, dt, o, nb in self._out_layout]
+    self._graphs = {}
+
+  def _host(self, nbytes):
+    t = torch.zeros(nbytes, dtype=torch.uint8)
+    return t.pin_memory() if self.cuda else t
+
+  def _body(self, has_instr):
+    """Device step: inputs -> packed outputs, state updated in place."""
+    m = self.model
+    la, rw, dn, fr, ids, ln = self._dev_in
+    action, logits, baseline, c2, h2 = m.step_device(
+        la, rw, dn, fr, ids, ln, self.c, self.h, has_instr=has_instr)
+    vals = [action, logits, baseline, c2, h2]
+    for (n, s, dt, o, nb), v in zip(self._out_layout, vals):
+      self._out_dev[o:o + nb].view(dt).view(*s).copy_(v)
+    self.c.copy_(c2)
+    self.h.copy_(h2)
+
+  def _capture(self, has_instr):
+    m = self.model
+    s = m.stream
+    with torch.cuda.stream(s):
+      # warm-up (lazy library init) then restore the state it advanced
+      c0, h0 = self.c.clone(), self.h.clone()
+      for _ in range(2):
+        self._body(has_instr)
+      self.c.copy_(c0)
+      self.h.copy_(h0)
+      s.synchronize()
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+        self._body(has_instr)
+    return g
+
+  @torch.no_grad()
+  def run(self):
+    m = self.model
+    has_instr = bool(m.use_instruction and
+                     int(self.inputs['instr_len'].max(initial=0)) > 0)
+    if not self.cuda:
+      self._body(has_instr)
+      return tuple(self._outs)
+    with m._lock, torch.cuda.stream(m.stream):
+      self._in_dev.copy_(self._in_host, non_blocking=True)
+      if self.use_graph:
+        g = self._graphs.get(has_instr)
+        if g is None:
+          g = self._graphs[has_instr] = self._capture(has_instr)
+        g.replay()
+      else:
+        self._body(has_instr)
+      self._out_host.copy_(self._out_dev, non_blocking=True)
+      m.stream.synchronize()
+    return tuple(self._outs)

@@ -346,12 +346,20 @@ class EnvProcess(object):
         pass
 
   def _rpc(self, name, *args):
+    return self._recv(self._send(name, args))
+
+  def _send(self, name, args):
     if self._closed:
       raise OutOfRangeError('env process closed')
     self._seq += 1
-    seq = self._seq
     try:
-      self._conn.send((seq, name, args))
+      self._conn.send((self._seq, name, args))
+    except (EOFError, OSError):
+      raise OutOfRangeError('env process closed')
+    return self._seq
+
+  def _recv(self, seq):
+    try:
       while True:
         if self._timeout and not self._conn.poll(self._timeout):
           self._kill_worker()  # hung: the supervisor forks a replacement
@@ -374,6 +382,27 @@ class EnvProcess(object):
   def step(self, action):
     reward, done, instr = self._rpc('step', action)
     return np.float32(reward), np.bool_(done), [self._frames.copy(), instr]
+
+  # split-phase calls for vectorised actors (runtime/actor_group.py): send
+  # the step of every env first, then collect the replies, so the envs of a
+  # group step in parallel; the frame is read in place from `frame_view`
+  def step_send(self, action):
+    return self._send('step', (action,))
+
+  def step_recv(self, seq):
+    """-> (reward, done, instruction); the frame is in `frame_view`."""
+    reward, done, instr = self._recv(seq)
+    return reward, done, instr
+
+  def initial_nocopy(self):
+    (instr,) = self._rpc('initial')
+    return instr
+
+  @property
+  def frame_view(self):
+    """The shared-memory frame of the last initial()/step() (overwritten by
+    the next call)."""
+    return self._frames
 
   def close(self):
     if self._closed or self._process is None:

@@ -1,0 +1,483 @@
+"""Vectorised actor groups in their own processes (--actor_groups=G).
+
+The reference runs every actor as a TF thread of the learner process
+(experiment.py:534-546: one env per actor, per-step `dynamic_batching`
+inference, experiment.py:240-321 for the unroll loop); the threads share
+one interpreter, so with tens of actors the learner's own host work waits on
+the GIL.  Here the `num_actors` envs are split over G group processes, each
+forked before the learner initialises the GPU:
+
+  group g:  M = num_actors / G envs (EnvProcess children, stepped in
+            parallel: every env's step is sent before any reply is read)
+            one VectorInfer: a pinned [M] input slab -> one H2D -> one
+            captured hipGraph (torso/core/heads/sampler, LSTM state resident
+            on the device) -> one D2H of the packed outputs
+            writes every step of every env straight into its claimed column
+            of the learner's time-major TrajectoryQueue slab
+  learner:  consumes full slabs (experiment._TrajFeeder), publishes weights
+            into a SharedWeights seqlock region with ONE async D2H copy per
+            step; groups pick a new version up with an async H2D copy into a
+            staging buffer, validated by the seqlock before it becomes the
+            inference snapshot (never a torn snapshot).
+
+Each env's unroll keeps the reference's layout: element 0 repeats the last
+element of the previous unroll, the recorded agent state is the state at the
+start of the unroll.  An env worker that dies mid-unroll is replaced and its
+column continues from the new episode's first frame with done=True (the
+learner's V-trace and the LSTM reset treat it as an episode boundary).
+"""
+
+import logging
+import mmap
+import os
+import time
+
+import numpy as np
+
+log = logging.getLogger('scalable_agent_amd')
+
+
+class SharedWeights(object):
+  """fp32 parameter snapshots in an anonymous shared mapping (inherited by
+  forked groups): TWO buffers, each with its own seqlock count (odd = being
+  written), plus `latest` (the buffer of the newest complete snapshot) and
+  `version` (number of completed publishes; 0 = none yet).
+
+  Learner: `publish(flat_params)` enqueues ONE async D2H copy, ordered after
+  the learner's stream, into the buffer that is NOT `latest`, straight from
+  the device into the (hipHostRegister-ed) mapping; the next publish (or
+  `flush()`) that finds the copy landed flips `latest` to it.  A publish
+  while the previous copy is still in flight is skipped (the groups take the
+  next one), so `latest` always names a complete snapshot and readers never
+  wait on the learner's GPU work.
+  Group: ActorGroupWorker._sync_weights (copy `latest`, then re-check its
+  seqlock count: a torn copy is discarded)."""
+
+  HDR = 4096
+  MAGIC = 0x5341574549474854
+
+  def __init__(self, name, numel=0, create=False):
+    """name: a POSIX shm name ('/...'); the learner creates it once it
+    knows the parameter count, the groups (forked earlier) attach to it."""
+    self.name = name
+    self._path = '/dev/shm' + name
+    self._owner = create
+    if create:
+      fd = os.open(self._path, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+      os.ftruncate(fd, self.HDR + 8 * int(numel))
+    else:
+      fd = os.open(self._path, os.O_RDWR)
+    size = os.fstat(fd).st_size
+    self._mm = mmap.mmap(fd, size)
+    os.close(fd)
+    self.numel = (size - self.HDR) // 8
+    # [0] latest buffer (-1 none), [1] version, [2:4] per-buffer seqlock,
+    # [4] magic (written last by the creator)
+    self._hdr = np.frombuffer(self._mm, dtype=np.int64, count=5)
+    if create:
+      self._hdr[0] = -1
+      self._hdr[4] = self.MAGIC
+    self._all = np.frombuffer(self._mm, dtype=np.float32,
+                              count=2 * self.numel, offset=self.HDR)
+    self.data = [self._all[:self.numel], self._all[self.numel:]]
+    self._pinned = False
+    self._tensors = None
+    self._pending = None
+    self._stream = None
+    self.skipped = 0
+
+  # --------------------------------------------------------------- both
+  def version(self):
+    return int(self._hdr[1])
+
+  def latest(self):
+    return int(self._hdr[0])
+
+  def seq(self, b):
+    return int(self._hdr[2 + b])
+
+  def tensors(self, device):
+    """Torch views of the two buffers (host-registered on a GPU device)."""
+    import torch
+    from .traj_queue import _hip_host_register
+    if self._tensors is None:
+      if device.type == 'cuda':
+        self._pinned = _hip_host_register(self._all.ctypes.data,
+                                          8 * self.numel)
+      self._tensors = [torch.from_numpy(d) for d in self.data]
+    return self._tensors
+
+  # --------------------------------------------------------------- learner
+  def _finish(self, block):
+    if self._pending is None:
+      return True
+    b, ev = self._pending
+    if not block and not ev.query():
+      return False
+    ev.synchronize()
+    self._pending = None
+    self._hdr[2 + b] += 1  # even: complete
+    self._hdr[0] = b
+    self._hdr[1] += 1
+    return True
+
+  def _target(self):
+    b = 1 - self.latest() if self.latest() >= 0 else 0
+    self._hdr[2 + b] += 1  # odd: being written
+    return b
+
+  def publish(self, flat_params):
+    import torch
+    if not flat_params.is_cuda:
+      b = self._target()
+      self.data[b][...] = flat_params.detach().numpy()
+      self._pending = (b, _Done())
+      self._finish(block=True)
+      return True
+    if not self._finish(block=False):
+      self.skipped += 1
+      return False
+    host = self.tensors(flat_params.device)
+    if self._stream is None:
+      self._stream = torch.cuda.Stream(flat_params.device)
+    self._stream.wait_stream(torch.cuda.current_stream(flat_params.device))
+    b = self._target()
+    with torch.cuda.stream(self._stream):
+      host[b].copy_(flat_params.detach(), non_blocking=self._pinned)
+      ev = torch.cuda.Event()
+      ev.record(self._stream)
+    self._pending = (b, ev)
+    return True
+
+  def flush(self):
+    self._finish(block=True)
+
+  @classmethod
+  def attach(cls, name, alive, timeout_s=600):
+    """Group side: wait until the learner created `name` (alive() False or
+    the timeout -> None)."""
+    deadline = time.time() + timeout_s
+    while alive() and time.time() < deadline:
+      try:
+        w = cls(name)
+        if w.numel > 0 and int(w._hdr[4]) == cls.MAGIC:
+          return w
+        w.close()
+      except (OSError, ValueError):
+        pass
+      time.sleep(0.01)
+    return None
+
+  def close(self):
+    self.flush() if self._owner else None
+    self._tensors = None
+    self.data = self._all = self._hdr = None
+    try:
+      self._mm.close()
+    except BufferError:
+      pass  # views still referenced elsewhere; the mapping dies with them
+    if self._owner:
+      try:
+        os.unlink(self._path)
+      except OSError:
+        pass
+
+  # --------------------------------------------------------------- group
+  def read_into(self, out):
+    """Host reader: consistent copy of the latest snapshot -> version."""
+    while True:
+      v, b = self.version(), self.latest()
+      if b < 0:
+        return 0
+      s = self.seq(b)
+      if s & 1:
+        continue
+      out[...] = self.data[b]
+      if self.seq(b) == s:
+        return v
+
+
+class _Done(object):
+  def query(self):
+    return True
+
+  def synchronize(self):
+    pass
+
+
+def split_actors(num_actors, groups):
+  """Actor indices per group: contiguous, sizes differ by at most one."""
+  groups = max(1, min(int(groups), int(num_actors)))
+  base, extra = divmod(int(num_actors), groups)
+  out, start = [], 0
+  for g in range(groups):
+    n = base + (1 if g < extra else 0)
+    out.append(list(range(start, start + n)))
+    start += n
+  return out
+
+
+class ActorGroupWorker(object):
+  """Body of one group process (see the module docstring)."""
+
+  def __init__(self, gid, spec, tq, weights, counters, device_str):
+    self.gid = gid
+    self.spec = spec
+    self.tq = tq
+    self.weights = weights
+    self.counters = counters
+    self.device_str = device_str
+
+  def run(self):
+    import torch
+    from .. import py_process
+    from ..actor import encode_instruction
+    from ..experiment import _make_agent, create_environment
+    from ..inference import InferenceModel, VectorInfer
+
+    sp = self.spec
+    flags = sp['flags']
+    envs = [create_environment(flags, lvl, seed)
+            for lvl, seed in zip(sp['levels'], sp['seeds'])]
+    py_process.start_all(envs)  # forked before this process touches the GPU
+    try:
+      device = torch.device(self.device_str)
+      if device.type == 'cuda':
+        torch.cuda.set_device(device)
+      agent = _make_agent(flags, sp['num_actions'], sp['frame_shape'], device,
+                          flags.seed, dtype=sp['dtype'])
+      model = InferenceModel(agent, device, sp['use_instr'],
+                             seed=flags.seed + 7919 * (self.gid + 1))
+      M = len(envs)
+      vi = VectorInfer(model, M, sp['frame_shape'], sp['num_actions'])
+      parent = os.getppid()
+      self.weights = SharedWeights.attach(
+          self.weights, lambda: os.getppid() == parent and not self.tq.closed)
+      if self.weights is None:
+        return
+      self._loop(envs, model, vi, encode_instruction, py_process)
+    finally:
+      py_process.close_all(envs)
+
+  # ------------------------------------------------------------ weights
+  def _sync_weights(self, model, state):
+    """Non-blocking fetch of a newer snapshot: an async H2D of the `latest`
+    buffer into a staging buffer; once it has landed and that buffer's
+    seqlock count is unchanged, a D2D copy (ordered before the next
+    inference) makes it the inference snapshot."""
+    import torch
+    w = self.weights
+    v = w.version()
+    if model.device.type != 'cuda':
+      if v and v != state['version']:
+        host = np.empty(w.numel, np.float32)
+        state['version'] = w.read_into(host)
+        model.flat.params.copy_(torch.from_numpy(host))
+      return
+    if state.get('inflight') is not None:
+      v, b, s, ev = state['inflight']
+      if not ev.query():
+        return
+      state['inflight'] = None
+      if w.seq(b) == s:  # not overwritten while the copy ran
+        with torch.cuda.stream(model.stream):
+          model.flat.params.copy_(state['staging'], non_blocking=True)
+        state['version'] = v
+      return
+    if v == 0 or v == state['version']:
+      return
+    b = w.latest()
+    s = w.seq(b)
+    if s & 1:
+      return
+    if state.get('staging') is None:
+      state['staging'] = torch.empty(w.numel, dtype=torch.float32,
+                                     device=model.device)
+      state['copy_stream'] = torch.cuda.Stream(model.device)
+    host = w.tensors(model.device)
+    cs = state['copy_stream']
+    # the previous D2D out of the staging buffer must be done first
+    cs.wait_stream(model.stream)
+    with torch.cuda.stream(cs):
+      state['staging'].copy_(host[b], non_blocking=w._pinned)
+      ev = torch.cuda.Event()
+      ev.record(cs)
+    state['inflight'] = (v, b, s, ev)
+
+  # ------------------------------------------------------------ loop
+  def _loop(self, envs, model, vi, encode_instruction, py_process):
+    sp = self.spec
+    T = sp['unroll_length']
+    action_set = sp['action_set']
+    level_index = sp['level_index']
+    use_instr = sp['use_instr']
+    M = len(envs)
+    inp = vi.inputs
+    wstate = {'version': -1}
+    # per-env step bookkeeping (FlowEnvironment semantics)
+    reward = np.zeros(M, np.float32)
+    done = np.ones(M, np.bool_)
+    ep_ret = np.zeros(M, np.float32)
+    ep_step = np.zeros(M, np.int32)
+    run_ret = np.zeros(M, np.float32)
+    run_step = np.zeros(M, np.int32)
+    instr = [None] * M
+    action = np.zeros(M, np.int64)
+    logits = np.zeros((M, sp['num_actions']), np.float32)
+    baseline = np.zeros(M, np.float32)
+    c_host = np.zeros((M, vi.c.shape[1]), np.float32)
+    h_host = np.zeros((M, vi.h.shape[1]), np.float32)
+    for i, env in enumerate(envs):
+      instr[i] = env.initial_nocopy()
+    restarts = 0
+    deadline_check = time.time()
+    parent = os.getppid()
+    # the first snapshot (e.g. a restored checkpoint) before any inference
+    while wstate['version'] <= 0:
+      if os.getppid() != parent or self.tq.closed:
+        return
+      self._sync_weights(model, wstate)
+      time.sleep(0.002)
+    while True:
+      if time.time() - deadline_check > 1.0:
+        deadline_check = time.time()
+        if os.getppid() != parent:
+          return  # the learner went away
+      self._sync_weights(model, wstate)
+      # claim one column per env
+      cols = []
+      for i in range(M):
+        while True:
+          s, col, v = self.tq.claim(timeout_ms=200)
+          if s >= 0:
+            break
+          if s == -2 or os.getppid() != parent:
+            return
+        cols.append((s, col, v))
+        v['level'][col] = level_index[i]
+        v['c'][col] = c_host[i]
+        v['h'][col] = h_host[i]
+
+      def record(t):
+        for i, (s, col, v) in enumerate(cols):
+          v['frame'][t, col] = envs[i].frame_view
+          v['reward'][t, col] = reward[i]
+          v['done'][t, col] = done[i]
+          v['episode_return'][t, col] = ep_ret[i]
+          v['episode_step'][t, col] = ep_step[i]
+          v['action'][t, col] = action[i]
+          v['policy_logits'][t, col] = logits[i]
+          v['baseline'][t, col] = baseline[i]
+          if use_instr and 'instr_ids' in v:
+            v['instr_ids'][t, col], v['instr_len'][t, col] = (
+                encode_instruction(instr[i]))
+
+      record(0)
+      for t in range(1, T + 1):
+        inp['last_action'][:] = action
+        inp['reward'][:] = reward
+        inp['done'][:] = done
+        for i in range(M):
+          inp['frame'][i] = envs[i].frame_view
+          if use_instr:
+            inp['instr_ids'][i], inp['instr_len'][i] = encode_instruction(
+                instr[i])
+        a, lg, b, c2, h2 = vi.run()
+        action[:] = a
+        logits[:] = lg
+        baseline[:] = b
+        c_host[:] = c2
+        h_host[:] = h2
+        seqs = [None] * M
+        for i in range(M):
+          try:
+            seqs[i] = envs[i].step_send(action_set[int(action[i])])
+          except py_process.EnvRestartedError:
+            seqs[i] = None
+        for i in range(M):
+          try:
+            if seqs[i] is None:
+              raise py_process.EnvRestartedError('send failed')
+            r, d, instr[i] = envs[i].step_recv(seqs[i])
+          except py_process.EnvRestartedError as e:
+            restarts += 1
+            self.counters[self.gid] = restarts
+            log.warning('actor group %d env %d: %s; episode truncated (the '
+                        'column continues from a fresh episode)', self.gid, i, e)
+            instr[i] = envs[i].initial_nocopy()
+            r, d = 0.0, True
+          reward[i] = r
+          done[i] = d
+          run_ret[i] += r
+          run_step[i] += 1
+          ep_ret[i] = run_ret[i]
+          ep_step[i] = run_step[i]
+          if d:
+            run_ret[i] = 0.0
+            run_step[i] = 0
+        record(t)
+      for s, col, v in cols:
+        self.tq.commit(s)
+
+
+def _group_main(gid, spec, tq, weights, counters, device_str):
+  import faulthandler
+  import signal
+  faulthandler.enable()
+  signal.signal(signal.SIGINT, signal.SIG_IGN)
+  logging.basicConfig(level=logging.INFO,
+                      format='[%(asctime)s %(levelname)s group%(gid)s] '
+                             '%(message)s'.replace('%(gid)s', str(gid)))
+  try:
+    ActorGroupWorker(gid, spec, tq, weights, counters, device_str).run()
+  except Exception:  # pylint: disable=broad-except
+    log.exception('actor group %d failed', gid)
+    os._exit(3)
+  os._exit(0)
+
+
+class ActorGroups(object):
+  """Learner-side handle: forks the groups (call BEFORE the learner process
+  initialises the GPU), liveness checks, shutdown."""
+
+  def __init__(self, flags, level_names, actor_levels, actor_seeds, tq,
+               weights, frame_shape, action_set, use_instr, device_str,
+               dtype):
+    import multiprocessing
+    ctx = multiprocessing.get_context('fork')
+    self.tq = tq
+    self.counters = ctx.RawArray('q', max(1, flags.actor_groups))
+    self.procs = []
+    index = {l: i for i, l in enumerate(level_names)}
+    for gid, members in enumerate(split_actors(flags.num_actors,
+                                               flags.actor_groups)):
+      spec = dict(flags=flags, levels=[actor_levels[i] for i in members],
+                  seeds=[actor_seeds[i] for i in members],
+                  level_index=[index[actor_levels[i]] for i in members],
+                  num_actions=len(action_set), action_set=action_set,
+                  frame_shape=tuple(frame_shape), use_instr=use_instr,
+                  unroll_length=flags.unroll_length, dtype=dtype)
+      p = ctx.Process(target=_group_main,
+                      args=(gid, spec, tq, weights, self.counters, device_str),
+                      daemon=False, name='actor-group-%d' % gid)
+      p.start()
+      self.procs.append(p)
+
+  @property
+  def env_restarts(self):
+    return int(sum(self.counters))
+
+  def check(self):
+    for p in self.procs:
+      if p.exitcode is not None:
+        raise RuntimeError('actor group %s exited with code %s' %
+                           (p.name, p.exitcode))
+
+  def close(self, timeout=30):
+    self.tq.close()
+    deadline = time.time() + timeout
+    for p in self.procs:
+      p.join(max(0.1, deadline - time.time()))
+      if p.is_alive():
+        p.terminate()
+        p.join(5)

@@ -127,20 +127,27 @@ class TrajectoryQueue(object):
                    for s in range(self.q.num_slabs)]
     self.pinned = False
     self._pin_addr = None
-    if pin_device is not None and torch.cuda.is_available():
-      # hipHostRegister the whole payload once: each slab is then a valid
-      # async-DMA source (torch sees a pinned pointer)
-      torch.cuda.init()
-      self.pinned = _hip_host_register(self.q.payload_address,
-                                       self.q.payload_bytes)
-      if self.pinned:
-        self._pin_addr = self.q.payload_address
-      else:
-        log.warning('hipHostRegister of the trajectory queue failed; the '
-                    'H2D copy will be a staged (pageable) copy')
+    if pin_device is not None:
+      self.pin()
     self._tensors = [torch.frombuffer(self.q.slab_view(s),
                                       dtype=torch.uint8)[:layout.nbytes]
                      for s in range(self.q.num_slabs)]
+
+  def pin(self):
+    """hipHostRegister the whole payload once: each slab is then a valid
+    async-DMA source (torch sees a pinned pointer).  Call after any fork of
+    producer processes (the registration is per process)."""
+    if self.pinned or not torch.cuda.is_available():
+      return self.pinned
+    torch.cuda.init()
+    self.pinned = _hip_host_register(self.q.payload_address,
+                                     self.q.payload_bytes)
+    if self.pinned:
+      self._pin_addr = self.q.payload_address
+    else:
+      log.warning('hipHostRegister of the trajectory queue failed; the '
+                  'H2D copy will be a staged (pageable) copy')
+    return self.pinned
 
   # ---------------------------------------------------------- producers
   def claim(self, timeout_ms=-1):
@@ -164,6 +171,10 @@ class TrajectoryQueue(object):
 
   def host_views(self, slab):
     return self._views[slab]
+
+  @property
+  def closed(self):
+    return bool(self.q.closed)
 
   @property
   def num_ready(self):
