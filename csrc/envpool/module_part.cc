@@ -59,6 +59,10 @@ void register_envpool(py::module& m) {
              py::gil_scoped_release nogil;
              return q.Claim(t);
            }, py::arg("timeout_ms") = -1)
+      .def("claim_n", [](TrajQueue& q, int64_t n, int64_t t) {
+             py::gil_scoped_release nogil;
+             return q.ClaimN(n, t);
+           }, py::arg("n"), py::arg("timeout_ms") = -1)
       .def("commit", &TrajQueue::Commit)
       .def("acquire", [](TrajQueue& q, int64_t t) {
              py::gil_scoped_release nogil;

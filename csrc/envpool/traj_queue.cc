@@ -127,36 +127,62 @@ bool TrajQueue::WaitChange(uint32_t seen, int64_t timeout_ms) {
 }
 
 std::pair<int64_t, int64_t> TrajQueue::Claim(int64_t timeout_ms) {
-  using clock = std::chrono::steady_clock;
-  const auto deadline = clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+  auto r = ClaimN(1, timeout_ms);
+  if (r.first < 0) return {r.first, r.first};
+  return r.second[0];
+}
+
+int64_t TrajQueue::CapacityLocked() const {
+  int64_t cap = 0;
+  const int64_t f = hdr_->filling.load(std::memory_order_relaxed);
+  if (f >= 0) cap += batch_ - static_cast<int64_t>(slabs_[f].claimed.load(std::memory_order_relaxed));
+  for (int64_t i = 0; i < num_slabs_; ++i)
+    if (slabs_[i].state.load(std::memory_order_acquire) == kFree) cap += batch_;
+  return cap;
+}
+
+std::pair<int64_t, int64_t> TrajQueue::ClaimLocked() {
   const uint32_t B = static_cast<uint32_t>(batch_);
+  const int64_t s = hdr_->filling.load(std::memory_order_relaxed);
+  if (s >= 0) {
+    const uint32_t col = slabs_[s].claimed.fetch_add(1, std::memory_order_relaxed);
+    if (col + 1 >= B) hdr_->filling.store(-1, std::memory_order_relaxed);
+    return {s, static_cast<int64_t>(col)};
+  }
+  for (int64_t i = 0; i < num_slabs_; ++i) {
+    if (slabs_[i].state.load(std::memory_order_acquire) == kFree) {
+      slabs_[i].claimed.store(1, std::memory_order_relaxed);
+      slabs_[i].done.store(0, std::memory_order_relaxed);
+      slabs_[i].seq.store(hdr_->fill_seq.fetch_add(1), std::memory_order_relaxed);
+      slabs_[i].state.store(kFilling, std::memory_order_release);
+      hdr_->filling.store(B > 1 ? i : -1, std::memory_order_relaxed);
+      return {i, 0};
+    }
+  }
+  return {-1, -1};  // unreachable when the capacity was checked
+}
+
+std::pair<int64_t, std::vector<std::pair<int64_t, int64_t>>> TrajQueue::ClaimN(
+    int64_t n, int64_t timeout_ms) {
+  using clock = std::chrono::steady_clock;
+  if (n <= 0 || n > batch_ * num_slabs_) throw std::invalid_argument("ClaimN: bad column count");
+  const auto deadline = clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+  std::vector<std::pair<int64_t, int64_t>> out;
   while (true) {
-    if (hdr_->closed.load()) return {-2, -2};
+    if (hdr_->closed.load()) return {-2, {}};
     const uint32_t seen = hdr_->futex_word.load(std::memory_order_acquire);
     Lock();
-    int64_t s = hdr_->filling.load(std::memory_order_relaxed);
-    if (s >= 0) {
-      const uint32_t col = slabs_[s].claimed.fetch_add(1, std::memory_order_relaxed);
-      if (col + 1 >= B) hdr_->filling.store(-1, std::memory_order_relaxed);
+    if (CapacityLocked() >= n) {
+      out.reserve(static_cast<size_t>(n));
+      for (int64_t k = 0; k < n; ++k) out.push_back(ClaimLocked());
       Unlock();
-      return {s, static_cast<int64_t>(col)};
-    }
-    for (int64_t i = 0; i < num_slabs_; ++i) {
-      if (slabs_[i].state.load(std::memory_order_acquire) == kFree) {
-        slabs_[i].claimed.store(1, std::memory_order_relaxed);
-        slabs_[i].done.store(0, std::memory_order_relaxed);
-        slabs_[i].seq.store(hdr_->fill_seq.fetch_add(1), std::memory_order_relaxed);
-        slabs_[i].state.store(kFilling, std::memory_order_release);
-        hdr_->filling.store(B > 1 ? i : -1, std::memory_order_relaxed);
-        Unlock();
-        return {i, 0};
-      }
+      return {0, std::move(out)};
     }
     Unlock();
     int64_t left = -1;
     if (timeout_ms >= 0) {
       left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - clock::now()).count();
-      if (left <= 0) return {-1, -1};
+      if (left <= 0) return {-1, {}};
     }
     WaitChange(seen, left < 0 ? 100 : std::min<int64_t>(left, 100));
   }

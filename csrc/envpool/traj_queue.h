@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <string>
 #include <utility>
+#include <vector>
 
 namespace sa {
 
@@ -43,6 +44,12 @@ class TrajQueue {
   // -> (slab, column); (-1, -1) on timeout, (-2, -2) when closed.
   // timeout_ms < 0 waits forever.
   std::pair<int64_t, int64_t> Claim(int64_t timeout_ms);
+  // All-or-nothing claim of n columns (a producer that steps several envs in
+  // lockstep must never hold some columns while it waits for the rest: the
+  // slabs those sit in could then never fill).  -> status 0 and the n
+  // (slab, column) pairs, or status -1 timeout / -2 closed and no columns.
+  std::pair<int64_t, std::vector<std::pair<int64_t, int64_t>>> ClaimN(int64_t n,
+                                                                      int64_t timeout_ms);
   // Marks one claimed column of `slab` written; the last one publishes it.
   void Commit(int64_t slab);
   // Oldest READY slab (by fill order); -1 timeout, -2 closed.
@@ -80,6 +87,8 @@ class TrajQueue {
     std::atomic<uint64_t> seq;         // fill order
   };
 
+  std::pair<int64_t, int64_t> ClaimLocked();  // lock held, capacity checked
+  int64_t CapacityLocked() const;
   void Lock();
   void Unlock();
   void Bump();

@@ -107,6 +107,9 @@ def build_parser() -> argparse.ArgumentParser:
                       'captured inference graph per step, writes into the '
                       'trajectory queue); 0 = actor threads in the learner '
                       'process.')
+  p.add_argument('--actor_group_splits', type=int, default=2,
+                 help='Pipeline stages per actor group: split k\'s inference '
+                      'runs on the GPU while the envs of another split step.')
   p.add_argument('--popart', type=_str2bool, default=False,
                  help='PopArt value normalisation (north-star config #4).')
   p.add_argument('--popart_beta', type=float, default=3e-4)

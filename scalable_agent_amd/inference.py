@@ -428,6 +428,7 @@ class VectorInfer(object):
     self._outs = [onp[o:o + nb].view(npdt(dt)).reshape(s)
                   for n, s, dt, o, nb in self._out_layout]
     self._graphs = {}
+    self._done = None
 
   def _host(self, nbytes):
     t = torch.zeros(nbytes, dtype=torch.uint8)
@@ -462,13 +463,15 @@ class VectorInfer(object):
     return g
 
   @torch.no_grad()
-  def run(self):
+  def launch(self):
+    """Enqueues H2D + step + D2H on the model's stream; the input slab may
+    be rewritten (and the outputs read) only after `wait()`."""
     m = self.model
     has_instr = bool(m.use_instruction and
                      int(self.inputs['instr_len'].max(initial=0)) > 0)
     if not self.cuda:
       self._body(has_instr)
-      return tuple(self._outs)
+      return
     with m._lock, torch.cuda.stream(m.stream):
       self._in_dev.copy_(self._in_host, non_blocking=True)
       if self.use_graph:
@@ -479,5 +482,19 @@ class VectorInfer(object):
       else:
         self._body(has_instr)
       self._out_host.copy_(self._out_dev, non_blocking=True)
-      m.stream.synchronize()
+      if self._done is None:
+        self._done = torch.cuda.Event()
+      self._done.record(m.stream)
+
+  def wait(self):
+    if self.cuda:
+      # poll + yield: a spinning hipEventSynchronize per group process would
+      # take CPU from the env workers, a blocking (interrupt) wait adds
+      # wake-up latency to every step
+      while not self._done.query():
+        time.sleep(0)
     return tuple(self._outs)
+
+  def run(self):
+    self.launch()
+    return self.wait()

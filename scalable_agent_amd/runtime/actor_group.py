@@ -227,6 +227,7 @@ class ActorGroupWorker(object):
     self.weights = weights
     self.counters = counters
     self.device_str = device_str
+    self.restarts = 0
 
   def run(self):
     import torch
@@ -248,14 +249,16 @@ class ActorGroupWorker(object):
                           flags.seed, dtype=sp['dtype'])
       model = InferenceModel(agent, device, sp['use_instr'],
                              seed=flags.seed + 7919 * (self.gid + 1))
-      M = len(envs)
-      vi = VectorInfer(model, M, sp['frame_shape'], sp['num_actions'])
+      K = max(1, min(int(sp['splits']), len(envs)))
+      vis = [VectorInfer(model, len(part), sp['frame_shape'],
+                         sp['num_actions'])
+             for part in split_actors(len(envs), K)]
       parent = os.getppid()
       self.weights = SharedWeights.attach(
           self.weights, lambda: os.getppid() == parent and not self.tq.closed)
       if self.weights is None:
         return
-      self._loop(envs, model, vi, encode_instruction, py_process)
+      self._loop(envs, model, vis, encode_instruction, py_process)
     finally:
       py_process.close_all(envs)
 
@@ -305,32 +308,19 @@ class ActorGroupWorker(object):
     state['inflight'] = (v, b, s, ev)
 
   # ------------------------------------------------------------ loop
-  def _loop(self, envs, model, vi, encode_instruction, py_process):
-    sp = self.spec
-    T = sp['unroll_length']
-    action_set = sp['action_set']
-    level_index = sp['level_index']
-    use_instr = sp['use_instr']
-    M = len(envs)
-    inp = vi.inputs
+  def _loop(self, envs, model, vis, encode_instruction, py_process):
+    """K splits of the group's envs, each with its own VectorInfer, run as a
+    pipeline: while split k's inference runs on the GPU, the host steps the
+    envs of the split whose inference just finished (their env processes
+    step in parallel), so neither the GPU latency nor the env latency is
+    exposed once per step of the group."""
+    K = len(vis)
+    sizes = [vi.rows for vi in vis]
+    offs = np.cumsum([0] + sizes)
+    splits = [_Split(self, envs[offs[k]:offs[k + 1]], vis[k],
+                     self.spec['level_index'][offs[k]:offs[k + 1]],
+                     encode_instruction, py_process) for k in range(K)]
     wstate = {'version': -1}
-    # per-env step bookkeeping (FlowEnvironment semantics)
-    reward = np.zeros(M, np.float32)
-    done = np.ones(M, np.bool_)
-    ep_ret = np.zeros(M, np.float32)
-    ep_step = np.zeros(M, np.int32)
-    run_ret = np.zeros(M, np.float32)
-    run_step = np.zeros(M, np.int32)
-    instr = [None] * M
-    action = np.zeros(M, np.int64)
-    logits = np.zeros((M, sp['num_actions']), np.float32)
-    baseline = np.zeros(M, np.float32)
-    c_host = np.zeros((M, vi.c.shape[1]), np.float32)
-    h_host = np.zeros((M, vi.h.shape[1]), np.float32)
-    for i, env in enumerate(envs):
-      instr[i] = env.initial_nocopy()
-    restarts = 0
-    deadline_check = time.time()
     parent = os.getppid()
     # the first snapshot (e.g. a restored checkpoint) before any inference
     while wstate['version'] <= 0:
@@ -338,86 +328,162 @@ class ActorGroupWorker(object):
         return
       self._sync_weights(model, wstate)
       time.sleep(0.002)
+    # a split is either waiting for its columns (all-or-nothing claims: a
+    # split never holds columns while it waits, so slabs always fill) or has
+    # one inference in flight
+    pending = list(splits)
+    last_check = time.time()
     while True:
-      if time.time() - deadline_check > 1.0:
-        deadline_check = time.time()
-        if os.getppid() != parent:
-          return  # the learner went away
-      self._sync_weights(model, wstate)
-      # claim one column per env
-      cols = []
-      for i in range(M):
-        while True:
-          s, col, v = self.tq.claim(timeout_ms=200)
-          if s >= 0:
-            break
-          if s == -2 or os.getppid() != parent:
+      progressed = False
+      for sp in splits:
+        if sp in pending:
+          got = sp.try_begin_unroll()
+          if got == -2:
             return
-        cols.append((s, col, v))
-        v['level'][col] = level_index[i]
-        v['c'][col] = c_host[i]
-        v['h'][col] = h_host[i]
+          if not got:
+            continue
+          pending.remove(sp)
+          self._sync_weights(model, wstate)
+          sp.launch()
+          progressed = True
+          continue
+        sp.finish_step()  # wait for its inference, step its envs, record
+        progressed = True
+        if sp.t == sp.T:
+          sp.commit()
+          pending.append(sp)
+          continue
+        self._sync_weights(model, wstate)
+        sp.launch()
+      if not progressed:
+        time.sleep(0.0002)  # every split waits for queue room
+      if time.time() - last_check > 1.0:
+        last_check = time.time()
+        if os.getppid() != parent or self.tq.closed:
+          return  # the learner went away / closed the queue
 
-      def record(t):
-        for i, (s, col, v) in enumerate(cols):
-          v['frame'][t, col] = envs[i].frame_view
-          v['reward'][t, col] = reward[i]
-          v['done'][t, col] = done[i]
-          v['episode_return'][t, col] = ep_ret[i]
-          v['episode_step'][t, col] = ep_step[i]
-          v['action'][t, col] = action[i]
-          v['policy_logits'][t, col] = logits[i]
-          v['baseline'][t, col] = baseline[i]
-          if use_instr and 'instr_ids' in v:
-            v['instr_ids'][t, col], v['instr_len'][t, col] = (
-                encode_instruction(instr[i]))
 
-      record(0)
-      for t in range(1, T + 1):
-        inp['last_action'][:] = action
-        inp['reward'][:] = reward
-        inp['done'][:] = done
-        for i in range(M):
-          inp['frame'][i] = envs[i].frame_view
-          if use_instr:
-            inp['instr_ids'][i], inp['instr_len'][i] = encode_instruction(
-                instr[i])
-        a, lg, b, c2, h2 = vi.run()
-        action[:] = a
-        logits[:] = lg
-        baseline[:] = b
-        c_host[:] = c2
-        h_host[:] = h2
-        seqs = [None] * M
-        for i in range(M):
-          try:
-            seqs[i] = envs[i].step_send(action_set[int(action[i])])
-          except py_process.EnvRestartedError:
-            seqs[i] = None
-        for i in range(M):
-          try:
-            if seqs[i] is None:
-              raise py_process.EnvRestartedError('send failed')
-            r, d, instr[i] = envs[i].step_recv(seqs[i])
-          except py_process.EnvRestartedError as e:
-            restarts += 1
-            self.counters[self.gid] = restarts
-            log.warning('actor group %d env %d: %s; episode truncated (the '
-                        'column continues from a fresh episode)', self.gid, i, e)
-            instr[i] = envs[i].initial_nocopy()
-            r, d = 0.0, True
-          reward[i] = r
-          done[i] = d
-          run_ret[i] += r
-          run_step[i] += 1
-          ep_ret[i] = run_ret[i]
-          ep_step[i] = run_step[i]
-          if d:
-            run_ret[i] = 0.0
-            run_step[i] = 0
-        record(t)
-      for s, col, v in cols:
-        self.tq.commit(s)
+class _Split(object):
+  """One pipeline stage of a group: its envs, their per-env bookkeeping
+  (FlowEnvironment semantics) and their claimed trajectory-queue columns."""
+
+  def __init__(self, worker, envs, vi, level_index, encode_instruction,
+               py_process):
+    sp = worker.spec
+    self.w = worker
+    self.envs = envs
+    self.vi = vi
+    self.level_index = level_index
+    self.encode = encode_instruction
+    self.pp = py_process
+    self.T = sp['unroll_length']
+    self.action_set = sp['action_set']
+    self.use_instr = sp['use_instr']
+    M = len(envs)
+    self.reward = np.zeros(M, np.float32)
+    self.done = np.ones(M, np.bool_)
+    self.ep_ret = np.zeros(M, np.float32)
+    self.ep_step = np.zeros(M, np.int32)
+    self.run_ret = np.zeros(M, np.float32)
+    self.run_step = np.zeros(M, np.int32)
+    self.action = np.zeros(M, np.int64)
+    self.logits = np.zeros((M, sp['num_actions']), np.float32)
+    self.baseline = np.zeros(M, np.float32)
+    self.c = np.zeros((M, vi.c.shape[1]), np.float32)
+    self.h = np.zeros((M, vi.h.shape[1]), np.float32)
+    self.instr = [env.initial_nocopy() for env in envs]
+    self.cols = []
+    self.t = 0
+
+  def try_begin_unroll(self):
+    """Claims one column per env at once (or none): True when claimed
+    (element 0 = the previous unroll's last element, and the agent state at
+    the unroll start, are written), False if the queue has no room yet, -2
+    when it is closed."""
+    got = self.w.tq.claim_n(len(self.envs), timeout_ms=0)
+    if got == -2:
+      return -2
+    if got == -1:
+      return False
+    self.cols = got
+    for i, (s, col, v) in enumerate(got):
+      v['level'][col] = self.level_index[i]
+      v['c'][col] = self.c[i]
+      v['h'][col] = self.h[i]
+    self.t = 0
+    self._record(0)
+    return True
+
+  def commit(self):
+    for s, col, v in self.cols:
+      self.w.tq.commit(s)
+    self.cols = []
+
+  def _record(self, t):
+    use_instr = self.use_instr
+    for i, (s, col, v) in enumerate(self.cols):
+      v['frame'][t, col] = self.envs[i].frame_view
+      v['reward'][t, col] = self.reward[i]
+      v['done'][t, col] = self.done[i]
+      v['episode_return'][t, col] = self.ep_ret[i]
+      v['episode_step'][t, col] = self.ep_step[i]
+      v['action'][t, col] = self.action[i]
+      v['policy_logits'][t, col] = self.logits[i]
+      v['baseline'][t, col] = self.baseline[i]
+      if use_instr and 'instr_ids' in v:
+        v['instr_ids'][t, col], v['instr_len'][t, col] = self.encode(
+            self.instr[i])
+
+  def launch(self):
+    inp = self.vi.inputs
+    inp['last_action'][:] = self.action
+    inp['reward'][:] = self.reward
+    inp['done'][:] = self.done
+    for i, env in enumerate(self.envs):
+      inp['frame'][i] = env.frame_view
+      if self.use_instr:
+        inp['instr_ids'][i], inp['instr_len'][i] = self.encode(self.instr[i])
+    self.vi.launch()
+
+  def finish_step(self):
+    pp = self.pp
+    a, lg, b, c2, h2 = self.vi.wait()
+    self.action[:] = a
+    self.logits[:] = lg
+    self.baseline[:] = b
+    self.c[:] = c2
+    self.h[:] = h2
+    envs = self.envs
+    seqs = [None] * len(envs)
+    for i, env in enumerate(envs):
+      try:
+        seqs[i] = env.step_send(self.action_set[int(a[i])])
+      except pp.EnvRestartedError:
+        seqs[i] = None
+    for i, env in enumerate(envs):
+      try:
+        if seqs[i] is None:
+          raise pp.EnvRestartedError('send failed')
+        r, d, self.instr[i] = env.step_recv(seqs[i])
+      except pp.EnvRestartedError as e:
+        w = self.w
+        w.restarts += 1
+        w.counters[w.gid] = w.restarts
+        log.warning('actor group %d: %s; episode truncated (the column '
+                    'continues from a fresh episode)', w.gid, e)
+        self.instr[i] = env.initial_nocopy()
+        r, d = 0.0, True
+      self.reward[i] = r
+      self.done[i] = d
+      self.run_ret[i] += r
+      self.run_step[i] += 1
+      self.ep_ret[i] = self.run_ret[i]
+      self.ep_step[i] = self.run_step[i]
+      if d:
+        self.run_ret[i] = 0.0
+        self.run_step[i] = 0
+    self.t += 1
+    self._record(self.t)
 
 
 def _group_main(gid, spec, tq, weights, counters, device_str):
@@ -456,7 +522,8 @@ class ActorGroups(object):
                   level_index=[index[actor_levels[i]] for i in members],
                   num_actions=len(action_set), action_set=action_set,
                   frame_shape=tuple(frame_shape), use_instr=use_instr,
-                  unroll_length=flags.unroll_length, dtype=dtype)
+                  unroll_length=flags.unroll_length, dtype=dtype,
+                  splits=flags.actor_group_splits)
       p = ctx.Process(target=_group_main,
                       args=(gid, spec, tq, weights, self.counters, device_str),
                       daemon=False, name='actor-group-%d' % gid)

@@ -155,6 +155,14 @@ class TrajectoryQueue(object):
     s, col = self.q.claim(int(timeout_ms))
     return s, col, (self._views[s] if s >= 0 else None)
 
+  def claim_n(self, n, timeout_ms=-1):
+    """All-or-nothing claim of n columns -> list of (slab, column, views),
+    or -1 (timeout) / -2 (closed)."""
+    status, pairs = self.q.claim_n(int(n), int(timeout_ms))
+    if status < 0:
+      return status
+    return [(s, c, self._views[s]) for s, c in pairs]
+
   def commit(self, slab):
     self.q.commit(int(slab))
 

@@ -113,3 +113,21 @@ def test_named_queue_across_processes():
     assert p.exitcode == 0
   assert sorted(seen) == sorted(list(range(6)) + list(range(100, 106)))
   tq.close()
+
+
+def test_claim_n_is_all_or_nothing():
+  layout = BatchLayout(2, 4, (2, 2, 1), 3)
+  tq = TrajectoryQueue(layout, num_slabs=2)
+  got = tq.claim_n(3, timeout_ms=0)
+  assert [(s, c) for s, c, _ in got] == [(got[0][0], 0), (got[0][0], 1),
+                                         (got[0][0], 2)]
+  got2 = tq.claim_n(5, timeout_ms=0)  # 1 left in slab A + 4 in slab B
+  assert len(got2) == 5 and got2[0][0] == got[0][0]
+  assert tq.claim_n(1, timeout_ms=20) == -1  # full: nothing handed out
+  for s, _, _ in got + got2:
+    tq.commit(s)
+  a = tq.acquire(timeout_ms=100)
+  tq.release(a)
+  assert len(tq.claim_n(4, timeout_ms=100)) == 4
+  tq.close()
+  assert tq.claim_n(1, timeout_ms=10) == -2
