@@ -362,7 +362,13 @@ def train(flags):
   # Env processes (and actor-group processes) are forked BEFORE the GPU is
   # initialised.
   distributed_actors = flags.task >= 0 and flags.job_name == 'learner'
-  use_groups = (flags.actor_groups > 0 and not distributed_actors and
+  n_groups = flags.actor_groups
+  if n_groups < 0:  # auto: one group process when the learner is on a GPU
+    on_gpu = (flags.device.startswith('cuda') or
+              (flags.device == 'auto' and torch.cuda.device_count() > 0))
+    n_groups = 1 if on_gpu else 0
+  flags.actor_groups = n_groups
+  use_groups = (n_groups > 0 and not distributed_actors and
                 flags.trajectory_queue and not flags.deterministic)
   envs, actors_levels, actor_seeds = [], [], []
   groups = shared_w = None

@@ -101,12 +101,14 @@ def build_parser() -> argparse.ArgumentParser:
                  help='Local actors write time-major batches in place into '
                       'a pinned shared-memory slab queue (one H2D copy per '
                       'learner step); false: per-unroll queue + stacking.')
-  p.add_argument('--actor_groups', type=int, default=0,
+  p.add_argument('--actor_groups', type=int, default=-1,
                  help='Run the num_actors envs as G vectorised actor-group '
                       'processes (each: its envs stepped in parallel, one '
                       'captured inference graph per step, writes into the '
                       'trajectory queue); 0 = actor threads in the learner '
-                      'process.')
+                      'process; -1 = auto: 1 group on a GPU (more GPU '
+                      'processes share the card badly: profiles/'
+                      'r2_e2e_actors.md), threads on CPU.')
   p.add_argument('--actor_group_splits', type=int, default=2,
                  help='Pipeline stages per actor group: split k\'s inference '
                       'runs on the GPU while the envs of another split step.')

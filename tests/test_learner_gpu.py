@@ -87,11 +87,13 @@ def test_pipelined_unroll_matches_serial(cuda):
   assert not torch.equal(before, lrn4.flat.params)
 
 
-def test_experiment_train_and_test_on_gpu(tmp_path):
+@pytest.mark.parametrize('groups', [0, -1])
+def test_experiment_train_and_test_on_gpu(tmp_path, groups):
   """The full driver on the GPU: actor threads with batched GPU inference
-  (fused core at T=1), the HIP-graph learner on the fused path, checkpoint,
-  then --mode=test from the checkpoint (reference Dockerfile smoke, deep
-  torso)."""
+  (groups=0) or the default actor-group process (groups=-1: one group,
+  pipelined splits, captured fixed-batch inference), the HIP-graph learner,
+  checkpoint, then --mode=test from the checkpoint (reference Dockerfile
+  smoke, deep torso)."""
   import os
   import subprocess
   import sys
@@ -103,6 +105,7 @@ def test_experiment_train_and_test_on_gpu(tmp_path):
             '--synthetic_episode_length=10', '--logdir=' + str(tmp_path)]
   env = dict(os.environ, PYTHONPATH=root)
   r = subprocess.run(common + ['--num_actors=4', '--batch_size=4',
+                               '--actor_groups=%d' % groups,
                                '--total_environment_frames=1280',
                                '--save_summaries_secs=0'],
                      capture_output=True, text=True, timeout=100, env=env)
