@@ -9,6 +9,13 @@ Saved atomically (write to a temp file, fsync, rename), every
 `save_checkpoint_secs` (600 by default), keeping the newest `keep` (5, the TF
 Saver default).  Restore happens automatically on start; `--mode=test` reads
 the same files.  Files are loaded with `torch.load(weights_only=True)`.
+
+`--checkpoint_format=tf` writes the reference's own layout instead
+(experiment.py:608-616): `model.ckpt-<frames>.{index,data-00000-of-00001}`
+plus a TF `checkpoint` index (tf_checkpoint.export_tf_checkpoint), with the
+RMSProp slots, the frame counter and PopArt statistics as extra variables.
+`latest_checkpoint` / `restore` / `load_state` accept either layout, so
+training resumes and `--mode=test` evaluates from whichever a logdir holds.
 """
 
 import glob
@@ -31,16 +38,30 @@ def _list(logdir):
   return sorted(out)
 
 
+def is_tf(path):
+  """True for a TF checkpoint prefix (model.ckpt-N), False for a .pt file."""
+  return path is not None and not path.endswith('.pt') and os.path.exists(
+      path + '.index')
+
+
 def latest_checkpoint(logdir):
-  """Path of the latest checkpoint in logdir, or None."""
+  """Path of the latest checkpoint in logdir (a .pt file or a TF prefix), or
+  None."""
+  from . import tf_checkpoint
   idx = os.path.join(logdir, 'checkpoint')
   if os.path.exists(idx):
-    name = open(idx).read().strip()
-    p = os.path.join(logdir, name)
-    if os.path.exists(p):
-      return p
-  ckpts = _list(logdir)
-  return ckpts[-1][1] if ckpts else None
+    text = open(idx).read()
+    if 'model_checkpoint_path' in text:
+      p = tf_checkpoint.latest_checkpoint(logdir)
+      if p is not None and is_tf(p):
+        return p
+    else:
+      p = os.path.join(logdir, text.strip())
+      if os.path.exists(p):
+        return p
+  # no (usable) index: the newest of either layout
+  cands = _list(logdir) + tf_checkpoint.list_tf_checkpoints(logdir)
+  return max(cands)[1] if cands else None
 
 
 def _to_cpu(x):
@@ -51,8 +72,23 @@ def _to_cpu(x):
   return x
 
 
-def save(logdir, learner, flags=None, keep=5, extra=None):
-  """Writes checkpoint_<frames>.pt atomically and prunes old ones."""
+def save_tf(logdir, learner, keep=5):
+  """The reference layout: model.ckpt-<frames> + `checkpoint`."""
+  from . import tf_checkpoint
+  os.makedirs(logdir, exist_ok=True)
+  extra = {}
+  if getattr(learner, 'popart', None) is not None:
+    for k, v in learner.popart.state_dict().items():
+      extra['popart/' + k] = v.detach().cpu().numpy()
+  return tf_checkpoint.export_tf_checkpoint(logdir, learner, keep=keep,
+                                            extra=extra)
+
+
+def save(logdir, learner, flags=None, keep=5, extra=None, fmt='pt'):
+  """Writes checkpoint_<frames>.pt atomically and prunes old ones (fmt='tf':
+  save_tf)."""
+  if fmt == 'tf':
+    return save_tf(logdir, learner, keep)
   os.makedirs(logdir, exist_ok=True)
   frames = int(learner.frames.item())
   names = learner.agent.tf_variable_names()
@@ -92,6 +128,21 @@ def save(logdir, learner, flags=None, keep=5, extra=None):
 
 
 def load_state(path):
+  """-> {'params': {tf_name: tensor}, 'num_environment_frames', ...}."""
+  if is_tf(path):
+    from . import tf_checkpoint
+    t = tf_checkpoint.read_checkpoint(path)
+    params = {k: torch.from_numpy(v.copy()) for k, v in t.items()
+              if not k.endswith(('/RMSProp', '/RMSProp_1')) and
+              k != 'num_environment_frames' and not k.startswith('popart/')}
+    state = {'params': params, 'format': 'tf',
+             'num_environment_frames': int(t.get('num_environment_frames',
+                                                 0))}
+    pop = {k[len('popart/'):]: torch.from_numpy(v.copy())
+           for k, v in t.items() if k.startswith('popart/')}
+    if pop:
+      state['popart'] = pop
+    return state
   return torch.load(path, map_location='cpu', weights_only=True)
 
 
@@ -109,6 +160,14 @@ def restore(logdir, learner):
   path = latest_checkpoint(logdir)
   if path is None:
     return None
+  if is_tf(path):
+    from . import tf_checkpoint
+    frames = tf_checkpoint.import_tf_checkpoint(path, learner=learner)
+    if getattr(learner, 'popart', None) is not None:
+      pop = load_state(path).get('popart')
+      if pop:
+        learner.popart.load_state_dict(pop)
+    return int(frames or 0)
   state = load_state(path)
   restore_agent(learner.agent, state)
   learner.opt.ms.copy_(state['rmsprop']['ms'].to(learner.opt.ms.device))
@@ -127,10 +186,12 @@ class PeriodicSaver(object):
   def __init__(self, logdir, learner, flags, secs=600, keep=5):
     self.logdir, self.learner, self.flags = logdir, learner, flags
     self.secs, self.keep = secs, keep
+    self.fmt = getattr(flags, 'checkpoint_format', 'pt') if flags else 'pt'
     self._last = time.time()
 
   def maybe_save(self, force=False):
     if force or time.time() - self._last >= self.secs:
       self._last = time.time()
-      return save(self.logdir, self.learner, self.flags, self.keep)
+      return save(self.logdir, self.learner, self.flags, self.keep,
+                  fmt=self.fmt)
     return None

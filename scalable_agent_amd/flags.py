@@ -120,6 +120,11 @@ def build_parser() -> argparse.ArgumentParser:
                  help='TF V2 checkpoint prefix (or a logdir with a '
                       '`checkpoint` file) of a reference run to start from '
                       'when --logdir has no checkpoint of its own.')
+  p.add_argument('--checkpoint_format', default='pt', choices=['pt', 'tf'],
+                 help='pt: checkpoint_<frames>.pt (torch, weights_only); tf: '
+                      'the reference\'s model.ckpt-<frames>.{index,data} + '
+                      '`checkpoint` (TF V2 bundle, no TensorFlow needed).  '
+                      'Restore and --mode=test read either.')
   p.add_argument('--save_summaries_secs', type=float, default=30)
   p.add_argument('--keep_checkpoints', type=int, default=5)
   p.add_argument('--log_every_frames', type=int, default=50000,

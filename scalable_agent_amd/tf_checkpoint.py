@@ -23,6 +23,7 @@ installed here, so compatibility with TF-written files is pinned only by the
 format description above (parity unpinned); the round trip is tested.
 """
 
+import glob
 import os
 import re
 import struct
@@ -341,9 +342,26 @@ def import_tf_checkpoint(prefix_or_logdir, learner=None, agent=None):
   return frames
 
 
-def export_tf_checkpoint(logdir, learner):
+def list_tf_checkpoints(logdir):
+  """[(frames, prefix)] of the complete model.ckpt-N in logdir, oldest first."""
+  out = []
+  for idx in glob.glob(os.path.join(logdir, 'model.ckpt-*.index')):
+    m = re.search(r'model\.ckpt-(\d+)\.index$', idx)
+    prefix = idx[:-len('.index')]
+    if m and os.path.exists(prefix + '.data-00000-of-00001'):
+      out.append((int(m.group(1)), prefix))
+  return sorted(out)
+
+
+def export_tf_checkpoint(logdir, learner, keep=None, extra=None):
   """Writes `logdir/model.ckpt-<frames>` (+ `checkpoint`) in the reference's
-  variable layout; returns the prefix."""
+  variable layout (weights, RMSProp `ms`/`mom` slots as `<var>/RMSProp` and
+  `<var>/RMSProp_1`, `num_environment_frames`; reference experiment.py:
+  608-616); `extra` {name: array} adds further tensors (PopArt statistics).
+  The shards are written under temporary names and renamed (data, then
+  index), then the `checkpoint` file is replaced atomically; with `keep`,
+  older model.ckpt-N beyond the newest `keep` are removed.  Returns the
+  prefix."""
   frames = int(learner.frames.item())
   names = learner.agent.tf_variable_names()
   t = {}
@@ -354,9 +372,29 @@ def export_tf_checkpoint(logdir, learner):
     t[names[n] + '/RMSProp_1'] = learner.flat.view_of(
         learner.opt.mom, n).detach().float().cpu().numpy()
   t['num_environment_frames'] = np.asarray(frames, np.int64)
-  prefix = os.path.join(logdir, 'model.ckpt-%d' % frames)
-  write_checkpoint(prefix, t)
-  with open(os.path.join(logdir, 'checkpoint'), 'w') as f:
-    f.write('model_checkpoint_path: "model.ckpt-%d"\n' % frames)
-    f.write('all_model_checkpoint_paths: "model.ckpt-%d"\n' % frames)
+  for k, v in (extra or {}).items():
+    t[k] = np.asarray(v)
+  name = 'model.ckpt-%d' % frames
+  prefix = os.path.join(logdir, name)
+  tmp = os.path.join(logdir, '.tmp-' + name)
+  write_checkpoint(tmp, t)
+  for suffix in ('.data-00000-of-00001', '.index'):
+    with open(tmp + suffix, 'rb') as f:
+      os.fsync(f.fileno())
+    os.replace(tmp + suffix, prefix + suffix)
+  ckpts = list_tf_checkpoints(logdir)
+  if keep:
+    for _, old in ckpts[:-keep]:
+      for suffix in ('.index', '.data-00000-of-00001'):
+        try:
+          os.remove(old + suffix)
+        except OSError:
+          pass
+    ckpts = ckpts[-keep:]
+  idx_tmp = os.path.join(logdir, 'checkpoint.tmp')
+  with open(idx_tmp, 'w') as f:
+    f.write('model_checkpoint_path: "%s"\n' % name)
+    for _, p in ckpts:
+      f.write('all_model_checkpoint_paths: "%s"\n' % os.path.basename(p))
+  os.replace(idx_tmp, os.path.join(logdir, 'checkpoint'))
   return prefix
