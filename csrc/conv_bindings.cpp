@@ -30,6 +30,14 @@ void check_grad(const at::Tensor& dw, const at::Tensor& db, int64_t cin, int64_t
 }
 bool supported(int64_t c) { return c == 16 || c == 32; }
 
+// Deterministic mode: a stream-ordered slot workspace for the wgrad flush
+// (empty when the mode is off).
+at::Tensor wgrad_part(const at::Tensor& like, int64_t cin, int64_t cout, bool conv1) {
+  const int64_t n = sa::conv::wgrad_part_floats((int)cin, (int)cout, conv1);
+  return n ? at::empty({n}, like.options()) : at::Tensor();
+}
+float* ptr_or_null(const at::Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; }
+
 std::vector<at::Tensor> conv1_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
                                        int64_t pb_h, int64_t pb_w) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kByte &&
@@ -123,10 +131,11 @@ at::Tensor res_conv_bwd(at::Tensor dy, at::Tensor act, c10::optional<at::Tensor>
   }
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty_like(act);
+  auto part = wgrad_part(dw, C, C, false);
   sa::conv::res_conv_bwd_launch(dy.data_ptr(), act.data_ptr(), sp, w.data_ptr<float>(),
                                 dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(),
                                 act.size(0), act.size(1), act.size(2), C, relu_act,
-                                stream());
+                                stream(), ptr_or_null(part));
   return dx;
 }
 
@@ -151,10 +160,11 @@ c10::optional<at::Tensor> pool_conv_bwd(at::Tensor dP, at::Tensor arg, at::Tenso
     dx = at::empty_like(x);
     dxp = dx->data_ptr();
   }
+  auto part = wgrad_part(dw, CIN, COUT, false);
   sa::conv::pool_conv_bwd_launch(dP.data_ptr(), arg.data_ptr<uint8_t>(), x.data_ptr(),
                                  w.data_ptr<float>(), dxp, dw.data_ptr<float>(),
                                  db.data_ptr<float>(), x.size(0), x.size(1), x.size(2),
-                                 CIN, COUT, pb_h, pb_w, stream());
+                                 CIN, COUT, pb_h, pb_w, stream(), ptr_or_null(part));
   return dx;
 }
 
@@ -168,10 +178,11 @@ void conv1_pool_bwd(at::Tensor dP, at::Tensor arg, at::Tensor x, at::Tensor dw,
               "pooled shape");
   check_grad(dw, db, 3, 16);
   const c10::DeviceGuard g(x.device());
+  auto part = wgrad_part(dw, 3, 16, true);
   sa::conv::conv1_pool_bwd_launch(dP.data_ptr(), arg.data_ptr<uint8_t>(),
                                   x.data_ptr<uint8_t>(), dw.data_ptr<float>(),
                                   db.data_ptr<float>(), x.size(0), x.size(1),
-                                  x.size(2), pb_h, pb_w, stream());
+                                  x.size(2), pb_h, pb_w, stream(), ptr_or_null(part));
 }
 
 }  // namespace

@@ -31,14 +31,20 @@ void res_block_fwd_launch(const void* x, const float* w1, const float* b1,
                           hipStream_t s);
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
-                         int H, int W, int C, bool relu_act, hipStream_t s);
+                         int H, int W, int C, bool relu_act, hipStream_t s,
+                         float* part = nullptr);
 void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           const float* w, void* dx, float* dw, float* db, int N,
                           int H, int W, int CIN, int COUT, int pb_h, int pb_w,
-                          hipStream_t s);
+                          hipStream_t s, float* part = nullptr);
 void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
-                           int H, int W, int pb_h, int pb_w, hipStream_t s);
+                           int H, int W, int pb_h, int pb_w, hipStream_t s,
+                           float* part = nullptr);
+// Deterministic mode (conv_tune("deterministic", 1)): the wgrad launches
+// above take a slot workspace of this many floats (0 = mode off) and add the
+// per-workgroup slots in a fixed order instead of with float atomics.
+int64_t wgrad_part_floats(int cin, int cout, bool conv1);
 
 }  // namespace conv
 }  // namespace sa

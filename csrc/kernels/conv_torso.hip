@@ -587,11 +587,17 @@ __device__ __forceinline__ void conv_tile_wgrad(const bf16_t* a_s,
 // Sums the waves' accumulators through LDS (scratch: >= 4*CIN*COUT floats,
 // 16-B aligned; all tile work must be finished) and adds the workgroup's
 // total to dw/db with one float atomic per element.
+// part != nullptr (deterministic mode): the workgroup's totals go to its own
+// slot part[blockIdx.x][9*CIN*COUT + COUT] instead (every element written
+// once), and slot_reduce_kernel adds the slots in a fixed order.
 template <int CIN, int COUT>
 __device__ __forceinline__ void flush_wgrad(const WgradAcc<CIN, COUT>& acc,
                                             float scale, float* __restrict__ dw,
                                             float* __restrict__ db,
-                                            float* scratch) {
+                                            float* scratch,
+                                            float* __restrict__ part) {
+  float* slot = part ? part + static_cast<int64_t>(blockIdx.x) * (9 * CIN * COUT + COUT)
+                     : nullptr;
   using A = WgradAcc<CIN, COUT>;
   constexpr int HC = A::HC, HO = A::HO, TG = A::TG, TPG = A::TPG;
   constexpr int PER = CIN * COUT;  // floats per wave per tap
@@ -626,9 +632,15 @@ __device__ __forceinline__ void flush_wgrad(const WgradAcc<CIN, COUT>& acc,
       const int co = 16 * co_h + (l & 15);
       const int tap = tg * TPG + k;
       if (k < TPG) {
-        if (tap < 9) atomicAdd(dw + (tap * CIN + ci) * COUT + co, v * scale);
+        if (tap < 9) {
+          const int o = (tap * CIN + ci) * COUT + co;
+          if (slot) slot[o] = v * scale;
+          else atomicAdd(dw + o, v * scale);
+        }
       } else if (tg == 0 && ci_h == 0 && (l >> 4) == 0 && i == 0) {
-        atomicAdd(db + co, v);  // bias: every D row holds the column sum
+        // bias: every D row holds the column sum
+        if (slot) slot[9 * CIN * COUT + co] = v;
+        else atomicAdd(db + co, v);
       }
     }
     __syncthreads();
@@ -1145,7 +1157,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ act,
     const bf16_t* __restrict__ skip, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    int N, int H_, int W_, int R_, int xcd) {
+    int N, int H_, int W_, int R_, int xcd, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   const int RP = row_pitch(C, W);
@@ -1199,7 +1211,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     conv_tile_wgrad<C, C>(a_s, d_s, W, npix, tile_elems, tile_elems, acc);
     if (kLatePrefetch && it.valid(it.next(tile))) issue(it.next(tile));
   }
-  flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
+  flush_wgrad<C, C>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem), part);
 }
 
 // dY of the conv feeding a max-pool as an LDS halo tile (rows [r_begin,
@@ -1301,7 +1313,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const bf16_t* __restrict__ x, const float* __restrict__ w,
     bf16_t* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
-    int N, int H_, int W_, int R_, int pb_h, int pb_w, int xcd) {
+    int N, int H_, int W_, int R_, int pb_h, int pb_w, int xcd,
+    float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
   const int Hp = (H + 1) / 2, Wo = (W + 1) / 2;
@@ -1364,7 +1377,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if (kKeep(xcd, 2))
     conv_tile_wgrad<CIN, COUT>(x_s, d_s, W, npix, x_elems, d_elems, acc);
   }
-  flush_wgrad<CIN, COUT>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem));
+  flush_wgrad<CIN, COUT>(acc, 1.f, dw, db, reinterpret_cast<float*>(smem), part);
 }
 
 // First-layer weight gradient on the bf16x4 frame tile: for each kernel row
@@ -1376,7 +1389,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const uint8_t* __restrict__ x, float* __restrict__ dw,
     float* __restrict__ db, int N, int H_, int W_, int R_, int pb_h, int pb_w,
-    int xcd) {
+    int xcd, float* __restrict__ part) {
   constexpr int COUT = 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = HC ? HC : H_, W = WC ? WC : W_, R = RC ? RC : R_;
@@ -1451,16 +1464,56 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
       accb = mfma16(ones, bd, accb);
     }
   }
+  // deterministic mode: one slot per WAVE (27*16 + 16 floats), reduced in a
+  // fixed order by slot_reduce_kernel; otherwise float atomics
+  float* slot = part ? part + (static_cast<int64_t>(blockIdx.x) * kWaves + wave) *
+                                  (27 * COUT + COUT)
+                     : nullptr;
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kx = lane >> 4, ci = i;
-      if (kx < 3 && ci < 3)
-        atomicAdd(dw + ((ky * 3 + kx) * 3 + ci) * COUT + sub,
-                  accw[ky][i] * (1.0f / 255.0f));
+      if (kx < 3 && ci < 3) {
+        const int o = ((ky * 3 + kx) * 3 + ci) * COUT + sub;
+        const float v = accw[ky][i] * (1.0f / 255.0f);
+        if (slot) slot[o] = v;
+        else atomicAdd(dw + o, v);
+      }
     }
-  if ((lane >> 4) == 0) atomicAdd(db + sub, accb[0]);
+  if ((lane >> 4) == 0) {
+    if (slot) slot[27 * COUT + sub] = accb[0];
+    else atomicAdd(db + sub, accb[0]);
+  }
+}
+
+// dw[e] (e < ndw) / db[e - ndw] += sum over S slots of part[s][e], in a fixed
+// order (deterministic mode of the wgrad flushes): thread = element x one of
+// 4 slot groups, 8 independent accumulators, the groups combined in LDS.
+__global__ __launch_bounds__(256) void slot_reduce_kernel(
+    const float* __restrict__ part, int S, int nel, int ndw, float* __restrict__ dw,
+    float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sg = threadIdx.x >> 6;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < nel) {
+    for (int k = sg; k < S; k += 32) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int kk = k + 4 * u;
+        if (kk < S) acc[u] += part[static_cast<int64_t>(kk) * nel + e];
+      }
+    }
+  }
+  red[sg][threadIdx.x & 63] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                              ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (sg != 0 || e >= nel) return;
+  const int l = threadIdx.x;
+  const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  if (e < ndw) dw[e] += v;
+  else db[e - ndw] += v;
 }
 
 int num_cus() {
@@ -1576,6 +1629,7 @@ struct ConvTune {
   int px_conv1_bwd = 1152;
   int specialize = 1;     // use compile-time-geometry kernels when they match
   int ablate = 0;         // timing-only, -DSA_CONV_ABLATE builds: skip phases
+  int deterministic = 0;  // wgrad: per-workgroup slots + fixed-order reduce
 };
 constexpr ConvTune kDef{};
 static ConvTune g_tune;
@@ -1588,7 +1642,8 @@ int conv_tune_set(const char* key, int value) {
       {"px_conv1_fwd", &g_tune.px_conv1_fwd},
       {"px_pool_bwd", &g_tune.px_pool_bwd},
       {"px_conv1_bwd", &g_tune.px_conv1_bwd},
-      {"specialize", &g_tune.specialize}, {"ablate", &g_tune.ablate}};
+      {"specialize", &g_tune.specialize}, {"ablate", &g_tune.ablate},
+      {"deterministic", &g_tune.deterministic}};
   for (auto& e : table) {
     if (std::strcmp(e.k, key) == 0) {
       const int old = *e.v;
@@ -1807,9 +1862,26 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
   });
 }
 
+// Deterministic mode: floats of the slot workspace a wgrad launch needs (0
+// when off); the slots are summed by slot_reduce_kernel after the launch.
+int64_t wgrad_part_floats(int cin, int cout, bool conv1) {
+  if (!g_tune.deterministic) return 0;
+  const int64_t nel = conv1 ? 27 * 16 + 16 : 9 * cin * cout + cout;
+  const int64_t slots = static_cast<int64_t>(num_cus()) *
+                        std::max(1, std::max(g_tune.cap_bwd, 1)) * (conv1 ? kWaves : 1);
+  return slots * nel;
+}
+
+static void reduce_slots(const float* part, int slots, int nel, int ndw, float* dw,
+                         float* db, hipStream_t s) {
+  hipLaunchKernelGGL(slot_reduce_kernel, dim3((nel + 63) / 64), dim3(256), 0, s, part,
+                     slots, nel, ndw, dw, db);
+}
+
 void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
                          const float* w, void* dx, float* dw, float* db, int N,
-                         int H, int W, int C, bool relu_act, hipStream_t s) {
+                         int H, int W, int C, bool relu_act, hipStream_t s,
+                         float* part) {
   const int R = rows_for(H, W, C, g_tune.px_res_bwd);
   require_fit((R + 2) * W * C / 8 <= NREG * kThreads &&
                   tile_groups(C, R, W) <= kMaxTilePx(C) / 16,
@@ -1825,7 +1897,7 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DY, A, SK,
-                       w, DX, dw, db, N, H, W, R, xcd);
+                       w, DX, dw, db, N, H, W, R, xcd, part);
   };
 #define SA_RB(CC, SKP, RA, STG)                                                \
   with_geo<STG, RowsResBwd<CC>>(H, W, R, [&](auto h, auto ww, auto r) {        \
@@ -1846,12 +1918,13 @@ void res_conv_bwd_launch(const void* dy, const void* act, const void* skip,
   }
 #undef SA_RB_C
 #undef SA_RB
+  if (part) reduce_slots(part, grid, 9 * C * C + C, 9 * C * C, dw, db, s);
 }
 
 void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           const float* w, void* dx, float* dw, float* db, int N,
                           int H, int W, int CIN, int COUT, int pb_h, int pb_w,
-                          hipStream_t s) {
+                          hipStream_t s, float* part) {
   const int Wo = (W + 1) / 2;
   const int R = rows_pool_bwd(H, W, CIN, COUT, g_tune.px_pool_bwd);
   require_fit((R + 2) * W * CIN / 8 <= NREG * kThreads &&
@@ -1872,7 +1945,7 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
   auto go = [&](auto kernel) {
     set_smem(kernel, smem);
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kThreads), smem, s, DP, argmax,
-                       X, w, DX, dw, db, N, H, W, R, pb_h, pb_w, xcd);
+                       X, w, DX, dw, db, N, H, W, R, pb_h, pb_w, xcd, part);
   };
 #define SA_PB(CI, CO, NDX, STG)                                                \
   with_geo<STG, RowsPoolBwd<CI, CO>>(H, W, R, [&](auto h, auto ww, auto r) {   \
@@ -1891,11 +1964,14 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
     else SA_PB(16, 16, false, kStage1);
   }
 #undef SA_PB
+  if (part)
+    reduce_slots(part, grid, 9 * CIN * COUT + COUT, 9 * CIN * COUT, dw, db, s);
 }
 
 void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
-                           int H, int W, int pb_h, int pb_w, hipStream_t s) {
+                           int H, int W, int pb_h, int pb_w, hipStream_t s,
+                           float* part) {
   const int Wo = (W + 1) / 2;
   const int R = rows_conv1_bwd(H, W, g_tune.px_conv1_bwd);
   require_fit(((R + 2) * W + 3) / 4 <= kU8Groups * kThreads &&
@@ -1914,8 +1990,9 @@ void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                                    decltype(r)::value>;
     set_smem(k, smem);
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, DP, argmax, x,
-                       dw, db, N, H, W, R, pb_h, pb_w, xcd);
+                       dw, db, N, H, W, R, pb_h, pb_w, xcd, part);
   });
+  if (part) reduce_slots(part, grid * kWaves, 27 * 16 + 16, 27 * 16, dw, db, s);
 }
 
 }  // namespace conv

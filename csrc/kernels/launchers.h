@@ -121,22 +121,30 @@ void learner_head_fwd_launch(const float* core, const float* wp, const float* bp
                              float* dlogits, float* dvalues, float* partial,
                              unsigned* ticket, float* loss, hipStream_t stream);
 // dcore [N1,256] = g (dlogits Wp^T + dv Wb^T) (rows >= Ng zero); heads'
-// gradients accumulated (atomics) into gwp [256,A], gbp [A], gwb [256], gbb.
+// gradients accumulated into gwp [256,A], gbp [A], gwb [256], gbb through
+// per-row-chunk slots `part` (learner_head_bwd_part_floats) summed in a fixed
+// order (bitwise reproducible).
+int64_t learner_head_bwd_part_floats(int N1, int A);
 void learner_head_bwd_launch(const float* gscale, const float* core,
                              const float* dlogits, const float* dvalues,
                              const float* wp, const float* wb, int N1, int Ng,
                              int A, float* dcore, float* gwp, float* gbp,
-                             float* gwb, float* gbb, hipStream_t stream);
+                             float* gwb, float* gbb, float* part,
+                             hipStream_t stream);
 // h_aug (bf16 [N, ld]) <- [h (bf16 [N, c0]), clip(r), one_hot(a), 0...]
 void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
                          const int64_t* actions, int N, int ld, int c0,
                          int clip_mode, hipStream_t stream);
-// out[c] += sum_r x[r,c], x fp32 [N,C]
-void colsum_f32_launch(const float* x, int N, int C, float* out,
+// out[c] += sum_r x[r,c], x fp32 [N,C]; per-row-chunk slots in `part`
+// (colsum_f32_part_floats), added in a fixed order
+int64_t colsum_f32_part_floats(int N, int C);
+void colsum_f32_launch(const float* x, int N, int C, float* out, float* part,
                        hipStream_t stream);
 // dy bf16 [N,C] *= (y > 0) (y bf16 with row stride ldy); out[c] += colsum
+// (slots in `part`: relu_bwd_colsum_part_floats)
+int64_t relu_bwd_colsum_part_floats(int N, int C);
 void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
-                            float* out, hipStream_t stream);
+                            float* out, float* part, hipStream_t stream);
 // dx bf16 *= (x > 0), n % 8 == 0
 void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,
                            hipStream_t stream);

@@ -375,8 +375,7 @@ __global__ __launch_bounds__(256) void learner_head_bwd_kernel(
     const float* __restrict__ gscale, const float* __restrict__ core,
     const float* __restrict__ dlogits, const float* __restrict__ dvalues,
     const float* __restrict__ wp, const float* __restrict__ wb, int N1, int Ng,
-    int A, float* __restrict__ dcore, float* __restrict__ gwp,
-    float* __restrict__ gbp, float* __restrict__ gwb, float* __restrict__ gbb) {
+    int A, float* __restrict__ dcore, float* __restrict__ part) {
   constexpr int H = 256;
   __shared__ float dl_s[kBwdRows][MAXC];
   __shared__ float red_s[4][16][MAXC];
@@ -447,19 +446,61 @@ __global__ __launch_bounds__(256) void learner_head_bwd_kernel(
     }
   }
   __syncthreads();
+  // this row chunk's totals go to its slot part[blockIdx.y][257 * A1]
+  // ([unit k][A1] weight rows, then the A1 bias sums); head_grad_reduce
+  // adds the slots in a fixed order (bitwise reproducible, no atomics)
+  float* slot = part + static_cast<int64_t>(blockIdx.y) * 257 * A1;
   for (int i = tid; i < 16 * A1; i += 256) {
     const int u = i / A1, c = i - u * A1;
     const float v = g * (red_s[0][u][c] + red_s[1][u][c] + red_s[2][u][c] +
                          red_s[3][u][c]);
-    const int ku = blockIdx.x * 16 + u;
-    atomicAdd(c < A ? gwp + ku * A + c : gwb + ku, v);
+    slot[(blockIdx.x * 16 + u) * A1 + c] = v;
   }
   if (blockIdx.x == 0 && tid >= 256 - A1) {  // bias grads: column sums
     const int c = tid - (256 - A1);
     float s = 0.f;
     for (int rr = 0; rr < rows; ++rr) s += dl_s[rr][c];
-    atomicAdd(c < A ? gbp + c : gbb, g * s);
+    slot[256 * A1 + c] = g * s;
   }
+}
+
+// Fixed-order sum of the head-gradient slots into gwp [256, A], gwb [256],
+// gbp [A], gbb [1].
+__global__ __launch_bounds__(256) void head_grad_reduce_kernel(
+    const float* __restrict__ part, int S, int A, float* __restrict__ gwp,
+    float* __restrict__ gbp, float* __restrict__ gwb, float* __restrict__ gbb) {
+  const int A1 = A + 1;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 257 * A1) return;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[static_cast<int64_t>(s) * 257 * A1 + e];
+  if (e < 256 * A1) {
+    const int ku = e / A1, c = e - ku * A1;
+    if (c < A) gwp[ku * A + c] += v;
+    else gwb[ku] += v;
+  } else {
+    const int c = e - 256 * A1;
+    if (c < A) gbp[c] += v;
+    else gbb[0] += v;
+  }
+}
+
+// out[c] += sum_s part[s][c] in slot order (the colsum kernels' partials).
+__global__ __launch_bounds__(256) void rows_reduce_kernel(const float* __restrict__ part,
+                                                          int S, int C,
+                                                          float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= S; s += 4) {
+    a0 += part[static_cast<int64_t>(s) * C + c];
+    a1 += part[static_cast<int64_t>(s + 1) * C + c];
+    a2 += part[static_cast<int64_t>(s + 2) * C + c];
+    a3 += part[static_cast<int64_t>(s + 3) * C + c];
+  }
+  for (; s < S; ++s) a0 += part[static_cast<int64_t>(s) * C + c];
+  out[c] += (a0 + a1) + (a2 + a3);
 }
 
 // -------------------------------------------------------------- core input
@@ -491,7 +532,7 @@ constexpr int kColRows = 64;
 constexpr int kColBatch = 16;
 
 __global__ __launch_bounds__(256) void colsum_f32_kernel(
-    const float* __restrict__ x, int N, int C, float* __restrict__ out) {
+    const float* __restrict__ x, int N, int C, float* __restrict__ part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int r0 = blockIdx.y * kColRows;
   const int r1 = min(r0 + kColRows, N);
@@ -505,7 +546,7 @@ __global__ __launch_bounds__(256) void colsum_f32_kernel(
 #pragma unroll
     for (int j = 0; j < kColBatch; ++j) s += v[j];
   }
-  atomicAdd(out + c, s);
+  part[static_cast<int64_t>(blockIdx.y) * C + c] = s;  // slot of this row chunk
 }
 
 // dy [N, C] bf16 *= (y > 0); out[c] += sum_r dy[r, c] (after masking).
@@ -516,7 +557,7 @@ constexpr int kRbRows = 32;
 
 __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
     bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, int N, int C,
-    int ldy, float* __restrict__ out) {
+    int ldy, float* __restrict__ part) {
   __shared__ float red[256][2];
   const int pairs = C >> 1;
   const int lanes = 256 / pairs;  // row lanes (host: C/2 divides 256)
@@ -550,14 +591,15 @@ __global__ __launch_bounds__(256) void relu_bwd_colsum_kernel(
   red[threadIdx.x][0] = s0;
   red[threadIdx.x][1] = s1;
   __syncthreads();
-  if (out && threadIdx.x < pairs) {
+  if (part && threadIdx.x < pairs) {
     float t0 = 0.f, t1 = 0.f;
     for (int l = 0; l < lanes; ++l) {
       t0 += red[l * pairs + threadIdx.x][0];
       t1 += red[l * pairs + threadIdx.x][1];
     }
-    atomicAdd(out + 2 * threadIdx.x, t0);
-    atomicAdd(out + 2 * threadIdx.x + 1, t1);
+    float* slot = part + static_cast<int64_t>(blockIdx.x) * C;  // this block's slot
+    slot[2 * threadIdx.x] = t0;
+    slot[2 * threadIdx.x + 1] = t1;
   }
 }
 
@@ -613,20 +655,28 @@ void learner_head_fwd_launch(const float* core, const float* wp, const float* bp
                      ticket, loss);
 }
 
+int64_t learner_head_bwd_part_floats(int N1, int A) {
+  return static_cast<int64_t>((N1 + kBwdRows - 1) / kBwdRows) * 257 * (A + 1);
+}
+
 void learner_head_bwd_launch(const float* gscale, const float* core,
                              const float* dlogits, const float* dvalues,
                              const float* wp, const float* wb, int N1, int Ng,
                              int A, float* dcore, float* gwp, float* gbp,
-                             float* gwb, float* gbb, hipStream_t stream) {
+                             float* gwb, float* gbb, float* part,
+                             hipStream_t stream) {
   const dim3 grid(256 / 16, (N1 + kBwdRows - 1) / kBwdRows);
   if (A + 1 <= 16)
     hipLaunchKernelGGL(learner_head_bwd_kernel<16>, grid, dim3(256), 0, stream,
                        gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, dcore,
-                       gwp, gbp, gwb, gbb);
+                       part);
   else
     hipLaunchKernelGGL(learner_head_bwd_kernel<kMaxA + 1>, grid, dim3(256), 0,
                        stream, gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A,
-                       dcore, gwp, gbp, gwb, gbb);
+                       dcore, part);
+  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3((257 * (A + 1) + 255) / 256),
+                     dim3(256), 0, stream, part, static_cast<int>(grid.y), A, gwp,
+                     gbp, gwb, gbb);
 }
 
 void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
@@ -639,17 +689,31 @@ void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
                      clip_mode);
 }
 
-void colsum_f32_launch(const float* x, int N, int C, float* out,
+int64_t colsum_f32_part_floats(int N, int C) {
+  return static_cast<int64_t>((N + kColRows - 1) / kColRows) * C;
+}
+
+void colsum_f32_launch(const float* x, int N, int C, float* out, float* part,
                        hipStream_t stream) {
   dim3 grid((C + 255) / 256, (N + kColRows - 1) / kColRows);
-  hipLaunchKernelGGL(colsum_f32_kernel, grid, dim3(256), 0, stream, x, N, C, out);
+  hipLaunchKernelGGL(colsum_f32_kernel, grid, dim3(256), 0, stream, x, N, C, part);
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
+                     part, static_cast<int>(grid.y), C, out);
+}
+
+int64_t relu_bwd_colsum_part_floats(int N, int C) {
+  return static_cast<int64_t>((N + kRbRows - 1) / kRbRows) * C;
 }
 
 void relu_bwd_colsum_launch(void* dy, const void* y, int N, int C, int ldy,
-                            float* out, hipStream_t stream) {
-  hipLaunchKernelGGL(relu_bwd_colsum_kernel, dim3((N + kRbRows - 1) / kRbRows),
-                     dim3(256), 0, stream, static_cast<bf16_t*>(dy),
-                     static_cast<const bf16_t*>(y), N, C, ldy, out);
+                            float* out, float* part, hipStream_t stream) {
+  const int nb = (N + kRbRows - 1) / kRbRows;
+  hipLaunchKernelGGL(relu_bwd_colsum_kernel, dim3(nb), dim3(256), 0, stream,
+                     static_cast<bf16_t*>(dy), static_cast<const bf16_t*>(y), N, C,
+                     ldy, out ? part : nullptr);
+  if (out)
+    hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, stream,
+                       part, nb, C, out);
 }
 
 void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,

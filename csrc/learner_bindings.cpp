@@ -83,12 +83,13 @@ at::Tensor learner_head_bwd(at::Tensor gscale, at::Tensor core, at::Tensor dlogi
               gwb.numel() == 256 && gbb.numel() == 1, "gradient sink shapes");
   const c10::DeviceGuard guard(core.device());
   auto dcore = at::empty_like(core);
+  auto part = at::empty({sa::learner_head_bwd_part_floats(T1 * B, A)}, core.options());
   sa::learner_head_bwd_launch(
       gscale.data_ptr<float>(), core.data_ptr<float>(), dlogits.data_ptr<float>(),
       dvalues.data_ptr<float>(), wp.data_ptr<float>(), wb.data_ptr<float>(),
       T1 * B, (T1 - 1) * B, A, dcore.data_ptr<float>(), gwp.data_ptr<float>(),
       gbp.data_ptr<float>(), gwb.data_ptr<float>(), gbb.data_ptr<float>(),
-      stream());
+      part.data_ptr<float>(), stream());
   return dcore;
 }
 
@@ -115,8 +116,9 @@ void colsum_f32_(at::Tensor x, at::Tensor out) {
   const int64_t N = x.numel() / C;
   TORCH_CHECK(out.numel() == C, "out must have one entry per column");
   const c10::DeviceGuard guard(x.device());
+  auto part = at::empty({sa::colsum_f32_part_floats((int)N, C)}, x.options());
   sa::colsum_f32_launch(x.data_ptr<float>(), (int)N, C, out.data_ptr<float>(),
-                        stream());
+                        part.data_ptr<float>(), stream());
 }
 
 // dy bf16 [N,C] *= (y > 0); y may be a column slice (row stride >= C)
@@ -134,8 +136,12 @@ void relu_bwd_colsum_(at::Tensor dy, at::Tensor y, c10::optional<at::Tensor> out
     op = out->data_ptr<float>();
   }
   const c10::DeviceGuard guard(dy.device());
+  at::Tensor part;
+  if (op)
+    part = at::empty({sa::relu_bwd_colsum_part_floats(N, C)},
+                     dy.options().dtype(at::kFloat));
   sa::relu_bwd_colsum_launch(dy.data_ptr(), y.data_ptr(), N, C, (int)y.stride(0),
-                             op, stream());
+                             op, op ? part.data_ptr<float>() : nullptr, stream());
 }
 
 void relu_mask_bf16_(at::Tensor dx, at::Tensor x) {

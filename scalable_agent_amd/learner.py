@@ -127,6 +127,12 @@ class Learner:
     use_hip = getattr(agent, 'backend', 'torch') == 'hip'
     self.use_fused = use_hip
     lstm_err = None
+    if use_hip and getattr(flags, 'deterministic', False):
+      # bf16 torso: per-workgroup weight-gradient slots summed in a fixed
+      # order instead of float atomics (the fp32 torso and the learner-head /
+      # column-sum reductions always reduce in a fixed order)
+      from . import ops
+      ops.load().conv_tune('deterministic', 1)
     if use_hip and self.device.type == 'cuda':
       # a cooperative LSTM unroll that timed out skips the update (and is
       # counted) instead of applying gradients of stale activations
