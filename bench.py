@@ -35,7 +35,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from scalable_agent_amd import flags as flags_lib  # noqa: E402
-from scalable_agent_amd.envs.synthetic import make_synthetic_batch  # noqa
+from scalable_agent_amd.envs.synthetic import (  # noqa: E402
+    add_synthetic_instructions, make_synthetic_batch)
 from scalable_agent_amd.learner import FlatStaging, Learner  # noqa
 from scalable_agent_amd.models import Agent  # noqa: E402
 from scalable_agent_amd.models.agent import torso_precision  # noqa: E402
@@ -66,6 +67,12 @@ def measure(args, dtype, device, backend, rank, world):
       make_synthetic_batch(args.batch_size, args.unroll_length, frame_shape,
                            num_actions, seed=1000 * rank + i, pin_memory=False)
       for i in range(2)]
+  if args.instructions:
+    # DMLab-style levels: instruction strings through the language LSTM
+    # (reference experiment.py:123-146) as part of the core input
+    host_batches = [add_synthetic_instructions(hb, agent.embed.shape[0],
+                                               seed=77 + i)
+                    for i, hb in enumerate(host_batches)]
   cuda = device.type == 'cuda'
   use_graph = bool(args.graph) and cuda
   graphs = []
@@ -162,6 +169,9 @@ def main():
                   help='precision of the reported value (fp32 = reference)')
   ap.add_argument('--also_bf16', type=int, default=1,
                   help='with --dtype fp32: also time the bf16 learner')
+  ap.add_argument('--instructions', type=int, default=0,
+                 help='1: DMLab-style batches with instruction strings '
+                      '(language LSTM in the core input).')
   ap.add_argument('--graph', type=int, default=1)
   ap.add_argument('--device', default='auto')
   ap.add_argument('--pipeline_chunks', type=int, default=1,
@@ -214,6 +224,7 @@ def main():
            'loss_finite': main_res['loss_finite'],
            'learner_health': main_res['health'],
            'pipeline_chunks': args.pipeline_chunks,
+           'instructions': bool(args.instructions),
            'host_enqueue_ms_per_step': round(
                1000 * main_res['enqueue_s'] / args.steps, 3),
            'h2d_prefetch': main_res['h2d_prefetch'],

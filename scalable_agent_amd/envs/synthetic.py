@@ -155,3 +155,18 @@ def make_synthetic_batch(batch_size, unroll_length, frame_shape, num_actions,
     if device != 'cpu':
       out = _map_tensors(out, lambda t: t.to(device))
   return out
+
+
+def add_synthetic_instructions(batch, vocab, seed=0, max_len=16):
+  """Adds DMLab-style instruction observations to a time-major batch:
+  word ids [T+1, B, max_len] (< vocab, zero past the length) and lengths
+  [T+1, B] in 0..max_len (0 = no instruction on that step)."""
+  g = torch.Generator().manual_seed(seed)
+  T1, B = batch.env_outputs.reward.shape
+  ids = torch.randint(1, vocab, (T1, B, max_len), generator=g)
+  lengths = torch.randint(0, max_len + 1, (T1, B), generator=g)
+  ids = ids * (torch.arange(max_len).view(1, 1, max_len) <
+               lengths.unsqueeze(-1))
+  eo = batch.env_outputs
+  return batch._replace(env_outputs=eo._replace(
+      observation=(eo.observation[0], (ids, lengths))))

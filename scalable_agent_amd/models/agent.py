@@ -245,7 +245,7 @@ class Agent(nn.Module):
     capturing = lengths.is_cuda and torch.cuda.is_current_stream_capturing()
     if lengths.numel() == 0 or (not capturing and int(lengths.max()) == 0):
       return torch.zeros(n, INSTR_LSTM, device=device, dtype=self.embed.dtype)
-    emb = F.embedding(ids, self.embed)  # [N, L, 20]
+    emb = layers.embedding_lookup(ids, self.embed)  # [N, L, 20]
     if self.backend == 'hip' and emb.is_cuda:
       # words are the time axis of the fused H=64 LSTM step kernels (K7
       # shares K9's kernels); the output is h at the last valid word
@@ -254,7 +254,8 @@ class Agent(nn.Module):
       done = torch.zeros(ids.shape[1], n, dtype=torch.bool, device=device)
       hs, _ = ops.lstm_unroll(emb.transpose(0, 1).contiguous(), done, (z, z),
                               self.language_lstm_kernel,
-                              self.language_lstm_bias)
+                              self.language_lstm_bias,
+                              exact=self.compute_dtype == torch.float32)
       last = (lengths - 1).clamp(min=0).view(1, n, 1).expand(1, n, INSTR_LSTM)
       out = hs.gather(0, last).squeeze(0)
       return out * (lengths > 0).unsqueeze(-1).to(out.dtype)
@@ -371,10 +372,10 @@ class Agent(nn.Module):
   # ------------------------------------------------------------------ API
   def fused_core_ready(self, instr=None):
     """True when the HIP learner path (fused torso-FC/core-input/LSTM op,
-    fused heads+V-trace loss) applies: HIP backend, HIP torso, no
-    instruction strings, bf16 compute."""
-    return (self.backend == 'hip' and _bf16_torso_ready(self) and
-            instr is None)
+    fused heads+V-trace loss) applies: HIP backend, HIP bf16 torso; the
+    instruction encoding (language LSTM) joins the fused core input."""
+    del instr
+    return self.backend == 'hip' and _bf16_torso_ready(self)
 
   def unroll_core(self, actions, env_outputs, core_state):
     """Everything of `unroll` up to the LSTM output: -> (core_out [T,B,256],
@@ -393,10 +394,12 @@ class Agent(nn.Module):
     if self.fused_core_ready(instr) and frames.is_cuda:
       from .. import ops
       feats = self.conv_features(frames)
+      instr_enc = (None if instr is None else
+                   self.instruction_encoding(instr, T * B, frames.device))
       return ops.core_lstm(feats, self.linear_w, self.linear_b,
                            self.lstm_kernel, self.lstm_bias,
                            reward.reshape(T * B), actions.reshape(T * B), done,
-                           core_state, self.num_actions)
+                           core_state, self.num_actions, instr_enc=instr_enc)
     x = self.core_inputs(frames, reward.reshape(T * B),
                          actions.reshape(T * B), instr)
     x = x.view(T, B, -1)

@@ -91,3 +91,35 @@ def glorot_uniform_(w, generator=None):
   with torch.no_grad():
     w.uniform_(-limit, limit, generator=generator)
   return w
+
+
+class _EmbeddingLookup(torch.autograd.Function):
+  """table[ids] whose backward is a fixed-size scatter-add: graph-capture
+  safe on the GPU (torch's embedding backward sorts and compacts the ids,
+  sizing work from the data, which a replayed hipGraph cannot follow).
+  Deterministic mode (torch.are_deterministic_algorithms_enabled()): the
+  gradient is one_hot(ids)^T @ g, a GEMM with a fixed summation order."""
+
+  @staticmethod
+  def forward(ctx, ids, table):
+    flat = ids.reshape(-1)
+    ctx.save_for_backward(flat)
+    ctx.V = table.shape[0]
+    return table.index_select(0, flat).view(*ids.shape, table.shape[1])
+
+  @staticmethod
+  def backward(ctx, g):
+    (flat,) = ctx.saved_tensors
+    g2 = g.reshape(flat.numel(), -1).float()
+    if torch.are_deterministic_algorithms_enabled():
+      onehot = F.one_hot(flat, ctx.V).to(g2.dtype)
+      grad = onehot.t() @ g2
+    else:
+      grad = torch.zeros(ctx.V, g2.shape[1], dtype=g2.dtype, device=g2.device)
+      grad.index_add_(0, flat, g2)
+    return None, grad
+
+
+def embedding_lookup(ids, table):
+  """tf.nn.embedding_lookup (reference experiment.py:131-133)."""
+  return _EmbeddingLookup.apply(ids, table)

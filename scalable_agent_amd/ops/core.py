@@ -6,10 +6,11 @@ instruction]) and :228-235 (LSTMBlockCell(256) unrolled with done-reset).
 
 Forward (one autograd node: 4 launches + the recurrence):
   h      = relu(feats W_fc + b_fc)              hipBLASLt bf16, bias+ReLU epilogue
-  h_aug  = [h, clip(r), one_hot(a), 0...]      core_aug_fwd (the instruction
-                                               encoding is all-zero without
-                                               instructions, so its W_x rows
-                                               drop out of the product)
+  h_aug  = [h, clip(r), one_hot(a), instr|0]   core_aug_fwd (+ the 64
+                                               language-LSTM columns on
+                                               instruction levels; without
+                                               instructions they are zero
+                                               and their W_x rows drop out)
   xw     = h_aug W_x[:K] + b_lstm               hipBLASLt bf16 in, fp32 out
   hs, cs = LSTM recurrence                      lstm.hip fwd steps (fp32)
 Backward:
@@ -47,21 +48,31 @@ class _CoreLSTM(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions):
+              done_u8, num_actions, instr_enc):
     C = ext()
     T, B = done_u8.shape
     N = T * B
     f_in = CORE + 1 + num_actions + 64
-    K = aug_width(num_actions)
-    assert K <= f_in and kernel.shape[0] == f_in + CORE
+    c_instr = CORE + 1 + num_actions
+    assert kernel.shape[0] == f_in + CORE
     bf = torch.bfloat16
     w16_fc = w_fc.to(bf)
-    wx16 = kernel[:K].to(bf)
     h = torch._addmm_activation(b_fc.to(bf), feats, w16_fc)
+    if instr_enc is None:
+      # the instruction columns are all zero: their W_x rows drop out
+      K = ld = aug_width(num_actions)
+    else:
+      # the 64 language-LSTM columns join the core input (experiment.py:
+      # 191-198); rows padded to 16 columns, the product uses the f_in first
+      K, ld = f_in, (f_in + 15) // 16 * 16
+    assert K <= f_in
+    wx16 = kernel[:K].to(bf)
     # reward clipping of the core input is always abs_one (experiment.py:194)
-    h_aug = C.core_aug_fwd(h, rewards, actions, K, 0)
+    h_aug = C.core_aug_fwd(h, rewards, actions, ld, 0)
     del h
-    xw = torch.addmm(bias, h_aug, wx16, out_dtype=torch.float32)
+    if instr_enc is not None:
+      h_aug[:, c_instr:f_in].copy_(instr_enc)
+    xw = torch.addmm(bias, h_aug[:, :K], wx16, out_dtype=torch.float32)
     mode = C.lstm_mode(CORE, B, T, False)  # bf16 path: the gang may run
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
                                        kernel[f_in:], mode)
@@ -70,6 +81,8 @@ class _CoreLSTM(torch.autograd.Function):
                           wt, acts, cs, c0, hpm, done_u8)
     ctx.f_in = f_in
     ctx.K = K
+    ctx.c_instr = c_instr
+    ctx.has_instr = instr_enc is not None
     return hs, cs[-1]
 
   @staticmethod
@@ -104,7 +117,8 @@ class _CoreLSTM(torch.autograd.Function):
     with torch.cuda.stream(side) if side is not None else _nullctx():
       gk[f_in:].addmm_(hpm.view(N, CORE).t(), dg2)                  # W_h
       gxk = gk[:K]
-      torch.addmm(gxk, h_aug.t(), dg16_2, out_dtype=f32, out=gxk)   # W_x rows
+      torch.addmm(gxk, h_aug[:, :K].t(), dg16_2, out_dtype=f32,
+                  out=gxk)                                          # W_x rows
       C.colsum_f32_(dg2, gb)                                        # b_lstm
       torch.addmm(gwfc, feats.t(), dh, out_dtype=f32, out=gwfc)     # W_fc
     dh0 = None
@@ -113,20 +127,27 @@ class _CoreLSTM(torch.autograd.Function):
       dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
     if not ctx.needs_input_grad[7]:
       dc0 = None
+    d_instr = None
+    if ctx.has_instr and ctx.needs_input_grad[11]:
+      # into the language LSTM: dG W_x[instruction rows]^T
+      d_instr = torch.mm(dg16_2, wx16[ctx.c_instr:f_in].t(), out_dtype=f32)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
-    return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None)
+    return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
+            d_instr)
 
 
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
-              num_actions):
+              num_actions, instr_enc=None):
   """feats bf16 [T*B, F] (ReLU'd torso output), rewards [T*B] f32, actions
-  [T*B] (last actions), done [T,B] bool, state (c, h) [B,256] ->
-  (hs [T,B,256] f32, (c_T, h_T))."""
+  [T*B] (last actions), done [T,B] bool, state (c, h) [B,256], instr_enc
+  None or the language-LSTM output [T*B, 64] (gradients flow back into it)
+  -> (hs [T,B,256] f32, (c_T, h_T))."""
   c0, h0 = state
   hs, c_last = _CoreLSTM.apply(
       feats.contiguous(), w_fc, b_fc, kernel, bias,
       rewards.reshape(-1).to(torch.float32).contiguous(),
       actions.reshape(-1).to(torch.int64).contiguous(),
       c0.float().contiguous(), h0.float().contiguous(),
-      done.to(torch.uint8).contiguous(), int(num_actions))
+      done.to(torch.uint8).contiguous(), int(num_actions),
+      None if instr_enc is None else instr_enc.contiguous())
   return hs, (c_last, hs[-1])

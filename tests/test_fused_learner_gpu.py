@@ -8,7 +8,8 @@ import torch.nn.functional as F
 from scalable_agent_amd import flags as flags_lib
 from scalable_agent_amd import losses as losses_lib
 from scalable_agent_amd import vtrace as vtrace_lib
-from scalable_agent_amd.envs.synthetic import make_synthetic_batch
+from scalable_agent_amd.envs.synthetic import (add_synthetic_instructions,
+                                                make_synthetic_batch)
 from scalable_agent_amd.learner import Learner, batch_to_device, compute_loss
 from scalable_agent_amd.models import Agent
 
@@ -146,14 +147,61 @@ def test_core_lstm_matches_reference(cuda, T, B, A):
   assert K <= f_in
 
 
-def test_fused_learner_loss_matches_generic_hip_path(cuda):
+@pytest.mark.parametrize('T,B,A', [(26, 32, 9), (5, 3, 4)])
+def test_core_lstm_with_instructions_matches_reference(cuda, T, B, A):
+  """The fused core with the 64 language-LSTM columns in the core input
+  (instruction levels): outputs, every weight gradient and the gradient
+  into the instruction encoding against the fp32 reference."""
+  ops = _ops()
+  torch.manual_seed(7)
+  N, Fd = T * B, 3456
+  f_in = 256 + 1 + A + 64
+  feats = torch.randn(N, Fd, device=cuda).relu().bfloat16().requires_grad_()
+  w_fc = (torch.randn(Fd, 256, device=cuda) * 0.02).requires_grad_()
+  b_fc = (torch.randn(256, device=cuda) * 0.1).requires_grad_()
+  kernel = (torch.randn(f_in + 256, 1024, device=cuda) * 0.05).requires_grad_()
+  bias = (torch.randn(1024, device=cuda) * 0.1).requires_grad_()
+  enc = (torch.randn(N, 64, device=cuda) * 0.5).tanh().requires_grad_()
+  rew = torch.randn(N, device=cuda) * 2
+  act = torch.randint(0, A, (N,), device=cuda)
+  done = torch.rand(T, B, device=cuda) < 0.1
+  c0 = torch.randn(B, 256, device=cuda) * 0.3
+  h0 = torch.randn(B, 256, device=cuda) * 0.3
+  leaves = [feats, w_fc, b_fc, kernel, bias, enc]
+  bfr = lambda t: t.bfloat16().float()
+  h = F.relu(feats.float() @ bfr(w_fc) + bfr(b_fc))
+  x = torch.cat([h, rew.clamp(-1, 1).unsqueeze(1), F.one_hot(act, A).float(),
+                 bfr(enc)], 1).view(T, B, -1)
+  kx = torch.cat([bfr(kernel[:f_in]), kernel[f_in:]], 0)
+  hs_ref, _ = _ref_lstm(x, done, c0, h0, kx, bias)
+  go = torch.randn_like(hs_ref)
+  (hs_ref * go).sum().backward()
+  gref = [t.grad.clone() for t in leaves]
+  for t in leaves:
+    t.grad = None
+  hs, _ = ops.core_lstm(feats, w_fc, b_fc, kernel, bias, rew, act, done,
+                        (c0, h0), A, instr_enc=enc)
+  assert _cos(hs, hs_ref) > 0.9999
+  (hs * go).sum().backward()
+  for name, t, g in zip(['feats', 'w_fc', 'b_fc', 'kernel', 'bias', 'enc'],
+                        leaves, gref):
+    assert _cos(t.grad, g) > 0.999, (name, _cos(t.grad, g))
+  # the instruction rows of W_x do receive gradient now
+  assert torch.count_nonzero(kernel.grad[257 + A:f_in]) > 0
+
+
+@pytest.mark.parametrize('instructions', [False, True])
+def test_fused_learner_loss_matches_generic_hip_path(cuda, instructions):
   """compute_loss on the fused path vs the per-op HIP path (torso + torch FC
   + lstm_unroll + fused V-trace kernel) on the same agent."""
   _ops()
   f = flags_lib.default_flags(batch_size=4, unroll_length=12)
-  b = batch_to_device(make_synthetic_batch(4, 12, (72, 96, 3), 9, seed=2), cuda)
+  b = make_synthetic_batch(4, 12, (72, 96, 3), 9, seed=2)
   agent = Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=4,
                 backend='hip', compute_dtype=torch.bfloat16)
+  if instructions:
+    b = add_synthetic_instructions(b, agent.embed.shape[0], seed=3)
+  b = batch_to_device(b, cuda)
   lrn = Learner(agent, f, cuda)
   out = []
   for fused in (True, False):
@@ -170,6 +218,9 @@ def test_fused_learner_loss_matches_generic_hip_path(cuda):
   (l1, g1), (l2, g2) = out
   torch.testing.assert_close(l1, l2, rtol=2e-3, atol=2e-2)
   assert _cos(g1, g2) > 0.999
+  if instructions:  # the language LSTM and embedding get gradient
+    emb = lrn.flat.view_of(lrn.flat.grads, 'embed')
+    assert float(emb.abs().sum()) > 0
 
 
 @pytest.mark.parametrize('N,C,ld', [(3232, 256, 272), (37, 16, 16), (5, 64, 80)])
@@ -203,3 +254,32 @@ def test_glue_kernels_match_torch(cuda, N, C, ld):
   assert torch.equal(aug[:, C].float(), rw.clamp(-1, 1).bfloat16().float())
   oh = torch.nn.functional.one_hot(act, 15).bfloat16()
   assert torch.equal(aug[:, C + 1:], oh)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_instruction_learner_graph_replay_matches_eager(cuda, dtype):
+  """Instruction levels under hipGraph capture (more than 3072 word lookups:
+  the embedding gradient must be a fixed-size scatter, not a data-sized
+  sort/compact): replayed steps match eager steps from the same state."""
+  _ops()
+  f = flags_lib.default_flags(batch_size=8, unroll_length=30)
+  mk = lambda: Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=4,
+                     backend='hip', compute_dtype=dtype)
+  ref_agent = mk()
+  b = make_synthetic_batch(8, 30, (72, 96, 3), 9, seed=2)
+  b = batch_to_device(add_synthetic_instructions(b, ref_agent.embed.shape[0],
+                                                 seed=3), cuda)
+  eager = Learner(ref_agent, f, cuda)
+  graph = Learner(mk(), f, cuda)
+  graph.capture(b)
+  losses = []
+  for _ in range(2):
+    le = eager.step(b)
+    lg = graph.graph_step()
+    losses.append((float(le), float(lg)))
+  torch.cuda.synchronize()
+  for le, lg in losses:
+    assert abs(le - lg) <= 1e-3 * max(1.0, abs(le)), losses
+  emb_e = eager.flat.view_of(eager.flat.params, 'embed')
+  emb_g = graph.flat.view_of(graph.flat.params, 'embed')
+  assert torch.allclose(emb_e, emb_g, rtol=1e-4, atol=1e-6)
