@@ -4,6 +4,7 @@
 
 #include <vector>
 
+#include "envpool/env_channel.h"
 #include "envpool/shm_ring.h"
 #include "envpool/traj_queue.h"
 
@@ -12,6 +13,38 @@ namespace py = pybind11;
 namespace sa {
 
 void register_envpool(py::module& m) {
+  py::class_<EnvChannel>(m, "EnvChannel")
+      .def(py::init<>())
+      .def("request", &EnvChannel::Request, py::arg("method"), py::arg("kind"),
+           py::arg("action"))
+      .def("wait_response", [](EnvChannel& c, uint32_t seq, int64_t t) {
+             py::gil_scoped_release nogil;
+             return c.WaitResponse(seq, t);
+           }, py::arg("seq"), py::arg("timeout_ms"))
+      .def_property_readonly("status", &EnvChannel::status)
+      .def_property_readonly("reward", &EnvChannel::reward)
+      .def_property_readonly("done", &EnvChannel::done)
+      .def_property_readonly("instr", [](EnvChannel& c) -> py::object {
+             if (!c.has_instr()) return py::none();
+             return py::bytes(c.instr());
+           })
+      .def("wait_request", [](EnvChannel& c, int64_t t) {
+             std::tuple<int64_t, int32_t, int32_t, std::vector<double>> r;
+             {
+               py::gil_scoped_release nogil;
+               r = c.WaitRequest(t);
+             }
+             return r;
+           }, py::arg("timeout_ms"))
+      .def("discard_pending", &EnvChannel::DiscardPending)
+      .def("respond", [](EnvChannel& c, uint32_t seq, int32_t status, float reward,
+                         bool done, py::object instr) {
+             const bool has = !instr.is_none();
+             std::string s = has ? instr.cast<std::string>() : std::string();
+             c.Respond(seq, status, reward, done, has, s);
+           }, py::arg("seq"), py::arg("status"), py::arg("reward"), py::arg("done"),
+           py::arg("instr"));
+
   py::class_<ShmRing>(m, "ShmRing", py::buffer_protocol())
       .def(py::init<const std::string&, int64_t, int64_t, bool>(),
            py::arg("name"), py::arg("num_slots") = 0, py::arg("slot_bytes") = 0,

@@ -219,14 +219,94 @@ class _Faults(object):
       time.sleep(3600)
 
 
+# Hot env calls over the native shared-memory channel (runtime/native
+# EnvChannel, csrc/envpool/env_channel.cc): method codes and action encoding.
+_M_INITIAL, _M_STEP, _M_CLOSE = 0, 1, 2
+
+
+def _encode_action(action):
+  """-> (kind, values) for the channel, or None (send over the pipe)."""
+  if isinstance(action, (bool, np.bool_)):
+    return None
+  if isinstance(action, (int, np.integer)):
+    return 0, [float(action)]
+  a = np.asarray(action)
+  if a.ndim == 1 and a.size <= 16 and a.dtype.kind in 'iu':
+    return 1, a.astype(np.float64).tolist()
+  if a.ndim == 1 and a.size <= 16 and a.dtype.kind == 'f':
+    return 2, a.astype(np.float64).tolist()
+  return None
+
+
+def _decode_action(kind, values):
+  if kind == 0:
+    return int(values[0])
+  if kind == 1:
+    return np.asarray(values, dtype=np.int64)
+  return np.asarray(values, dtype=np.float64)
+
+
+def _encode_instr(instr):
+  if instr is None:
+    return None
+  if isinstance(instr, bytes):
+    return b'b' + instr
+  return b's' + str(instr).encode('utf-8')
+
+
+def _decode_instr(raw):
+  if raw is None:
+    return None
+  return raw[1:] if raw[:1] == b'b' else raw[1:].decode('utf-8', 'replace')
+
+
+def _serve_channel(env, chan, conn, frames, faults):
+  """One channel request, if any arrives within 20 ms: True = served (or
+  closed -> 'close'), False = none."""
+  seq, method, kind, vals = chan.wait_request(20)
+  if seq < 0:
+    return False
+  if method == _M_CLOSE:
+    chan.respond(seq, 0, 0.0, False, None)
+    return 'close'
+  try:
+    if method == _M_INITIAL:
+      frame, instr = env.initial()
+      frames[...] = frame
+      chan.respond(seq, 0, 0.0, False, _encode_instr(instr))
+    else:
+      faults.on_step()
+      reward, done, (frame, instr) = env.step(_decode_action(kind, vals))
+      frames[...] = frame
+      chan.respond(seq, 0, float(reward), bool(done), _encode_instr(instr))
+  except Exception as e:  # pylint: disable=broad-except
+    try:
+      e.remote_traceback = traceback.format_exc()
+      conn.send(('error', -1, e))
+    except Exception:  # pylint: disable=broad-except
+      conn.send(('error', -1, _RemoteError(repr(e))))
+    chan.respond(seq, 1, 0.0, False, None)
+  return True
+
+
 def _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape,
-                restarted, faults):
+                restarted, faults, chan=None):
   env = None
   frames = np.frombuffer(frame_buf, dtype=np.uint8).reshape(frame_shape)
   try:
     env = env_ctor(*args, **kwargs)
+    if chan is not None:
+      chan.discard_pending()  # a request the dead predecessor never answered
     conn.send(('restarted' if restarted else 'ready', -1, None))
     while True:
+      if chan is not None:
+        served = _serve_channel(env, chan, conn, frames, faults)
+        if served == 'close':
+          env.close()
+          conn.close()
+          return
+        if served or not conn.poll(0):
+          continue
       msg = conn.recv()
       if msg is None:
         env.close()
@@ -259,7 +339,7 @@ def _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape,
 
 
 def _supervisor(env_ctor, args, kwargs, conn, frame_buf, frame_shape, pid_box,
-                restarts_box, fault_spec, seed, max_restarts):
+                restarts_box, fault_spec, seed, max_restarts, chan=None):
   import os
   import signal
   signal.signal(signal.SIGINT, signal.SIG_IGN)
@@ -270,7 +350,8 @@ def _supervisor(env_ctor, args, kwargs, conn, frame_buf, frame_shape, pid_box,
       code = 0
       try:
         _env_worker(env_ctor, args, kwargs, conn, frame_buf, frame_shape,
-                    restarts > 0, _Faults(fault_spec, seed * 7919 + restarts))
+                    restarts > 0, _Faults(fault_spec, seed * 7919 + restarts),
+                    chan)
       except BaseException:  # pylint: disable=broad-except
         code = 1
       os._exit(code)
@@ -315,6 +396,15 @@ class EnvProcess(object):
     self._process = None
     self._closed = False
     self._seq = 0
+    # initial/step over the native futex channel (created before the fork);
+    # the pipe stays for other methods, errors and restart notices
+    self._chan = None
+    if kwargs.pop('channel', True):
+      try:
+        from .runtime import native
+        self._chan = native.EnvChannel()
+      except Exception:  # pylint: disable=broad-except  (no native module)
+        self._chan = None
 
   @property
   def restarts(self):
@@ -326,7 +416,7 @@ class EnvProcess(object):
         target=_supervisor,
         args=(self._ctor, self._args, self._kwargs, child, self._buf,
               self._shape, self._pid, self._restarts, self._fault_spec,
-              self._fault_seed, self._max_restarts), daemon=True)
+              self._fault_seed, self._max_restarts, self._chan), daemon=True)
     self._process.start()
     child.close()
     status, _, payload = self._conn.recv()
@@ -375,26 +465,76 @@ class EnvProcess(object):
     except (EOFError, OSError):
       raise OutOfRangeError('env process closed')
 
+  # ---------------------------------------------------- channel calls
+  def _chan_send(self, method, action=None):
+    if self._closed:
+      raise OutOfRangeError('env process closed')
+    if method == _M_STEP:
+      enc = _encode_action(action)
+      if enc is None:
+        return None
+      kind, vals = enc
+    else:
+      kind, vals = 0, []
+    return ('chan', self._chan.request(method, kind, vals))
+
+  def _chan_recv(self, seq):
+    """Waits for the channel response in 50 ms slices, watching the pipe
+    for a restart notice / error and enforcing the hang watchdog."""
+    import time
+    start = time.time()
+    try:
+      while not self._chan.wait_response(seq, 50):
+        if self._conn.poll(0):
+          status, _, payload = self._conn.recv()
+          if status == 'restarted':
+            raise EnvRestartedError('env worker replaced (restart %d)' %
+                                    self._restarts.value)
+          if status == 'error':
+            raise payload
+        if self._closed:
+          raise OutOfRangeError('env process closed')
+        if self._timeout and time.time() - start > self._timeout:
+          self._kill_worker()  # hung: the supervisor forks a replacement
+          start = time.time()
+      if self._chan.status != 0:  # the exception follows on the pipe
+        status, _, payload = self._conn.recv()
+        if status == 'restarted':
+          raise EnvRestartedError('env worker replaced (restart %d)' %
+                                  self._restarts.value)
+        raise payload
+    except (EOFError, OSError):
+      raise OutOfRangeError('env process closed')
+    return (self._chan.reward, self._chan.done,
+            _decode_instr(self._chan.instr))
+
   def initial(self):
-    (instr,) = self._rpc('initial')
-    return [self._frames.copy(), instr]
+    return [self._frames.copy(), self.initial_nocopy()]
 
   def step(self, action):
-    reward, done, instr = self._rpc('step', action)
+    reward, done, instr = self.step_recv(self.step_send(action))
     return np.float32(reward), np.bool_(done), [self._frames.copy(), instr]
 
   # split-phase calls for vectorised actors (runtime/actor_group.py): send
   # the step of every env first, then collect the replies, so the envs of a
   # group step in parallel; the frame is read in place from `frame_view`
   def step_send(self, action):
+    if self._chan is not None:
+      t = self._chan_send(_M_STEP, action)
+      if t is not None:
+        return t
     return self._send('step', (action,))
 
   def step_recv(self, seq):
     """-> (reward, done, instruction); the frame is in `frame_view`."""
+    if isinstance(seq, tuple):
+      return self._chan_recv(seq[1])
     reward, done, instr = self._recv(seq)
     return reward, done, instr
 
   def initial_nocopy(self):
+    if self._chan is not None:
+      return self._chan_recv(self._chan_send(_M_INITIAL)[1])[2]
     (instr,) = self._rpc('initial')
     return instr
 
