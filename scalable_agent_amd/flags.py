@@ -76,6 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
                  help='sum: N learners x B == one learner with N*B (reference '
                       'losses are sums).')
+  p.add_argument('--grad_overlap', type=_str2bool, default=True,
+                 help='Data-parallel: all-reduce the heads/core/FC gradients '
+                      'while the conv-torso backward runs (two-phase '
+                      'backward), then the torso gradients.')
   p.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
                  help='Compute dtype of convs/GEMMs: fp32 = the reference\'s '
                       'precision (exact-fp32 MFMA kernels on HIP); bf16 = '

@@ -162,22 +162,73 @@ class Learner:
       from .popart import PopArt
       self.popart = PopArt(self.agent.num_value_heads, flags.popart_beta,
                            self.device)
+    # data-parallel overlap: backward in two phases - heads/core/torso-FC
+    # (whose gradients are all-reduced at once, asynchronously) then the
+    # conv torso - so the bulk of the all-reduce runs under the torso
+    # backward.  Needs the torso parameters at the tail of
+    # the flat buffer.
+    self._split = False
+    self._split_pairs = None
     if world_size > 1:
       from .parallel import GradientSynchronizer
       self.grad_sync = GradientSynchronizer(self.flat, process_group,
                                             reduce=flags.grad_reduce)
+      off = self._torso_offset()
+      if getattr(flags, 'grad_overlap', True) and off is not None:
+        self.grad_sync.set_split(off)
+        self._split = self.grad_sync.split is not None
+
+  def _torso_offset(self):
+    """Flat offset where the conv-torso parameters start, if they are
+    exactly the buffer's tail."""
+    torso = [o for (n, _), o in zip(self.flat.named, self.flat.offsets)
+             if n.startswith('convnet.')]
+    other = [o for (n, _), o in zip(self.flat.named, self.flat.offsets)
+             if not n.startswith('convnet.')]
+    if not torso or not other or min(torso) < max(other):
+      return None
+    return min(torso)
 
   # ------------------------------------------------------------ eager step
-  def _fwd_bwd(self, data):
+  def _grad_ctx(self):
+    from .ops import grad_sink
+    return (grad_sink.direct_grads(self.use_fused),
+            grad_sink.overlap_weight_grads(self.use_fused and self._overlap))
+
+  def _fwd_late(self, data):
+    """Forward + the backward down to the torso features (all of it when
+    not splitting)."""
     self.flat.zero_grad()
-    with trace('forward'):
-      loss = compute_loss(self.agent, data, self.flags, self.use_fused,
-                          self.popart, self._aux)
+    pairs = [] if self._split else None
+    self.agent._split_torso = pairs
+    try:
+      with trace('forward'):
+        loss = compute_loss(self.agent, data, self.flags, self.use_fused,
+                            self.popart, self._aux)
+    finally:
+      self.agent._split_torso = None
     with trace('backward'):
-      from .ops import grad_sink
-      with grad_sink.direct_grads(self.use_fused), \
-          grad_sink.overlap_weight_grads(self.use_fused and self._overlap):
+      a, b = self._grad_ctx()
+      with a, b:
         loss.backward()
+    self._split_pairs = pairs
+    return loss
+
+  def _bwd_torso(self):
+    """Second backward phase: the conv torso from its features' gradient."""
+    pairs = self._split_pairs
+    if not pairs:
+      return
+    with trace('backward_torso'):
+      a, b = self._grad_ctx()
+      with a, b:
+        torch.autograd.backward([f for f, _ in pairs],
+                                [leaf.grad for _, leaf in pairs])
+
+  def _fwd_bwd(self, data):
+    loss = self._fwd_late(data)
+    self._bwd_torso()
+    self._split_pairs = None
     return loss
 
   def _apply(self):
@@ -200,7 +251,11 @@ class Learner:
   def step(self, data):
     """One learner update from a device-resident time-major batch."""
     self._popart_tasks = data.level_name if self.popart is not None else None
-    loss = self._fwd_bwd(data)
+    loss = self._fwd_late(data)
+    if self._split:
+      self.grad_sync.begin_early()  # under the torso backward
+    self._bwd_torso()
+    self._split_pairs = None
     self.flat.rebind_grads()
     self._apply()
     self.last_loss = loss.detach()
@@ -228,6 +283,22 @@ class Learner:
     # thread_local: actor-inference threads keep using the GPU (and the
     # caching allocator) while the learner captures
     mode = os.environ.get('SA_CAPTURE_MODE', 'thread_local')
+    if self._split:
+      # two graphs on one pool, replayed in capture order: forward + late
+      # backward, then the torso backward (the early all-reduce is launched
+      # between the two replays)
+      pool = torch.cuda.graph_pool_handle()
+      with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
+        self._static_loss = self._fwd_late(self._static_in).detach()
+      g2 = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g2, pool=pool, capture_error_mode=mode):
+        self._bwd_torso()
+      # the features / their gradients live in the pool: keep them
+      self._graph_keep = self._split_pairs
+      self._split_pairs = None
+      self.flat.params.copy_(saved_p)
+      self._graph = (g, g2)
+      return
     with torch.cuda.graph(g, capture_error_mode=mode):
       # detached: holding the autograd graph would keep its AccumulateGrad
       # nodes (and the streams they were created on) alive into later
@@ -242,7 +313,12 @@ class Learner:
   def graph_step(self):
     if self.popart is not None:
       self._popart_tasks = self._static_in.level_name
-    self._graph.replay()
+    if isinstance(self._graph, tuple):
+      self._graph[0].replay()
+      self.grad_sync.begin_early()
+      self._graph[1].replay()
+    else:
+      self._graph.replay()
     self._apply()
     self.last_loss = self._static_loss
     return self._static_loss

@@ -108,6 +108,10 @@ class Agent(nn.Module):
     # conv torso of chunk k+1 runs on the main stream (see _pipelined_core).
     self.pipeline_chunks = int(pipeline_chunks)
     self._core_streams = {}
+    # data-parallel learner: when a list, conv_features hands the core a
+    # detached leaf and records (features, leaf) so the torso backward can
+    # run as a separate phase (learner.Learner, gradient all-reduce overlap)
+    self._split_torso = None
     self.num_actions = num_actions
     # > 1: one (PopArt-normalised) value output per task (popart.py)
     self.num_value_heads = int(num_value_heads)
@@ -193,6 +197,15 @@ class Agent(nn.Module):
 
   def conv_features(self, frames):
     """frames uint8 [N,H,W,C] -> flattened conv features [N, flat]."""
+    feats = self._conv_features(frames)
+    split = self._split_torso
+    if split is not None and feats.requires_grad:
+      leaf = feats.detach().requires_grad_()
+      split.append((feats, leaf))
+      return leaf
+    return feats
+
+  def _conv_features(self, frames):
     if self.backend == 'hip' and frames.is_cuda:
       from .. import ops
       if _bf16_torso_ready(self):

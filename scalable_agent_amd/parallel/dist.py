@@ -117,23 +117,59 @@ class GradientSynchronizer:
       hi = lo
     self.buckets = bounds
     self.overlap = overlap
-    self._pending = []
+    self.split = None  # set_split(): [0, split) reduced before the rest
+    self._works = []
     self._events = None
     self.last_time_s = 0.0  # device time of the latest finished all-reduce
+
+  def set_split(self, offset):
+    """Two-phase reduction: the gradients in [0, offset) (heads, core, torso
+    FC: ~85 % of the parameters, produced first by backward) are all-reduced
+    by begin_early() while the conv-torso backward still runs; all_reduce()
+    then reduces [offset, n) and waits for both."""
+    self.split = int(offset) if 0 < offset < self.flat.numel else None
+
+  def _mark_start(self):
+    g = self.flat.grads
+    if not g.is_cuda:
+      return
+    if self._events is None:
+      self._events = (torch.cuda.Event(enable_timing=True),
+                      torch.cuda.Event(enable_timing=True))
+    elif self._events[1].query():
+      # previous step's collective has finished: harvest its duration
+      self.last_time_s = self._events[0].elapsed_time(self._events[1]) / 1e3
+    self._events[0].record()
+
+  def begin_early(self):
+    """Launches the all-reduce of the early bucket (async; RCCL runs it on
+    its own stream, ordered after the work already enqueued)."""
+    if self.world <= 1 or self.split is None or self._works:
+      return
+    self._mark_start()
+    self._works = [dist.all_reduce(self.flat.grads[:self.split],
+                                   group=self.group, async_op=True)]
 
   def all_reduce(self):
     if self.world <= 1:
       return
     g = self.flat.grads
     timed = g.is_cuda
+    if self.split is not None:
+      if not self._works:  # no early phase this step: reduce both now
+        self.begin_early()
+      works = self._works + [dist.all_reduce(g[self.split:], group=self.group,
+                                             async_op=True)]
+      self._works = []
+      for w in works:
+        w.wait()
+      if self.reduce == 'mean':
+        g.div_(self.world)
+      if timed:
+        self._events[1].record()
+      return
     if timed:
-      if self._events is None:
-        self._events = (torch.cuda.Event(enable_timing=True),
-                        torch.cuda.Event(enable_timing=True))
-      elif self._events[1].query():
-        # previous step's collective has finished: harvest its duration
-        self.last_time_s = self._events[0].elapsed_time(self._events[1]) / 1e3
-      self._events[0].record()
+      self._mark_start()
     if len(self.buckets) == 1:
       dist.all_reduce(g, group=self.group)
     else:

@@ -43,16 +43,20 @@ def _slice_batch(batch, lo, hi):
           baseline=sl_time(out.agent_outputs.baseline)))
 
 
-def _worker(rank, world, port, result_path):
+def _worker(rank, world, port, result_path, overlap=True):
   os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                     MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
   from scalable_agent_amd import parallel
   parallel.init_distributed(backend='gloo')
   torch.manual_seed(0)
   f = flags_lib.default_flags(batch_size=B // world, unroll_length=T,
-                              torso='shallow', grad_reduce='sum')
+                              torso='shallow', grad_reduce='sum',
+                              grad_overlap=overlap)
   agent = Agent(9, torso='shallow', frame_shape=SHAPE, seed=rank + 10)
   learner = Learner(agent, f, 'cpu', world_size=world)
+  # two-phase backward (early all-reduce of heads/core/FC under the torso
+  # backward) exactly when asked
+  assert learner._split == overlap
   parallel.broadcast_params(learner.flat.params)   # rank 0's init wins
   full = make_synthetic_batch(B, T, SHAPE, 9, seed=7)
   per = B // world
@@ -65,9 +69,10 @@ def _worker(rank, world, port, result_path):
   parallel.cleanup()
 
 
-def test_dp_sum_equals_single_learner_with_full_batch(tmp_path):
+@pytest.mark.parametrize('overlap', [True, False])
+def test_dp_sum_equals_single_learner_with_full_batch(tmp_path, overlap):
   path = str(tmp_path / 'dp.pt')
-  mp.spawn(_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+  mp.spawn(_worker, args=(2, _free_port(), path, overlap), nprocs=2, join=True)
   dp = torch.load(path, weights_only=True)
   # single learner, full batch, same init as rank 0
   torch.manual_seed(0)
