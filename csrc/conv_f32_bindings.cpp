@@ -201,8 +201,10 @@ std::vector<at::Tensor> maxpool_fwd(at::Tensor x, int64_t pb_h, int64_t pb_w) {
   const int64_t Hp = (H + 1) / 2, Wp = (W + 1) / 2;
   auto y = at::empty({N, Hp, Wp, C}, x.options());
   auto arg = at::empty({N, Hp, Wp, C}, x.options().dtype(at::kByte));
-  sa::cf32::maxpool_fwd_launch(x.data_ptr<float>(), y.data_ptr<float>(), arg.data_ptr<uint8_t>(),
-                               N, H, W, C, Hp, Wp, pb_h, pb_w, stream());
+  TORCH_CHECK(sa::cf32::maxpool_fwd_launch(x.data_ptr<float>(), y.data_ptr<float>(),
+                                           arg.data_ptr<uint8_t>(), N, H, W, C, Hp, Wp,
+                                           pb_h, pb_w, stream()),
+              "maxpool: C / 4 must be a power of two");
   check_launch("cf32_maxpool_fwd");
   return {y, arg};
 }
@@ -216,9 +218,11 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int6
   TORCH_CHECK(dy.size(1) == (H + 1) / 2 && dy.size(2) == (W + 1) / 2, "pooled shape");
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
-  sa::cf32::maxpool_bwd_launch(dy.data_ptr<float>(), arg.data_ptr<uint8_t>(), dx.data_ptr<float>(),
-                               dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2), pb_h, pb_w,
-                               stream());
+  TORCH_CHECK(sa::cf32::maxpool_bwd_launch(dy.data_ptr<float>(), arg.data_ptr<uint8_t>(),
+                                           dx.data_ptr<float>(), dy.size(0), H, W,
+                                           dy.size(3), dy.size(1), dy.size(2), pb_h, pb_w,
+                                           stream()),
+              "maxpool: C / 4 must be a power of two");
   check_launch("cf32_maxpool_bwd");
   return dx;
 }

@@ -86,12 +86,13 @@ bool conv_pool_fwd_launch(const ConvArgs& a, int src_kind, int pbh, int pbw,
                           float* pooled, uint8_t* arg, hipStream_t s);
 
 // 3x3/2 max-pool, TF SAME (pads pb_h/pb_w before, -inf padding):
-// y [N, Hp, Wp, C] and the first maximal tap dy*3+dx per element.
-void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H,
+// y [N, Hp, Wp, C] and the first maximal tap dy*3+dx per element.  C / 4
+// must be a power of two (false otherwise).
+bool maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H,
                         int W, int C, int Hp, int Wp, int pb_h, int pb_w,
                         hipStream_t s);
 // dx[n, y, x, c] = sum of dy over the windows whose argmax is (y, x).
-void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N,
+bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N,
                         int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w,
                         hipStream_t s);
 // uint8 frames [P pixels][Cs <= 4] -> fp32 [P][4] (x / 255, zero-padded)

@@ -726,13 +726,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
 // accumulates into dW (HWIO) / db.  64 elements per block, the slots split
 // over the block's 4 waves (8 loads in flight per thread), the 4 wave sums
 // combined in LDS in wave order: deterministic.
+// Fixed-order sum of the per-workgroup weight-gradient slots: block = 16
+// outputs x 16 slot groups (enough blocks to fill the GPU for the small
+// 16/32-channel layers); slot group sg adds slots sg, sg+16, ... through 8
+// independent accumulators, and the 16 groups are combined in LDS in a fixed
+// tree order, so every run gives the same bits.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
     const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
     int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][17];
   const int per = MT16 * CG;
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int sg = threadIdx.x >> 6;
+  const int l = threadIdx.x & 15;
+  const int e = blockIdx.x * 16 + l;
+  const int sg = threadIdx.x >> 4;
   const bool live = e < ngrp * per;
   const int ng = live ? e / per : 0, rem = live ? e - ng * per : 0;
   const int m = rem / CG, c = rem - (rem / CG) * CG;
@@ -740,20 +746,23 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (want) {
     const float* p = part + static_cast<int64_t>(ng) * G * per + rem;
-    for (int k = sg; k < G; k += 32) {
+    for (int k = sg; k < G; k += 128) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int kk = k + 4 * u;
+        const int kk = k + 16 * u;
         if (kk < G) acc[u] += p[static_cast<int64_t>(kk) * per];
       }
     }
   }
-  red[sg][threadIdx.x & 63] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
-                               ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  red[sg][l] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+               ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (sg != 0 || !want) return;
-  const int l = threadIdx.x;
-  const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  float t[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    t[q] = (red[4 * q][l] + red[4 * q + 1][l]) + (red[4 * q + 2][l] + red[4 * q + 3][l]);
+  const float s = (t[0] + t[1]) + (t[2] + t[3]);
   const int co = ng * CG + c;
   if (m < M) {
     const int tap = m / CINP, ci = m - (m / CINP) * CINP;
@@ -764,18 +773,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
 }
 
 // ------------------------------------------------------------------ pooling
+// Max-pool 3x3/2 (TF SAME) with first-max argmax codes.  One workgroup row
+// of the grid = one output row (n, py); thread = 4 channels of one pooled
+// pixel; 32-bit in-row index math (a 64-bit div/mod per element made the
+// first version VALU bound), 64-bit row bases.  c4_shift = log2(C / 4).
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(
     const float* __restrict__ x, float* __restrict__ y, uint8_t* __restrict__ arg, int N,
-    int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w) {
-  const int C4 = C / 4;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (idx >= static_cast<int64_t>(N) * Hp * Wp * C4) return;
-  const int c4 = static_cast<int>(idx % C4);
-  int64_t t = idx / C4;
-  const int px = static_cast<int>(t % Wp);
-  t /= Wp;
-  const int py = static_cast<int>(t % Hp);
-  const int n = static_cast<int>(t / Hp);
+    int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w, int c4_shift) {
+  const int row = blockIdx.x;  // n * Hp + py
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  if (e >= (Wp << c4_shift)) return;
+  const int n = row / Hp, py = row - n * Hp;
+  const int c4 = e & ((1 << c4_shift) - 1);
+  const int px = e >> c4_shift;
+  const float* img = x + static_cast<int64_t>(n) * H * W * C + 4 * c4;
   float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   int code[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -786,8 +797,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(
     for (int dx = 0; dx < 3; ++dx) {
       const int xx = 2 * px - pb_w + dx;
       if (xx < 0 || xx >= W) continue;
-      const f4 v = *reinterpret_cast<const f4*>(
-          x + ((static_cast<int64_t>(n) * H + yy) * W + xx) * C + 4 * c4);
+      const f4 v = *reinterpret_cast<const f4*>(img + (yy * W + xx) * C);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (v[r] > best[r]) {  // strict: the first maximal tap wins
@@ -797,24 +807,28 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(
       }
     }
   }
-  *reinterpret_cast<f4*>(y + idx * 4) = f4{best[0], best[1], best[2], best[3]};
-  *reinterpret_cast<uint32_t*>(arg + idx * 4) =
+  const int64_t o = static_cast<int64_t>(row) * Wp * C + 4 * e;
+  *reinterpret_cast<f4*>(y + o) = f4{best[0], best[1], best[2], best[3]};
+  *reinterpret_cast<uint32_t*>(arg + o) =
       static_cast<uint32_t>(code[0]) | (static_cast<uint32_t>(code[1]) << 8) |
       (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
 }
 
+// Pool gradient gather: one grid row = one pre-pool row (n, y); thread = 4
+// channels of one pixel, summing the (<= 4) windows whose argmax is this
+// pixel in ascending (py, px) order (bitwise the sums of pool_grad_gather).
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(
     const float* __restrict__ dy, const uint8_t* __restrict__ arg, float* __restrict__ dx,
-    int N, int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w) {
-  const int C4 = C / 4;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (idx >= static_cast<int64_t>(N) * H * W * C4) return;
-  const int c4 = static_cast<int>(idx % C4);
-  int64_t t = idx / C4;
-  const int x = static_cast<int>(t % W);
-  t /= W;
-  const int y = static_cast<int>(t % H);
-  const int n = static_cast<int>(t / H);
+    int N, int H, int W, int C, int Hp, int Wp, int pb_h, int pb_w, int c4_shift) {
+  const int row = blockIdx.x;  // n * H + y
+  const int e = blockIdx.y * 256 + threadIdx.x;
+  if (e >= (W << c4_shift)) return;
+  const int n = row / H, y = row - n * H;
+  const int c4 = e & ((1 << c4_shift) - 1);
+  const int x = e >> c4_shift;
+  const int64_t pbase = static_cast<int64_t>(n) * Hp * Wp * C + 4 * c4;
+  const float* dP = dy + pbase;
+  const uint8_t* ag = arg + pbase;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   const int py_hi = (y + pb_h) >> 1, px_hi = (x + pb_w) >> 1;
 #pragma unroll
@@ -827,16 +841,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(
       const int px = px_hi - b;
       const int ox = x - (2 * px - pb_w);
       if (px < 0 || px >= Wp || ox < 0 || ox > 2) continue;
-      const int64_t o = ((static_cast<int64_t>(n) * Hp + py) * Wp + px) * C + 4 * c4;
-      const uint32_t codes = *reinterpret_cast<const uint32_t*>(arg + o);
-      const f4 g = *reinterpret_cast<const f4*>(dy + o);
+      const int o = (py * Wp + px) * C;
+      const uint32_t codes = *reinterpret_cast<const uint32_t*>(ag + o);
+      const f4 g = *reinterpret_cast<const f4*>(dP + o);
       const uint32_t want = static_cast<uint32_t>(oy * 3 + ox);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (((codes >> (8 * r)) & 0xFFu) == want) acc[r] += g[r];
     }
   }
-  *reinterpret_cast<f4*>(dx + idx * 4) = acc;
+  *reinterpret_cast<f4*>(dx + static_cast<int64_t>(row) * W * C + 4 * e) = acc;
 }
 
 // uint8 frames [P, Cs<=4] -> [P, 4] fp32 x / 255 (tf.to_float(frame) / 255,
@@ -993,7 +1007,7 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
   const int total = ngrp * MT * 16 * CG;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 63) / 64), dim3(256), 0, s, ws, G,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, s, ws, G,
                      ngrp, MT * 16, CG, CINP, M, a.Cin, a.Cout, a.dw, a.db);
   return true;
 }
@@ -1081,18 +1095,31 @@ bool conv_pool_fwd_launch(const ConvArgs& a, int src, int pbh, int pbw, float* p
   return false;
 }
 
-void maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H, int W, int C,
-                        int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
-  const int64_t total = static_cast<int64_t>(N) * Hp * Wp * (C / 4);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, x, y,
-                     arg, N, H, W, C, Hp, Wp, pb_h, pb_w);
+static int c4_shift_of(int C) {
+  const int c4 = C / 4;
+  int sh = 0;
+  while ((1 << sh) < c4) ++sh;
+  return (C % 4 == 0 && (1 << sh) == c4) ? sh : -1;
 }
 
-void maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, int H, int W,
+bool maxpool_fwd_launch(const float* x, float* y, uint8_t* arg, int N, int H, int W, int C,
+                        int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
+  const int sh = c4_shift_of(C);
+  if (sh < 0) return false;
+  const dim3 grid(static_cast<unsigned>(N) * Hp, ((Wp << sh) + 255) / 256);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, grid, dim3(256), 0, s, x, y, arg, N, H, W, C, Hp,
+                     Wp, pb_h, pb_w, sh);
+  return true;
+}
+
+bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, int H, int W,
                         int C, int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
-  const int64_t total = static_cast<int64_t>(N) * H * W * (C / 4);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, dy, arg,
-                     dx, N, H, W, C, Hp, Wp, pb_h, pb_w);
+  const int sh = c4_shift_of(C);
+  if (sh < 0) return false;
+  const dim3 grid(static_cast<unsigned>(N) * H, ((W << sh) + 255) / 256);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, grid, dim3(256), 0, s, dy, arg, dx, N, H, W, C, Hp,
+                     Wp, pb_h, pb_w, sh);
+  return true;
 }
 
 void frames_f32_launch(const uint8_t* x, float* y, int64_t P, int Cs, hipStream_t s) {
