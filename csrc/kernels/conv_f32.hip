@@ -25,6 +25,7 @@
 #include "conv_f32.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 namespace sa {
@@ -37,6 +38,19 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kThreads = 256;
 constexpr size_t kLdsSoft = 80 * 1024;   // two workgroups per CU
 constexpr size_t kLdsHard = 156 * 1024;  // one workgroup per CU
+
+// Launch-shape knobs read once from the environment (measurement sweeps;
+// the defaults are the tuned values): resident workgroups per CU targeted by
+// the persistent forward / stage-head grids (capped by LDS), and the maximum
+// number of weight-gradient slots.
+int env_knob(const char* name, int def) {
+  const char* e = std::getenv(name);
+  return (e && *e) ? std::atoi(e) : def;
+}
+int occupancy(size_t lds_bytes, int cap) {
+  const int fit = static_cast<int>((160 * 1024) / (lds_bytes + 512));
+  return std::max(1, std::min(cap, fit));
+}
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -931,7 +945,11 @@ bool run_conv(const ConvArgs& a, hipStream_t s) {
   const int nt = (a.Ho + R - 1) / R;
   const int ntiles = a.N * nt;
   const int gy = a.Cout / COUT_T;
-  const int per_cu = bytes(R) <= kLdsSoft ? 2 : 1;
+  // 16-in/16-out layers gain from a third resident workgroup per CU (res16
+  // fwd/dgrad 313 -> 284-292 us); 16->32 loses (518 -> 659 us)
+  static const int occ_env = env_knob("SA_F32_FWD_OCC", 0);
+  const int occ_cap = occ_env ? occ_env : (CINP <= 16 && COUT_T <= 16 ? 3 : 2);
+  const int per_cu = occupancy(bytes(R), occ_cap);
   const int G = std::max(1, std::min(ntiles, 256 * per_cu / gy));
   auto kern = conv_fwd_kernel<CINP, COUT_T, K, S, SRC, FLIP>;
   allow_lds(kern, bytes(R));
@@ -959,7 +977,8 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
   const int nt = (Hp + R - 1) / R;
   R = (Hp + nt - 1) / nt;
   const int ntiles = a.N * nt;
-  const int per_cu = bytes(R) <= kLdsSoft ? 2 : 1;
+  static const int occ_cap = env_knob("SA_F32_POOL_OCC", 3);
+  const int per_cu = occupancy(bytes(R), occ_cap);
   const int G = std::max(1, std::min(ntiles, 256 * per_cu));
   auto kern = conv_pool_fwd_kernel<CINP, COUT, SRC>;
   allow_lds(kern, bytes(R));
@@ -1017,8 +1036,9 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
 // Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
 // least 128 slots (before the tile-count cap) so the reduction fills the GPU.
 int64_t wgrad_slots(int K, int cinp, int cout) {
+  static const int cap = env_knob("SA_F32_WG_SLOTS", 512);
   const int64_t rows = ((K * K * cinp + 16) / 16) * 16;
-  return std::max<int64_t>(128, std::min<int64_t>(512, (8ll << 20) / (rows * cout)));
+  return std::max<int64_t>(128, std::min<int64_t>(cap, (8ll << 20) / (rows * cout)));
 }
 
 int64_t wgrad_workspace_floats(int K, int Cin, int Cout) {
