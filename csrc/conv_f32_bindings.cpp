@@ -3,6 +3,8 @@
 // allocator and launches on the current stream (graph-capturable); a shape
 // with no compiled instance raises instead of falling back.
 #include <torch/extension.h>
+
+#include <cstdlib>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -103,6 +105,51 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
   const int64_t K = w.size(0), Cin = w.size(2);
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, Cin}, dy.options());
+  static const bool phase = [] {
+    const char* e = std::getenv("SA_F32_DGRAD_PHASE");
+    return !(e && e[0] == '0');
+  }();
+  if (stride > 1 && !(pool_arg.has_value() && pool_arg->defined()) && phase) {
+    // Phase decomposition: dX rows i = S q + r - pt get the taps k = r + S j
+    // only, so each of the S x S output phases is a stride-1 correlation of
+    // the UNDILATED dY with a ceil(K/S)^2 sub-kernel (missing taps zero) -
+    // no MFMA work on the dilation zeros (1/S^2 of the dilated form's).
+    const int64_t S = stride, Kq = (K + S - 1) / S;
+    const int64_t Hy = dy.size(1), Wy = dy.size(2);
+    for (int64_t ry = 0; ry < S; ++ry) {
+      // q range with 0 <= S q + ry - pt < H
+      const int64_t qy0 = (pt - ry + S - 1) >= 0 ? (pt - ry + S - 1) / S : 0;
+      const int64_t qy1 = (H - 1 + pt - ry) / S;
+      if (qy1 < qy0) continue;
+      for (int64_t rx = 0; rx < S; ++rx) {
+        const int64_t qx0 = (pl - rx + S - 1) >= 0 ? (pl - rx + S - 1) / S : 0;
+        const int64_t qx1 = (W - 1 + pl - rx) / S;
+        if (qx1 < qx0) continue;
+        auto wsub = at::zeros({Kq, Kq, Cin, w.size(3)}, w.options());
+        const int64_t ny = (K - ry + S - 1) / S, nx = (K - rx + S - 1) / S;
+        wsub.narrow(0, 0, ny).narrow(1, 0, nx).copy_(
+            w.slice(0, ry, K, S).slice(1, rx, K, S));
+        sa::cf32::ConvArgs a{};
+        a.src = dy.data_ptr();
+        a.w = wsub.data_ptr<float>();
+        a.mask = opt_f32(mask, dx, "mask");
+        a.add = opt_f32(add, dx, "add");
+        a.out = dx.data_ptr<float>();
+        a.N = dy.size(0); a.Hs = Hy; a.Ws = Wy; a.Cs = dy.size(3);
+        a.Ho = qy1 - qy0 + 1; a.Wo = qx1 - qx0 + 1; a.Cout = Cin;
+        // out[q] = sum_j dy[q - j] wsub[j]: flipped taps, Kq - 1 rows above
+        a.pt = Kq - 1 - qy0; a.pl = Kq - 1 - qx0; a.D = 1;
+        a.wcin = Cin; a.wcout = w.size(3);
+        a.ostr = S; a.ooy = S * qy0 + ry - pt; a.oox = S * qx0 + rx - pl;
+        a.Hf = H; a.Wf = W;
+        TORCH_CHECK(sa::cf32::conv_launch(a, Kq, 1, sa::cf32::kSrcF32, true, stream()),
+                    "conv_f32 dgrad: no phase kernel for K=", Kq, " dy channels=",
+                    dy.size(3), " dx channels=", Cin);
+        check_launch("cf32_conv_dgrad(phase)");
+      }
+    }
+    return dx;
+  }
   // dy is the conv output's gradient, or (pool_arg) the gradient of its
   // 3x3/2 max-pool, gathered on load
   const int64_t Hc = (H + stride - 1) / stride, Wc = (W + stride - 1) / stride;

@@ -51,6 +51,10 @@ struct ConvArgs {
   int wcin, wcout;
   int relu_in, relu_out;
   PoolGeom pool;       // src_kind == kSrcPoolGrad: src is dP, (Hs, Ws) pre-pool
+  // strided output placement (0 = identity): launch output (oy, ox) lands at
+  // out[n, oy*ostr + ooy, ox*ostr + oox] of an [N, Hf, Wf, Cout] array (and
+  // mask / add are read there): one phase of a phase-decomposed dgrad
+  int ostr, ooy, oox, Hf, Wf;
 };
 
 // Weight gradient of the FORWARD conv (stride S, pads pt/pl):

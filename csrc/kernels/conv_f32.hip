@@ -60,8 +60,14 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 __host__ __device__ constexpr int fwd_pitch(int c) { return c >= 16 ? c + 8 : c; }
 // pixel pitch of the wgrad input image: the A operand is read with
 // ds_read_b32 (lane halves of 2 pixels x 16 consecutive channels), so the
-// pitch is 16 mod 32 dwords
-__host__ __device__ constexpr int wg_pitch(int c) { return c >= 16 ? c + 16 : c; }
+// pitch is the smallest >= c that is 16 mod 32 dwords (16 -> 16, 32 -> 48;
+// c + 16 made the 16-channel image 2-way bank conflicted: 2.8 conflict
+// cycles per LDS instruction in rocprof)
+__host__ __device__ constexpr int wg_pitch(int c) {
+  return c >= 16 ? c + (48 - c % 32) % 32 : c;
+}
+static_assert(wg_pitch(16) == 16 && wg_pitch(32) == 48 && wg_pitch(64) == 80 &&
+                  wg_pitch(128) == 144, "wg_pitch");
 
 template <int VPL>
 __device__ __forceinline__ void lds_get(const float* p, float (&v)[VPL]) {
@@ -396,12 +402,15 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
         mma(std::integral_constant<int, 1>{}, i);
     }
     // epilogue (after all MFMAs of the tile)
+    const int os = a.ostr > 0 ? a.ostr : 1;
+    const int Hf = a.Hf > 0 ? a.Hf : a.Ho, Wf = a.Wf > 0 ? a.Wf : a.Wo;
 #pragma unroll
     for (int i = 0; i < kGmax; ++i) {
       const int p = (wave + 4 * i) * 16 + c16;
       if (p >= P) continue;
       const int oy = p / a.Wo, ox = p - (p / a.Wo) * a.Wo;
-      const int64_t pix = (static_cast<int64_t>(n) * a.Ho + oy0 + oy) * a.Wo + ox;
+      const int64_t pix = (static_cast<int64_t>(n) * Hf + (oy0 + oy) * os + a.ooy) * Wf +
+                          ox * os + a.oox;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int64_t o = pix * a.Cout + co0 + 16 * h + 4 * g;
@@ -1075,6 +1084,10 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   SA_CONV_CASE(32, 32, 3, 1, kSrcF32, true)
   SA_CONV_CASE(64, 16, 4, 1, kSrcF32, true)
   SA_CONV_CASE(128, 16, 3, 1, kSrcF32, true)
+  // phase-decomposed dgrad of the shallow torso's stride-2 convs: one 2x2
+  // sub-kernel per output phase over the undilated dY
+  SA_CONV_CASE(64, 32, 2, 1, kSrcF32, true)
+  SA_CONV_CASE(128, 16, 2, 1, kSrcF32, true)
   // data gradient of a stage-head conv straight from the pooled gradient
   SA_CONV_CASE(32, 16, 3, 1, kSrcPoolGrad, true)
   SA_CONV_CASE(32, 32, 3, 1, kSrcPoolGrad, true)
