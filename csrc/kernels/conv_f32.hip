@@ -273,7 +273,7 @@ struct DyStager {
     }
   }
 };
-constexpr int kMaxD = 4;  // staged dY chunks per thread per tile
+constexpr int kMaxD = 8;  // staged dY chunks per thread per tile (taller tiles: more MFMA work per prefetch)
 
 template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R,
@@ -674,14 +674,22 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
     if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
     const int nq = (P + 3) >> 2;
     // software-pipelined: quad qd+PG's operand reads are issued ahead of
-    // quad qd's MFMAs
+    // quad qd's MFMAs.  The lane's pixel p = 4 qd + g advances by 4 PG per
+    // quad: its (oy, ox) is stepped incrementally (no integer division in
+    // the loop), and the row blocks that lie inside the image for every
+    // wave need no bias-row select (compile-time).
     float av[MTW], bv[NTT];
+    const int step = 4 * PG;
+    int cy = 0, cx = 4 * pg + g;  // (oy, ox) of the next quad to load
+    while (cx >= a.Wo) {
+      cx -= a.Wo;
+      ++cy;
+    }
     auto load_quad = [&](int qd) {
       const int p = 4 * qd + g;
       const bool valid = p < P;
       const int pp = valid ? p : 0;
-      const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
-      const int xb = (oy * S * Wl + ox * S) * XP;
+      const int xb = valid ? (cy * S * Wl + cx * S) * XP : 0;
 #pragma unroll
       for (int nb = 0; nb < NTT; ++nb) {
         const float d = d_s[pp * DP + 16 * nb + c16];
@@ -690,7 +698,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
         const float x = x_s[xb + moff[i]];
-        av[i] = kimg[i] ? x : kconst[i];
+        // block i of every wave (mb <= WSM - 1 + WSM i) inside the image:
+        // no select (folded at compile time after unrolling)
+        av[i] = (16 * (WSM - 1 + WSM * i) + 15 < M) ? x : (kimg[i] ? x : kconst[i]);
+      }
+      cx += step;
+      while (cx >= a.Wo) {
+        cx -= a.Wo;
+        ++cy;
       }
     };
     if (pg < nq) load_quad(pg);
