@@ -1013,6 +1013,8 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
 
 // output-channel tile: 32 when the weight slice stays small, else 16
 int cout_tile(int cinp, int cout, int K) {
+  static const int force = env_knob("SA_F32_COUT_T", 0);  // sweeps: 16 forces 16
+  if (force == 16) return 16;
   if (cout % 32 == 0 && 4ll * K * K * 32 * cinp <= 48 * 1024) return 32;
   return 16;
 }
@@ -1088,6 +1090,7 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   SA_CONV_CASE(16, 16, 3, 1, kSrcF32, false)
   SA_CONV_CASE(16, 32, 3, 1, kSrcF32, false)
   SA_CONV_CASE(32, 32, 3, 1, kSrcF32, false)
+  SA_CONV_CASE(32, 16, 3, 1, kSrcF32, false)  // SA_F32_COUT_T=16 sweeps
   SA_CONV_CASE(4, 32, 8, 4, kSrcU8, false)
   SA_CONV_CASE(32, 32, 4, 2, kSrcF32, false)
   SA_CONV_CASE(32, 16, 4, 2, kSrcF32, false)
