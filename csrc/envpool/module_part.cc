@@ -4,6 +4,13 @@
 
 #include <vector>
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
+#include <atomic>
+#include <climits>
+
 #include "envpool/env_channel.h"
 #include "envpool/shm_ring.h"
 #include "envpool/traj_queue.h"
@@ -12,7 +19,41 @@ namespace py = pybind11;
 
 namespace sa {
 
+namespace {
+// Futex wait/wake on a 32-bit word of a process-shared mapping (inference
+// board slots): wait returns when *addr != expected or after timeout_ms.
+int FutexWaitAddr(uintptr_t addr, uint32_t expected, int64_t timeout_ms) {
+  auto* w = reinterpret_cast<std::atomic<uint32_t>*>(addr);
+  if (w->load(std::memory_order_acquire) != expected) return 1;
+  struct timespec ts;
+  ts.tv_sec = timeout_ms / 1000;
+  ts.tv_nsec = (timeout_ms % 1000) * 1000000L;
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), FUTEX_WAIT, expected,
+          timeout_ms < 0 ? nullptr : &ts, nullptr, 0);
+  return w->load(std::memory_order_acquire) != expected ? 1 : 0;
+}
+}  // namespace
+
 void register_envpool(py::module& m) {
+  m.def("futex_wait", [](uintptr_t addr, uint32_t expected, int64_t timeout_ms) {
+          py::gil_scoped_release nogil;
+          return FutexWaitAddr(addr, expected, timeout_ms);
+        }, py::arg("addr"), py::arg("expected"), py::arg("timeout_ms"));
+  m.def("futex_wake", [](uintptr_t addr) {
+          return static_cast<int>(syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr),
+                                          FUTEX_WAKE, INT_MAX, nullptr, nullptr, 0));
+        }, py::arg("addr"));
+  m.def("atomic_store_u32", [](uintptr_t addr, uint32_t v) {
+          reinterpret_cast<std::atomic<uint32_t>*>(addr)->store(v, std::memory_order_release);
+        });
+  m.def("atomic_load_u32", [](uintptr_t addr) {
+          return reinterpret_cast<std::atomic<uint32_t>*>(addr)->load(std::memory_order_acquire);
+        });
+  m.def("atomic_add_u32", [](uintptr_t addr, uint32_t v) {
+          return reinterpret_cast<std::atomic<uint32_t>*>(addr)->fetch_add(
+              v, std::memory_order_acq_rel);
+        });
+
   py::class_<EnvChannel>(m, "EnvChannel")
       .def(py::init<>())
       .def("request", &EnvChannel::Request, py::arg("method"), py::arg("kind"),

@@ -313,6 +313,19 @@ class _TrajFeeder(object):
 
 
 # --------------------------------------------------------------- train
+def _checker(groups, server):
+  """Health probe the trajectory feeder runs while it waits for a slab."""
+  if groups is None and server is None:
+    return None
+
+  def check():
+    if server is not None:
+      server.check()
+    if groups is not None:
+      groups.check()
+  return check
+
+
 class _Terminated(BaseException):
   """Raised in the main thread by SIGTERM: stop cleanly and checkpoint."""
 
@@ -371,7 +384,7 @@ def train(flags):
   use_groups = (n_groups > 0 and not distributed_actors and
                 flags.trajectory_queue and not flags.deterministic)
   envs, actors_levels, actor_seeds = [], [], []
-  groups = shared_w = None
+  groups = shared_w = board = server = None
   if not distributed_actors:
     for i in range(flags.num_actors):
       actors_levels.append(level_names[i % len(level_names)])
@@ -392,11 +405,18 @@ def train(flags):
     else:  # device_count() does not initialise the GPU in this process
       ndev = torch.cuda.device_count()
       group_dev = 'cuda:%d' % (local_rank % ndev) if ndev else 'cpu'
+    if flags.inference_server:
+      from .runtime.actor_group import board_geometry
+      from .runtime.inference_board import InferenceBoard
+      slots, rows = board_geometry(flags.num_actors, n_groups,
+                                   flags.actor_group_splits)
+      board = InferenceBoard(slots, rows, frame_shape, num_actions)
+      group_dev = 'cpu (board served by the learner process)'
     groups = ActorGroups(
         flags, level_names, actors_levels, actor_seeds, tq, shared_w_name,
         frame_shape, action_set, use_instr, group_dev,
         flags.dtype if flags.inference_dtype == 'auto' else
-        flags.inference_dtype)
+        flags.inference_dtype, board=board)
     log.info('%d actor group(s) over %d envs, inference on %s',
              len(groups.procs), flags.num_actors, group_dev)
   elif not distributed_actors:
@@ -459,9 +479,26 @@ def train(flags):
     feeder = _TrajFeeder(tq, learner, device,
                          flags.use_hip_graph and device.type == 'cuda')
     feeder.prepare()
-    shared_w = SharedWeights(shared_w_name, learner.flat.numel, create=True)
-    shared_w.publish(learner.flat.params)  # groups start on these weights
-    shared_w.flush()
+    if board is not None:
+      # the groups' inference: one captured graph over the whole board, on
+      # its own stream of the learner's GPU context
+      from .runtime.inference_board import BoardServer
+      inf_device = (device if flags.inference_device == 'auto' else
+                    torch.device(flags.inference_device))
+      inf_agent = _make_agent(
+          flags, num_actions, frame_shape, inf_device, flags.seed,
+          dtype=(flags.dtype if flags.inference_dtype == 'auto' else
+                 flags.inference_dtype))
+      model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
+                                           seed=flags.seed + 17 * rank)
+      model.publish(learner.flat.params)
+      server = BoardServer(model, board)
+      server.prepare(has_instr=use_instr)
+      server.start()
+    else:
+      shared_w = SharedWeights(shared_w_name, learner.flat.numel, create=True)
+      shared_w.publish(learner.flat.params)  # groups start on these weights
+      shared_w.flush()
   else:
     inf_device = (device if flags.inference_device == 'auto' else
                   torch.device(flags.inference_device))
@@ -557,7 +594,7 @@ def train(flags):
           loss, info, wait = feeder.step(
               flags.queue_timeout_secs,
               poison=faults.get('learner_nan') == steps + 1,
-              check=groups.check if groups is not None else None)
+              check=_checker(groups, server))
         timer.add_wait(wait)
         steps += 1
         if (world > 1 and flags.consistency_check_steps and
@@ -565,7 +602,7 @@ def train(flags):
             not parallel.param_checksum_consistent(learner.flat.params)):
           raise RuntimeError('data-parallel replicas diverged at step %d' %
                              steps)
-        if infer is not None:
+        if infer is not None or server is not None:
           model.publish(learner.flat.params)
         elif shared_w is not None:
           shared_w.publish(learner.flat.params)
@@ -660,6 +697,9 @@ def train(flags):
                    'env_restarts': (sum(a.env_restarts for a in actors) +
                                     (groups.env_restarts if groups else 0))}
         scalars.update(learner.health())
+        if server is not None and server.batches:
+          scalars['inference_batch_size_mean'] = (server.rows_served /
+                                                  server.batches)
         if infer is not None and infer.stats()['batches']:
           st = infer.stats()
           scalars['inference_batch_size_mean'] = (st['requests'] /
@@ -701,7 +741,11 @@ def train(flags):
     if infer is not None:
       infer.close()
     if groups is not None:
+      if board is not None:
+        board.close()
       groups.close()
+      if server is not None:
+        server.stop()
       if shared_w is not None:
         shared_w.close()
     for t in threads:

@@ -113,6 +113,10 @@ def build_parser() -> argparse.ArgumentParser:
                       'process; -1 = auto: 1 group on a GPU (more GPU '
                       'processes share the card badly: profiles/'
                       'r2_e2e_actors.md), threads on CPU.')
+  p.add_argument('--inference_server', type=_str2bool, default=False,
+                 help='Actor groups stay CPU-only and post their rows to a '
+                      'shared-memory inference board served by a thread of '
+                      'the learner process (one GPU context in total).')
   p.add_argument('--actor_group_splits', type=int, default=2,
                  help='Pipeline stages per actor group: split k\'s inference '
                       'runs on the GPU while the envs of another split step.')

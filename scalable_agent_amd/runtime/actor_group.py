@@ -205,6 +205,15 @@ class _Done(object):
     pass
 
 
+def board_geometry(num_actors, groups, splits):
+  """(slots, rows per slot) of the inference board for this actor layout."""
+  parts = split_actors(num_actors, groups)
+  splits = max(1, int(splits))
+  rows = max(max(len(p) for p in split_actors(len(g), min(splits, len(g))))
+             for g in parts)
+  return len(parts) * splits, rows
+
+
 def split_actors(num_actors, groups):
   """Actor indices per group: contiguous, sizes differ by at most one."""
   groups = max(1, min(int(groups), int(num_actors)))
@@ -228,6 +237,7 @@ class ActorGroupWorker(object):
     self.counters = counters
     self.device_str = device_str
     self.restarts = 0
+    self.board_mode = False
 
   def run(self):
     import torch
@@ -241,6 +251,23 @@ class ActorGroupWorker(object):
     envs = [create_environment(flags, lvl, seed)
             for lvl, seed in zip(sp['levels'], sp['seeds'])]
     py_process.start_all(envs)  # forked before this process touches the GPU
+    board = sp.get('board')
+    if board is not None:
+      # CPU-only group: inference is served from the learner process
+      from .inference_board import BoardClient
+      parent = os.getppid()
+      alive = lambda: os.getppid() == parent
+      K = max(1, min(int(sp['splits']), len(envs)))
+      vis = [BoardClient(board, sp['slot0'] + k, len(part), alive)
+             for k, part in enumerate(split_actors(len(envs), K))]
+      self.board_mode = True
+      try:
+        self._loop(envs, None, vis, encode_instruction, py_process)
+      except EOFError:
+        pass  # the learner closed the board: shutting down
+      finally:
+        py_process.close_all(envs)
+      return
     try:
       device = torch.device(self.device_str)
       if device.type == 'cuda':
@@ -268,6 +295,9 @@ class ActorGroupWorker(object):
     buffer into a staging buffer; once it has landed and that buffer's
     seqlock count is unchanged, a D2D copy (ordered before the next
     inference) makes it the inference snapshot."""
+    if self.board_mode:
+      state['version'] = max(1, state['version'])  # weights live in the server
+      return
     import torch
     w = self.weights
     v = w.version()
@@ -508,7 +538,7 @@ class ActorGroups(object):
 
   def __init__(self, flags, level_names, actor_levels, actor_seeds, tq,
                weights, frame_shape, action_set, use_instr, device_str,
-               dtype):
+               dtype, board=None):
     import multiprocessing
     ctx = multiprocessing.get_context('fork')
     self.tq = tq
@@ -523,7 +553,8 @@ class ActorGroups(object):
                   num_actions=len(action_set), action_set=action_set,
                   frame_shape=tuple(frame_shape), use_instr=use_instr,
                   unroll_length=flags.unroll_length, dtype=dtype,
-                  splits=flags.actor_group_splits)
+                  splits=flags.actor_group_splits, board=board,
+                  slot0=gid * max(1, flags.actor_group_splits))
       p = ctx.Process(target=_group_main,
                       args=(gid, spec, tq, weights, self.counters, device_str),
                       daemon=False, name='actor-group-%d' % gid)

@@ -1,0 +1,293 @@
+"""Batched actor inference served from the learner process over shared memory.
+
+Actor-group processes (runtime/actor_group.py) can either run their own
+inference on the GPU (a second GPU context per group) or, with
+`--inference_server`, stay CPU-only and post their rows to this board:
+
+  board (anonymous MAP_SHARED, created before the groups are forked):
+    header  : seq word (bumped on every request, the server's futex), closed
+              flag, per-slot state words (0 idle, 1 request, 2 response) and
+              per-slot row counts
+    inputs  : every input field for ALL rows (slot s owns rows [s*M, s*M+M)),
+              field-major - ONE H2D copy moves the whole board to the device
+    outputs : slot-major [action | logits | baseline | c | h] per slot, so a
+              slot's response is ONE D2H copy and responding to one slot
+              never overwrites the rows another worker is still reading
+  server (a thread in the learner process, one GPU context in total):
+    wait for request slots -> mask of their rows -> H2D inputs + mask ->
+    ONE captured graph over all rows (torso, core, heads + Gumbel sampler; the
+    LSTM state of every row resident on the device, updated only where the
+    mask is set) -> D2H of each ready slot's outputs -> state 2 + futex wake
+
+Replaces the reference's per-request dynamic batching (experiment.py:534-546
++ batcher.cc) for process actors: the "batch" is every slot that is ready
+when the server looks, the batch shape is fixed (no padding buckets).
+"""
+
+import logging
+import mmap
+import threading
+import time
+
+import numpy as np
+
+from . import native
+
+log = logging.getLogger('scalable_agent_amd')
+
+_ALIGN = 256
+IDLE, REQUEST, RESPONSE = 0, 1, 2
+
+
+def _align(x):
+  return (x + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class InferenceBoard(object):
+  """The shared request/response board (see the module docstring)."""
+
+  HDR = 4096
+
+  def __init__(self, num_slots, rows, frame_shape, num_actions, instr_len=16,
+               core_size=256):
+    self.S, self.M = int(num_slots), int(rows)
+    assert 0 < self.S <= 250
+    R = self.R = self.S * self.M
+    self.num_actions, self.core = int(num_actions), int(core_size)
+    fields = [('last_action', (), np.int64), ('reward', (), np.float32),
+              ('done', (), np.bool_), ('frame', tuple(frame_shape), np.uint8),
+              ('instr_ids', (int(instr_len),), np.int64),
+              ('instr_len', (), np.int64)]
+    self.in_fields, off = [], 0
+    for name, shape, dt in fields:
+      nb = R * int(np.prod(shape, dtype=np.int64)) * np.dtype(dt).itemsize
+      self.in_fields.append((name, (R,) + tuple(shape), np.dtype(dt), off, nb))
+      off = _align(off + nb)
+    self.in_bytes = off
+    outs = [('action', (), np.int64), ('logits', (num_actions,), np.float32),
+            ('baseline', (), np.float32), ('c', (core_size,), np.float32),
+            ('h', (core_size,), np.float32)]
+    self.out_fields, off = [], 0
+    for name, shape, dt in outs:
+      nb = self.M * int(np.prod(shape, dtype=np.int64)) * np.dtype(dt).itemsize
+      self.out_fields.append((name, (self.M,) + tuple(shape), np.dtype(dt), off,
+                              nb))
+      off = _align(off + nb)
+    self.slot_out_bytes = off
+    self.out_bytes = off * self.S
+    self.nbytes = self.HDR + self.in_bytes + self.out_bytes
+    self._mm = mmap.mmap(-1, self.nbytes)
+    self.buf = np.frombuffer(self._mm, dtype=np.uint8)
+    self.base = self.buf.ctypes.data
+    self.words = self.buf[:self.HDR].view(np.uint32)
+    # words[0] seq, [1] closed, [16 + s] state, [16 + S + s] rows of slot s
+    self.seq_addr = self.base
+    self.inputs = {n: self.buf[self.HDR + o:self.HDR + o + nb].view(dt).reshape(s)
+                   for n, s, dt, o, nb in self.in_fields}
+
+  # -------------------------------------------------------------- words
+  def state_addr(self, slot):
+    return self.base + 4 * (16 + slot)
+
+  def state(self, slot):
+    return int(self.words[16 + slot])
+
+  def set_rows(self, slot, n):
+    self.words[16 + self.S + slot] = int(n)
+
+  def rows_of(self, slot):
+    return int(self.words[16 + self.S + slot])
+
+  @property
+  def closed(self):
+    return bool(self.words[1])
+
+  def close(self):
+    self.words[1] = 1
+    native.futex_wake(self.seq_addr)
+    for s in range(self.S):
+      native.futex_wake(self.state_addr(s))
+
+  def slot_outputs(self, slot):
+    """numpy views of slot's outputs (action, logits, baseline, c, h)."""
+    o0 = self.HDR + self.in_bytes + slot * self.slot_out_bytes
+    return tuple(self.buf[o0 + o:o0 + o + nb].view(dt).reshape(s)
+                 for n, s, dt, o, nb in self.out_fields)
+
+
+class BoardClient(object):
+  """Worker side of one board slot, with VectorInfer's interface (inputs /
+  launch / wait / rows / c / h) so the actor-group pipeline drives either."""
+
+  def __init__(self, board, slot, rows, alive=None):
+    assert rows <= board.M
+    self.board, self.slot, self.rows = board, int(slot), int(rows)
+    lo, hi = slot * board.M, slot * board.M + rows
+    self.inputs = {n: v[lo:hi] for n, v in board.inputs.items()}
+    self._outs = tuple(o[:rows] for o in board.slot_outputs(slot))
+    self.c, self.h = self._outs[3], self._outs[4]
+    self._alive = alive or (lambda: True)
+    board.set_rows(slot, rows)
+
+  def launch(self):
+    b = self.board
+    native.atomic_store_u32(b.state_addr(self.slot), REQUEST)
+    native.atomic_add_u32(b.seq_addr, 1)
+    native.futex_wake(b.seq_addr)
+
+  def wait(self):
+    b = self.board
+    addr = b.state_addr(self.slot)
+    while native.atomic_load_u32(addr) != RESPONSE:
+      if b.closed or not self._alive():
+        raise EOFError('inference board closed')
+      native.futex_wait(addr, REQUEST, 50)
+    return self._outs
+
+
+class BoardServer(object):
+  """Learner-process side: one captured inference graph over the board."""
+
+  def __init__(self, model, board, use_graph=True):
+    import torch
+    self.torch = torch
+    self.model, self.board = model, board
+    dev = model.device
+    self.cuda = dev.type == 'cuda'
+    self.use_graph = bool(use_graph) and self.cuda
+    b = board
+    # the board's input + output regions as host tensors (pinned on a GPU)
+    self._host_in = torch.from_numpy(b.buf[b.HDR:b.HDR + b.in_bytes])
+    self._host_out = torch.from_numpy(b.buf[b.HDR + b.in_bytes:])
+    self.pinned = False
+    if self.cuda:
+      from .traj_queue import _hip_host_register
+      torch.cuda.init()
+      self.pinned = _hip_host_register(b.base + b.HDR, b.in_bytes + b.out_bytes)
+    self.in_dev = torch.empty(b.in_bytes, dtype=torch.uint8, device=dev)
+    self.out_dev = torch.empty(b.out_bytes, dtype=torch.uint8, device=dev)
+    tdt = lambda dt: torch.from_numpy(np.empty(0, dt)).dtype
+    self._dev_in = [self.in_dev[o:o + nb].view(tdt(dt)).view(*s)
+                    for n, s, dt, o, nb in b.in_fields]
+    self.c = torch.zeros(b.R, b.core, device=dev)
+    self.h = torch.zeros(b.R, b.core, device=dev)
+    self.mask_host = torch.zeros(b.R, dtype=torch.float32)
+    if self.cuda:
+      self.mask_host = self.mask_host.pin_memory()
+    self.mask_dev = torch.zeros(b.R, 1, device=dev)
+    self._graphs = {}
+    self._thread = None
+    self._stop = False
+    self.error = None
+    self.batches = 0
+    self.rows_served = 0
+
+  def _body(self, has_instr):
+    torch = self.torch
+    b = self.board
+    la, rw, dn, fr, ids, ln = self._dev_in
+    action, logits, baseline, c2, h2 = self.model.step_device(
+        la, rw, dn, fr, ids, ln, self.c, self.h, has_instr=has_instr)
+    m = self.mask_dev
+    self.c.copy_(torch.where(m > 0, c2, self.c))
+    self.h.copy_(torch.where(m > 0, h2, self.h))
+    out = self.out_dev.view(b.S, b.slot_out_bytes)
+    for (n, s, dt, o, nb), v in zip(b.out_fields,
+                                    (action, logits, baseline, c2, h2)):
+      per = nb // b.M  # bytes per row
+      src = v.reshape(b.S, b.M, -1).contiguous().view(torch.uint8).view(
+          b.S, b.M * per)
+      out[:, o:o + b.M * per].copy_(src)
+
+  def _capture(self, has_instr):
+    torch = self.torch
+    s = self.model.stream
+    with torch.cuda.stream(s):
+      c0, h0 = self.c.clone(), self.h.clone()
+      for _ in range(2):
+        self._body(has_instr)
+      self.c.copy_(c0)
+      self.h.copy_(h0)
+      s.synchronize()
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+        self._body(has_instr)
+    return g
+
+  def prepare(self, has_instr=False):
+    """Captures the graph before any traffic (main thread)."""
+    if self.use_graph:
+      with self.torch.no_grad():
+        self._graphs[has_instr] = self._capture(has_instr)
+
+  def serve_once(self, timeout_ms=50):
+    """One batch over every slot in REQUEST state; False when none came."""
+    torch = self.torch
+    b, m = self.board, self.model
+    seq = native.atomic_load_u32(b.seq_addr)
+    ready = [s for s in range(b.S) if b.state(s) == REQUEST]
+    if not ready:
+      native.futex_wait(b.seq_addr, seq, timeout_ms)
+      return False
+    mask = self.mask_host
+    mask.zero_()
+    rows = 0
+    for s in ready:
+      n = b.rows_of(s)
+      mask[s * b.M:s * b.M + n] = 1.0
+      rows += n
+    has_instr = bool(m.use_instruction and
+                     int(b.inputs['instr_len'].max(initial=0)) > 0)
+    with torch.no_grad(), m._lock:
+      if not self.cuda:
+        self.in_dev.copy_(self._host_in)
+        self.mask_dev.copy_(mask.view(-1, 1))
+        self._body(has_instr)
+        self._host_out.copy_(self.out_dev)
+      else:
+        with torch.cuda.stream(m.stream):
+          self.in_dev.copy_(self._host_in, non_blocking=self.pinned)
+          self.mask_dev.copy_(mask.view(-1, 1), non_blocking=True)
+          if self.use_graph:
+            g = self._graphs.get(has_instr)
+            if g is None:
+              g = self._graphs[has_instr] = self._capture(has_instr)
+            g.replay()
+          else:
+            self._body(has_instr)
+          so = b.slot_out_bytes
+          for s in ready:
+            self._host_out[s * so:(s + 1) * so].copy_(
+                self.out_dev[s * so:(s + 1) * so], non_blocking=self.pinned)
+          m.stream.synchronize()
+    for s in ready:
+      native.atomic_store_u32(b.state_addr(s), RESPONSE)
+      native.futex_wake(b.state_addr(s))
+    self.batches += 1
+    self.rows_served += rows
+    return True
+
+  # ------------------------------------------------------------ thread
+  def _run(self):
+    try:
+      while not self._stop and not self.board.closed:
+        self.serve_once()
+    except Exception as e:  # pylint: disable=broad-except
+      self.error = e
+      log.exception('inference server failed')
+      self.board.close()
+
+  def start(self):
+    self._thread = threading.Thread(target=self._run, daemon=True,
+                                    name='inference-board-server')
+    self._thread.start()
+
+  def check(self):
+    if self.error is not None:
+      raise RuntimeError('inference server failed: %r' % (self.error,))
+
+  def stop(self):
+    self._stop = True
+    native.futex_wake(self.board.seq_addr)
+    if self._thread is not None:
+      self._thread.join(timeout=10)

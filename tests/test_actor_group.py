@@ -146,3 +146,64 @@ def test_vector_infer_graph_on_gpu(cuda, dtype):
     np.testing.assert_allclose(baseline, rb, rtol=tol, atol=tol)
     np.testing.assert_allclose(h2, rh, rtol=tol, atol=tol)
     c, h = rc, rh
+
+
+def _board_worker(board, slot, rows, n_steps, seed):
+  import os as _os
+  from scalable_agent_amd.runtime.inference_board import BoardClient
+  cl = BoardClient(board, slot, rows)
+  rng = np.random.RandomState(seed)
+  for _ in range(n_steps):
+    cl.inputs['frame'][:] = rng.randint(0, 256, cl.inputs['frame'].shape)
+    cl.inputs['done'][:] = False
+    cl.launch()
+    a, lg, b, c, h = cl.wait()
+    assert a.shape == (rows,) and np.all((a >= 0) & (a < 9))
+    assert np.all(np.isfinite(lg)) and np.all(np.isfinite(c))
+  _os._exit(0)
+
+
+def test_inference_board_serves_forked_workers():
+  """Two forked workers (different row counts) post to the shared board; a
+  CPU server answers each with its own rows; the LSTM state of rows that
+  were not in a batch does not move."""
+  import multiprocessing as mp
+  from scalable_agent_amd.inference import InferenceModel
+  from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.runtime.inference_board import (BoardServer,
+                                                          InferenceBoard)
+  shape = (24, 32, 3)
+  board = InferenceBoard(3, 4, shape, 9)
+  model = InferenceModel(Agent(9, torso='shallow', frame_shape=shape, seed=2),
+                         'cpu', use_instruction=False, seed=1)
+  server = BoardServer(model, board, use_graph=False)
+  ctx = mp.get_context('fork')
+  procs = [ctx.Process(target=_board_worker, args=(board, s, r, 5, s))
+           for s, r in ((0, 4), (2, 3))]
+  for p in procs:
+    p.start()
+  served = 0
+  deadline = __import__('time').time() + 60
+  while any(p.is_alive() for p in procs) and __import__('time').time() < deadline:
+    served += server.serve_once(timeout_ms=20)
+  for p in procs:
+    p.join(10)
+    assert p.exitcode == 0
+  assert served >= 5 and server.rows_served == 5 * (4 + 3)
+  # slot 1 never asked: its rows' state is untouched; slot 2's 4th row is
+  # padding (3 rows): untouched too
+  assert float(server.c[4:8].abs().sum()) == 0.0
+  assert float(server.c[8 + 3:].abs().sum()) == 0.0
+  assert float(server.c[0:4].abs().sum()) > 0.0
+  board.close()
+
+
+def test_train_with_inference_server(tmp_path):
+  logdir = str(tmp_path / 'board')
+  r = _run(['--logdir=' + logdir, '--num_actors=6', '--batch_size=2',
+            '--actor_groups=2', '--inference_server=true',
+            '--total_environment_frames=480', '--save_summaries_secs=0'])
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'board served by the learner process' in r.stderr
+  assert 'Episode return' in r.stderr
+  assert os.path.exists(os.path.join(logdir, 'checkpoint'))

@@ -87,8 +87,9 @@ def test_pipelined_unroll_matches_serial(cuda):
   assert not torch.equal(before, lrn4.flat.params)
 
 
-@pytest.mark.parametrize('groups', [0, -1])
-def test_experiment_train_and_test_on_gpu(tmp_path, groups):
+@pytest.mark.parametrize('groups,server', [(0, False), (-1, False),
+                                           (2, True)])
+def test_experiment_train_and_test_on_gpu(tmp_path, groups, server):
   """The full driver on the GPU: actor threads with batched GPU inference
   (groups=0) or the default actor-group process (groups=-1: one group,
   pipelined splits, captured fixed-batch inference), the HIP-graph learner,
@@ -106,6 +107,7 @@ def test_experiment_train_and_test_on_gpu(tmp_path, groups):
   env = dict(os.environ, PYTHONPATH=root)
   r = subprocess.run(common + ['--num_actors=4', '--batch_size=4',
                                '--actor_groups=%d' % groups,
+                               '--inference_server=%s' % server,
                                '--total_environment_frames=1280',
                                '--save_summaries_secs=0'],
                      capture_output=True, text=True, timeout=100, env=env)
