@@ -583,6 +583,7 @@ def train(flags):
   use_graph = flags.use_hip_graph and device.type == 'cuda'
   staging = dev_stage = copied = None
   host_ms, loop_ms = [], []
+  failed = False
   try:
     frames = int(learner.frames.item())
     while frames < flags.total_environment_frames:
@@ -733,11 +734,15 @@ def train(flags):
   except _Terminated:
     log.warning('SIGTERM: stopping and checkpointing at %d frames',
                 int(learner.frames.item()))
+  except BaseException:
+    failed = True
+    raise
   finally:
     stop.set()
     if use_traj:
       tq.close()
-      feeder.close()
+      if not failed:  # after a GPU fault, waiting on its events could hang
+        feeder.close()
     if infer is not None:
       infer.close()
     if groups is not None:

@@ -288,8 +288,10 @@ class Agent(nn.Module):
     torso_out = self.torso_fc(feats)
     dt = torso_out.dtype
     clipped_reward = torch.clamp(rewards.reshape(n, 1).to(dt), -1, 1)
-    one_hot = F.one_hot(last_actions.reshape(n).long(),
-                        self.num_actions).to(dt)
+    # tf.one_hot semantics: an out-of-range index gives a zero row (a
+    # comparison, never a scatter - no out-of-bounds write under graphs)
+    one_hot = (last_actions.reshape(n, 1).long() == torch.arange(
+        self.num_actions, device=last_actions.device)).to(dt)
     instr_out = self.instruction_encoding(instr, n, frames.device)
     return torch.cat([torso_out, clipped_reward, one_hot, instr_out], dim=1)
 

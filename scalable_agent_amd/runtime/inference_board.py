@@ -164,8 +164,10 @@ class BoardServer(object):
       from .traj_queue import _hip_host_register
       torch.cuda.init()
       self.pinned = _hip_host_register(b.base + b.HDR, b.in_bytes + b.out_bytes)
-    self.in_dev = torch.empty(b.in_bytes, dtype=torch.uint8, device=dev)
-    self.out_dev = torch.empty(b.out_bytes, dtype=torch.uint8, device=dev)
+    # zero-filled: the capture's warm-up steps read the board before any
+    # worker wrote it
+    self.in_dev = torch.zeros(b.in_bytes, dtype=torch.uint8, device=dev)
+    self.out_dev = torch.zeros(b.out_bytes, dtype=torch.uint8, device=dev)
     tdt = lambda dt: torch.from_numpy(np.empty(0, dt)).dtype
     self._dev_in = [self.in_dev[o:o + nb].view(tdt(dt)).view(*s)
                     for n, s, dt, o, nb in b.in_fields]
