@@ -5,6 +5,8 @@
 #include <torch/extension.h>
 
 #include <cstdlib>
+#include <climits>
+#include <algorithm>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -94,6 +96,14 @@ sa::cf32::PoolGeom pool_geom(const c10::optional<at::Tensor>& arg, const at::Ten
   return pg;
 }
 
+bool phase_stacked() {
+  static const bool on = [] {
+    const char* e = std::getenv("SA_F32_DGRAD_STACK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, int64_t pl,
                       int64_t H, int64_t W, c10::optional<at::Tensor> mask,
                       c10::optional<at::Tensor> add, c10::optional<at::Tensor> pool_arg,
@@ -116,6 +126,44 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
     // no MFMA work on the dilation zeros (1/S^2 of the dilated form's).
     const int64_t S = stride, Kq = (K + S - 1) / S;
     const int64_t Hy = dy.size(1), Wy = dy.size(2);
+    if (Cin % 16 == 0 && phase_stacked()) {
+      // ONE launch for all S*S phases: their sub-kernels stacked along the
+      // output channels (Cout = S*S*Cin), the epilogue routes each 16-channel
+      // block to its phase's pixels - dY staged once, S*S times the MFMA
+      // columns per tile (tiny 9x12 / 18x24 outputs fill the waves)
+      int64_t qy0 = INT64_MAX, qy1 = INT64_MIN, qx0 = INT64_MAX, qx1 = INT64_MIN;
+      for (int64_t r = 0; r < S; ++r) {
+        qy0 = std::min(qy0, (pt - r + S - 1) / S);
+        qy1 = std::max(qy1, (H - 1 + pt - r) / S);
+        qx0 = std::min(qx0, (pl - r + S - 1) / S);
+        qx1 = std::max(qx1, (W - 1 + pl - r) / S);
+      }
+      auto wst = at::zeros({Kq, Kq, S * S * Cin, w.size(3)}, w.options());
+      for (int64_t ry = 0; ry < S; ++ry)
+        for (int64_t rx = 0; rx < S; ++rx) {
+          const int64_t ny = (K - ry + S - 1) / S, nx = (K - rx + S - 1) / S;
+          const int64_t k = ry * S + rx;
+          wst.narrow(0, 0, ny).narrow(1, 0, nx).narrow(2, k * Cin, Cin).copy_(
+              w.slice(0, ry, K, S).slice(1, rx, K, S));
+        }
+      sa::cf32::ConvArgs a{};
+      a.src = dy.data_ptr();
+      a.w = wst.data_ptr<float>();
+      a.mask = opt_f32(mask, dx, "mask");
+      a.add = opt_f32(add, dx, "add");
+      a.out = dx.data_ptr<float>();
+      a.N = dy.size(0); a.Hs = Hy; a.Ws = Wy; a.Cs = dy.size(3);
+      a.Ho = qy1 - qy0 + 1; a.Wo = qx1 - qx0 + 1; a.Cout = S * S * Cin;
+      a.pt = Kq - 1 - qy0; a.pl = Kq - 1 - qx0; a.D = 1;
+      a.wcin = S * S * Cin; a.wcout = w.size(3);
+      a.ostr = S; a.ooy = qy0; a.oox = qx0; a.Hf = H; a.Wf = W;
+      a.phase_c = Cin; a.pt_ph = pt; a.pl_ph = pl;
+      TORCH_CHECK(sa::cf32::conv_launch(a, Kq, 1, sa::cf32::kSrcF32, true, stream()),
+                  "conv_f32 dgrad: no phase-stacked kernel for K=", Kq, " dy channels=",
+                  dy.size(3), " dx channels=", S * S * Cin);
+      check_launch("cf32_conv_dgrad(stacked)");
+      return dx;
+    }
     for (int64_t ry = 0; ry < S; ++ry) {
       // q range with 0 <= S q + ry - pt < H
       const int64_t qy0 = (pt - ry + S - 1) >= 0 ? (pt - ry + S - 1) / S : 0;

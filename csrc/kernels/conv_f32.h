@@ -55,6 +55,11 @@ struct ConvArgs {
   // out[n, oy*ostr + ooy, ox*ostr + oox] of an [N, Hf, Wf, Cout] array (and
   // mask / add are read there): one phase of a phase-decomposed dgrad
   int ostr, ooy, oox, Hf, Wf;
+  // phase-stacked dgrad (phase_c > 0): output channel co of the launch is
+  // channel co % phase_c of phase k = co / phase_c = (ry, rx) (S = ostr);
+  // launch output (oy, ox) lands at dX[ostr*(oy+ooy) + ry - pt_ph,
+  // ostr*(ox+oox) + rx - pl_ph] when inside [0,Hf) x [0,Wf), else dropped
+  int phase_c, pt_ph, pl_ph;
 };
 
 // Weight gradient of the FORWARD conv (stride S, pads pt/pl):

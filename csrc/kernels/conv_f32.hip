@@ -142,6 +142,10 @@ __device__ __forceinline__ void stage_image(const void* __restrict__ src, int n,
 // force the in-flight prefetch to drain early (vmcnt is in order).
 constexpr int kGmax = 4;   // 16-pixel groups per wave per tile
 constexpr int kMaxC = 8;   // staged 16-B chunks per thread per tile
+// forward staging depth per input width: 64+ channel layers (the shallow
+// torso's 9x12 stage) need 16 chunks for a whole 5-row output image per tile
+// instead of a 4-row tile plus a 1-row tail tile
+__host__ __device__ constexpr int fwd_maxc(int cinp) { return cinp >= 64 ? 16 : kMaxC; }
 
 // Pre-pool gradient at (n, y, x), channels 4ch..4ch+3, gathered from the
 // pooled gradient dP [N, Hp, Wp, C] through the argmax codes: windows in
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
-  Stager<CINP, SRC> st;
+  Stager<CINP, SRC, fwd_maxc(CINP)> st;
   auto prefetch = [&](int t) {
     const int n = t / tiles_per_img;
     const int oy0 = (t - n * tiles_per_img) * R;
@@ -413,7 +417,17 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
                           ox * os + a.oox;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        const int64_t o = pix * a.Cout + co0 + 16 * h + 4 * g;
+        int64_t o = pix * a.Cout + co0 + 16 * h + 4 * g;
+        if (a.phase_c > 0) {
+          // phase-stacked dgrad: this 16-channel block is one phase's slice
+          const int co = co0 + 16 * h;
+          const int k = co / a.phase_c, ry = k / os, rx = k - (k / os) * os;
+          const int yy = os * (oy0 + oy + a.ooy) + ry - a.pt_ph;
+          const int xx = os * (ox + a.oox) + rx - a.pl_ph;
+          if (yy < 0 || yy >= Hf || xx < 0 || xx >= Wf) continue;
+          o = ((static_cast<int64_t>(n) * Hf + yy) * Wf + xx) * a.phase_c + (co - k * a.phase_c) +
+              4 * g;
+        }
         f4 v = acc[i][h];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bias[h][r];
@@ -950,7 +964,7 @@ bool run_conv(const ConvArgs& a, hipStream_t s) {
   double best_cost = 1e30;
   for (int R = 1; R <= a.Ho; ++R) {
     const int rows = (R - 1) * S + K;
-    if (bytes(R) > budget || rows * Wl * (CINP / 4) > kMaxC * kThreads ||
+    if (bytes(R) > budget || rows * Wl * (CINP / 4) > fwd_maxc(CINP) * kThreads ||
         (R * a.Wo + 15) / 16 > 4 * kGmax)
       break;
     const int nt = (a.Ho + R - 1) / R;
