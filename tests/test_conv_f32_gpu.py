@@ -261,3 +261,22 @@ def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
     dx1 = C.cf32_conv_dgrad(dconv, w, 1, 1, 1, H, W)
     dx2 = C.cf32_conv_dgrad(dP, w, 1, 1, 1, H, W, pool_arg=a, pool_pbh=pbh, pool_pbw=pbw)
     assert torch.equal(dx1, dx2)
+
+
+@pytest.mark.parametrize('env', [{'SA_F32_DGRAD_STACK': '1'},
+                                 {'SA_F32_DGRAD_PHASE': '0'}])
+def test_strided_dgrad_alternative_paths(cuda, env):
+  """The opt-in strided-dgrad forms (phase-stacked single launch; the
+  correlation over the stride-dilated dY) pass the same dgrad tests (the
+  switches are read once per process, hence a subprocess)."""
+  import os
+  import subprocess
+  import sys
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  r = subprocess.run(
+      [sys.executable, '-m', 'pytest', '-q', '-p', 'no:cacheprovider',
+       os.path.abspath(__file__), '-k', 'test_conv_f32_dgrad and shallow'],
+      capture_output=True, text=True, timeout=240, cwd=root,
+      env=dict(os.environ, PYTHONPATH=root, **env))
+  assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+  assert ' passed' in r.stdout
