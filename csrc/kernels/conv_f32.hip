@@ -824,6 +824,124 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   }
 }
 
+// ------------------------------------------------- stage-head wgrad (scatter)
+// Weight / bias gradient of a stage-head conv3x3/1 SAME (4 input channels,
+// 16 output channels: the deep torso's first conv) straight from the pooled
+// gradient dP and the max-pool's argmax codes.  The pre-pool gradient is
+// dP routed to ONE position per (pooled pixel, channel), so
+//   dW[ky,kx,ci,co] = sum_{n,py,px} dP[n,py,px,co] * X[n, y*+ky-1, x*+kx-1, ci]
+// with (y*, x*) the argmax position of window (py, px) for channel co: a
+// quarter of the dense pre-pool reduction's terms, and the dense pre-pool
+// gradient (72x96x16 fp32 per frame, 4x the pooled map) is never written or
+// read.  The patch depends on co, so this is VALU work (fp32 FMA, exact)
+// with the input tile in LDS: thread = (pooled-pixel slot, co), 36 + 1
+// accumulators.  Per-workgroup partials in the wgrad slot layout
+// ([48 rows = tap*4 + ci, row 36 = bias][16 co]), summed by
+// wgrad_reduce_kernel in slot order: bitwise reproducible.
+constexpr int kPwRows = 4;  // pooled rows per tile
+__global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
+    const f4* __restrict__ x, const float* __restrict__ dP, const uint8_t* __restrict__ arg,
+    int H, int W, int Hp, int Wp, int pbh, int pbw, int tiles_per_img, int ntiles,
+    float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) f4 xs[];  // [2*kPwRows+3][W+2]
+  const int co = threadIdx.x & 15, ps = threadIdx.x >> 4;
+  const int Wl = W + 2;
+  float acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[t][c] = 0.f;
+  float accb = 0.f;
+  constexpr int kPer = (kPwRows * 64 + 15) / 16;  // pooled pixels per thread (Wp <= 64)
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int n = tile / tiles_per_img;
+    const int py0 = (tile - n * tiles_per_img) * kPwRows;
+    const int rp = min(kPwRows, Hp - py0);
+    const int ybase = 2 * py0 - pbh - 1;  // image row of LDS row 0
+    const int rows = 2 * rp + 3;
+    const int np = rp * Wp;
+    // this tile's pooled gradient and codes: loads in flight with the staging
+    float g[kPer];
+    uint32_t code[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int p = ps + 16 * k;
+      g[k] = 0.f;
+      code[k] = 0;
+      if (p < np) {
+        const int64_t o = (static_cast<int64_t>(n) * Hp + py0) * Wp * 16 + p * 16 + co;
+        g[k] = dP[o];
+        code[k] = arg[o];
+      }
+    }
+    __syncthreads();  // the previous tile's LDS reads are done
+    for (int e = threadIdx.x; e < rows * Wl; e += kThreads) {
+      const int r = e / Wl, c = e - r * Wl;
+      const int yy = ybase + r, xx = c - 1;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = x[(static_cast<int64_t>(n) * H + yy) * W + xx];
+      xs[e] = v;
+    }
+    __syncthreads();
+    int pyl = 0, px = ps;  // (row, col) of pooled pixel p = ps + 16 k
+    while (px >= Wp) {
+      px -= Wp;
+      ++pyl;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (ps + 16 * k < np) {
+        const int dy = (code[k] * 11) >> 5;  // code / 3 for code <= 8
+        const int dx = code[k] - 3 * dy;
+        // LDS position of tap (0, 0): row 2 pyl + dy, col 2 px - pbw + dx
+        // (the argmax never lies in the pool's padding; clamp for safety)
+        const int base = max(0, (2 * pyl + dy) * Wl + 2 * px - pbw + dx);
+        const float gv = g[k];
+        accb += gv;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const f4 v = xs[base + ky * Wl + kx];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[3 * ky + kx][c] = fmaf(gv, v[c], acc[3 * ky + kx][c]);
+          }
+      }
+      px += 16;
+      while (px >= Wp) {
+        px -= Wp;
+        ++pyl;
+      }
+    }
+  }
+  // sum the 16 pixel slots of each co in a fixed order: lanes co, co+16,
+  // co+32, co+48 of a wave by butterfly, then the 4 waves through LDS
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);  // [4 waves][37][16]
+  const int wave = threadIdx.x >> 6;
+  auto wsum = [&](float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+  };
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float v = wsum(acc[t][c]);
+      if ((threadIdx.x & 63) < 16) red[(wave * 37 + 4 * t + c) * 16 + co] = v;
+    }
+  {
+    const float v = wsum(accb);
+    if ((threadIdx.x & 63) < 16) red[(wave * 37 + 36) * 16 + co] = v;
+  }
+  __syncthreads();
+  float* dst = part + static_cast<int64_t>(blockIdx.x) * (48 * 16);
+  for (int e = threadIdx.x; e < 37 * 16; e += kThreads)
+    dst[e] = (red[e] + red[37 * 16 + e]) + (red[2 * 37 * 16 + e] + red[3 * 37 * 16 + e]);
+}
+
 // ------------------------------------------------------------------ pooling
 // Max-pool 3x3/2 (TF SAME) with first-max argmax codes.  One workgroup row
 // of the grid = one output row (n, py); thread = 4 channels of one pooled
@@ -1073,6 +1191,17 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
 
 }  // namespace
 
+// Scatter-form stage-head wgrad from (dP, argmax) (pool_wgrad_kernel): on
+// unless SA_F32_POOL_SCATTER=0 (then the dense-gather MFMA wgrad runs).
+static bool pool_scatter_on() {
+  static const bool on = env_knob("SA_F32_POOL_SCATTER", 1) != 0;
+  return on;
+}
+static bool pool_scatter_shape(int K, int S, int cinp, int cout) {
+  return K == 3 && S == 1 && cinp == 4 && cout == 16;
+}
+constexpr int kPwSlots = 2048;  // workgroups of a pool_wgrad launch (<= tiles)
+
 // Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
 // least 128 slots (before the tile-count cap) so the reduction fills the GPU.
 int64_t wgrad_slots(int K, int cinp, int cout) {
@@ -1084,7 +1213,9 @@ int64_t wgrad_slots(int K, int cinp, int cout) {
 int64_t wgrad_workspace_floats(int K, int Cin, int Cout) {
   const int cinp = Cin <= 4 ? 4 : Cin;
   const int64_t rows = ((K * K * cinp + 16) / 16) * 16;
-  return wgrad_slots(K, cinp, Cout) * rows * Cout;
+  int64_t n = wgrad_slots(K, cinp, Cout) * rows * Cout;
+  if (pool_scatter_shape(K, 1, cinp, Cout)) n = std::max<int64_t>(n, int64_t{kPwSlots} * 48 * 16);
+  return n;
 }
 
 bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_t s) {
@@ -1127,11 +1258,35 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   return false;
 }
 
+static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
+  const PoolGeom& pg = a.pool;
+  // pooled 3x3/2 SAME geometry of the (stride-1) conv output, Wp <= 64
+  if (pg.Hp != (a.Ho + 1) / 2 || pg.Wp != (a.Wo + 1) / 2 || pg.Wp > 64 || a.Ho != a.H ||
+      a.Wo != a.W || a.pt != 1 || a.pl != 1 || a.relu_in || pg.pbh < 0 || pg.pbh > 1 ||
+      pg.pbw < 0 || pg.pbw > 1)
+    return false;
+  const int tpi = (pg.Hp + kPwRows - 1) / kPwRows;
+  const int ntiles = a.N * tpi;
+  const int G = std::min(ntiles, kPwSlots);
+  const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * (a.W + 2),
+                                      sizeof(float) * 4 * 37 * 16);
+  allow_lds(pool_wgrad_kernel, lds);
+  hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s,
+                     static_cast<const f4*>(a.src), a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh,
+                     pg.pbw, tpi, ntiles, ws);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((48 * 16 + 15) / 16), dim3(256), 0, s, ws, G, 1,
+                     48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db);
+  return true;
+}
+
 bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStream_t s) {
   const int cinp = src == kSrcU8 ? 4 : a.Cin;
   if (src == kSrcU8 && (a.Cin < 1 || a.Cin > 4)) return false;
   if (src == kSrcF32 && a.Cin % 4 != 0) return false;
   const bool gather = a.pool.arg != nullptr;
+  if (gather && src == kSrcF32 && pool_scatter_on() && pool_scatter_shape(K, S, cinp, a.Cout) &&
+      run_pool_wgrad(a, ws, s))
+    return true;
 #define SA_WG_CASE(CINP, KK, SS, SRC, COUT, NTT, WSM)                                     \
   if (cinp == CINP && K == KK && S == SS && src == SRC && a.Cout == COUT) {               \
     if (gather) return run_wgrad<CINP, KK, SS, SRC, NTT, WSM, true>(a, ws, s);            \

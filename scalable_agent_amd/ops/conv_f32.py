@@ -36,7 +36,15 @@ DEBUG_TAPE = None
 # kernels' loads instead of materialising it with maxpool_bwd.
 FUSED_POOL_STAGES = tuple(int(c) for c in os.environ.get('SA_F32_FUSED_POOL', '0')
                           if c.isdigit())
-POOL_GATHER = os.environ.get('SA_F32_POOL_GATHER', '0') == '1'
+# SA_F32_POOL_GATHER=1: every stage; a digit string (e.g. '0'): those stages
+_pg = os.environ.get('SA_F32_POOL_GATHER', '')
+POOL_GATHER_STAGES = (0, 1, 2) if _pg == '1' else tuple(
+    int(c) for c in _pg if c.isdigit())
+POOL_GATHER = bool(POOL_GATHER_STAGES)
+# Stage 0 (4-channel frames -> 16): the conv's weight gradient is computed
+# straight from (dP, argmax) in scatter form (pool_wgrad_kernel) instead of
+# maxpool_bwd + the dense wgrad; SA_F32_POOL_SCATTER=0 restores the latter.
+POOL_SCATTER = os.environ.get('SA_F32_POOL_SCATTER', '1') != '0'
 
 
 def supports(agent):
@@ -178,7 +186,9 @@ class _DeepTorsoF32(torch.autograd.Function):
       if s == 0 and gw.shape[2] != 4:
         gw = torch.zeros(gw.shape[:2] + (4,) + gw.shape[3:], dtype=torch.float32,
                          device=dy.device)
-      if POOL_GATHER:
+      scatter = (s == 0 and POOL_SCATTER and stage_in.shape[3] == 4
+                 and dy.shape[3] == 16)
+      if s in POOL_GATHER_STAGES or scatter:
         # the conv kernels gather the pre-pool gradient from (dP, argmax)
         C.cf32_conv_wgrad(stage_in, dy, 1, 1, 1, False, gw, gv[pb + 1],
                           pool_arg=arg, pool_pbh=pbh, pool_pbw=pbw)

@@ -263,6 +263,35 @@ def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
     assert torch.equal(dx1, dx2)
 
 
+@pytest.mark.parametrize('N,H,W,Cs', [(5, 72, 96, 3), (3, 84, 84, 4), (4, 9, 13, 1)])
+def test_stage0_scatter_wgrad(cuda, N, H, W, Cs):
+  """Stage-0 weight gradient in scatter form straight from (dP, argmax)
+  (pool_wgrad_kernel) == the float64 weight gradient of the dense pre-pool
+  gradient; bitwise reproducible run to run (fixed-order partials)."""
+  C = _C()
+  g = torch.Generator().manual_seed(11)
+  fr = torch.randint(0, 256, (N, H, W, Cs), generator=g, dtype=torch.uint8).to(cuda)
+  x = C.cf32_frames_f32(fr)
+  w = (torch.randn(3, 3, 4, 16, generator=g) / 6.0).to(cuda)
+  b = (torch.randn(16, generator=g) * 0.1).to(cuda)
+  pbh, pbw = layers.same_pads(H, 3, 2)[0], layers.same_pads(W, 3, 2)[0]
+  p, a = C.cf32_conv_pool_fwd(x, w, b, pbh, pbw)
+  dP = torch.randn(p.shape, generator=g).to(cuda)
+  dconv = C.cf32_maxpool_bwd(dP, a, H, W, pbh, pbw)
+  ref = torch.nn.grad.conv2d_weight(
+      x.permute(0, 3, 1, 2).double(), (16, 4, 3, 3),
+      dconv.permute(0, 3, 1, 2).double(), padding=1).permute(2, 3, 1, 0)
+  outs = []
+  for _ in range(2):
+    dw, db = torch.zeros_like(w), torch.zeros_like(b)
+    C.cf32_conv_wgrad(x, dP, 1, 1, 1, False, dw, db, pool_arg=a, pool_pbh=pbh,
+                      pool_pbw=pbw)
+    outs.append((dw, db))
+  assert rel_err(outs[0][0].double(), ref) <= 1e-5
+  assert rel_err(outs[0][1].double(), dconv.double().sum((0, 1, 2))) <= 1e-5
+  assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize('env', [{'SA_F32_DGRAD_STACK': '1'},
                                  {'SA_F32_DGRAD_PHASE': '0'}])
 def test_strided_dgrad_alternative_paths(cuda, env):
