@@ -145,7 +145,12 @@ constexpr int kMaxC = 8;   // staged 16-B chunks per thread per tile
 // forward staging depth per input width: 64+ channel layers (the shallow
 // torso's 9x12 stage) need 16 chunks for a whole 5-row output image per tile
 // instead of a 4-row tile plus a 1-row tail tile
-__host__ __device__ constexpr int fwd_maxc(int cinp) { return cinp >= 64 ? 16 : kMaxC; }
+// and 32-channel layers 9: the 18x24 res32 convs then take 8-row tiles (12
+// MFMA groups = 3 per wave, balanced) instead of 7-row tiles (11 groups:
+// 3,3,3,2 per wave, the short wave idling at the tile barrier)
+__host__ __device__ constexpr int fwd_maxc(int cinp) {
+  return cinp >= 64 ? 16 : (cinp == 32 ? 9 : kMaxC);
+}
 
 // Pre-pool gradient at (n, y, x), channels 4ch..4ch+3, gathered from the
 // pooled gradient dP [N, Hp, Wp, C] through the argmax codes: windows in
@@ -516,7 +521,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
     if (tile < ntiles) prefetch(tile);
     const int n = cur / tiles_per_img;
     const int pi0 = (cur - n * tiles_per_img) * R;
-    const int cr0 = 2 * pi0 - pbh;
     auto mma = [&](auto NGc, int g0) {
       constexpr int NG = decltype(NGc)::value;
       f4 acc[NG][NH];
@@ -571,32 +575,41 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
       }
     };
     int grp = wave;
+    if constexpr (CINP == 4) {
+      // one MFMA per (tap, group): four groups in flight per wave cover the
+      // LDS latency of the next tap's operands (two left the pipe idle)
+      for (; grp + 12 < ngroups; grp += 16) mma(std::integral_constant<int, 4>{}, grp);
+    }
     for (; grp + 4 < ngroups; grp += 8) mma(std::integral_constant<int, 2>{}, grp);
     if (grp < ngroups) mma(std::integral_constant<int, 1>{}, grp);
     __syncthreads();
-    // pool the tile's conv rows (rows outside the image are never a max)
+    // pool the tile's conv rows (rows outside the image are never a max).
+    // Branch-free: every window tap reads a clamped in-tile address and an
+    // out-of-image tap is masked out of the compare (the divergent per-tap
+    // `continue`s of the first version made this phase VALU/SALU bound)
     const int Rv = min(R, Hp - pi0);
-    for (int e = threadIdx.x; e < Rv * Wp * C4; e += kThreads) {
-      const int c4 = e % C4;
+    const int nel = Rv * Wp * C4;
+    for (int e = threadIdx.x; e < nel; e += kThreads) {
+      const int c4 = e % C4;  // C4 is a power of two
       const int t = e / C4;
-      const int pc = t % Wp, pr = t / Wp;
+      const int pr = t / Wp, pc = t - pr * Wp;
+      const int crb = 2 * (pi0 + pr) - pbh, ccb = 2 * pc - pbw;
       float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       int code[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
-        const int cr = 2 * (pi0 + pr) - pbh + dy;
-        if (cr < 0 || cr >= H) continue;
+        const bool rok = crb + dy >= 0 && crb + dy < H;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          const int cc = 2 * pc - pbw + dx;
-          if (cc < 0 || cc >= W) continue;
-          const f4 v = *reinterpret_cast<const f4*>(y_s + ((cr - cr0) * W + cc) * YP + 4 * c4);
+          const bool ok = rok && ccb + dx >= 0 && ccb + dx < W;
+          // in-tile conv row 2 pr + dy (cr - cr0), column clamped
+          const int off = ok ? ((2 * pr + dy) * W + ccb + dx) * YP : 0;
+          const f4 v = *reinterpret_cast<const f4*>(y_s + off + 4 * c4);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if (v[r] > best[r]) {
-              best[r] = v[r];
-              code[r] = dy * 3 + dx;
-            }
+            const bool gt = ok && v[r] > best[r];
+            best[r] = gt ? v[r] : best[r];
+            code[r] = gt ? dy * 3 + dx : code[r];
           }
         }
       }
@@ -839,13 +852,21 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
 // ([48 rows = tap*4 + ci, row 36 = bias][16 co]), summed by
 // wgrad_reduce_kernel in slot order: bitwise reproducible.
 constexpr int kPwRows = 4;  // pooled rows per tile
+// LDS row pitch (16-B pixels) of the input tile: >= W + 2 and 5 mod 16.  A
+// ds_read_b128 quarter-wave (16 lanes: two adjacent pooled pixels x 8 co)
+// reads inside a 3-row x 5-column window; with the row pitch 5 mod 16 its 15
+// positions fall in 15 distinct 16-B bank slots, so lanes either share an
+// address (broadcast) or a slot never (the W + 2 pitch, 2 mod 16, measured
+// 4.6 bank conflicts per LDS instruction in rocprof).
+__host__ __device__ constexpr int pw_pitch(int W) { return W + 2 + ((5 - (W + 2)) % 16 + 16) % 16; }
+static_assert(pw_pitch(96) == 101 && pw_pitch(84) == 101 && pw_pitch(3) == 5, "pw pitch");
 __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
     const f4* __restrict__ x, const float* __restrict__ dP, const uint8_t* __restrict__ arg,
     int H, int W, int Hp, int Wp, int pbh, int pbw, int tiles_per_img, int ntiles,
     float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) f4 xs[];  // [2*kPwRows+3][W+2]
   const int co = threadIdx.x & 15, ps = threadIdx.x >> 4;
-  const int Wl = W + 2;
+  const int Wl = pw_pitch(W);
   float acc[9][4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -1124,8 +1145,11 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
            (9 * CINP * COUT + (2 * R + 3) * Wl * PP + (2 * R + 1) * W * (COUT + 4));
   };
   const size_t budget = bytes(2) <= kLdsSoft ? kLdsSoft : kLdsHard;
+  // pooled rows per tile cap: 2 for the 4-channel stage head (51.7 KB of LDS,
+  // three workgroups per CU: 16.57 -> 16.46 ms/step against 3 rows, two)
+  static const int rcap = env_knob("SA_F32_POOL_R", CINP == 4 ? 2 : 1 << 20);
   int R = 0;
-  for (int r = 1; r <= Hp; ++r) {
+  for (int r = 1; r <= std::min(Hp, rcap); ++r) {
     if (bytes(r) > budget || (2 * r + 3) * Wl * (CINP / 4) > kMaxC * kThreads) break;
     R = r;
   }
@@ -1267,8 +1291,9 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
     return false;
   const int tpi = (pg.Hp + kPwRows - 1) / kPwRows;
   const int ntiles = a.N * tpi;
-  const int G = std::min(ntiles, kPwSlots);
-  const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * (a.W + 2),
+  static const int slots = std::max(1, std::min(kPwSlots, env_knob("SA_F32_PW_SLOTS", kPwSlots)));
+  const int G = std::min(ntiles, slots);
+  const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
                                       sizeof(float) * 4 * 37 * 16);
   allow_lds(pool_wgrad_kernel, lds);
   hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s,
