@@ -24,6 +24,8 @@
 // bitwise reproducible run to run (no float atomics).
 #include "conv_f32.h"
 
+#include <utility>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
@@ -282,6 +284,16 @@ struct DyStager {
     }
   }
 };
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <typename F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 constexpr int kMaxD = 8;  // staged dY chunks per thread per tile (taller tiles: more MFMA work per prefetch)
 
 template <int CINP, int COUT_T, int K, int S, int SRC, bool FLIP>
@@ -700,6 +712,79 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
     tile += gridDim.x;
     if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
     const int nq = (P + 3) >> 2;
+    if constexpr (CINP % 16 == 0 && WSM == 1) {
+      // 16-channel-multiple inputs, one wave row set (res16 391 vs 438 us,
+      // conv2 648 vs 715; the WSM = 2 res32 wgrad measured slower with it,
+      // 342 vs 317 us, and keeps the generic loop): row block mb (16 rows m = 16 mb + c16) is
+      // one tap and 16 consecutive input channels, so with the wave's block
+      // set known at compile time (MG) every A-operand read is a per-ky lane
+      // base plus an IMMEDIATE offset (no per-read address VALU), the
+      // bias-row block is a per-lane constant, blocks past the last are
+      // skipped, the pixel walk is branch-free and the two operand buffers
+      // alternate without copies (valu/mfma 6.1 in rocprof before)
+      auto run = [&](auto MGc) {
+        constexpr int MG = decltype(MGc)::value;
+        const int WlXP = Wl * XP;
+        const int step = 4 * PG;
+        const int dcy = step / a.Wo, dcx = step - (step / a.Wo) * a.Wo;
+        int cy = (4 * pg + g) / a.Wo;
+        int cx = (4 * pg + g) - cy * a.Wo;
+        const float bias_row = c16 == 0 ? 1.f : 0.f;
+        float a0[MTW], b0[NTT], a1[MTW], b1[NTT];
+        auto load = [&](int qd, float (&av)[MTW], float (&bv)[NTT]) {
+          const int p = 4 * qd + g;
+          const bool valid = p < P;
+          const int lb = valid ? (cy * S * Wl + cx * S) * XP + c16 : c16;
+          const float* d = d_s + (valid ? p : 0) * DP + c16;
+#pragma unroll
+          for (int nb = 0; nb < NTT; ++nb) bv[nb] = valid ? d[16 * nb] : 0.f;
+          int rb[K];
+#pragma unroll
+          for (int ky = 0; ky < K; ++ky) rb[ky] = lb + ky * WlXP;
+          sfor<MTW>([&](auto Ic) {
+            constexpr int i = decltype(Ic)::value;
+            constexpr int mb = MG + WSM * i;
+            if constexpr (16 * mb + 15 < M) {
+              constexpr int tap = 16 * mb / CINP, ci0 = 16 * mb % CINP;
+              av[i] = x_s[rb[tap / K] + (tap % K) * XP + ci0];
+            } else if constexpr (16 * mb == M) {
+              av[i] = bias_row;
+            } else {
+              av[i] = 0.f;
+            }
+          });
+          cx += dcx;
+          cy += dcy;
+          const bool wrap = cx >= a.Wo;
+          cx = wrap ? cx - a.Wo : cx;
+          cy = wrap ? cy + 1 : cy;
+        };
+        auto mma = [&](const float (&av)[MTW], const float (&bv)[NTT]) {
+          sfor<MTW>([&](auto Ic) {
+            constexpr int i = decltype(Ic)::value;
+            if constexpr (MG + WSM * i < MT) {
+#pragma unroll
+              for (int nb = 0; nb < NTT; ++nb) acc[i][nb] = mfma4(av[i], bv[nb], acc[i][nb]);
+            }
+          });
+        };
+        int qd = pg;
+        if (qd < nq) load(qd, a0, b0);
+        while (qd < nq) {
+          if (qd + PG < nq) load(qd + PG, a1, b1);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(a0, b0);
+          qd += PG;
+          if (qd >= nq) break;
+          if (qd + PG < nq) load(qd + PG, a0, b0);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(a1, b1);
+          qd += PG;
+        }
+      };
+      run(std::integral_constant<int, 0>{});
+      continue;
+    }
     // software-pipelined: quad qd+PG's operand reads are issued ahead of
     // quad qd's MFMAs.  The lane's pixel p = 4 qd + g advances by 4 PG per
     // quad: its (oy, ox) is stepped incrementally (no integer division in
