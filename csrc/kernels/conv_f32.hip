@@ -284,6 +284,14 @@ struct DyStager {
     }
   }
 };
+// x / d for 0 <= x < 2^20 and 1 <= d <= 2^10 via fp32: (x + 0.5) / d is at
+// least 0.5 / d away from an integer, far above the fp32 rounding error of
+// (x + 0.5) * rcp(d), so the truncation is exact (a 32-bit integer division
+// is ~20 VALU instructions; this is 3).  rd = 1.f / d, computed once.
+__device__ __forceinline__ int fdiv(int x, float rd) {
+  return static_cast<int>((static_cast<float>(x) + 0.5f) * rd);
+}
+
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
 template <typename F, int... I>
 __device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -348,6 +356,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
     for (int r = 0; r < 4; ++r)
       bias[h][r] = a.bias != nullptr ? a.bias[co0 + 16 * h + 4 * g + r] : 0.f;
   const float* wl = w_s + (g * COUT_T + c16) * VPL;
+  const float rwo = 1.f / static_cast<float>(a.Wo);
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
@@ -379,7 +388,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
       for (int gi = 0; gi < NG; ++gi) {
         const int p = (wave + 4 * (i0 + gi)) * 16 + c16;
         const int pp = p < P ? p : 0;
-        const int oy = pp / a.Wo, ox = pp - oy * a.Wo;
+        const int oy = fdiv(pp, rwo), ox = pp - oy * a.Wo;
         xb[gi] = (oy * S * Wl + ox * S) * PP + VPL * g;
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[i0 + gi][h] = f4{0.f, 0.f, 0.f, 0.f};
@@ -429,7 +438,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
     for (int i = 0; i < kGmax; ++i) {
       const int p = (wave + 4 * i) * 16 + c16;
       if (p >= P) continue;
-      const int oy = p / a.Wo, ox = p - (p / a.Wo) * a.Wo;
+      const int oy = fdiv(p, rwo), ox = p - oy * a.Wo;
       const int64_t pix = (static_cast<int64_t>(n) * Hf + (oy0 + oy) * os + a.ooy) * Wf +
                           ox * os + a.oox;
 #pragma unroll
@@ -512,6 +521,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[h][r] = a.bias[16 * h + 4 * g + r];
   const float* wl = w_s + (g * COUT + c16) * VPL;
+  const float rw = 1.f / static_cast<float>(W), rwp = 1.f / static_cast<float>(Hp > 0 ? Wp : 1);
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
@@ -542,7 +552,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
         const int p = (g0 + 4 * gi) * 16 + c16;
         q[gi] = p < P ? p : -1;
         const int pp = p < P ? p : 0;
-        const int oy = pp / W, ox = pp - oy * W;
+        const int oy = fdiv(pp, rw), ox = pp - oy * W;
         xb[gi] = (oy * Wl + ox) * PP + VPL * g;
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
@@ -604,7 +614,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
     for (int e = threadIdx.x; e < nel; e += kThreads) {
       const int c4 = e % C4;  // C4 is a power of two
       const int t = e / C4;
-      const int pr = t / Wp, pc = t - pr * Wp;
+      const int pr = fdiv(t, rwp), pc = t - pr * Wp;
       const int crb = 2 * (pi0 + pr) - pbh, ccb = 2 * pc - pbw;
       float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       int code[4] = {0, 0, 0, 0};
