@@ -946,7 +946,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
 // accumulators.  Per-workgroup partials in the wgrad slot layout
 // ([48 rows = tap*4 + ci, row 36 = bias][16 co]), summed by
 // wgrad_reduce_kernel in slot order: bitwise reproducible.
-constexpr int kPwRows = 4;  // pooled rows per tile
+constexpr int kPwRows = 2;  // pooled rows per tile
 // LDS row pitch (16-B pixels) of the input tile: >= W + 2 and 5 mod 16.  A
 // ds_read_b128 quarter-wave (16 lanes: two adjacent pooled pixels x 8 co)
 // reads inside a 3-row x 5-column window; with the row pitch 5 mod 16 its 15
@@ -1319,7 +1319,10 @@ static bool pool_scatter_on() {
 static bool pool_scatter_shape(int K, int S, int cinp, int cout) {
   return K == 3 && S == 1 && cinp == 4 && cout == 16;
 }
-constexpr int kPwSlots = 2048;  // workgroups of a pool_wgrad launch (<= tiles)
+// workgroups of a pool_wgrad launch (<= tiles): the resident count, 5 per CU
+// at its 96 VGPRs (2-row tiles: 298 -> 228 us against 4-row tiles at 138
+// VGPRs and 2048 slots)
+constexpr int kPwSlots = 1280;
 
 // Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
 // least 128 slots (before the tile-count cap) so the reduction fills the GPU.
