@@ -1058,6 +1058,66 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
     dst[e] = (red[e] + red[37 * 16 + e]) + (red[2 * 37 * 16 + e] + red[3 * 37 * 16 + e]);
 }
 
+// The same fixed-order slot sum for small layers (total < 4096 outputs: the
+// stage-0 scatter wgrad's 768, res16's 2560): block = 4 outputs x 64 slot
+// groups, so the launch still fills the GPU (the 16 x 16 blocks gave the
+// stage-0 reduction 48 workgroups and 38 us).
+__global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(
+    const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+  constexpr int OPB = 4, SG = 256 / OPB;
+  __shared__ float red[SG][OPB + 1];
+  const int per = MT16 * CG;
+  const int l = threadIdx.x % OPB;
+  const int e = blockIdx.x * OPB + l;
+  const int sg = threadIdx.x / OPB;
+  const bool live = e < ngrp * per;
+  const int ng = live ? e / per : 0, rem = live ? e - ng * per : 0;
+  const int m = rem / CG, c = rem - (rem / CG) * CG;
+  const bool want = live && ((m < M && (m % CINP) < Cin) || (db != nullptr && m == M));
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (want) {
+    const float* p = part + static_cast<int64_t>(ng) * G * per + rem;
+    for (int k = sg; k < G; k += 4 * SG) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = k + SG * u;
+        if (kk < G) acc[u] += p[static_cast<int64_t>(kk) * per];
+      }
+    }
+  }
+  red[sg][l] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (sg != 0 || !want) return;
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < SG; q += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] += red[q + j][l];
+  }
+  const float sum = (t[0] + t[1]) + (t[2] + t[3]);
+  const int co = ng * CG + c;
+  if (m < M) {
+    const int tap = m / CINP, ci = m - (m / CINP) * CINP;
+    dw[(static_cast<int64_t>(tap) * Cin + ci) * Cout + co] += sum;
+  } else {
+    db[co] += sum;
+  }
+}
+
+// launches the fixed-order slot sum (the narrow form for small layers)
+void wgrad_reduce(const float* part, int G, int ngrp, int MT16, int CG, int CINP, int M, int Cin,
+                  int Cout, float* dw, float* db, hipStream_t s) {
+  const int total = ngrp * MT16 * CG;
+  if (total < 4096) {
+    hipLaunchKernelGGL(wgrad_reduce_narrow_kernel, dim3((total + 3) / 4), dim3(256), 0, s, part,
+                       G, ngrp, MT16, CG, CINP, M, Cin, Cout, dw, db);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, s, part, G,
+                       ngrp, MT16, CG, CINP, M, Cin, Cout, dw, db);
+  }
+}
+
 // ------------------------------------------------------------------ pooling
 // Max-pool 3x3/2 (TF SAME) with first-max argmax codes.  One workgroup row
 // of the grid = one output row (n, py); thread = 4 channels of one pooled
@@ -1302,9 +1362,7 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   auto kern = conv_wgrad_kernel<CINP, K, S, SRC, NTT, WSM, GATHER>;
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
-  const int total = ngrp * MT * 16 * CG;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, s, ws, G,
-                     ngrp, MT * 16, CG, CINP, M, a.Cin, a.Cout, a.dw, a.db);
+  wgrad_reduce(ws, G, ngrp, MT * 16, CG, CINP, M, a.Cin, a.Cout, a.dw, a.db, s);
   return true;
 }
 
@@ -1397,8 +1455,7 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s,
                      static_cast<const f4*>(a.src), a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh,
                      pg.pbw, tpi, ntiles, ws);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((48 * 16 + 15) / 16), dim3(256), 0, s, ws, G, 1,
-                     48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db);
+  wgrad_reduce(ws, G, 1, 48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db, s);
   return true;
 }
 
