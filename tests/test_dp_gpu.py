@@ -51,3 +51,35 @@ def test_two_ranks_match_one_rank_with_the_whole_batch(cuda, tmp_path, dtype, to
   assert b['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
   # the RMSProp update built from them agrees too
   assert torch.allclose(a['params'], b['params'], rtol=0, atol=atol)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_card(cuda):
+  """bench.py's multi-rank path on the GPU (the driver's N>1 launch shape,
+  here two ranks sharing one card over gloo): captured split-backward graphs,
+  the early all-reduce between their replays, fp32 and bf16 learners, one
+  JSON line from rank 0 reporting both ranks."""
+  import json
+  root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  port = s.getsockname()[1]
+  s.close()
+  cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+         '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+         '--master-port', str(port), os.path.join(root, 'bench.py'),
+         '--gpus', '2', '--steps', '3', '--warmup', '2', '--batch_size', '4',
+         '--unroll_length', '10']
+  env = dict(os.environ, PYTHONPATH=root, SA_DIST_BACKEND='gloo',
+             OMP_NUM_THREADS='2')
+  r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+  assert r.returncode == 0, r.stderr[-3000:]
+  lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+  assert len(lines) == 1, r.stdout
+  out = json.loads(lines[0])
+  cfg = out['config']
+  assert out['n_gpus'] == 2 and cfg['parallelism'] == 'dp2'
+  assert cfg['dist']['world_size'] == 2 and cfg['dist']['backend'] == 'gloo'
+  assert cfg['global_batch'] == 8 and cfg['hip_graph'] and cfg['loss_finite']
+  assert cfg['torso_kernels'] == 'fp32' and cfg['bf16']['loss_finite']
+  assert cfg['learner_health']['skipped_updates'] == 0
