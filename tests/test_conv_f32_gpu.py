@@ -263,11 +263,13 @@ def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
     assert torch.equal(dx1, dx2)
 
 
-@pytest.mark.parametrize('N,H,W,Cs', [(5, 72, 96, 3), (3, 84, 84, 4), (4, 9, 13, 1)])
+@pytest.mark.parametrize('N,H,W,Cs', [(5, 72, 96, 3), (3, 84, 84, 4), (4, 9, 13, 1),
+                                      (2, 10, 136, 3)])
 def test_stage0_scatter_wgrad(cuda, N, H, W, Cs):
   """Stage-0 weight gradient in scatter form straight from (dP, argmax)
   (pool_wgrad_kernel) == the float64 weight gradient of the dense pre-pool
-  gradient; bitwise reproducible run to run (fixed-order partials)."""
+  gradient; bitwise reproducible run to run (fixed-order partials).  W = 136
+  (pooled width 68 > 64) takes the dense-gather MFMA fallback instead."""
   C = _C()
   g = torch.Generator().manual_seed(11)
   fr = torch.randint(0, 256, (N, H, W, Cs), generator=g, dtype=torch.uint8).to(cuda)
