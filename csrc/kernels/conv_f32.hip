@@ -503,7 +503,17 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
   const int total = rows * Wl * (CINP / 4);
   float* w_s = smem;
   float* x_s = w_s + KK * CINP * COUT;
+  // conv rows in LDS with a -inf column on each side (column c at c + 1) and
+  // rows outside the image stored as -inf: the pool phase needs no bounds
+  // masks and reads every tap at an immediate offset from a per-row base
+  const int YW = W + 2;
   float* y_s = x_s + rows * Wl * PP;
+  for (int e = threadIdx.x; e < CR * 2 * (YP / 4); e += kThreads) {
+    const int q4 = e % (YP / 4), t = e / (YP / 4);
+    const int col = (t & 1) ? W + 1 : 0;
+    *reinterpret_cast<f4*>(y_s + ((t >> 1) * YW + col) * YP + 4 * q4) =
+        f4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  }
   for (int e = threadIdx.x; e < KK * COUT * CINP; e += kThreads) {
     const int o = e % COUT, i = (e / COUT) % CINP, tap = e / (COUT * CINP);
     float v = 0.f;
@@ -543,16 +553,19 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
     if (tile < ntiles) prefetch(tile);
     const int n = cur / tiles_per_img;
     const int pi0 = (cur - n * tiles_per_img) * R;
+    const int cr0 = 2 * pi0 - pbh;  // image row of the tile's conv row 0
     auto mma = [&](auto NGc, int g0) {
       constexpr int NG = decltype(NGc)::value;
       f4 acc[NG][NH];
       int xb[NG], q[NG];
+      bool inimg[NG];
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
         const int p = (g0 + 4 * gi) * 16 + c16;
-        q[gi] = p < P ? p : -1;
         const int pp = p < P ? p : 0;
         const int oy = fdiv(pp, rw), ox = pp - oy * W;
+        q[gi] = p < P ? (oy * YW + ox + 1) * YP : -1;
+        inimg[gi] = cr0 + oy >= 0 && cr0 + oy < H;
         xb[gi] = (oy * Wl + ox) * PP + VPL * g;
 #pragma unroll
         for (int h = 0; h < NH; ++h) acc[gi][h] = f4{0.f, 0.f, 0.f, 0.f};
@@ -591,8 +604,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
         for (int h = 0; h < NH; ++h) {
           f4 v = acc[gi][h];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += bias[h][r];
-          *reinterpret_cast<f4*>(y_s + q[gi] * YP + 16 * h + 4 * g) = v;
+          for (int r = 0; r < 4; ++r) v[r] = inimg[gi] ? v[r] + bias[h][r] : -INFINITY;
+          *reinterpret_cast<f4*>(y_s + q[gi] + 16 * h + 4 * g) = v;
         }
       }
     };
@@ -605,31 +618,27 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
     for (; grp + 4 < ngroups; grp += 8) mma(std::integral_constant<int, 2>{}, grp);
     if (grp < ngroups) mma(std::integral_constant<int, 1>{}, grp);
     __syncthreads();
-    // pool the tile's conv rows (rows outside the image are never a max).
-    // Branch-free: every window tap reads a clamped in-tile address and an
-    // out-of-image tap is masked out of the compare (the divergent per-tap
-    // `continue`s of the first version made this phase VALU/SALU bound)
+    // pool the tile's conv rows: out-of-image taps read the -inf border /
+    // rows, which never win the strict first-max compare
     const int Rv = min(R, Hp - pi0);
     const int nel = Rv * Wp * C4;
     for (int e = threadIdx.x; e < nel; e += kThreads) {
       const int c4 = e % C4;  // C4 is a power of two
       const int t = e / C4;
       const int pr = fdiv(t, rwp), pc = t - pr * Wp;
-      const int crb = 2 * (pi0 + pr) - pbh, ccb = 2 * pc - pbw;
+      // tap (0, 0): in-tile conv row 2 pr, column 2 pc - pbw (+1 border)
+      const float* yb = y_s + ((2 * pr) * YW + 2 * pc - pbw + 1) * YP + 4 * c4;
       float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
       int code[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
-        const bool rok = crb + dy >= 0 && crb + dy < H;
+        const float* yr = yb + dy * YW * YP;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          const bool ok = rok && ccb + dx >= 0 && ccb + dx < W;
-          // in-tile conv row 2 pr + dy (cr - cr0), column clamped
-          const int off = ok ? ((2 * pr + dy) * W + ccb + dx) * YP : 0;
-          const f4 v = *reinterpret_cast<const f4*>(y_s + off + 4 * c4);
+          const f4 v = *reinterpret_cast<const f4*>(yr + dx * YP);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const bool gt = ok && v[r] > best[r];
+            const bool gt = v[r] > best[r];
             best[r] = gt ? v[r] : best[r];
             code[r] = gt ? dy * 3 + dx : code[r];
           }
@@ -1297,7 +1306,7 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
   const int Hp = (a.Ho + 1) / 2, Wp = (a.Wo + 1) / 2;
   auto bytes = [&](int R) {
     return static_cast<size_t>(4) *
-           (9 * CINP * COUT + (2 * R + 3) * Wl * PP + (2 * R + 1) * W * (COUT + 4));
+           (9 * CINP * COUT + (2 * R + 3) * Wl * PP + (2 * R + 1) * (W + 2) * (COUT + 4));
   };
   const size_t budget = bytes(2) <= kLdsSoft ? kLdsSoft : kLdsHard;
   // pooled rows per tile cap: 2 for the 4-channel stage head (51.7 KB of LDS,
