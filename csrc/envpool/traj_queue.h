@@ -18,6 +18,16 @@
 // committed) -> READING (consumer) -> FREE.  Column hand-out and slab
 // selection run under a tiny process-shared spinlock; blocking waits use a
 // process-shared futex on a header word that every transition bumps.
+//
+// Failure model (fail-stop, by design): a producer that dies between
+// ClaimN() and Commit() keeps its columns, so that slab never becomes READY.
+// Nothing reclaims them - a half-written unroll must never reach the
+// learner.  The learner side detects it instead: actor-group processes are
+// supervised (ActorGroups.check() raises as soon as a group exits), and for
+// actor threads the learner's Acquire() loop raises 'learner starved' after
+// --queue_timeout_secs; either way train() stops and the last checkpoint is
+// the restart point (tests/test_traj_queue.py covers a producer that claims
+// and never commits).
 #pragma once
 
 #include <atomic>

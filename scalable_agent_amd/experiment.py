@@ -235,7 +235,8 @@ class _TrajFeeder(object):
       self.torch.cuda.synchronize(self.device)
       learner.capture(self.views[j], clone=False)
       self.graphs[j] = (learner._graph, learner._static_in,
-                        learner._static_loss)
+                        learner._static_loss,
+                        getattr(learner, '_graph_keep', None))
 
   def _reap(self, block):
     while self.pending:
@@ -297,8 +298,12 @@ class _TrajFeeder(object):
         copied.synchronize()  # capture runs on the data in place
         learner.capture(self.views[j], clone=False)
         self.graphs[j] = (learner._graph, learner._static_in,
-                          learner._static_loss)
-      learner._graph, learner._static_in, learner._static_loss = self.graphs[j]
+                          learner._static_loss,
+                          getattr(learner, '_graph_keep', None))
+      # split-backward graphs: each slot keeps its own pool tensors
+      # (features / leaf gradients) alive alongside its graphs
+      (learner._graph, learner._static_in, learner._static_loss,
+       learner._graph_keep) = self.graphs[j]
       loss = learner.graph_step()
     else:
       loss = learner.step(self.views[j])
@@ -310,6 +315,22 @@ class _TrajFeeder(object):
 
   def close(self):
     self._reap(block=True)
+
+  def drain(self, timeout_s=10.0):
+    """Waits (bounded, polling) until every H2D copy still reading a host
+    slab has completed -> True; False if one is still in flight at the
+    deadline (e.g. after a GPU fault), when the slabs must stay registered."""
+    if not self.cuda:
+      return True
+    deadline = time.time() + timeout_s
+    while self.pending:
+      if self.pending[0][1].query():
+        self.pending.popleft()  # the queue is closing: no release needed
+        continue
+      if time.time() > deadline:
+        return False
+      time.sleep(0.001)
+    return True
 
 
 # --------------------------------------------------------------- train
@@ -740,9 +761,11 @@ def train(flags):
   finally:
     stop.set()
     if use_traj:
-      tq.close()
-      if not failed:  # after a GPU fault, waiting on its events could hang
-        feeder.close()
+      # every in-flight H2D of a host slab must finish before the slabs are
+      # unregistered; after a failure the wait is bounded (a GPU fault may
+      # never complete the copies: then the slabs stay registered)
+      drained = feeder.drain(10.0 if failed else 600.0)
+      tq.close(unregister=drained)
     if infer is not None:
       infer.close()
     if groups is not None:

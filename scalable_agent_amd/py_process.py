@@ -497,6 +497,17 @@ class EnvProcess(object):
         if self._timeout and time.time() - start > self._timeout:
           self._kill_worker()  # hung: the supervisor forks a replacement
           start = time.time()
+      # a worker that died BETWEEN requests leaves its restart notice on the
+      # pipe while the replacement answers this request on a fresh env that
+      # never ran initial(): report the episode boundary here, not on some
+      # later step
+      while self._chan.status == 0 and self._conn.poll(0):
+        status, _, payload = self._conn.recv()
+        if status == 'restarted':
+          raise EnvRestartedError('env worker replaced (restart %d)' %
+                                  self._restarts.value)
+        if status == 'error':
+          raise payload
       if self._chan.status != 0:  # the exception follows on the pipe
         status, _, payload = self._conn.recv()
         if status == 'restarted':

@@ -84,6 +84,7 @@ class SharedWeights(object):
     self._tensors = None
     self._pending = None
     self._stream = None
+    self._snap = None
     self.skipped = 0
 
   # --------------------------------------------------------------- both
@@ -140,10 +141,19 @@ class SharedWeights(object):
     host = self.tensors(flat_params.device)
     if self._stream is None:
       self._stream = torch.cuda.Stream(flat_params.device)
-    self._stream.wait_stream(torch.cuda.current_stream(flat_params.device))
+    # the D2H reads a device-side snapshot taken on the learner's stream (a
+    # few us of HBM copy), never flat_params itself: the next optimizer step
+    # may overwrite the parameters while the slow D2H is still in flight.
+    # The snapshot is only rewritten after the previous D2H completed
+    # (_finish above), so it is never torn either.
+    cur = torch.cuda.current_stream(flat_params.device)
+    if self._snap is None or self._snap.shape != flat_params.shape:
+      self._snap = torch.empty_like(flat_params.detach())
+    self._snap.copy_(flat_params.detach())
+    self._stream.wait_stream(cur)
     b = self._target()
     with torch.cuda.stream(self._stream):
-      host[b].copy_(flat_params.detach(), non_blocking=self._pinned)
+      host[b].copy_(self._snap, non_blocking=self._pinned)
       ev = torch.cuda.Event()
       ev.record(self._stream)
     self._pending = (b, ev)

@@ -188,8 +188,11 @@ class TrajectoryQueue(object):
   def num_ready(self):
     return self.q.num_ready
 
-  def close(self):
+  def close(self, unregister=True):
+    """Closes the native queue (wakes every waiter).  unregister=False
+    leaves the payload host-registered: the caller could not prove that no
+    DMA still reads it (unregistering under a live copy can fault the GPU)."""
     self.q.close()
-    if self._pin_addr is not None:
+    if self._pin_addr is not None and unregister:
       _hip_host_unregister(self._pin_addr)
       self._pin_addr = None

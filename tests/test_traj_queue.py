@@ -131,3 +131,22 @@ def test_claim_n_is_all_or_nothing():
   assert len(tq.claim_n(4, timeout_ms=100)) == 4
   tq.close()
   assert tq.claim_n(1, timeout_ms=10) == -2
+
+
+def test_dead_producer_is_fail_stop():
+  """A producer that dies after claiming a column never publishes that slab
+  (no half-written unroll reaches the learner): the consumer's acquire times
+  out instead, which train() turns into a 'learner starved' stop."""
+  T1, B = 3, 2
+  layout = BatchLayout(T1, B, (4, 4, 3), 3)
+  tq = TrajectoryQueue(layout, num_slabs=3)
+  s, col, v = tq.claim(timeout_ms=1000)
+  _fill(v, col, 7, T1)
+  tq.commit(s)
+  # the second column of the same slab is claimed by a thread that then
+  # "dies" (never commits)
+  s2, col2, _ = tq.claim(timeout_ms=1000)
+  assert s2 == s and col2 != col
+  assert tq.acquire(timeout_ms=300) < 0
+  assert tq.num_ready == 0
+  tq.close()
