@@ -78,6 +78,12 @@ struct WgradArgs {
   PoolGeom pool;       // pool.arg != null: dy is dP, (Ho, Wo) pre-pool dims
 };
 
+// Winograd F(2x2,3x3) fp32 path (conv_wino.hip) for 3x3/1 SAME convs with
+// 16/32 channels in and out (forward and data gradient); false when the
+// shape is not covered.  SA_F32_WINO=0 disables it (direct implicit GEMM).
+bool wino_enabled();
+bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
+
 // Returns false (and launches nothing) when no instance matches the shape;
 // the bindings turn that into an error naming the shape.
 bool conv_launch(const ConvArgs& a, int K, int S, int src_kind, bool flip,

@@ -1417,6 +1417,8 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   if (src == kSrcU8 && (a.Cs < 1 || a.Cs > 4)) return false;
   if (src != kSrcU8 && a.Cs % 4 != 0) return false;
   if (src == kSrcPoolGrad && (a.pool.arg == nullptr || a.D != 1)) return false;
+  if (K == 3 && S == 1 && src == kSrcF32 && wino_enabled() && wino_conv_launch(a, flip, s))
+    return true;
   const int ct = cout_tile(cinp, a.Cout, K);
   if (a.Cout % ct != 0) return false;
 #define SA_CONV_CASE(CINP, CT, KK, SS, SRC, FL)                                          \

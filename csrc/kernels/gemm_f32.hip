@@ -1,0 +1,259 @@
+// Exact-fp32 GEMM with fused epilogues for the learner's torso-FC / LSTM
+// input projection / their gradients (v_mfma_f32_32x32x2_f32: f32 in, f32
+// accumulate, one rounding per product).
+//
+// Reference: experiment.py:185-198 (Linear(256) + ReLU on the flattened
+// conv features, concat [torso, clip(r), one_hot(a), instruction]) and the
+// LSTMBlockCell's x W_x projection (:228-235); their gradients are the
+// backward of the same products.  Every learner GEMM is one of
+//   C[M, N] (+)= op(A)[M, K] op(B)[K, N]      op = identity or transpose
+// with the epilogue  v = acc [+ bias[n]] [* (mask[m, n] > 0)] [relu] [+= C]
+// and two learner-specific extras:
+//   * ones_row: op(A) gets an extra row of ones, whose result row is the
+//     column sum of op(B) over K - the bias gradient of a weight-gradient
+//     GEMM (db = 1^T dY) comes out of the same pass, accumulated into
+//     `colsum`;
+//   * aug: the core-input columns [clip(r), one_hot(a), 0...] are written
+//     next to the FC output (C's columns N .. ldc-1), so the concat of
+//     experiment.py:191-198 is never a separate kernel.
+//
+// Tiling: 64 x 64 output tile per 256-thread workgroup (2 x 2 waves of one
+// 32 x 32 MFMA accumulator each), K in steps of 16 staged through a double-
+// buffered LDS image [row][k] (pitch 20 floats: conflict-free 16-B reads)
+// with the next step's global loads in flight under the current MFMAs.  The
+// k order inside a step is permuted (MFMA s uses k = 8 h + s for lane half
+// h) on both operands, so each lane reads its 8 k values of a step with two
+// ds_read_b128.  Large-K products (the weight gradients, K = T*B = 3232)
+// split K over grid.z into per-split partial slabs that one reduction
+// kernel sums in split order: deterministic, no float atomics.
+#include "gemm_f32.h"
+
+#include <algorithm>
+
+namespace sa {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 64, BN = 64, BK = 16, PK = 20;
+
+struct Args {
+  const float* A;
+  const float* B;
+  int M, N, K, lda, ldb, ta, tb, ones_row;
+  int splits, kchunk;
+  float* part;  // [splits][Mr][N] when splits > 1
+  GemmEpilogue ep;
+};
+
+// epilogue of one output element (row m < M)
+__device__ __forceinline__ void store_out(const GemmEpilogue& e, int m, int n, float v) {
+  if (e.bias != nullptr) v += e.bias[n];
+  if (e.mask != nullptr) v = e.mask[static_cast<int64_t>(m) * e.ldm + n] > 0.f ? v : 0.f;
+  if (e.relu) v = fmaxf(v, 0.f);
+  float* c = e.C + static_cast<int64_t>(m) * e.ldc + n;
+  if (e.accumulate) v += *c;
+  *c = v;
+}
+
+// the core-input columns [clip(r), one_hot(a), 0...] of row m (aug mode)
+__device__ __forceinline__ void store_aug(const GemmEpilogue& e, int m, int j) {
+  // j in [0, ldc - N): column N + j
+  float v = 0.f;
+  if (j == 0) {
+    v = fminf(fmaxf(e.aug_reward[m], -1.f), 1.f);  // core input: always abs_one
+  } else if (j - 1 == static_cast<int>(e.aug_action[m])) {
+    v = 1.f;
+  }
+  e.C[static_cast<int64_t>(m) * e.ldc + e.aug_c0 + j] = v;
+}
+
+__global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) float As[2][BM * PK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * PK];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int Mr = a.M + a.ones_row;
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+
+  // global -> register staging of one K step (one f4 per thread and operand)
+  f4 ra, rb;
+  auto load = [&](int k0) {
+    f4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+    if (!a.ta) {  // A[m][k]: thread = (m, k quad)
+      const int m = m0 + (t >> 2), k = k0 + 4 * (t & 3);
+      if (m < a.M && k < kend)
+        va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(m) * a.lda + k);
+      else if (m == a.M && a.ones_row && k < kend)
+        va = f4{1.f, 1.f, 1.f, 1.f};
+    } else {  // A[k][m]: thread = (k, m quad)
+      const int k = k0 + (t >> 4), m = m0 + 4 * (t & 15);
+      if (k < kend) {
+        if (m + 3 < a.M) {
+          va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(k) * a.lda + m);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (m + q < a.M) va[q] = a.A[static_cast<int64_t>(k) * a.lda + m + q];
+            else if (m + q == a.M && a.ones_row) va[q] = 1.f;
+          }
+        }
+      }
+    }
+    if (!a.tb) {  // B[k][n]: thread = (k, n quad)
+      const int k = k0 + (t >> 4), n = n0 + 4 * (t & 15);
+      if (k < kend && n < a.N)
+        vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(k) * a.ldb + n);
+    } else {  // B[n][k]: thread = (n, k quad)
+      const int n = n0 + (t >> 2), k = k0 + 4 * (t & 3);
+      if (n < a.N && k < kend)
+        vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(n) * a.ldb + k);
+    }
+    ra = va;
+    rb = vb;
+  };
+  auto commit = [&](int buf) {
+    if (!a.ta) {
+      *reinterpret_cast<f4*>(&As[buf][(t >> 2) * PK + 4 * (t & 3)]) = ra;
+    } else {
+      const int k = t >> 4, m = 4 * (t & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[q];
+    }
+    if (!a.tb) {
+      const int k = t >> 4, n = 4 * (t & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Bs[buf][(n + q) * PK + k] = rb[q];
+    } else {
+      *reinterpret_cast<f4*>(&Bs[buf][(t >> 2) * PK + 4 * (t & 3)]) = rb;
+    }
+  };
+
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int arow = (wm * 32 + l32) * PK + 8 * h;
+  const int brow = (wn * 32 + l32) * PK + 8 * h;
+  int buf = 0;
+  if (kbeg < kend) {
+    load(kbeg);
+    commit(0);
+    __syncthreads();
+  }
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
+    if (more) load(k0 + BK);  // in flight under the MFMAs
+    const f4 a0 = *reinterpret_cast<const f4*>(&As[buf][arow]);
+    const f4 a1 = *reinterpret_cast<const f4*>(&As[buf][arow + 4]);
+    const f4 b0 = *reinterpret_cast<const f4*>(&Bs[buf][brow]);
+    const f4 b1 = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc, 0, 0, 0);
+    if (more) {
+      commit(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+
+  // D[i][j]: j = lane & 31, i = (r & 3) + 8 (r >> 2) + 4 h
+  const int n = n0 + wn * 32 + l32;
+  if (a.splits > 1) {
+    float* p = a.part + static_cast<int64_t>(blockIdx.z) * Mr * a.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < Mr && n < a.N) p[static_cast<int64_t>(m) * a.N + n] = acc[r];
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (n >= a.N) continue;
+    if (m < a.M) store_out(a.ep, m, n, acc[r]);
+    else if (m == a.M && a.ones_row) a.ep.colsum[n] += acc[r];
+  }
+  if (a.ep.aug_c0 > 0 && blockIdx.y == 0) {
+    const int naug = a.ep.ldc - a.ep.aug_c0;
+    for (int e = t; e < BM * naug; e += 256) {
+      const int m = m0 + e / naug;
+      if (m < a.M) store_aug(a.ep, m, e % naug);
+    }
+  }
+}
+
+// Fixed-order sum of the split partials + the epilogue.
+__global__ __launch_bounds__(256) void gemm_f32_reduce_kernel(Args a) {
+  const int Mr = a.M + a.ones_row;
+  const int64_t total = static_cast<int64_t>(Mr) * a.N;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < total) {
+    const int m = static_cast<int>(i / a.N), n = static_cast<int>(i - static_cast<int64_t>(m) * a.N);
+    float s = 0.f;
+    for (int z = 0; z < a.splits; ++z) s += a.part[static_cast<int64_t>(z) * total + i];
+    if (m < a.M) store_out(a.ep, m, n, s);
+    else a.ep.colsum[n] += s;
+  }
+  if (a.ep.aug_c0 > 0) {
+    const int naug = a.ep.ldc - a.ep.aug_c0;
+    const int64_t j = i;  // one aug element per thread over the first M*naug threads
+    if (j < static_cast<int64_t>(a.M) * naug)
+      store_aug(a.ep, static_cast<int>(j / naug), static_cast<int>(j % naug));
+  }
+}
+
+}  // namespace
+
+int64_t gemm_f32_part_floats(int M, int N, int K, int ones_row, int splits) {
+  (void)K;
+  return splits > 1 ? static_cast<int64_t>(splits) * (M + ones_row) * N : 0;
+}
+
+int gemm_f32_splits(int M, int N, int K, int ones_row) {
+  const int tiles = ((M + ones_row + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int s = 1;
+  // enough workgroups to fill 256 CUs twice over, each K chunk >= 128
+  while (tiles * s < 512 && K / (2 * s) >= 128 && s < 16) s *= 2;
+  return s;
+}
+
+bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int lda,
+                     int ldb, bool ta, bool tb, bool ones_row, int splits, float* part,
+                     const GemmEpilogue& ep, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return false;
+  if (lda % 4 || ldb % 4 || K % 4) return false;
+  if (ones_row && ep.colsum == nullptr) return false;
+  if (splits > 1 && part == nullptr) return false;
+  Args a{};
+  a.A = A;
+  a.B = B;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb;
+  a.ta = ta; a.tb = tb; a.ones_row = ones_row;
+  a.splits = std::max(1, splits);
+  a.kchunk = ((K + a.splits - 1) / a.splits + BK - 1) / BK * BK;
+  a.part = part;
+  a.ep = ep;
+  const int Mr = M + (ones_row ? 1 : 0);
+  dim3 grid((Mr + BM - 1) / BM, (N + BN - 1) / BN, a.splits);
+  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, stream, a);
+  if (a.splits > 1) {
+    const int64_t total = static_cast<int64_t>(Mr) * N;
+    const int64_t aug = ep.aug_c0 > 0 ? static_cast<int64_t>(M) * (ep.ldc - ep.aug_c0) : 0;
+    const int64_t work = std::max(total, aug);
+    hipLaunchKernelGGL(gemm_f32_reduce_kernel, dim3(static_cast<unsigned>((work + 255) / 256)),
+                       dim3(256), 0, stream, a);
+  }
+  return true;
+}
+
+}  // namespace sa

@@ -6,6 +6,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include "kernels/launchers.h"
+#include "kernels/gemm_f32.h"
 
 namespace {
 
@@ -190,12 +191,84 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
   return {logits, baseline, action};
 }
 
+
+// C[:, :N] (+)= op(A) op(B) with the fused epilogue of kernels/gemm_f32.h.
+// A / B / C / mask may be row slices of wider row-major matrices (row stride
+// = stride(0), unit column stride).  op(A) = A^T when ta (A is [K, M]),
+// op(B) = B^T when tb (B is [N, K]).  colsum: ones-row column sums of op(B)
+// accumulated into it; aug_*: the core-input columns [clip(r), one_hot(a),
+// 0...] written at C[:, aug_c0:] (aug_c0 = N).
+void gemm_f32(at::Tensor A, at::Tensor B, bool ta, bool tb, at::Tensor C,
+              c10::optional<at::Tensor> bias, c10::optional<at::Tensor> mask, bool relu,
+              bool accumulate, c10::optional<at::Tensor> colsum,
+              c10::optional<at::Tensor> aug_reward, c10::optional<at::Tensor> aug_action) {
+  auto rm = [](const at::Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 && t.scalar_type() == at::kFloat,
+                n, " must be a row-major float32 GPU matrix");
+    TORCH_CHECK(t.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n,
+                " rows must be 16-byte aligned");
+  };
+  rm(A, "A"); rm(B, "B"); rm(C, "C");
+  const int64_t M = ta ? A.size(1) : A.size(0), K = ta ? A.size(0) : A.size(1);
+  const int64_t Kb = tb ? B.size(1) : B.size(0), N = tb ? B.size(0) : B.size(1);
+  TORCH_CHECK(K == Kb, "gemm_f32: inner dimensions ", K, " vs ", Kb);
+  TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "gemm_f32: C must be [M, >= N]");
+  TORCH_CHECK(K % 4 == 0, "gemm_f32: K must be a multiple of 4");
+  sa::GemmEpilogue ep{};
+  ep.C = C.data_ptr<float>();
+  ep.ldc = C.stride(0);
+  if (bias.has_value() && bias->defined()) {
+    LB_CHECK(*bias); LB_F32(*bias);
+    TORCH_CHECK(bias->numel() == N, "bias size");
+    ep.bias = bias->data_ptr<float>();
+  }
+  if (mask.has_value() && mask->defined()) {
+    rm(*mask, "mask");
+    TORCH_CHECK(mask->size(0) == M && mask->size(1) >= N, "mask shape");
+    ep.mask = mask->data_ptr<float>();
+    ep.ldm = mask->stride(0);
+  }
+  ep.relu = relu;
+  ep.accumulate = accumulate;
+  const bool ones = colsum.has_value() && colsum->defined();
+  if (ones) {
+    LB_CHECK(*colsum); LB_F32(*colsum);
+    TORCH_CHECK(colsum->numel() == N, "colsum size");
+    ep.colsum = colsum->data_ptr<float>();
+  }
+  if (aug_reward.has_value() && aug_reward->defined()) {
+    TORCH_CHECK(aug_action.has_value() && aug_action->defined(), "aug needs actions");
+    LB_CHECK(*aug_reward); LB_F32(*aug_reward); LB_CHECK(*aug_action);
+    TORCH_CHECK(aug_action->scalar_type() == at::kLong, "actions must be int64");
+    TORCH_CHECK(aug_reward->numel() == M && aug_action->numel() == M, "aug rows");
+    TORCH_CHECK(C.size(1) > N && C.size(1) == C.stride(0), "aug: C must be [M, ld > N]");
+    ep.aug_reward = aug_reward->data_ptr<float>();
+    ep.aug_action = aug_action->data_ptr<int64_t>();
+    ep.aug_c0 = N;
+  }
+  const c10::DeviceGuard guard(A.device());
+  const int splits = sa::gemm_f32_splits(M, N, K, ones);
+  at::Tensor part;
+  if (splits > 1)
+    part = at::empty({sa::gemm_f32_part_floats(M, N, K, ones, splits)}, A.options());
+  TORCH_CHECK(sa::gemm_f32_launch(A.data_ptr<float>(), B.data_ptr<float>(), M, N, K,
+                                  A.stride(0), B.stride(0), ta, tb, ones, splits,
+                                  splits > 1 ? part.data_ptr<float>() : nullptr, ep, stream()),
+              "gemm_f32: launch refused");
+}
+
 }  // namespace
 
 void register_learner_ops(pybind11::module& m) {
   m.def("learner_head_fwd", &learner_head_fwd);
   m.def("learner_head_bwd", &learner_head_bwd);
   m.def("core_aug_fwd", &core_aug_fwd);
+  m.def("gemm_f32", &gemm_f32, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("ta"),
+        pybind11::arg("tb"), pybind11::arg("C"), pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("relu") = false,
+        pybind11::arg("accumulate") = false, pybind11::arg("colsum") = pybind11::none(),
+        pybind11::arg("aug_reward") = pybind11::none(),
+        pybind11::arg("aug_action") = pybind11::none());
   m.def("colsum_f32_", &colsum_f32_);
   m.def("relu_bwd_colsum_", &relu_bwd_colsum_, pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("out") = pybind11::none());

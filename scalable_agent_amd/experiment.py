@@ -601,6 +601,8 @@ def train(flags):
   last_log_frames = int(learner.frames.item())
   reported_skips = 0
   steps = 0
+  checks_ok = 0
+  first_loss = float('nan')
   use_graph = flags.use_hip_graph and device.type == 'cuda'
   staging = dev_stage = copied = None
   host_ms, loop_ms = [], []
@@ -620,10 +622,13 @@ def train(flags):
         timer.add_wait(wait)
         steps += 1
         if (world > 1 and flags.consistency_check_steps and
-            steps % flags.consistency_check_steps == 0 and
-            not parallel.param_checksum_consistent(learner.flat.params)):
-          raise RuntimeError('data-parallel replicas diverged at step %d' %
-                             steps)
+            steps % flags.consistency_check_steps == 0):
+          if not parallel.param_checksum_consistent(learner.flat.params):
+            raise RuntimeError('data-parallel replicas diverged at step %d' %
+                               steps)
+          checks_ok += 1
+        if steps == 1:
+          first_loss = float(loss)
         if infer is not None or server is not None:
           model.publish(learner.flat.params)
         elif shared_w is not None:
@@ -691,10 +696,13 @@ def train(flags):
             loss = learner.step(data)
         steps += 1
         if (world > 1 and flags.consistency_check_steps and
-            steps % flags.consistency_check_steps == 0 and
-            not parallel.param_checksum_consistent(learner.flat.params)):
-          raise RuntimeError('data-parallel replicas diverged at step %d' %
-                             steps)
+            steps % flags.consistency_check_steps == 0):
+          if not parallel.param_checksum_consistent(learner.flat.params):
+            raise RuntimeError('data-parallel replicas diverged at step %d' %
+                               steps)
+          checks_ok += 1
+        if steps == 1:
+          first_loss = float(loss)
         if infer is not None:
           model.publish(learner.flat.params)
         elif transport is not None:
@@ -786,6 +794,13 @@ def train(flags):
     if writer is not None:
       writer.close()
     parallel.cleanup()
+  # per-rank summary (data-parallel runs: every rank trains on its OWN
+  # actors' unrolls; the replicas stay identical through the all-reduce)
+  log.info('rank %d/%d: %d learner steps, %d env frames (all ranks), %d '
+           'episodes from this rank\'s actors, %d replica-consistency checks '
+           'passed, first loss %.6f', rank, world, steps,
+           int(learner.frames.item()), episode_logger.episodes, checks_ok,
+           first_loss)
   return learner
 
 

@@ -387,10 +387,12 @@ class Agent(nn.Module):
   # ------------------------------------------------------------------ API
   def fused_core_ready(self, instr=None):
     """True when the HIP learner path (fused torso-FC/core-input/LSTM op,
-    fused heads+V-trace loss) applies: HIP backend, HIP bf16 torso; the
-    instruction encoding (language LSTM) joins the fused core input."""
+    fused heads+V-trace loss) applies: HIP backend and a HIP torso (bf16
+    kernels -> the bf16-operand core, exact-fp32 kernels -> the exact-fp32
+    core of ops/core.py); the instruction encoding (language LSTM) joins the
+    fused core input."""
     del instr
-    return self.backend == 'hip' and _bf16_torso_ready(self)
+    return self.backend == 'hip' and _hip_torso_ready(self)
 
   def unroll_core(self, actions, env_outputs, core_state):
     """Everything of `unroll` up to the LSTM output: -> (core_out [T,B,256],

@@ -1,4 +1,5 @@
-"""Fused torso-FC -> core input -> LSTM-256 core (HIP backend learner path).
+"""Fused torso-FC -> core input -> LSTM-256 core (HIP backend learner path):
+bf16-operand (_CoreLSTM, below) and exact-fp32 (_CoreLSTMF32) variants.
 
 Reference: experiment.py:185-198 (Linear(256)+ReLU on the flattened conv
 features; concat [torso, clip(reward, -1, 1), one_hot(last_action),
@@ -136,18 +137,114 @@ class _CoreLSTM(torch.autograd.Function):
             d_instr)
 
 
+class _CoreLSTMF32(torch.autograd.Function):
+  """Reference-precision (fp32) variant: every product is the exact-fp32
+  MFMA GEMM of kernels/gemm_f32.hip with its fused epilogue, the recurrence
+  the exact fp32 LSTM kernels (never the bf16 gang).
+
+  Forward (3 launches + the recurrence):
+    h_aug = [relu(feats W_fc + b_fc), clip(r), one_hot(a), 0...]   ONE GEMM
+            (bias + ReLU + the core-input columns in its epilogue)
+    xw    = h_aug W_x[:K] + b_lstm                                  GEMM
+  Backward:
+    dh     = (dG W_x[:256]^T) * (h > 0)                             GEMM + mask
+    dfeats = dh W_fc^T                                              GEMM
+    dW_h  += hpm^T dG                                               GEMM (split-K)
+    dW_x  += h_aug^T dG ; db_lstm += 1^T dG                         ONE GEMM (ones row)
+    dW_fc += feats^T dh ; db_fc   += 1^T dh                         ONE GEMM (ones row)
+  Weight-gradient reductions are split-K partial slabs summed in a fixed
+  order (deterministic).
+  """
+
+  @staticmethod
+  def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
+              done_u8, num_actions, instr_enc):
+    C = ext()
+    T, B = done_u8.shape
+    N = T * B
+    f_in = CORE + 1 + num_actions + 64
+    c_instr = CORE + 1 + num_actions
+    assert kernel.shape[0] == f_in + CORE
+    if instr_enc is None:
+      K = ld = aug_width(num_actions)
+    else:
+      # instruction columns join; K padded to 16 with zero columns (the
+      # matching kernel rows - W_h's first rows - meet zeros: no effect)
+      K = ld = (f_in + 15) // 16 * 16
+    h_aug = torch.empty(N, ld, dtype=torch.float32, device=feats.device)
+    C.gemm_f32(feats, w_fc, False, False, h_aug, bias=b_fc, relu=True,
+               aug_reward=rewards, aug_action=actions)
+    if instr_enc is not None:
+      h_aug[:, c_instr:f_in].copy_(instr_enc)
+    xw = torch.empty(N, 4 * CORE, dtype=torch.float32, device=feats.device)
+    C.gemm_f32(h_aug, kernel[:K], False, False, xw, bias=bias)
+    mode = C.lstm_mode(CORE, B, T, True)  # exact: never the bf16 gang
+    hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
+                                       kernel[f_in:], mode)
+    ctx.mode = mode
+    ctx.save_for_backward(feats, w_fc, b_fc, kernel, bias, h_aug, wt, acts, cs,
+                          c0, hpm, done_u8)
+    ctx.f_in, ctx.K, ctx.c_instr = f_in, K, c_instr
+    ctx.has_instr = instr_enc is not None
+    return hs, cs[-1]
+
+  @staticmethod
+  def backward(ctx, dhs, dc_last):
+    C = ext()
+    (feats, w_fc, b_fc, kernel, bias, h_aug, wt, acts, cs, c0, hpm,
+     done_u8) = ctx.saved_tensors
+    f_in, K = ctx.f_in, ctx.K
+    T, B, G = acts.shape
+    N = T * B
+    if dhs is None:
+      dhs = torch.zeros(T, B, CORE, dtype=acts.dtype, device=acts.device)
+    if dc_last is not None:
+      dc_last = dc_last.contiguous()
+    dg, dc0, _ = C.lstm_bwd(dhs.contiguous(), done_u8, wt, acts, cs, c0,
+                            dc_last, False, ctx.mode)
+    (gwfc, gbfc, gk, gb), direct = grad_sink.sinks([w_fc, b_fc, kernel, bias])
+    dg2 = dg.view(N, G)
+    dev = dg.device
+    # critical path first: dfeats feeds the conv-torso backward
+    dh = torch.empty(N, CORE, dtype=torch.float32, device=dev)
+    C.gemm_f32(dg2, kernel[:CORE], False, True, dh, mask=h_aug[:, :CORE])
+    dfeats = torch.empty_like(feats)
+    C.gemm_f32(dh, w_fc, False, True, dfeats)
+    C.gemm_f32(hpm.view(N, CORE), dg2, True, False, gk[f_in:],
+               accumulate=True)                                     # W_h
+    C.gemm_f32(h_aug[:, :K], dg2, True, False, gk[:K], accumulate=True,
+               colsum=gb)                                           # W_x, b_lstm
+    C.gemm_f32(feats, dh, True, False, gwfc, accumulate=True,
+               colsum=gbfc)                                         # W_fc, b_fc
+    dh0 = None
+    if ctx.needs_input_grad[8]:
+      keep0 = (done_u8[0] == 0).to(torch.float32).unsqueeze(-1)
+      dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
+    if not ctx.needs_input_grad[7]:
+      dc0 = None
+    d_instr = None
+    if ctx.has_instr and ctx.needs_input_grad[11]:
+      d_instr = torch.empty(N, 64, dtype=torch.float32, device=dev)
+      C.gemm_f32(dg2, kernel[ctx.c_instr:f_in], False, True, d_instr)
+    g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
+    return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
+            d_instr)
+
+
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
               num_actions, instr_enc=None):
-  """feats bf16 [T*B, F] (ReLU'd torso output), rewards [T*B] f32, actions
-  [T*B] (last actions), done [T,B] bool, state (c, h) [B,256], instr_enc
-  None or the language-LSTM output [T*B, 64] (gradients flow back into it)
+  """feats [T*B, F] (ReLU'd torso output: bf16 -> the bf16-operand path,
+  fp32 -> the exact-fp32 path), rewards [T*B] f32, actions [T*B] (last
+  actions), done [T,B] bool, state (c, h) [B,256], instr_enc None or the
+  language-LSTM output [T*B, 64] (gradients flow back into it)
   -> (hs [T,B,256] f32, (c_T, h_T))."""
   c0, h0 = state
-  hs, c_last = _CoreLSTM.apply(
+  fn = _CoreLSTMF32 if feats.dtype == torch.float32 else _CoreLSTM
+  hs, c_last = fn.apply(
       feats.contiguous(), w_fc, b_fc, kernel, bias,
       rewards.reshape(-1).to(torch.float32).contiguous(),
       actions.reshape(-1).to(torch.int64).contiguous(),
       c0.float().contiguous(), h0.float().contiguous(),
       done.to(torch.uint8).contiguous(), int(num_actions),
-      None if instr_enc is None else instr_enc.contiguous())
+      None if instr_enc is None else instr_enc.float().contiguous())
   return hs, (c_last, hs[-1])

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Winograd fp32 conv (csrc/kernels/conv_wino.hip) vs a float64 oracle at
+learner-like batch sizes, every deep-torso 3x3/1 shape, forward (+ReLU-in,
+residual, ReLU-out) and data gradient (+mask, skip add).  Prints the max
+error relative to the output scale.  Usage: python tools/wino_check.py [N]"""
+import sys
+import torch
+
+sys.path.insert(0, '.')
+from scalable_agent_amd import ops  # noqa: E402
+from scalable_agent_amd.models import layers  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 37
+C = ops.ext()
+dev = torch.device('cuda')
+g = torch.Generator().manual_seed(0)
+worst = 0.0
+for (H, W, Ci, Co) in [(36, 48, 16, 16), (36, 48, 16, 32), (18, 24, 32, 32),
+                       (9, 12, 32, 32), (11, 11, 32, 32), (36, 48, 32, 16)]:
+  x = torch.randn(N, H, W, Ci, generator=g)
+  w = torch.randn(3, 3, Ci, Co, generator=g) / (9 * Ci) ** 0.5
+  b = torch.randn(Co, generator=g) * 0.1
+  add = torch.randn(N, H, W, Co, generator=g)
+  ref = layers.conv2d_same_nhwc(x.double().clamp(min=0), w.double(), b.double(), 1)
+  ref = (ref + add.double()).clamp(min=0)
+  y = C.cf32_conv_fwd(x.to(dev), w.to(dev), b.to(dev), 1, 1, 1, H, W,
+                      relu_in=True, add=add.to(dev), relu_out=True)
+  e1 = ((y.double().cpu() - ref).abs().max() / ref.abs().max()).item()
+  dy = torch.randn(N, H, W, Co, generator=g)
+  mask = torch.randn(N, H, W, Ci, generator=g)
+  sk = torch.randn(N, H, W, Ci, generator=g)
+  x64 = x.double().requires_grad_(True)
+  yy = layers.conv2d_same_nhwc(x64, w.double(), None, 1)
+  (dref,) = torch.autograd.grad(yy, x64, dy.double())
+  dref = torch.where(mask.double() > 0, dref, torch.zeros_like(dref)) + sk.double()
+  dx = C.cf32_conv_dgrad(dy.to(dev), w.to(dev), 1, 1, 1, H, W, mask=mask.to(dev),
+                         add=sk.to(dev))
+  e2 = ((dx.double().cpu() - dref).abs().max() / dref.abs().max()).item()
+  worst = max(worst, e1, e2)
+  print('%2dx%2d %2d->%2d  fwd rel %.2e  dgrad rel %.2e' % (H, W, Ci, Co, e1, e2),
+        flush=True)
+print('worst %.2e %s' % (worst, 'OK' if worst <= 1e-5 else 'FAIL'))
+sys.exit(0 if worst <= 1e-5 else 1)
