@@ -135,15 +135,38 @@ def measure(args, dtype, device, backend, rank, world):
   t_enq = time.perf_counter() - t0  # host time to enqueue the K steps
   sync()
   dt = time.perf_counter() - t0
+  dist_extra = {}
   if world > 1:
-    t = torch.tensor([dt], dtype=torch.float64, device=device)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    # per-rank step time (the reported dt is the max), the all-reduce window
+    # of the last step (begin of the early bucket -> end of the last one, so
+    # it spans the overlapped torso backward) and a standalone all-reduce of
+    # the whole flat gradient buffer (the bare collective's cost)
+    per = [torch.zeros(1, dtype=torch.float64, device=device)
+           for _ in range(world)]
+    torch.distributed.all_gather(
+        per, torch.tensor([dt], dtype=torch.float64, device=device))
+    dt = max(float(x.item()) for x in per)
+    dist_extra['per_rank_ms_per_step'] = [
+        round(1000 * float(x.item()) / args.steps, 3) for x in per]
+    if learner.grad_sync is not None:
+      dist_extra['allreduce_window_ms'] = round(
+          1000 * learner.grad_sync.last_time_s, 3)
+      g = learner.flat.grads
+      reps = 10
+      sync()
+      t1 = time.perf_counter()
+      for _ in range(reps):
+        torch.distributed.all_reduce(g)
+      sync()
+      dist_extra['allreduce_ms_standalone'] = round(
+          1000 * (time.perf_counter() - t1) / reps, 3)
+      dist_extra['allreduce_mbytes'] = round(g.numel() * 4 / 1e6, 2)
   res = {
       'dt': dt, 'loss_finite': bool(torch.isfinite(loss).item()),
       'enqueue_s': t_enq, 'frames_per_step': learner.frames_per_step,
       'health': learner.health(), 'torso': torso_precision(agent),
       'hip_graph': use_graph, 'h2d_prefetch': not skip_h2d,
+      'dist_extra': dist_extra,
   }
   del learner, agent, graphs
   gc.collect()
@@ -178,6 +201,12 @@ def main():
                   help='time chunks of the torso || LSTM pipeline (1 = off)')
   args = ap.parse_args()
 
+  if args.device in ('auto', 'cuda') or args.device.startswith('cuda:'):
+    if torch.cuda.device_count() > 0:  # does not initialise the GPU
+      # this rank's host side (pinned staging, feeder) on its GPU's NUMA
+      # node, before any pinned allocation (sysfs only; no-op if unknown)
+      parallel.pin_to_gpu_numa(parallel.world_info()[2] %
+                               torch.cuda.device_count())
   rank, world, local = parallel.init_distributed()
   if args.gpus != world:
     raise SystemExit(
@@ -228,7 +257,7 @@ def main():
            'host_enqueue_ms_per_step': round(
                1000 * main_res['enqueue_s'] / args.steps, 3),
            'h2d_prefetch': main_res['h2d_prefetch'],
-           'dist': dist_info,
+           'dist': dict(dist_info, **main_res['dist_extra']),
            'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
                            'frames/s (BASELINE.md B), fp32 P100'}
     if extra is not None:

@@ -83,6 +83,15 @@ struct WgradArgs {
 // shape is not covered.  SA_F32_WINO=0 disables it (direct implicit GEMM).
 bool wino_enabled();
 bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
+// Winograd weight gradient (3x3/1 SAME, 16/32 channels; SA_F32_WINO_WG=0
+// disables): per-workgroup partials in the wgrad slot layout of `ws`, then
+// the same fixed-order slot reduction as the direct kernel.
+bool wino_wgrad_enabled();
+bool wino_wgrad_launch(const WgradArgs& a, float* ws, hipStream_t s);
+// Fixed-order sum of G slot partials [G][rows16][Cout] (rows tap*Cin + ci,
+// row 9*Cin = bias) accumulated into dW (HWIO 3x3) / db.
+void wgrad_reduce_slots(const float* part, int G, int rows16, int Cout, int Cin, float* dw,
+                        float* db, hipStream_t s);
 
 // Returns false (and launches nothing) when no instance matches the shape;
 // the bindings turn that into an error naming the shape.

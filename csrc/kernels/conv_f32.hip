@@ -1382,6 +1382,11 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
 
 }  // namespace
 
+void wgrad_reduce_slots(const float* part, int G, int rows16, int Cout, int Cin, float* dw,
+                        float* db, hipStream_t s) {
+  wgrad_reduce(part, G, 1, rows16, Cout, Cin, 9 * Cin, Cin, Cout, dw, db, s);
+}
+
 // Scatter-form stage-head wgrad from (dP, argmax) (pool_wgrad_kernel): on
 // unless SA_F32_POOL_SCATTER=0 (then the dense-gather MFMA wgrad runs).
 static bool pool_scatter_on() {
@@ -1476,6 +1481,8 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
 }
 
 bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStream_t s) {
+  if (K == 3 && S == 1 && src == kSrcF32 && wino_wgrad_enabled() && wino_wgrad_launch(a, ws, s))
+    return true;
   const int cinp = src == kSrcU8 ? 4 : a.Cin;
   if (src == kSrcU8 && (a.Cin < 1 || a.Cin > 4)) return false;
   if (src == kSrcF32 && a.Cin % 4 != 0) return false;

@@ -419,6 +419,379 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   return true;
 }
 
+
+// ------------------------------------------------------------ weight grad
+// Winograd F(2x2, 3x3) weight gradient.  With Z = A dY A^T (4x4 per 2x2 dY
+// tile) and V = B^T d B (the forward's input transform),
+//   dL/dU[xi][ci][co] = sum_tiles V[xi][tile][ci] Z[xi][tile][co]
+//   dW[ci][co] = G^T (dL/dU) G,  db[co] = sum dY[co]
+// (U = G g G^T is linear in g).  The 16 tile reductions are MFMA GEMMs with
+// k = tile: A[i = ci][k] = V, B[k][j = co] = Z; lane (c16, g) computes V for
+// its input channel and Z for its output channel of tile g, from the input
+// and dY rows of the range staged in LDS.  Waves own xi rows (XR of the 4)
+// and split the range's k-steps (4 tiles each) when they own all of them.
+// Each workgroup finishes with G^T P G of its partial sums and writes them in
+// the direct kernel's wgrad slot layout; the fixed-order slot reduction of
+// conv_f32.hip sums the slots (deterministic).
+struct WinoWgArgs {
+  const float* x;   // [N, H, W, CIN]
+  const float* dy;  // [N, H, W, COUT]
+  float* part;      // slots [G][rows16][COUT]
+  int N, H, W;
+  int TY, TX, NT, nranges, maxrows, rows16;
+  float rTX, rTY, rWl, rWd;
+  int relu_in;
+};
+
+// input patch rows used by B^T rows a = XG*XR .. XG*XR + XR - 1
+// (a = 0: d0 - d2, 1: d1 + d2, 2: d2 - d1, 3: d1 - d3)
+__host__ __device__ constexpr bool wg_need_row(int XR, int XG, int dy) {
+  return XR == 4 ? true
+       : XR == 2 ? (XG == 0 ? dy <= 2 : dy >= 1)
+       : (XG == 0 ? (dy == 0 || dy == 2)
+          : XG == 3 ? (dy == 1 || dy == 3) : (dy == 1 || dy == 2));
+}
+
+template <int CIN, int COUT, int XR, int RT, int MAXCX, int MAXCD>
+__global__ __launch_bounds__(256, 1) void wino_wgrad_kernel(WinoWgArgs a) {
+  constexpr int NW = 4, NTH = 256;
+  constexpr int PX = CIN + 8, PD = COUT + 8;  // 2*pitch = 16 mod 32 words
+  constexpr int C4X = CIN / 4, C4D = COUT / 4;
+  constexpr int LCX = C4X == 4 ? 2 : 3, LCD = C4D == 4 ? 2 : 3;
+  constexpr int NBI = CIN / 16, NBO = COUT / 16;
+  constexpr int NXG = 4 / XR;   // xi-row groups
+  constexpr int KS = NW / NXG;  // waves sharing one group's k-steps
+  constexpr int NSTEP = RT / 4;
+  static_assert(XR == 1 || XR == 2 || XR == 4, "XR");
+  static_assert(MAXCX <= 32 && MAXCD <= 32, "stager masks");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Wl = 2 * a.TX + 2, Wd = 2 * a.TX;
+  float* x_s = smem;                          // [maxrows][Wl][PX]
+  float* d_s = x_s + a.maxrows * Wl * PX;     // [maxrows][Wd][PD] (same rows)
+  int* tab_s = reinterpret_cast<int*>(d_s + a.maxrows * Wd * PD);  // [maxrows]
+  int* tile_s = tab_s + a.maxrows;                                  // [RT][2]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int xg = wave / KS, kq = wave - (wave / KS) * KS;
+
+  int r = blockIdx.x;
+  if (r >= a.nranges) return;
+
+  // ---- staging slots (see wino_conv_kernel): X with a zero halo, dY on the
+  // same LDS rows (the halo rows it does not need are staged and unused)
+  int sx_L[MAXCX], sx_o[MAXCX], sd_L[MAXCD], sd_o[MAXCD];
+#pragma unroll
+  for (int k = 0; k < MAXCX; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4X - 1), pix = e >> LCX;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sx_L[k] = L < a.maxrows ? L : -1;
+    sx_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * CIN + 4 * ch : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXCD; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4D - 1), pix = e >> LCD;
+    const int L = pix / Wd, col = pix - L * Wd;
+    sd_L[k] = L < a.maxrows ? L : -1;
+    sd_o[k] = col < a.W ? col * COUT + 4 * ch : -1;
+  }
+  // row table: global pixel index (n*H + y)*W of LDS row L, or -1
+  auto row_of = [&](const RangeGeom& gm, int L) {
+    int v = -1;
+    if (L < gm.rows) {
+      const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
+      const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+      const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
+      if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W;
+    }
+    return v;
+  };
+  auto geom = [&](int rr) {
+    RangeGeom g2;
+    WinoArgs t{};
+    t.NT = a.NT; t.TX = a.TX; t.TY = a.TY; t.rTX = a.rTX; t.rTY = a.rTY;
+    g2 = range_geom(t, rr, RT);
+    return g2;
+  };
+  f4 stx[MAXCX], std_[MAXCD];
+  uint32_t okx = 0, okd = 0;
+  auto prefetch = [&]() {  // reads tab_s
+    okx = 0;
+    okd = 0;
+#pragma unroll
+    for (int k = 0; k < MAXCX; ++k) {
+      const int rb = sx_L[k] >= 0 ? tab_s[sx_L[k]] : -1;
+      const bool in = rb >= 0 && sx_o[k] >= 0;
+      stx[k] = *reinterpret_cast<const f4*>(a.x + (in ? rb * CIN + sx_o[k] : 0));
+      okx |= static_cast<uint32_t>(in) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < MAXCD; ++k) {
+      const int rb = sd_L[k] >= 0 ? tab_s[sd_L[k]] : -1;
+      const bool in = rb >= 0 && sd_o[k] >= 0;
+      std_[k] = *reinterpret_cast<const f4*>(a.dy + (in ? rb * COUT + sd_o[k] : 0));
+      okd |= static_cast<uint32_t>(in) << k;
+    }
+  };
+  {
+    const RangeGeom gm = geom(r);
+    if (threadIdx.x < a.maxrows) tab_s[threadIdx.x] = row_of(gm, threadIdx.x);
+  }
+  __syncthreads();
+  prefetch();
+
+  f4 acc[XR][4][NBI][NBO];
+#pragma unroll
+  for (int i = 0; i < XR; ++i)
+#pragma unroll
+    for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+      for (int b = 0; b < NBI; ++b)
+#pragma unroll
+        for (int b2 = 0; b2 < NBO; ++b2) acc[i][bc][b][b2] = f4{0.f, 0.f, 0.f, 0.f};
+  float dbacc[NBO];
+#pragma unroll
+  for (int b2 = 0; b2 < NBO; ++b2) dbacc[b2] = 0.f;
+
+  const int rsx = Wl * PX, rsd = Wd * PD;
+  for (;;) {
+    __syncthreads();  // the previous range's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < MAXCX; ++k) {
+      if (sx_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        f4 v = stx[k];
+        const bool in = (okx >> k) & 1u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float t = in ? v[q] : 0.f;
+          v[q] = a.relu_in ? fmaxf(t, 0.f) : t;
+        }
+        *reinterpret_cast<f4*>(x_s + (e >> LCX) * PX + 4 * (e & (C4X - 1))) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXCD; ++k) {
+      if (sd_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        f4 v = std_[k];
+        const bool in = (okd >> k) & 1u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = in ? v[q] : 0.f;
+        *reinterpret_cast<f4*>(d_s + (e >> LCD) * PD + 4 * (e & (C4D - 1))) = v;
+      }
+    }
+    const int cur = r;
+    r += gridDim.x;
+    {
+      // tile table of the current range, row table of the next one
+      const RangeGeom gm = geom(cur);
+      for (int tt = threadIdx.x; tt < RT; tt += NTH) {
+        const int t = gm.t0 + tt;
+        int xb = -1, db = -1;
+        if (t < gm.t1) {
+          const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
+          const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+          const int p = n - gm.n0;
+          const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+          const int base = offp + 2 * (ty - (p == 0 ? gm.tya0 : 0));
+          xb = (base * Wl + 2 * tx) * PX;
+          db = ((base + 1) * Wd + 2 * tx) * PD;
+        }
+        tile_s[2 * tt] = xb;
+        tile_s[2 * tt + 1] = db;
+      }
+      if (r < a.nranges) {
+        const RangeGeom gn = geom(r);
+        if (threadIdx.x < a.maxrows) tab_s[threadIdx.x] = row_of(gn, threadIdx.x);
+      }
+    }
+    __syncthreads();
+    if (r < a.nranges) prefetch();  // in flight under the MFMAs below
+
+    auto run = [&](auto XGc) {
+      constexpr int XG = decltype(XGc)::value;
+      for (int st = kq; st < NSTEP; st += KS) {
+        const int tt = 4 * st + g;
+        int xb = tile_s[2 * tt], db = tile_s[2 * tt + 1];
+        const bool valid = xb >= 0;
+        xb = valid ? xb : 0;
+        db = valid ? db : 0;
+        // Z rows (this group's xi rows) for every output-channel block
+        f4 zf[XR][NBO];  // zf[i][b2][bcol] = Z[a = XG*XR + i][bcol] for co
+#pragma unroll
+        for (int b2 = 0; b2 < NBO; ++b2) {
+          const float* dp = d_s + db + 16 * b2 + c16;
+          float y00 = dp[0], y01 = dp[PD], y10 = dp[rsd], y11 = dp[rsd + PD];
+          if (!valid) y00 = y01 = y10 = y11 = 0.f;
+          if constexpr (XG == 0) dbacc[b2] += (y00 + y01) + (y10 + y11);
+#pragma unroll
+          for (int i = 0; i < XR; ++i) {
+            const int ar = XG * XR + i;
+            float r0, r1;
+            if (ar == 0) { r0 = y00; r1 = y01; }
+            else if (ar == 1) { r0 = y00 + y10; r1 = y01 + y11; }
+            else if (ar == 2) { r0 = y00 - y10; r1 = y01 - y11; }
+            else { r0 = -y10; r1 = -y11; }
+            zf[i][b2] = f4{r0, r0 + r1, r0 - r1, -r1};
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < NBI; ++b) {
+          const float* xp = x_s + xb + 16 * b + c16;
+          // patch rows this group needs (B^T row a combines two rows)
+          float d[4][4];
+#pragma unroll
+          for (int dy = 0; dy < 4; ++dy) {
+            if (wg_need_row(XR, XG, dy)) {
+#pragma unroll
+              for (int dx = 0; dx < 4; ++dx) d[dy][dx] = xp[dy * rsx + dx * PX];
+            } else {
+#pragma unroll
+              for (int dx = 0; dx < 4; ++dx) d[dy][dx] = 0.f;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < XR; ++i) {
+            const int ar = XG * XR + i;
+            float sq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (ar == 0) sq[q] = d[0][q] - d[2][q];
+              else if (ar == 1) sq[q] = d[1][q] + d[2][q];
+              else if (ar == 2) sq[q] = d[2][q] - d[1][q];
+              else sq[q] = d[1][q] - d[3][q];
+            }
+            float V[4] = {sq[0] - sq[2], sq[1] + sq[2], sq[2] - sq[1], sq[1] - sq[3]};
+            if (!valid) V[0] = V[1] = V[2] = V[3] = 0.f;
+#pragma unroll
+            for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+              for (int b2 = 0; b2 < NBO; ++b2)
+                acc[i][bc][b][b2] = mfma4(V[bc], zf[i][b2][bc], acc[i][bc][b][b2]);
+          }
+        }
+      }
+    };
+    if constexpr (NXG == 1) {
+      run(std::integral_constant<int, 0>{});
+    } else if constexpr (NXG == 2) {
+      if (xg == 0) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, 1>{});
+    } else {
+      if (xg == 0) run(std::integral_constant<int, 0>{});
+      else if (xg == 1) run(std::integral_constant<int, 1>{});
+      else if (xg == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 3>{});
+    }
+    if (r >= a.nranges) break;
+  }
+
+  // ---- workgroup epilogue: P = sum over the KS waves of a group (fixed
+  // order) in LDS, then dW = G^T P G per (ci, co) into this slot
+  __syncthreads();
+  float* P = smem;                      // [16][CIN][COUT]
+  float* dB = smem + 16 * CIN * COUT;   // [COUT]
+  for (int k = 0; k < KS; ++k) {
+    if (kq == k) {
+#pragma unroll
+      for (int i = 0; i < XR; ++i)
+#pragma unroll
+        for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+          for (int b = 0; b < NBI; ++b)
+#pragma unroll
+            for (int b2 = 0; b2 < NBO; ++b2)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int xi = 4 * (xg * XR + i) + bc;
+                const int ci = 16 * b + 4 * g + q, co = 16 * b2 + c16;
+                float* pp = P + (xi * CIN + ci) * COUT + co;
+                *pp = (k == 0 ? 0.f : *pp) + acc[i][bc][b][b2][q];
+              }
+      if (xg == 0) {
+#pragma unroll
+        for (int b2 = 0; b2 < NBO; ++b2) {
+          float v = dbacc[b2];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          if (g == 0) dB[16 * b2 + c16] = (k == 0 ? 0.f : dB[16 * b2 + c16]) + v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * COUT;
+  for (int e = threadIdx.x; e < CIN * COUT; e += NTH) {
+    const int ci = e / COUT, co = e - (e / COUT) * COUT;
+    float pm[4][4];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) pm[xi >> 2][xi & 3] = P[(xi * CIN + ci) * COUT + co];
+    float t[3][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      t[0][b] = pm[0][b] + 0.5f * (pm[1][b] + pm[2][b]);
+      t[1][b] = 0.5f * (pm[1][b] - pm[2][b]);
+      t[2][b] = 0.5f * (pm[1][b] + pm[2][b]) + pm[3][b];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float w0 = t[i][0] + 0.5f * (t[i][1] + t[i][2]);
+      const float w1 = 0.5f * (t[i][1] - t[i][2]);
+      const float w2 = 0.5f * (t[i][1] + t[i][2]) + t[i][3];
+      slot[((3 * i + 0) * CIN + ci) * COUT + co] = w0;
+      slot[((3 * i + 1) * CIN + ci) * COUT + co] = w1;
+      slot[((3 * i + 2) * CIN + ci) * COUT + co] = w2;
+    }
+  }
+  for (int co = threadIdx.x; co < COUT; co += NTH) slot[9 * CIN * COUT + co] = dB[co];
+}
+
+template <int CIN, int COUT, int XR, int RT, int MAXCX, int MAXCD>
+bool run_wino_wgrad(const WgradArgs& c, float* ws, hipStream_t s) {
+  const int H = c.H, W = c.W;
+  const int TY = (H + 1) / 2, TX = (W + 1) / 2;
+  const int64_t NT = static_cast<int64_t>(c.N) * TY * TX;
+  if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
+  const int per_img = TY * TX;
+  const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
+  if (maxparts > kMaxParts) return false;
+  const int Wl = 2 * TX + 2, Wd = 2 * TX;
+  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  if (maxrows * Wl * (CIN / 4) > MAXCX * 256 || maxrows * Wd * (COUT / 4) > MAXCD * 256 ||
+      maxrows > 256)
+    return false;
+  if (static_cast<int64_t>(c.N) * H * W >= (int64_t(1) << 31) / 32) return false;
+  const size_t stage = sizeof(float) * (static_cast<size_t>(maxrows) * (Wl * (CIN + 8) +
+                                                                        Wd * (COUT + 8))) +
+                       sizeof(int) * (maxrows + 2 * RT);
+  const size_t epi = sizeof(float) * (16 * CIN * COUT + COUT);
+  const size_t bytes = std::max(stage, epi);
+  if (bytes > 160 * 1024) return false;
+  const int M = 9 * CIN;
+  const int rows16 = ((M + 16) / 16) * 16;
+  const int nranges = static_cast<int>((NT + RT - 1) / RT);
+  // slots: one per resident workgroup (<= the direct kernel's workspace)
+  const int64_t cap = wgrad_workspace_floats(3, CIN, COUT) / (static_cast<int64_t>(rows16) * COUT);
+  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  WinoWgArgs a{};
+  a.x = static_cast<const float*>(c.src);
+  a.dy = c.dy;
+  a.part = ws;
+  a.N = c.N; a.H = H; a.W = W;
+  a.TY = TY; a.TX = TX; a.NT = static_cast<int>(NT); a.nranges = nranges;
+  a.maxrows = maxrows; a.rows16 = rows16;
+  a.rTX = 1.f / static_cast<float>(TX);
+  a.rTY = 1.f / static_cast<float>(TY);
+  a.relu_in = c.relu_in;
+  auto kern = wino_wgrad_kernel<CIN, COUT, XR, RT, MAXCX, MAXCD>;
+  allow_lds_w(kern, bytes);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(256), bytes, s, a);
+  wgrad_reduce_slots(ws, G, rows16, COUT, CIN, c.dw, c.db, s);
+  return true;
+}
+
 }  // namespace
 
 bool wino_enabled() {
@@ -448,6 +821,31 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
     if (cfg == 1) return run_wino<32, 32, 2, 4, 64, 15, 1>(c, flip, s);
     return run_wino<32, 32, 1, 8, 64, 8, 2>(c, flip, s);
   }
+  return false;
+}
+
+}  // namespace cf32
+}  // namespace sa
+
+namespace sa {
+namespace cf32 {
+
+bool wino_wgrad_enabled() {
+  static const bool on = env_int("SA_F32_WINO_WG", 1) != 0;
+  return on;
+}
+
+bool wino_wgrad_launch(const WgradArgs& c, float* ws, hipStream_t s) {
+  if (c.pool.arg != nullptr || c.pt != 1 || c.pl != 1 || c.Ho != c.H || c.Wo != c.W)
+    return false;
+  const int cin = c.Cin, cout = c.Cout;
+  // 16-channel inputs measured slower than the direct MFMA wgrad (res16
+  // 449 vs 369-387 us, the stage-1 head 720 vs 623-631 us: one workgroup of
+  // four waves per CU, VALU-heavy per MFMA); opt-in for sweeps
+  static const int all = env_int("SA_WINO_WG_ALL", 0);
+  if (all && cin == 16 && cout == 16) return run_wino_wgrad<16, 16, 4, 64, 10, 9>(c, ws, s);
+  if (all && cin == 16 && cout == 32) return run_wino_wgrad<16, 32, 2, 64, 10, 19>(c, ws, s);
+  if (cin == 32 && cout == 32) return run_wino_wgrad<32, 32, 1, 64, 15, 14>(c, ws, s);
   return false;
 }
 

@@ -61,6 +61,17 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
 // v outside [1, 8] only queries.  Returns the previous value.
 int lstm_xpack(int v);
 // W_h [H,4H] -> fwd-packed w4 and bwd-packed wt (one launch per unroll).
+// Instruction encoder (lang_lstm.hip): embedding + LSTM(64) over L words,
+// output at the last valid word; fwd saves acts [L][N][256], cs [L][N][64],
+// xh [L][N][84]; bwd -> dgates [L][N][256], dx [L][N][20].
+void lang_lstm_fwd_launch(const int64_t* ids, const int64_t* lengths, const float* embed,
+                          const float* kernel, const float* bias, int N, int L, int V,
+                          float* out, float* acts, float* cs, float* xh,
+                          hipStream_t stream);
+void lang_lstm_bwd_launch(const int64_t* lengths, const float* kernel, const float* dout,
+                          const float* acts, const float* cs, int N, int L, float* dgates,
+                          float* dx, hipStream_t stream);
+
 void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                               hipStream_t stream);
 

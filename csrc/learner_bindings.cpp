@@ -257,12 +257,64 @@ void gemm_f32(at::Tensor A, at::Tensor B, bool ta, bool tb, at::Tensor C,
               "gemm_f32: launch refused");
 }
 
+
+// Instruction encoder: ids [N, L] int64, lengths [N] int64, embed [V, 20],
+// kernel [84, 256], bias [256] -> {out [N, 64], acts, cs, xh} (saved for the
+// backward).
+std::vector<at::Tensor> lang_lstm_fwd(at::Tensor ids, at::Tensor lengths, at::Tensor embed,
+                                      at::Tensor kernel, at::Tensor bias) {
+  LB_CHECK(ids); LB_CHECK(lengths); LB_CHECK(embed); LB_CHECK(kernel); LB_CHECK(bias);
+  LB_F32(embed); LB_F32(kernel); LB_F32(bias);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && lengths.scalar_type() == at::kLong,
+              "ids / lengths must be int64");
+  TORCH_CHECK(ids.dim() == 2 && lengths.numel() == ids.size(0), "ids [N, L], lengths [N]");
+  TORCH_CHECK(embed.dim() == 2 && embed.size(1) == 20, "embedding width 20");
+  TORCH_CHECK(kernel.size(0) == 84 && kernel.size(1) == 256 && bias.numel() == 256,
+              "language LSTM kernel [84, 256]");
+  const int N = ids.size(0), L = ids.size(1);
+  const c10::DeviceGuard guard(ids.device());
+  auto o = embed.options();
+  auto out = at::empty({N, 64}, o);
+  auto acts = at::empty({L, N, 256}, o);
+  auto cs = at::empty({L, N, 64}, o);
+  auto xh = at::empty({L, N, 84}, o);
+  if (N > 0 && L > 0)
+    sa::lang_lstm_fwd_launch(ids.data_ptr<int64_t>(), lengths.data_ptr<int64_t>(),
+                             embed.data_ptr<float>(), kernel.data_ptr<float>(),
+                             bias.data_ptr<float>(), N, L, embed.size(0), out.data_ptr<float>(),
+                             acts.data_ptr<float>(), cs.data_ptr<float>(),
+                             xh.data_ptr<float>(), stream());
+  else
+    out.zero_();
+  return {out, acts, cs, xh};
+}
+
+// -> {dgates [L, N, 256], dx [L, N, 20]}
+std::vector<at::Tensor> lang_lstm_bwd(at::Tensor lengths, at::Tensor kernel, at::Tensor dout,
+                                      at::Tensor acts, at::Tensor cs) {
+  LB_CHECK(lengths); LB_CHECK(kernel); LB_CHECK(dout); LB_CHECK(acts); LB_CHECK(cs);
+  LB_F32(dout); LB_F32(acts); LB_F32(cs); LB_F32(kernel);
+  const int L = acts.size(0), N = acts.size(1);
+  TORCH_CHECK(dout.numel() == static_cast<int64_t>(N) * 64, "dout [N, 64]");
+  const c10::DeviceGuard guard(acts.device());
+  auto dg = at::empty({L, N, 256}, acts.options());
+  auto dx = at::empty({L, N, 20}, acts.options());
+  if (N > 0 && L > 0)
+    sa::lang_lstm_bwd_launch(lengths.data_ptr<int64_t>(), kernel.data_ptr<float>(),
+                             dout.data_ptr<float>(), acts.data_ptr<float>(),
+                             cs.data_ptr<float>(), N, L, dg.data_ptr<float>(),
+                             dx.data_ptr<float>(), stream());
+  return {dg, dx};
+}
+
 }  // namespace
 
 void register_learner_ops(pybind11::module& m) {
   m.def("learner_head_fwd", &learner_head_fwd);
   m.def("learner_head_bwd", &learner_head_bwd);
   m.def("core_aug_fwd", &core_aug_fwd);
+  m.def("lang_lstm_fwd", &lang_lstm_fwd);
+  m.def("lang_lstm_bwd", &lang_lstm_bwd);
   m.def("gemm_f32", &gemm_f32, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("ta"),
         pybind11::arg("tb"), pybind11::arg("C"), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("relu") = false,

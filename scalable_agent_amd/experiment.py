@@ -119,10 +119,15 @@ def uses_instruction(flags, level_names):
 
 # --------------------------------------------------------------- helpers
 def _device(flags, local_rank=0):
+  """The rank's device: 'auto' / 'cuda' (no index) -> cuda:local_rank
+  (modulo the visible GPUs: a one-card multi-rank rehearsal shares it)."""
   import torch
-  if flags.device == 'auto':
-    return (torch.device('cuda', local_rank) if torch.cuda.is_available()
-            else torch.device('cpu'))
+  if flags.device in ('auto', 'cuda'):
+    if torch.cuda.is_available():
+      return torch.device('cuda', local_rank % torch.cuda.device_count())
+    if flags.device == 'cuda':
+      raise RuntimeError('--device=cuda but no GPU is visible')
+    return torch.device('cpu')
   return torch.device(flags.device)
 
 
@@ -390,6 +395,14 @@ def train(flags):
                                            frame_shape, use_instr)
 
   rank, world, local_rank = parallel.world_info()
+  numa = getattr(flags, 'numa_affinity', 'auto')
+  if numa == 'on' or (numa == 'auto' and (
+      flags.device.startswith('cuda') or
+      (flags.device == 'auto' and torch.cuda.device_count() > 0))):
+    # before the actor processes fork and before any pinned allocation:
+    # the rank's host-side data path lives next to its GPU (sysfs only, the
+    # GPU is not initialised yet)
+    parallel.pin_to_gpu_numa(local_rank)
   # many actor threads share the GIL with the learner thread: a short switch
   # interval bounds how long the learner waits for it between GPU launches
   sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
@@ -421,7 +434,7 @@ def train(flags):
     shared_w_name = '/sa_w_%d_%d' % (os.getpid(), rank)
     if flags.inference_device != 'auto':
       group_dev = flags.inference_device
-    elif flags.device != 'auto':
+    elif flags.device not in ('auto', 'cuda'):
       group_dev = flags.device
     else:  # device_count() does not initialise the GPU in this process
       ndev = torch.cuda.device_count()

@@ -152,6 +152,10 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--env_timeout_secs', type=float, default=0.,
                  help='Env-call watchdog: a worker that does not answer in '
                       'time is killed and respawned (0 = off).')
+  p.add_argument('--numa_affinity', default='auto', choices=['auto', 'on', 'off'],
+                 help='pin each learner rank (and the actor processes it forks) '
+                 'to the NUMA node of its GPU before any pinned allocation; '
+                 'auto: when the learner runs on a GPU')
   p.add_argument('--consistency_check_steps', type=int, default=1000,
                  help='Data-parallel: every N steps all-reduce a parameter '
                       'checksum and fail on divergence (0 = off).')

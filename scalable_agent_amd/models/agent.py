@@ -255,6 +255,14 @@ class Agent(nn.Module):
     ids, lengths = instr
     ids = ids.reshape(n, -1).to(device)
     lengths = lengths.reshape(n).to(device)
+    if self.backend == 'hip' and lengths.is_cuda:
+      # embedding gather + the whole word loop + last-valid-word output in
+      # one fused HIP kernel per direction (ops/lang.py); graph-safe (no
+      # data-dependent host decisions)
+      from .. import ops
+      return ops.language_lstm(ids, lengths, self.embed,
+                               self.language_lstm_kernel,
+                               self.language_lstm_bias)
     capturing = lengths.is_cuda and torch.cuda.is_current_stream_capturing()
     if lengths.numel() == 0 or (not capturing and int(lengths.max()) == 0):
       return torch.zeros(n, INSTR_LSTM, device=device, dtype=self.embed.dtype)

@@ -14,5 +14,6 @@ from .lstm import lstm_unroll  # noqa: F401
 from .conv import torso_forward, linear_relu  # noqa: F401
 from .conv_f32 import torso_forward_f32, linear_relu_f32  # noqa: F401
 from .core import core_lstm  # noqa: F401
+from .lang import language_lstm  # noqa: F401
 from .heads import heads_vtrace_loss, actor_heads_sample, PhiloxStream  # noqa: F401
 from .grad_sink import direct_grads  # noqa: F401

@@ -1,0 +1,57 @@
+"""Instruction encoder on one fused HIP kernel per direction.
+
+Reference: experiment.py:123-146 - hashed word ids -> Embed(1000, 20) ->
+dynamic_rnn(LSTMBlockCell(64), sequence_length) -> the output at the last
+valid word (zeros for an empty instruction), gate order i, c~, f, o, forget
+bias +1.  csrc/kernels/lang_lstm.hip runs the whole word loop of 16 frames
+per workgroup (embedding gather, the [x_t, h_{t-1}] x K product on fp32
+MFMA, the cell update) forward and backward; the parameter gradients are
+dK = xh^T dgates and db = 1^T dgates (one exact-fp32 GEMM with the ones-row
+bias gradient, gemm_f32) and the embedding rows' scatter-add of dx.
+"""
+
+import torch
+
+from . import grad_sink
+from ._ext import ext
+
+
+class _LanguageLSTM(torch.autograd.Function):
+
+  @staticmethod
+  def forward(ctx, ids, lengths, embed, kernel, bias):
+    out, acts, cs, xh = ext().lang_lstm_fwd(ids, lengths, embed, kernel, bias)
+    ctx.save_for_backward(ids, lengths, embed, kernel, bias, acts, cs, xh)
+    return out
+
+  @staticmethod
+  def backward(ctx, dout):
+    ids, lengths, embed, kernel, bias, acts, cs, xh = ctx.saved_tensors
+    C = ext()
+    dg, dx = C.lang_lstm_bwd(lengths, kernel, dout.float().contiguous(), acts, cs)
+    L, N, G = dg.shape
+    (gemb, gk, gb), direct = grad_sink.sinks([embed, kernel, bias])
+    xh2, dg2 = xh.view(L * N, xh.shape[2]), dg.view(L * N, G)
+    if (L * N) % 4 == 0:
+      C.gemm_f32(xh2, dg2, True, False, gk, accumulate=True, colsum=gb)
+    else:  # tiny test shapes (the GEMM takes K % 4 == 0)
+      gk.add_(xh2.t() @ dg2)
+      gb.add_(dg2.sum(0))
+    # embedding rows: scatter-add of dx over the word ids (steps past an
+    # instruction's length carry dx = 0)
+    flat = ids.t().reshape(-1)  # [L*N] in the kernel's (t, n) order
+    dx2 = dx.view(L * N, dx.shape[2])
+    if torch.are_deterministic_algorithms_enabled():
+      onehot = torch.nn.functional.one_hot(flat, embed.shape[0]).to(dx2.dtype)
+      gemb.add_(onehot.t() @ dx2)
+    else:
+      gemb.index_add_(0, flat, dx2)
+    return (None, None) + grad_sink.returned((gemb, gk, gb), direct)
+
+
+def language_lstm(ids, lengths, embed, kernel, bias):
+  """ids [N, L] int64 word ids, lengths [N] -> [N, 64] (fp32)."""
+  return _LanguageLSTM.apply(ids.to(torch.int64).contiguous(),
+                             lengths.to(torch.int64).contiguous(),
+                             embed.contiguous(), kernel.contiguous(),
+                             bias.contiguous())

@@ -1,0 +1,127 @@
+"""CPU/NUMA affinity of a learner rank to its GPU's NUMA node.
+
+On a 2-socket 8 x MI355X node each GPU hangs off one socket.  A rank whose
+learner thread, H2D feeder and pinned trajectory slabs live on the other
+socket pays a cross-socket hop on every ~67 MB/step batch copy and on every
+kernel launch.  `pin_to_gpu_numa` restricts the calling process (and every
+process it forks afterwards: actor groups, env workers) to the CPUs of the
+NUMA node of the rank's GPU, in process and without re-executing anything,
+so it must run BEFORE the first pinned allocation and before the actor
+processes are forked (the slabs' pages are first-touched by those
+processes).
+
+The GPU -> NUMA node mapping is read from sysfs only (no HIP call, so it can
+run before the GPU is initialised): the KFD topology lists GPU nodes in HIP
+enumeration order with their PCI location; /sys/bus/pci/devices/<bdf>/
+numa_node gives the node and /sys/devices/system/node/node<N>/cpulist its
+CPUs.  HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES
+renumber the devices like the runtime does.  Every failure is a no-op.
+"""
+
+import logging
+import os
+
+log = logging.getLogger('scalable_agent_amd')
+
+
+def _read(path):
+  try:
+    with open(path) as f:
+      return f.read()
+  except OSError:
+    return None
+
+
+def parse_cpulist(text):
+  """'0-3,8,10-11' -> {0, 1, 2, 3, 8, 10, 11}."""
+  out = set()
+  for part in (text or '').strip().split(','):
+    if not part:
+      continue
+    if '-' in part:
+      a, b = part.split('-')
+      out.update(range(int(a), int(b) + 1))
+    else:
+      out.add(int(part))
+  return out
+
+
+def gpu_pci_addresses(root='/sys'):
+  """PCI addresses ('0000:05:00.0') of the GPUs in HIP enumeration order
+  (KFD topology GPU nodes, i.e. nodes with SIMDs)."""
+  base = os.path.join(root, 'class/kfd/kfd/topology/nodes')
+  try:
+    nodes = sorted(os.listdir(base), key=int)
+  except (OSError, ValueError):
+    return []
+  out = []
+  for n in nodes:
+    props = _read(os.path.join(base, n, 'properties')) or ''
+    kv = {}
+    for line in props.splitlines():
+      parts = line.split()
+      if len(parts) == 2:
+        kv[parts[0]] = parts[1]
+    if int(kv.get('simd_count', '0')) <= 0:
+      continue  # a CPU node
+    loc = int(kv.get('location_id', '0'))
+    dom = int(kv.get('domain', '0'))
+    bus, dev, fn = (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 0x7
+    out.append('%04x:%02x:%02x.%x' % (dom, bus, dev, fn))
+  return out
+
+
+def visible_index(local_rank, env=None):
+  """Physical GPU index of logical device `local_rank` under the
+  *_VISIBLE_DEVICES masks (ROCR first, then HIP / CUDA, as the runtime)."""
+  env = os.environ if env is None else env
+  idx = local_rank
+  for var in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
+    spec = env.get(var)
+    if spec:
+      ids = [int(x) for x in spec.split(',') if x.strip().isdigit()]
+      if idx < len(ids):
+        idx = ids[idx]
+  return idx
+
+
+def gpu_numa_node(local_rank, root='/sys', env=None):
+  """NUMA node of logical GPU `local_rank`, or None when unknown."""
+  addrs = gpu_pci_addresses(root)
+  phys = visible_index(local_rank, env)
+  if phys >= len(addrs):
+    return None
+  txt = _read(os.path.join(root, 'bus/pci/devices', addrs[phys], 'numa_node'))
+  try:
+    node = int(txt)
+  except (TypeError, ValueError):
+    return None
+  return node if node >= 0 else None
+
+
+def pin_to_gpu_numa(local_rank, root='/sys', env=None, apply=True):
+  """Restricts this process's CPU affinity to its GPU's NUMA node.
+
+  -> (node, sorted cpu list) when applied, None otherwise (unknown node,
+  single-node machine, or no overlap with the current affinity)."""
+  node = gpu_numa_node(local_rank, root, env)
+  if node is None:
+    return None
+  cpus = parse_cpulist(_read(os.path.join(
+      root, 'devices/system/node/node%d/cpulist' % node)))
+  try:
+    current = os.sched_getaffinity(0)
+  except AttributeError:
+    return None
+  target = cpus & current if apply else cpus
+  if not target or (apply and target == current):
+    return None
+  if apply:
+    try:
+      os.sched_setaffinity(0, target)
+    except OSError as e:
+      log.warning('NUMA pinning to node %d failed: %s', node, e)
+      return None
+    log.info('rank-local GPU %d on NUMA node %d: pinned to %d CPUs',
+             local_rank, node, len(target))
+  return node, sorted(target)

@@ -249,7 +249,12 @@ def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
   conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
   ref_p, ref_a = C.cf32_maxpool_fwd(conv, pbh, pbw)
   p, a = C.cf32_conv_pool_fwd(x, w, b, pbh, pbw)
-  assert torch.equal(p, ref_p) and torch.equal(a, ref_a)
+  # the stand-alone 3x3/1 conv of the 16/32-channel stages runs the Winograd
+  # kernels (different rounding than the fused direct conv+pool): values to
+  # fp32 accuracy, argmax codes equal except at fp32-level near-ties
+  assert rel_err(p, ref_p) <= 1e-6
+  assert (a != ref_a).float().mean().item() <= 1e-4
+  ref_a = a
   dP = torch.randn(p.shape, generator=g).to(cuda)
   dconv = C.cf32_maxpool_bwd(dP, a, H, W, pbh, pbw)
   dw1, db1 = torch.zeros_like(w), torch.zeros_like(b)
@@ -260,7 +265,7 @@ def test_fused_stage_head_matches_unfused(cuda, N, H, W, Cin, Cout, u8):
   if not u8:
     dx1 = C.cf32_conv_dgrad(dconv, w, 1, 1, 1, H, W)
     dx2 = C.cf32_conv_dgrad(dP, w, 1, 1, 1, H, W, pool_arg=a, pool_pbh=pbh, pool_pbw=pbw)
-    assert torch.equal(dx1, dx2)
+    assert rel_err(dx2, dx1) <= 1e-6
 
 
 @pytest.mark.parametrize('N,H,W,Cs', [(5, 72, 96, 3), (3, 84, 84, 4), (4, 9, 13, 1),
@@ -311,3 +316,45 @@ def test_strided_dgrad_alternative_paths(cuda, env):
       env=dict(os.environ, PYTHONPATH=root, **env))
   assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
   assert ' passed' in r.stdout
+
+
+@pytest.mark.parametrize('H,W,Cin,Cout', [(36, 48, 16, 16), (36, 48, 16, 32),
+                                          (18, 24, 32, 32), (9, 12, 32, 32)])
+def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
+  """The deep torso's 3x3/1 layers at N = 256 frames: every persistent
+  workgroup walks several tiles/ranges (cross-tile register prefetch, LDS
+  double use, range/image boundaries, slot-capped weight-gradient loops),
+  which the N <= 3 shape tests above never reach.  Forward with ReLU-in +
+  residual + ReLU-out, data gradient with mask + skip add, weight + bias
+  gradient with ReLU-in, all against float64."""
+  C = _C()
+  N = 256
+  g = torch.Generator().manual_seed(H * Cin + Cout)
+  x = torch.randn(N, H, W, Cin, generator=g)
+  w = torch.randn(3, 3, Cin, Cout, generator=g) / (9 * Cin) ** 0.5
+  b = torch.randn(Cout, generator=g) * 0.1
+  add = torch.randn(N, H, W, Cout, generator=g)
+  xr = x.double().clamp(min=0)
+  ref = (layers.conv2d_same_nhwc(xr, w.double(), b.double(), 1) +
+         add.double()).clamp(min=0)
+  y = C.cf32_conv_fwd(x.to(cuda), w.to(cuda), b.to(cuda), 1, 1, 1, H, W,
+                      relu_in=True, add=add.to(cuda), relu_out=True)
+  assert rel_err(y, ref) <= TOL
+  dy = torch.randn(N, H, W, Cout, generator=g)
+  mask = torch.randn(N, H, W, Cin, generator=g)
+  sk = torch.randn(N, H, W, Cin, generator=g)
+  x64 = x.double().requires_grad_(True)
+  (dref,) = torch.autograd.grad(
+      layers.conv2d_same_nhwc(x64, w.double(), None, 1), x64, dy.double())
+  dref = torch.where(mask.double() > 0, dref, torch.zeros_like(dref)) + sk.double()
+  dx = C.cf32_conv_dgrad(dy.to(cuda), w.to(cuda), 1, 1, 1, H, W,
+                         mask=mask.to(cuda), add=sk.to(cuda))
+  assert rel_err(dx, dref) <= TOL
+  w64 = w.double().requires_grad_(True)
+  b64 = b.double().requires_grad_(True)
+  rw, rb = torch.autograd.grad(layers.conv2d_same_nhwc(xr, w64, b64, 1),
+                               (w64, b64), dy.double())
+  dw, db = torch.zeros(3, 3, Cin, Cout, device=cuda), torch.zeros(Cout, device=cuda)
+  C.cf32_conv_wgrad(x.to(cuda), dy.to(cuda), 1, 1, 1, True, dw, db)
+  assert rel_err(dw, rw) <= TOL
+  assert rel_err(db, rb) <= TOL

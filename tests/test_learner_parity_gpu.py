@@ -61,9 +61,10 @@ def _step(backend, torso, dtype, cuda, shape=(72, 96, 3), B=4, T=8, aseed=3,
               health=learner.health())
 
 
-def _compare(ref, hip, cos_min, rel_max):
+def _compare(ref, hip, cos_min, rel_max, loss_rel=None):
   assert torch.equal(ref['p0'], hip['p0']), 'different init'
-  assert abs(hip['loss'] - ref['loss']) <= rel_max * max(abs(ref['loss']), 1.0)
+  loss_rel = rel_max if loss_rel is None else loss_rel
+  assert abs(hip['loss'] - ref['loss']) <= loss_rel * max(abs(ref['loss']), 1.0)
   worst = []
   for name, _ in ref['flat'].named:
     gr = ref['flat'].view_of(ref['grads'], name).double()
@@ -86,9 +87,15 @@ def _compare(ref, hip, cos_min, rel_max):
 
 @pytest.mark.parametrize('torso', ['deep', 'shallow'])
 def test_fp32_hip_learner_step_matches_torch(cuda, torso):
+  # 36 frames of this batch hold 15-26 max-pool near-ties / ReLU near-zeros
+  # (tests/_discontinuity.py at 1e-6): fp32 torch (MIOpen direct conv) and
+  # the HIP kernels (Winograd 3x3 convs) round differently and may branch
+  # differently at one of them, which moves one local gradient term - the
+  # exact gradient check is test_fp32_hip_learner_matches_fp64 below
+  # (discontinuity-free seeds, float64 oracle)
   ref = _step('torch', torso, torch.float32, cuda)
   hip = _step('hip', torso, torch.float32, cuda)
-  worst = _compare(ref, hip, cos_min=0.999999, rel_max=1e-4)
+  worst = _compare(ref, hip, cos_min=0.99999, rel_max=5e-3, loss_rel=1e-4)
   print('fp32 %s worst relative gradient error %.3g (%s)' % (torso, worst[0], worst[1]))
   assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
 

@@ -67,8 +67,23 @@ def main():
   ap.add_argument('--dtype', default='fp32')
   ap.add_argument('--torso', default='shallow')
   ap.add_argument('--out', default='')
+  # the headline configuration: --height 72 --width 96 --batch_size 32
+  # --unroll_length 100 --num_actors 48 (README.md:37-41 of the reference)
+  ap.add_argument('--height', type=int, default=36)
+  ap.add_argument('--width', type=int, default=48)
+  ap.add_argument('--batch_size', type=int, default=8)
+  ap.add_argument('--unroll_length', type=int, default=20)
+  ap.add_argument('--num_actors', type=int, default=16)
+  ap.add_argument('--episode_length', type=int, default=20)
+  ap.add_argument('--learning_rate', type=float, default=0.0006)
   args = ap.parse_args()
-  res = run(args.level, args.backend, args.frames, args.dtype, torso=args.torso)
+  res = run(args.level, args.backend, args.frames, args.dtype, torso=args.torso,
+            episode_length=args.episode_length, num_actors=args.num_actors,
+            batch_size=args.batch_size, unroll_length=args.unroll_length,
+            height=args.height, width=args.width,
+            learning_rate=args.learning_rate)
+  res.update(height=args.height, width=args.width, batch_size=args.batch_size,
+             unroll_length=args.unroll_length, num_actors=args.num_actors)
   line = json.dumps(res)
   print(line, flush=True)
   if args.out:

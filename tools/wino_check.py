@@ -36,8 +36,24 @@ for (H, W, Ci, Co) in [(36, 48, 16, 16), (36, 48, 16, 32), (18, 24, 32, 32),
   dx = C.cf32_conv_dgrad(dy.to(dev), w.to(dev), 1, 1, 1, H, W, mask=mask.to(dev),
                          add=sk.to(dev))
   e2 = ((dx.double().cpu() - dref).abs().max() / dref.abs().max()).item()
-  worst = max(worst, e1, e2)
-  print('%2dx%2d %2d->%2d  fwd rel %.2e  dgrad rel %.2e' % (H, W, Ci, Co, e1, e2),
-        flush=True)
+  # weight + bias gradient (ReLU on the input), accumulated into non-zero dW
+  xin = x.double().clamp(min=0).requires_grad_(True)
+  wd = w.double().requires_grad_(True)
+  bd = b.double().requires_grad_(True)
+  yy = layers.conv2d_same_nhwc(xin, wd, bd, 1)
+  gw, gb = torch.autograd.grad(yy, (wd, bd), dy.double())
+  if (Ci, Co) == (32, 16):  # only a data-gradient shape (no forward layer)
+    worst = max(worst, e1, e2)
+    print('%2dx%2d %2d->%2d  fwd rel %.2e  dgrad rel %.2e' % (H, W, Ci, Co, e1, e2))
+    continue
+  dw0 = torch.randn(3, 3, Ci, Co, generator=g)
+  db0 = torch.randn(Co, generator=g)
+  dw, db = dw0.to(dev), db0.to(dev)
+  C.cf32_conv_wgrad(x.to(dev), dy.to(dev), 1, 1, 1, True, dw, db)
+  e3 = ((dw.double().cpu() - dw0.double() - gw).abs().max() / gw.abs().max()).item()
+  e4 = ((db.double().cpu() - db0.double() - gb).abs().max() / gb.abs().max()).item()
+  worst = max(worst, e1, e2, e3, e4)
+  print('%2dx%2d %2d->%2d  fwd rel %.2e  dgrad rel %.2e  wgrad rel %.2e  bgrad rel %.2e'
+        % (H, W, Ci, Co, e1, e2, e3, e4), flush=True)
 print('worst %.2e %s' % (worst, 'OK' if worst <= 1e-5 else 'FAIL'))
 sys.exit(0 if worst <= 1e-5 else 1)
