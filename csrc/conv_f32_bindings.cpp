@@ -264,6 +264,50 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
   check_launch("cf32_conv_wgrad");
 }
 
+// Backward of a 3x3/1 SAME conv whose input x is also the data gradient's
+// ReLU mask (the deep torso's residual convs): returns dX = dgrad(dy, w) *
+// (x > 0) [+ add] and accumulates dw += relu?(x)^T dy, db += sum dy.  One
+// fused pass (dY and x read once) where a kernel covers the shape, else the
+// separate data-gradient and weight-gradient kernels.
+at::Tensor conv_bwd_fused(at::Tensor dy, at::Tensor w, at::Tensor x, bool relu_x,
+                          at::Tensor dw, c10::optional<at::Tensor> db,
+                          c10::optional<at::Tensor> add) {
+  check_nhwc(dy, "dy");
+  check_nhwc(x, "x");
+  check_w(w);
+  check_w(dw);
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "float32");
+  TORCH_CHECK(w.size(0) == 3 && w.size(2) == x.size(3) && w.size(3) == dy.size(3) &&
+                  dy.size(0) == x.size(0) && dy.size(1) == x.size(1) && dy.size(2) == x.size(2),
+              "conv_bwd_fused: 3x3/1 SAME conv (x and dy of one spatial shape)");
+  TORCH_CHECK(dw.sizes() == w.sizes(), "dw shape");
+  const c10::DeviceGuard g(dy.device());
+  auto dx = at::empty(x.sizes(), x.options());
+  const float* addp = opt_f32(add, dx, "add");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    TORCH_CHECK(db->numel() == dy.size(3) && db->scalar_type() == at::kFloat && db->is_contiguous(),
+                "db");
+    dbp = db->data_ptr<float>();
+  }
+  const int C = x.size(3);
+  if (w.size(2) == w.size(3) && dy.sizes() == x.sizes() && sa::cf32::wino_bwd_fused_enabled()) {
+    const int64_t wsf = sa::cf32::wgrad_workspace_floats(3, C, C);
+    auto ws = at::empty({wsf}, dy.options());
+    if (sa::cf32::wino_bwd_fused_launch(dy.data_ptr<float>(), w.data_ptr<float>(),
+                                        x.data_ptr<float>(), addp, dx.data_ptr<float>(),
+                                        relu_x ? 1 : 0, x.size(0), x.size(1), x.size(2), C,
+                                        ws.data_ptr<float>(), wsf, dw.data_ptr<float>(), dbp,
+                                        stream())) {
+      check_launch("cf32_conv_bwd_fused");
+      return dx;
+    }
+  }
+  // separate kernels: weight gradient, then the masked data gradient
+  conv_wgrad(x, dy, 1, 1, 1, relu_x, dw, db, c10::nullopt, 0, 0);
+  return conv_dgrad(dy, w, 1, 1, 1, x.size(1), x.size(2), x, add, c10::nullopt, 0, 0);
+}
+
 // Fused stage head: maxpool3x3/2(conv3x3/1(x) + b) -> {pooled, argmax}
 std::vector<at::Tensor> conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b, int64_t pbh,
                                       int64_t pbw) {
@@ -358,6 +402,8 @@ void register_conv_f32_ops(pybind11::module& m) {
   m.def("cf32_conv_wgrad", &conv_wgrad, arg("x"), arg("dy"), arg("stride"), arg("pt"), arg("pl"),
         arg("relu_in"), arg("dw"), arg("db") = pybind11::none(),
         arg("pool_arg") = pybind11::none(), arg("pool_pbh") = 0, arg("pool_pbw") = 0);
+  m.def("cf32_conv_bwd_fused", &conv_bwd_fused, arg("dy"), arg("w"), arg("x"), arg("relu_x"),
+        arg("dw"), arg("db") = pybind11::none(), arg("add") = pybind11::none());
   m.def("cf32_conv_pool_fwd", &conv_pool_fwd);
   m.def("cf32_maxpool_fwd", &maxpool_fwd);
   m.def("cf32_maxpool_bwd", &maxpool_bwd);

@@ -792,6 +792,335 @@ bool run_wino_wgrad(const WgradArgs& c, float* ws, hipStream_t s) {
   return true;
 }
 
+
+// ------------------------------------------------- fused data + weight grad
+// One backward pass of a 3x3/1 SAME conv whose input x is also the ReLU
+// mask of the data gradient (every residual conv of the deep torso:
+// experiment.py:166-172, t = relu(conv(relu(x))), y = conv(t) + x):
+//   dX = (dY (*) W_flipped^T) * (x > 0) [+ add]      Winograd, as above
+//   dW += sum_p relu?(x)[p + tap] dY[p],  db += sum_p dY[p]   direct MFMA
+// dY and x are staged ONCE per range (same rows, same halo) and serve the
+// data gradient's source and mask and both weight-gradient operands - the
+// separate dgrad + wgrad kernels read each of them twice from HBM (at the
+// 36x48x16 stage every such pass is 357 MB per learner step).  Waves 0-3
+// run the Winograd data-gradient tasks (16-tile groups) plus a few
+// weight-gradient k-steps, waves 4-7 the rest of the weight gradient
+// (k = one 2x2 tile = 4 pixels per MFMA).  Weight-gradient partials go to
+// the wgrad slot layout (fixed-order reduction: deterministic).
+struct WinoBwdArgs {
+  const float* dy;   // [N, H, W, C] (the dgrad source)
+  const float* w;    // forward weights HWIO [3, 3, C, C]
+  const float* x;    // [N, H, W, C] forward input: dgrad mask + wgrad operand
+  const float* add;  // [N, H, W, C] or null
+  float* out;        // dX [N, H, W, C]
+  float* part;       // wgrad slots [G][rows16][C]
+  int N, H, W;
+  int TY, TX, NT, nranges, maxrows, rows16;
+  float rTX, rTY;
+  int relu_x;        // wgrad operand = relu(x)
+};
+
+template <int C, int RT, int MAXC, int KD>
+__global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
+  constexpr int NW = 8, NTH = 512;
+  constexpr int PP = C + 4;
+  constexpr int C4 = C / 4;
+  constexpr int LC4 = C4 == 4 ? 2 : 3;
+  constexpr int NG = RT / 16;          // dgrad tasks (16-tile groups)
+  constexpr int USTR = 4 * C * 4;      // floats per xi in U_s (one ci block)
+  static_assert(C == 16, "fused backward: 16 channels (LDS)");
+  static_assert(NG == 4 && RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0, "work split");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Wl = 2 * a.TX + 2;
+  const int rowstr = Wl * PP;
+  float* U_s = smem;                         // [16 xi][4 g][C][4]
+  float* d_s = U_s + 16 * C * C;             // dY rows [maxrows][Wl][PP]
+  float* x_s = d_s + a.maxrows * rowstr;     // x rows, same geometry
+  int* tab_s = reinterpret_cast<int*>(x_s + a.maxrows * rowstr);  // [maxrows]
+  int* tile_s = tab_s + a.maxrows;                                // [RT]
+
+  // U = G g' G^T of the flipped / transposed weights (the dgrad conv)
+  for (int e = threadIdx.x; e < C * C; e += NTH) {
+    const int co = e % C, ci = e / C;  // ci = dY channel, co = dX channel
+    float gk[3][3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[(((2 - ky) * 3 + (2 - kx)) * C + co) * C + ci];
+    float t[4][3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      t[0][kx] = gk[0][kx];
+      t[1][kx] = 0.5f * ((gk[0][kx] + gk[1][kx]) + gk[2][kx]);
+      t[2][kx] = 0.5f * ((gk[0][kx] - gk[1][kx]) + gk[2][kx]);
+      t[3][kx] = gk[2][kx];
+    }
+    const int gq = (ci >> 2) & 3, v = ci & 3;
+#pragma unroll
+    for (int ra = 0; ra < 4; ++ra) {
+      const float u[4] = {t[ra][0], 0.5f * ((t[ra][0] + t[ra][1]) + t[ra][2]),
+                          0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) U_s[(4 * ra + rb) * USTR + (gq * C + co) * 4 + v] = u[rb];
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+
+  WinoArgs ga{};
+  ga.NT = a.NT; ga.TX = a.TX; ga.TY = a.TY; ga.rTX = a.rTX; ga.rTY = a.rTY;
+  int r = blockIdx.x;
+  if (r >= a.nranges) return;
+
+  // staging slots: element e of both images = (row L, col, quad)
+  int sl_L[MAXC], sl_o[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4 - 1), pix = e >> LC4;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sl_L[k] = L < a.maxrows ? L : -1;
+    sl_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * C + 4 * ch : -1;
+  }
+  auto build_tab = [&](int rr) {
+    const RangeGeom gm = range_geom(ga, rr, RT);
+    const int L = threadIdx.x;
+    if (L < a.maxrows) {
+      int v = -1;
+      if (L < gm.rows) {
+        const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
+        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
+        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W * C;
+      }
+      tab_s[L] = v;
+    }
+  };
+  f4 sd[MAXC], sx[MAXC];
+  uint32_t ok = 0;
+  auto prefetch = [&]() {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
+      const bool in = rb >= 0 && sl_o[k] >= 0;
+      const int off = in ? rb + sl_o[k] : 0;
+      sd[k] = *reinterpret_cast<const f4*>(a.dy + off);
+      sx[k] = *reinterpret_cast<const f4*>(a.x + off);
+      m |= static_cast<uint32_t>(in) << k;
+    }
+    ok = m;
+  };
+  build_tab(r);
+  __syncthreads();
+  prefetch();
+
+  f4 wacc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wacc[k] = f4{0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+
+  for (;;) {
+    __syncthreads();  // the previous range's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      if (sl_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        const bool in = (ok >> k) & 1u;
+        f4 vd = sd[k], vx = sx[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          vd[q] = in ? vd[q] : 0.f;
+          vx[q] = in ? vx[q] : 0.f;
+        }
+        const int o = (e >> LC4) * PP + 4 * (e & (C4 - 1));
+        *reinterpret_cast<f4*>(d_s + o) = vd;
+        *reinterpret_cast<f4*>(x_s + o) = vx;
+      }
+    }
+    const int cur = r;
+    r += gridDim.x;
+    const RangeGeom gm = range_geom(ga, cur, RT);
+    // tile table of this range: LDS offset of each tile's patch origin
+    if (threadIdx.x < RT) {
+      const int t = gm.t0 + threadIdx.x;
+      int v = -1;
+      if (t < gm.t1) {
+        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
+        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int p = n - gm.n0;
+        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        v = ((offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx) * PP;
+      }
+      tile_s[threadIdx.x] = v;
+    }
+    if (r < a.nranges) build_tab(r);
+    __syncthreads();
+    if (r < a.nranges) prefetch();
+
+    // ---- data gradient: waves 0..3, one 16-tile group each
+    if (wave < NG && gm.t0 + 16 * wave < gm.t1) {
+      int t = gm.t0 + 16 * wave + c16;
+      const bool valid = t < gm.t1;
+      if (!valid) t = gm.t0;
+      const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
+      const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+      const int base = tile_s[valid ? 16 * wave + c16 : 0];
+      const float* dp = d_s + base + 4 * g;
+      f4 acc[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
+      f4 d[16];
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx)
+          d[4 * dy + dx] = *reinterpret_cast<const f4*>(dp + dy * rowstr + dx * PP);
+      f4 sv[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sv[q] = d[q] - d[8 + q];
+        sv[4 + q] = d[4 + q] + d[8 + q];
+        sv[8 + q] = d[8 + q] - d[4 + q];
+        sv[12 + q] = d[4 + q] - d[12 + q];
+      }
+      f4 V[16];
+#pragma unroll
+      for (int ra = 0; ra < 4; ++ra) {
+        V[4 * ra + 0] = sv[4 * ra + 0] - sv[4 * ra + 2];
+        V[4 * ra + 1] = sv[4 * ra + 1] + sv[4 * ra + 2];
+        V[4 * ra + 2] = sv[4 * ra + 2] - sv[4 * ra + 1];
+        V[4 * ra + 3] = sv[4 * ra + 1] - sv[4 * ra + 3];
+      }
+      const float* up = U_s + (g * C + c16) * 4;
+#pragma unroll
+      for (int xp2 = 0; xp2 < 8; ++xp2) {
+        const f4 u0 = *reinterpret_cast<const f4*>(up + (2 * xp2) * USTR);
+        const f4 u1 = *reinterpret_cast<const f4*>(up + (2 * xp2 + 1) * USTR);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          acc[2 * xp2] = mfma4(u0[v], V[2 * xp2][v], acc[2 * xp2]);
+          acc[2 * xp2 + 1] = mfma4(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1]);
+        }
+      }
+      f4 tt[4][2];
+#pragma unroll
+      for (int ra = 0; ra < 4; ++ra) {
+        tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
+        tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+      }
+      f4 Y[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
+        Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+      }
+      const float* xm = x_s + base + 4 * g;
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const int oy = 2 * ty + dy, ox = 2 * tx + dx;
+          if (!valid || oy >= a.H || ox >= a.W) continue;
+          const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + 4 * g;
+          const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rowstr + (dx + 1) * PP);
+          f4 v = Y[2 * dy + dx];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
+          if (a.add != nullptr) v += *reinterpret_cast<const f4*>(a.add + o);
+          *reinterpret_cast<f4*>(a.out + o) = v;
+        }
+    }
+
+    // ---- weight gradient: k-step = one tile (lane group g = its pixel g)
+    {
+      constexpr int REST = (RT - 4 * KD) / 4;  // k-steps per wave 4..7
+      const int k0 = wave < 4 ? wave * KD : 4 * KD + (wave - 4) * REST;
+      const int k1 = wave < 4 ? k0 + KD : k0 + REST;
+      const int py = g >> 1, px = g & 1;
+      for (int kt = k0; kt < k1; ++kt) {
+        const int base = tile_s[kt];
+        if (base < 0) continue;  // past the batch's last tile (uniform)
+        const int pofs = base + c16 + py * rowstr + px * PP;
+        const float bv = d_s[pofs + rowstr + PP];  // dY at the pixel, co = c16
+        dbacc += bv;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            float av = x_s[pofs + ky * rowstr + kx * PP];  // x, ci = c16
+            av = a.relu_x ? fmaxf(av, 0.f) : av;
+            wacc[3 * ky + kx] = mfma4(av, bv, wacc[3 * ky + kx]);
+          }
+      }
+    }
+    if (r >= a.nranges) break;
+  }
+
+  // ---- weight-gradient partials of the workgroup (fixed wave order)
+  __syncthreads();
+  float* red = smem;  // [9 * C + 1][C]
+  for (int k = 0; k < NW; ++k) {
+    if (wave == k) {
+      // D[i = ci = 4g + q][j = co = c16]
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float* pp = red + (tap * C + 4 * g + q) * C + c16;
+          *pp = (k == 0 ? 0.f : *pp) + wacc[tap][q];
+        }
+      float v = dbacc;
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (g == 0) {
+        float* pb = red + 9 * C * C + c16;
+        *pb = (k == 0 ? 0.f : *pb) + v;
+      }
+    }
+    __syncthreads();
+  }
+  float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * C;
+  for (int e = threadIdx.x; e < (9 * C + 1) * C; e += NTH) slot[e] = red[e];
+}
+
+template <int C, int RT, int MAXC, int KD>
+bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
+                  float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
+                  float* dw, float* db, hipStream_t s) {
+  const int TY = (H + 1) / 2, TX = (W + 1) / 2;
+  const int64_t NT = static_cast<int64_t>(N) * TY * TX;
+  if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
+  if (static_cast<int64_t>(N) * H * W * C >= (int64_t(1) << 31)) return false;
+  const int per_img = TY * TX;
+  const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
+  if (maxparts > kMaxParts) return false;
+  const int Wl = 2 * TX + 2;
+  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  if (maxrows * Wl * (C / 4) > MAXC * 512 || maxrows > 512) return false;
+  const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * Wl * (C + 4)) +
+                       sizeof(int) * (maxrows + RT);
+  if (bytes > 160 * 1024) return false;
+  const int rows16 = ((9 * C + 16) / 16) * 16;
+  const int nranges = static_cast<int>((NT + RT - 1) / RT);
+  const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * C);
+  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  if (G < 1) return false;
+  WinoBwdArgs a{};
+  a.dy = dy; a.w = w; a.x = x; a.add = add; a.out = out; a.part = ws;
+  a.N = N; a.H = H; a.W = W;
+  a.TY = TY; a.TX = TX; a.NT = static_cast<int>(NT); a.nranges = nranges;
+  a.maxrows = maxrows; a.rows16 = rows16;
+  a.rTX = 1.f / static_cast<float>(TX);
+  a.rTY = 1.f / static_cast<float>(TY);
+  a.relu_x = relu_x;
+  auto kern = wino_bwd_fused_kernel<C, RT, MAXC, KD>;
+  allow_lds_w(kern, bytes);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
+  wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
+  return true;
+}
+
 }  // namespace
 
 bool wino_enabled() {
@@ -846,6 +1175,29 @@ bool wino_wgrad_launch(const WgradArgs& c, float* ws, hipStream_t s) {
   if (all && cin == 16 && cout == 16) return run_wino_wgrad<16, 16, 4, 64, 10, 9>(c, ws, s);
   if (all && cin == 16 && cout == 32) return run_wino_wgrad<16, 32, 2, 64, 10, 19>(c, ws, s);
   if (cin == 32 && cout == 32) return run_wino_wgrad<32, 32, 1, 64, 15, 14>(c, ws, s);
+  return false;
+}
+
+}  // namespace cf32
+}  // namespace sa
+
+namespace sa {
+namespace cf32 {
+
+bool wino_bwd_fused_enabled() {
+  static const bool on = env_int("SA_F32_FUSED_BWD", 1) != 0;
+  return on;
+}
+
+bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, const float* add,
+                           float* out, int relu_x, int N, int H, int W, int C, float* ws,
+                           int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+  static const int kd = env_int("SA_FUSED_BWD_KD", 4);
+  if (C == 16) {
+    if (kd == 0) return run_wino_bwd<16, 64, 5, 0>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
+    if (kd == 8) return run_wino_bwd<16, 64, 5, 8>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
+    return run_wino_bwd<16, 64, 5, 4>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
+  }
   return false;
 }
 

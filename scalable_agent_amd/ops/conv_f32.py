@@ -175,13 +175,15 @@ class _DeepTorsoF32(torch.autograd.Function):
         xa, tt = saved[k + 2 + 2 * blk], saved[k + 3 + 2 * blk]
         i1 = pb + 2 + 4 * blk
         w1, w2 = params[i1], params[i1 + 2]
-        C.cf32_conv_wgrad(tt, dy, 1, 1, 1, False, gv[i1 + 2], gv[i1 + 3])
-        dt = C.cf32_conv_dgrad(dy, w2, 1, 1, 1, h, w_, mask=tt)
-        C.cf32_conv_wgrad(xa, dt, 1, 1, 1, True, gv[i1], gv[i1 + 1])
+        # one pass per conv: its data gradient (masked by the conv's own
+        # input, + the skip for the block's first conv) and its weight/bias
+        # gradient read dY and the input once (conv_wino.hip fused backward
+        # where it covers the shape, else the separate kernels)
+        dt = C.cf32_conv_bwd_fused(dy, w2, tt, False, gv[i1 + 2], gv[i1 + 3])
         if DEBUG_TAPE is not None:
           DEBUG_TAPE[('dy', s, blk)] = dy.clone()
           DEBUG_TAPE[('dt', s, blk)] = dt.clone()
-        dy = C.cf32_conv_dgrad(dt, w1, 1, 1, 1, h, w_, mask=xa, add=dy)
+        dy = C.cf32_conv_bwd_fused(dt, w1, xa, True, gv[i1], gv[i1 + 1], add=dy)
       gw = gv[pb]
       if s == 0 and gw.shape[2] != 4:
         gw = torch.zeros(gw.shape[:2] + (4,) + gw.shape[3:], dtype=torch.float32,

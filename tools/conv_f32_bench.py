@@ -62,6 +62,25 @@ for name, H, W, Ci, Co, K, S, pt, pl, u8 in LAYERS:
     td = timeit(lambda: C.cf32_conv_dgrad(dy, w, S, pt, pl, H, W))
     line += ' | dgrad %8.1f us %6.1f TF' % (td, flop / td / 1e6)
   print(line, flush=True)
+# residual-conv backward: fused (one pass) vs separate wgrad + masked dgrad
+for name, H, W, Cc in [('res16 36x48', 36, 48, 16), ('res32 18x24', 18, 24, 32),
+                       ('res32 9x12', 9, 12, 32)]:
+  if ONLY and ONLY not in name and ONLY != 'bwd':
+    continue
+  x = torch.randn(N, H, W, Cc, device=dev)
+  w = torch.randn(3, 3, Cc, Cc, device=dev) * 0.1
+  dy = torch.randn(N, H, W, Cc, device=dev)
+  add = torch.randn(N, H, W, Cc, device=dev)
+  dw = torch.zeros_like(w)
+  db = torch.zeros(Cc, device=dev)
+  tf = timeit(lambda: C.cf32_conv_bwd_fused(dy, w, x, True, dw, db, add=add))
+
+  def sep():
+    C.cf32_conv_wgrad(x, dy, 1, 1, 1, True, dw, db)
+    C.cf32_conv_dgrad(dy, w, 1, 1, 1, H, W, mask=x, add=add)
+  ts = timeit(sep)
+  print('%-26s bwd fused %8.1f us | separate wgrad+dgrad %8.1f us' % (name, tf, ts),
+        flush=True)
 if ONLY:
   sys.exit(0)
 xp = torch.randn(N, 72, 96, 16, device=dev)

@@ -1,0 +1,4 @@
+set -e
+bash tools/gpu_session.sh \
+ "tests|400|python -u -m pytest tests/test_learner_parity_gpu.py tests/test_train_dp.py -q -m gpu --timeout 300 --timeout-method thread" \
+ "prof|300|cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --also_bf16 0 --steps 20 --warmup 3"

@@ -56,4 +56,46 @@ for (H, W, Ci, Co) in [(36, 48, 16, 16), (36, 48, 16, 32), (18, 24, 32, 32),
   print('%2dx%2d %2d->%2d  fwd rel %.2e  dgrad rel %.2e  wgrad rel %.2e  bgrad rel %.2e'
         % (H, W, Ci, Co, e1, e2, e3, e4), flush=True)
 print('worst %.2e %s' % (worst, 'OK' if worst <= 1e-5 else 'FAIL'))
-sys.exit(0 if worst <= 1e-5 else 1)
+if worst > 1e-5:
+  sys.exit(1)
+
+
+def check_fused_bwd(N=37):
+  """cf32_conv_bwd_fused == the float64 data + weight gradients."""
+  worst = 0.0
+  for (H, W, Cc) in [(36, 48, 16), (11, 11, 16), (9, 12, 32), (18, 24, 32)]:
+    x = torch.randn(N, H, W, Cc, generator=g)
+    w = torch.randn(3, 3, Cc, Cc, generator=g) / (9 * Cc) ** 0.5
+    dy = torch.randn(N, H, W, Cc, generator=g)
+    add = torch.randn(N, H, W, Cc, generator=g)
+    for relu_x, use_add in ((False, False), (True, True)):
+      x64 = x.double().requires_grad_(True)
+      xin = x64.clamp(min=0) if relu_x else x64
+      w64 = w.double().requires_grad_(True)
+      b64 = torch.zeros(Cc, dtype=torch.float64, requires_grad=True)
+      y = layers.conv2d_same_nhwc(xin, w64, b64, 1)
+      gx, gw, gb = torch.autograd.grad(y, (x64, w64, b64), dy.double())
+      # dX of the raw conv (x -> conv), masked by x > 0, + add
+      x2 = x.double().requires_grad_(True)
+      (gx2,) = torch.autograd.grad(layers.conv2d_same_nhwc(x2, w.double(), None, 1), x2,
+                                   dy.double())
+      ref = torch.where(x.double() > 0, gx2, torch.zeros_like(gx2))
+      if use_add:
+        ref = ref + add.double()
+      dw = torch.zeros(3, 3, Cc, Cc, device=dev)
+      db = torch.zeros(Cc, device=dev)
+      dx = C.cf32_conv_bwd_fused(dy.to(dev), w.to(dev), x.to(dev), relu_x, dw, db,
+                                 add=add.to(dev) if use_add else None)
+      e = [((dx.double().cpu() - ref).abs().max() / ref.abs().max()).item(),
+           ((dw.double().cpu() - gw).abs().max() / gw.abs().max()).item(),
+           ((db.double().cpu() - gb).abs().max() / gb.abs().max()).item()]
+      worst = max(worst, *e)
+      print('fused bwd %2dx%2d C=%2d relu_x=%d add=%d: dx %.2e dw %.2e db %.2e' %
+            (H, W, Cc, relu_x, use_add, *e), flush=True)
+  return worst
+
+
+if __name__ == '__main__':
+  wf = check_fused_bwd()
+  print('fused worst %.2e %s' % (wf, 'OK' if wf <= 1e-5 else 'FAIL'))
+  sys.exit(0 if wf <= 1e-5 else 1)
