@@ -257,6 +257,23 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       const int base = offp + 2 * (ty - (p == 0 ? gm.tya0 : 0));
       const float* xp = x_s + (base * Wl + 2 * tx) * PP + 4 * g;
       const float* up = U_s + (g * COUT + co0 + c16) * 4;
+      // epilogue operands (mask / residual) of the 4 outputs: global loads
+      // issued before the MFMAs, so their latency hides under them
+      f4 pm[NH][4], pa[NH][4];
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+          const bool in = valid && oy < a.H && ox < a.W;
+          const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT +
+                                     co0 + 16 * h + 4 * g
+                               : 0;
+          pm[h][q] = (a.mask != nullptr && in) ? *reinterpret_cast<const f4*>(a.mask + o)
+                                               : f4{1.f, 1.f, 1.f, 1.f};
+          pa[h][q] = (a.add != nullptr && in) ? *reinterpret_cast<const f4*>(a.add + o)
+                                              : f4{0.f, 0.f, 0.f, 0.f};
+        }
 
       f4 acc[NH][16];
 #pragma unroll
@@ -338,12 +355,10 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
             if (!valid || oy >= a.H || ox >= a.W || (a.ablate & 8)) continue;
             const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT + co;
             f4 v = Y[2 * dy + dx] + bv;
-            if (a.mask != nullptr) {
-              const f4 m = *reinterpret_cast<const f4*>(a.mask + o);
+            const f4 m = pm[h][2 * dy + dx];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
-            }
-            if (a.add != nullptr) v += *reinterpret_cast<const f4*>(a.add + o);
+            for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
+            v += pa[h][2 * dy + dx];
             if (a.relu_out) {
 #pragma unroll
               for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
@@ -967,6 +982,16 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
       const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
       const int base = tile_s[valid ? 16 * wave + c16 : 0];
       const float* dp = d_s + base + 4 * g;
+      // the skip operand of the 4 outputs: global loads issued before the
+      // MFMAs so their latency hides under them
+      f4 addv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+        const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
+        const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + 4 * g : 0;
+        addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
+      }
       f4 acc[16];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1027,31 +1052,42 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
           f4 v = Y[2 * dy + dx];
 #pragma unroll
           for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
-          if (a.add != nullptr) v += *reinterpret_cast<const f4*>(a.add + o);
+          v += addv[2 * dy + dx];
           *reinterpret_cast<f4*>(a.out + o) = v;
         }
     }
 
-    // ---- weight gradient: k-step = one tile (lane group g = its pixel g)
+    // ---- weight gradient: k-step = one tile (lane group g = its pixel g);
+    // the operands of four k-steps are loaded before their MFMAs
     {
       constexpr int REST = (RT - 4 * KD) / 4;  // k-steps per wave 4..7
       const int k0 = wave < 4 ? wave * KD : 4 * KD + (wave - 4) * REST;
       const int k1 = wave < 4 ? k0 + KD : k0 + REST;
       const int py = g >> 1, px = g & 1;
-      for (int kt = k0; kt < k1; ++kt) {
-        const int base = tile_s[kt];
-        if (base < 0) continue;  // past the batch's last tile (uniform)
-        const int pofs = base + c16 + py * rowstr + px * PP;
-        const float bv = d_s[pofs + rowstr + PP];  // dY at the pixel, co = c16
-        dbacc += bv;
+      const int poff = c16 + py * rowstr + px * PP;
+      for (int kt = k0; kt < k1; kt += 4) {
+        int bases[4];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int u = 0; u < 4; ++u) bases[u] = kt + u < k1 ? tile_s[kt + u] : -1;
+        float bv[4], av[4][9];
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            float av = x_s[pofs + ky * rowstr + kx * PP];  // x, ci = c16
-            av = a.relu_x ? fmaxf(av, 0.f) : av;
-            wacc[3 * ky + kx] = mfma4(av, bv, wacc[3 * ky + kx]);
+        for (int u = 0; u < 4; ++u) {
+          const int pofs = (bases[u] >= 0 ? bases[u] : 0) + poff;
+          bv[u] = bases[u] >= 0 ? d_s[pofs + rowstr + PP] : 0.f;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) av[u][3 * ky + kx] = x_s[pofs + ky * rowstr + kx * PP];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          dbacc += bv[u];
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) {
+            const float v = a.relu_x ? fmaxf(av[u][tap], 0.f) : av[u][tap];
+            wacc[tap] = mfma4(v, bv[u], wacc[tap]);
           }
+        }
       }
     }
     if (r >= a.nranges) break;

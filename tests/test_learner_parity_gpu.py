@@ -78,10 +78,13 @@ def _compare(ref, hip, cos_min, rel_max, loss_rel=None):
     worst.append((rel, name, cos))
     assert cos >= cos_min, (name, cos)
     assert rel <= rel_max, (name, rel)
-  # the RMSProp update itself (same formula on both sides)
+  # the RMSProp update itself (same formula on both sides).  The first
+  # update is ~lr * g (~1e-8) on weights of ~1e-1, so p1 - p0 carries fp32
+  # quantisation of p1 (ulp ~4e-9): gradients equal to 1e-7 still round a
+  # few updates differently, hence the looser bound
   dr = (ref['p1'] - ref['p0']).double()
   dh = (hip['p1'] - hip['p0']).double()
-  assert ((dh - dr).norm() / dr.norm()).item() <= rel_max
+  assert ((dh - dr).norm() / dr.norm()).item() <= max(rel_max, 1e-3)
   return max(worst)
 
 
