@@ -44,7 +44,9 @@ __device__ __forceinline__ f4v mfma_f32(float a, float b, f4v c) {
 // h_pk_in == nullptr (the first step) reads the A operand straight from the
 // unpacked h_prev [B,H] (no host-side packing pass).  hpm_t (optional) gets
 // keep_t * h_prev, the A operand of the dW_h = sum_t hpm_t^T dG_t GEMM.
-template <int H>
+// RW: batch rows per workgroup (32, or 16 = half a packed row tile: twice
+// the workgroups, each streaming half of h)
+template <int H, int RW = 32>
 __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     const float* __restrict__ xw_t, const float* __restrict__ h_pk_in,
     const float* __restrict__ h_prev, const float* __restrict__ c_prev,
@@ -64,13 +66,16 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   // dispatch all working blocks share one XCD (and its L2)
   if (blockIdx.x % xpack) return;
   const int blk = blockIdx.x / xpack;
-  const int r0 = blockIdx.y * 32;
-  // epilogue operands (thread = (row r, unit u) for tid < 128)
+  static_assert(RW == 32 || RW == 16, "rows per workgroup");
+  constexpr int NMT = RW / 16;  // MFMA row tiles
+  const int r0 = blockIdx.y * RW;
+  const int t32 = r0 >> 5, mt0 = (r0 >> 4) & 1;  // packed 32-row tile, half
+  // epilogue operands (thread = (row r, unit u) for tid < 4 RW)
   const int er = tid >> 2, eu = tid & 3;
   const int egr = r0 + er;
   const int ej = blk * 4 + eu;
   float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, hp = 0.f, ekeep = 0.f;
-  if (tid < 128 && egr < B) {
+  if (tid < 4 * RW && egr < B) {
     const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
     xi = xw_t[g0];
     xc = xw_t[g0 + H];
@@ -87,20 +92,20 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
 #pragma unroll
   for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 4 * 16];
   // A operand: h[row = r0 + 16 mt + (l&15)][k = kw0 + 4s + (l>>4)] * keep
-  float ha[2][NS];
+  float ha[NMT][NS];
   if (h_pk_in != nullptr) {
-    const float* pk = h_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * H +
+    const float* pk = h_pk_in + static_cast<int64_t>(t32) * 32 * H +
                       wave * 2 * NS * 64 + lane;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
+    for (int mt = 0; mt < NMT; ++mt) {
       const int row = r0 + 16 * mt + (lane & 15);
       const float kf = (row < B && !done_t[row < B ? row : 0]) ? 1.f : 0.f;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) ha[mt][s] = pk[(mt * NS + s) * 64] * kf;
+      for (int s = 0; s < NS; ++s) ha[mt][s] = pk[((mt0 + mt) * NS + s) * 64] * kf;
     }
   } else {
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
+    for (int mt = 0; mt < NMT; ++mt) {
       const int row = r0 + 16 * mt + (lane & 15);
       const bool ok = row < B && !done_t[row < B ? row : 0];
       const float* hr = h_prev + static_cast<int64_t>(ok ? row : 0) * H + kw0 + (lane >> 4);
@@ -110,15 +115,14 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   }
   f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    acc[0] = mfma_f32(ha[0][s], wb[s], acc[0]);
-    acc[1] = mfma_f32(ha[1][s], wb[s], acc[1]);
-  }
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) acc[mt] = mfma_f32(ha[mt][s], wb[s], acc[mt]);
   red[wave][0][lane] = acc[0];
-  red[wave][1][lane] = acc[1];
+  if (NMT == 2) red[wave][1][lane] = acc[1];
   __syncthreads();
-  // reduce: output (row m in 0..31, col n in 0..15); D[m=4(l>>4)+i][n=l&15]
-  {
+  // reduce: output (row m in 0..RW-1, col n in 0..15); D[m=4(l>>4)+i][n=l&15]
+  if (tid < 16 * RW) {
     const int m = tid >> 4, n = tid & 15;  // 512 threads == 32 x 16 outputs
     const int mt = m >> 4, mm = m & 15;
     const int src_lane = ((mm >> 2) << 4) | n;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     g_s[m][n] = sum;
   }
   __syncthreads();
-  if (tid < 128 && egr < B) {
+  if (tid < 4 * RW && egr < B) {
     const float i = sigm(g_s[er][eu * 4 + 0] + xi);
     const float g = tanhf(g_s[er][eu * 4 + 1] + xc);
     const float f = sigm(g_s[er][eu * 4 + 2] + xf + 1.0f);
@@ -141,9 +145,9 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     c_t[hj] = c;
     h_t[hj] = h;
     {  // packed copy for the next step's A operand
-      const int k = ej, rr = egr - r0;
+      const int k = ej, rr = egr - 32 * t32;
       const int w = k / KW, s2 = (k % KW) >> 2, q = k & 3;
-      h_pk_out[static_cast<int64_t>(blockIdx.y) * 32 * H +
+      h_pk_out[static_cast<int64_t>(t32) * 32 * H +
                ((w * 2 + (rr >> 4)) * NS + s2) * 64 + (q << 4) + (rr & 15)] = h;
     }
     acts_t[g0] = i;
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
 // columns of dG) in [4H/16 w, 4H/16 (w+1)).  dh_rec = dG_{t+1} W_h^T.
 // dg_pk_in/out: dG in MFMA-operand order [row tile][wave][mt][s][lane];
 // wt: W_h^T packed [H/16][wave][s][lane] (lane <-> unit l&15, n = 4s+(l>>4)).
-template <int H>
+template <int H, int RW = 32>
 __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     const float* __restrict__ dh_out_t, const float* __restrict__ dg_pk_in,
     const uint8_t* __restrict__ done_next, const uint8_t* __restrict__ done_t,
@@ -180,12 +184,15 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
   if (blockIdx.x % xpack) return;
   const int bx = blockIdx.x / xpack;
   const int u0 = bx * 16;
-  const int r0 = blockIdx.y * 32;
-  // epilogue operands: thread = (row er, unit eu) for tid < 512
+  static_assert(RW == 32 || RW == 16, "rows per workgroup");
+  constexpr int NMT = RW / 16;
+  const int r0 = blockIdx.y * RW;
+  const int t32 = r0 >> 5, mt0 = (r0 >> 4) & 1;
+  // epilogue operands: thread = (row er, unit eu) for tid < 16 RW
   const int er = tid >> 4, eu = tid & 15;
   const int egr = r0 + er;
   const int ej = u0 + eu;
-  const bool eok = tid < 512 && egr < B;
+  const bool eok = tid < 16 * RW && egr < B;
   float dho = 0.f, ai = 0.f, ag = 0.f, af = 0.f, ao = 0.f, cc = 0.f, cpv = 0.f,
         dci = 0.f, kf = 0.f, knext = 1.f;
   if (eok) {
@@ -208,23 +215,22 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     const float* wsrc = wt + (static_cast<int64_t>(bx) * NW + wave) * NS * 64 + lane;
 #pragma unroll
     for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 64];
-    float da[2][NS];
-    const float* pk = dg_pk_in + static_cast<int64_t>(blockIdx.y) * 32 * 4 * H +
+    float da[NMT][NS];
+    const float* pk = dg_pk_in + static_cast<int64_t>(t32) * 32 * 4 * H +
                       wave * 2 * NS * 64 + lane;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) da[mt][s] = pk[(mt * NS + s) * 64];
+      for (int s = 0; s < NS; ++s) da[mt][s] = pk[((mt0 + mt) * NS + s) * 64];
     f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      acc[0] = mfma_f32(da[0][s], wb[s], acc[0]);
-      acc[1] = mfma_f32(da[1][s], wb[s], acc[1]);
-    }
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int mt = 0; mt < NMT; ++mt) acc[mt] = mfma_f32(da[mt][s], wb[s], acc[mt]);
     red[wave][0][lane] = acc[0];
-    red[wave][1][lane] = acc[1];
+    if (NMT == 2) red[wave][1][lane] = acc[1];
     __syncthreads();
-    if (tid < 512) {
+    if (tid < 16 * RW) {
       const int m = tid >> 4, n = tid & 15;
       const int mt = m >> 4, mm = m & 15;
       const int src_lane = ((mm >> 2) << 4) | n;
@@ -246,8 +252,8 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     const float dgv[4] = {dc * ag * ai * (1.f - ai), dc * ai * (1.f - ag * ag),
                           dc * kf * cpv * af * (1.f - af),
                           dh * tc * ao * (1.f - ao)};
-    const int rr = egr - r0;
-    float* pko = dg_pk_out + static_cast<int64_t>(blockIdx.y) * 32 * 4 * H;
+    const int rr = egr - 32 * t32;
+    float* pko = dg_pk_out + static_cast<int64_t>(t32) * 32 * 4 * H;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       dg_t[g0 + g * H] = dgv[g];
@@ -298,6 +304,13 @@ static int g_xpack = [] {
   const int v = e ? std::atoi(e) : 4;
   return v >= 1 && v <= 8 ? v : 4;
 }();
+// 16 batch rows per step workgroup (twice the workgroups, each streaming
+// half the packed h / dG): fp32 learner 13.01/13.05 -> 12.75/12.81 ms per
+// step at B = 32 (A/B/A/B on one box); SA_LSTM_ROWS=32 restores 32 rows
+static bool g_rows16 = [] {
+  const char* e = std::getenv("SA_LSTM_ROWS");
+  return !(e && std::atoi(e) == 32);
+}();
 int lstm_xpack(int v) {
   const int old = g_xpack;
   if (v >= 1 && v <= 8) g_xpack = v;
@@ -310,6 +323,13 @@ void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           float* h_pk_out, float* c_t, float* acts_t,
                           float* hpm_t, int B, int H, hipStream_t stream) {
   const int xp = g_xpack;
+  if (H == 256 && g_rows16) {
+    dim3 grid16(H / 4 * xp, (B + 15) / 16);
+    hipLaunchKernelGGL((lstm_fwd_step_kernel<256, 16>), grid16, dim3(512), 0, stream,
+                       xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
+                       c_t, acts_t, hpm_t, B, xp);
+    return;
+  }
   dim3 grid(H / 4 * xp, (B + 31) / 32);
   if (H == 256) {
     hipLaunchKernelGGL(lstm_fwd_step_kernel<256>, grid, dim3(512), 0, stream,
@@ -332,6 +352,13 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
   const int xp = g_xpack;
   dim3 grid(H / 16 * xp, (B + 31) / 32);
   __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
+  if (H == 256 && g_rows16) {
+    dim3 grid16(H / 16 * xp, (B + 15) / 16);
+    hipLaunchKernelGGL((lstm_bwd_step_kernel<256, 16>), grid16, dim3(1024), 0, stream,
+                       dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B, xp);
+    return;
+  }
   if (H == 256) {
     hipLaunchKernelGGL(lstm_bwd_step_kernel<256>, grid, dim3(1024), 0, stream,
                        dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
