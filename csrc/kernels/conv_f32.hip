@@ -964,10 +964,15 @@ constexpr int kPwRows = 2;  // pooled rows per tile
 // 4.6 bank conflicts per LDS instruction in rocprof).
 __host__ __device__ constexpr int pw_pitch(int W) { return W + 2 + ((5 - (W + 2)) % 16 + 16) % 16; }
 static_assert(pw_pitch(96) == 101 && pw_pitch(84) == 101 && pw_pitch(3) == 5, "pw pitch");
+// x: the fp32 4-channel image, or (u8_cs > 0) the uint8 frames themselves
+// with u8_cs <= 4 channels, scaled by 1/255 on the way into LDS (the same
+// tf.to_float(frame) / 255 as the forward, experiment.py:153-155)
 __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
-    const f4* __restrict__ x, const float* __restrict__ dP, const uint8_t* __restrict__ arg,
-    int H, int W, int Hp, int Wp, int pbh, int pbw, int tiles_per_img, int ntiles,
-    float* __restrict__ part) {
+    const void* __restrict__ xsrc, int u8_cs, const float* __restrict__ dP,
+    const uint8_t* __restrict__ arg, int H, int W, int Hp, int Wp, int pbh, int pbw,
+    int tiles_per_img, int ntiles, float* __restrict__ part) {
+  const f4* __restrict__ x = static_cast<const f4*>(xsrc);
+  const uint8_t* __restrict__ xu = static_cast<const uint8_t*>(xsrc);
   extern __shared__ __attribute__((aligned(16))) f4 xs[];  // [2*kPwRows+3][W+2]
   const int co = threadIdx.x & 15, ps = threadIdx.x >> 4;
   const int Wl = pw_pitch(W);
@@ -1004,8 +1009,18 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
       const int r = e / Wl, c = e - r * Wl;
       const int yy = ybase + r, xx = c - 1;
       f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = x[(static_cast<int64_t>(n) * H + yy) * W + xx];
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const int64_t pix = (static_cast<int64_t>(n) * H + yy) * W + xx;
+        if (u8_cs > 0) {
+          const uint8_t* p = xu + pix * u8_cs;
+          v[0] = static_cast<float>(p[0]) / 255.f;
+          if (u8_cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
+          if (u8_cs > 2) v[2] = static_cast<float>(p[2]) / 255.f;
+          if (u8_cs > 3) v[3] = static_cast<float>(p[3]) / 255.f;
+        } else {
+          v = x[pix];
+        }
+      }
       xs[e] = v;
     }
     __syncthreads();
@@ -1459,7 +1474,7 @@ bool conv_launch(const ConvArgs& a, int K, int S, int src, bool flip, hipStream_
   return false;
 }
 
-static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
+static bool run_pool_wgrad(const WgradArgs& a, float* ws, int u8_cs, hipStream_t s) {
   const PoolGeom& pg = a.pool;
   // pooled 3x3/2 SAME geometry of the (stride-1) conv output, Wp <= 64
   if (pg.Hp != (a.Ho + 1) / 2 || pg.Wp != (a.Wo + 1) / 2 || pg.Wp > 64 || a.Ho != a.H ||
@@ -1473,9 +1488,9 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
                                       sizeof(float) * 4 * 37 * 16);
   allow_lds(pool_wgrad_kernel, lds);
-  hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s,
-                     static_cast<const f4*>(a.src), a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh,
-                     pg.pbw, tpi, ntiles, ws);
+  hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s, a.src,
+                     u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,
+                     ntiles, ws);
   wgrad_reduce(ws, G, 1, 48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db, s);
   return true;
 }
@@ -1487,8 +1502,9 @@ bool wgrad_launch(const WgradArgs& a, int K, int S, int src, float* ws, hipStrea
   if (src == kSrcU8 && (a.Cin < 1 || a.Cin > 4)) return false;
   if (src == kSrcF32 && a.Cin % 4 != 0) return false;
   const bool gather = a.pool.arg != nullptr;
-  if (gather && src == kSrcF32 && pool_scatter_on() && pool_scatter_shape(K, S, cinp, a.Cout) &&
-      run_pool_wgrad(a, ws, s))
+  if (gather && (src == kSrcF32 || src == kSrcU8) && pool_scatter_on() &&
+      pool_scatter_shape(K, S, cinp, a.Cout) &&
+      run_pool_wgrad(a, ws, src == kSrcU8 ? a.Cin : 0, s))
     return true;
 #define SA_WG_CASE(CINP, KK, SS, SRC, COUT, NTT, WSM)                                     \
   if (cinp == CINP && K == KK && S == SS && src == SRC && a.Cout == COUT) {               \

@@ -45,6 +45,14 @@ POOL_GATHER = bool(POOL_GATHER_STAGES)
 # straight from (dP, argmax) in scatter form (pool_wgrad_kernel) instead of
 # maxpool_bwd + the dense wgrad; SA_F32_POOL_SCATTER=0 restores the latter.
 POOL_SCATTER = os.environ.get('SA_F32_POOL_SCATTER', '1') != '0'
+# uint8 frames straight into the first conv (x / 255 on the way into LDS)
+# instead of one fp32 x/255 image written first: the deep stage-0 kernels
+# measured slower on bytes (conv+pool 639 vs 529 + 120 us, scatter wgrad
+# 463 vs 229 us: per-pixel byte loads) and the shallow learner step too
+# (5.15 vs 5.01 ms), so both default to the fp32 image; kept switchable
+U8_DIRECT = {
+    'deep': os.environ.get('SA_F32_U8_DEEP', '0') == '1',
+    'shallow': os.environ.get('SA_F32_U8_SHALLOW', '0') == '1'}
 
 
 def supports(agent):
@@ -63,15 +71,17 @@ class _ShallowTorsoF32(torch.autograd.Function):
   @staticmethod
   def forward(ctx, frames, *params):
     C = ext()
-    # x / 255 once, as a 4-channel fp32 image (one 16-B load per pixel in
-    # the conv kernels); layer 1 weights see zero rows for the pad channel
-    x = C.cf32_frames_f32(frames.contiguous())
+    # layer 1 reads the uint8 frames itself (x / 255 on the way into LDS),
+    # or a 4-channel fp32 x / 255 image (one 16-B load per pixel)
+    x = frames.contiguous()
+    if not U8_DIRECT['shallow']:
+      x = C.cf32_frames_f32(x)
     acts = [x]
     geoms = []
     for i in range(3):
       w, b = params[2 * i], params[2 * i + 1]
-      if i == 0 and w.shape[2] != 4:
-        w = _pad_cin(w, 4)
+      if i == 0 and w.shape[2] != x.shape[3]:
+        w = _pad_cin(w, x.shape[3])  # zero rows for the image's pad channel
       k = w.shape[0]
       s = (4, 2, 2)[i]
       H, W = x.shape[1], x.shape[2]
@@ -96,8 +106,8 @@ class _ShallowTorsoF32(torch.autograd.Function):
     C.cf32_relu_mask_(dy, out)
     for i in reversed(range(3)):
       s, pt, pl, H, W = ctx.geoms[i]
-      if i == 0 and gv[0].shape[2] != 4:
-        dw4 = torch.zeros(gv[0].shape[:2] + (4,) + gv[0].shape[3:],
+      if i == 0 and gv[0].shape[2] != acts[0].shape[3]:
+        dw4 = torch.zeros(gv[0].shape[:2] + (acts[0].shape[3],) + gv[0].shape[3:],
                           dtype=torch.float32, device=dy.device)
         C.cf32_conv_wgrad(acts[0], dy, s, pt, pl, False, dw4, gv[1])
         gv[0].add_(dw4[:, :, :gv[0].shape[2]])
@@ -114,14 +124,18 @@ class _DeepTorsoF32(torch.autograd.Function):
   @staticmethod
   def forward(ctx, frames, *params):
     C = ext()
-    x = C.cf32_frames_f32(frames.contiguous())  # x / 255, 4 channels
+    # stage 0 reads a 4-channel fp32 x / 255 image (one 16-B load per pixel
+    # in the conv+pool and scatter-wgrad stagers), or the uint8 frames
+    x = frames.contiguous()
+    if not U8_DIRECT['deep']:
+      x = C.cf32_frames_f32(x)
     saved, meta = [], []
     p = 0
     for s in range(3):
       w, b = params[p], params[p + 1]
       p += 2
-      if s == 0 and w.shape[2] != 4:
-        w = _pad_cin(w, 4)
+      if s == 0 and w.shape[2] != x.shape[3]:
+        w = _pad_cin(w, x.shape[3])  # zero rows for the image's pad channel
       H, W = x.shape[1], x.shape[2]
       pbh = layers.same_pads(H, 3, 2)[0]
       pbw = layers.same_pads(W, 3, 2)[0]
@@ -185,10 +199,10 @@ class _DeepTorsoF32(torch.autograd.Function):
           DEBUG_TAPE[('dt', s, blk)] = dt.clone()
         dy = C.cf32_conv_bwd_fused(dt, w1, xa, True, gv[i1], gv[i1 + 1], add=dy)
       gw = gv[pb]
-      if s == 0 and gw.shape[2] != 4:
-        gw = torch.zeros(gw.shape[:2] + (4,) + gw.shape[3:], dtype=torch.float32,
-                         device=dy.device)
-      scatter = (s == 0 and POOL_SCATTER and stage_in.shape[3] == 4
+      if s == 0 and gw.shape[2] != stage_in.shape[3]:
+        gw = torch.zeros(gw.shape[:2] + (stage_in.shape[3],) + gw.shape[3:],
+                         dtype=torch.float32, device=dy.device)
+      scatter = (s == 0 and POOL_SCATTER and stage_in.shape[3] <= 4
                  and dy.shape[3] == 16)
       if s in POOL_GATHER_STAGES or scatter:
         # the conv kernels gather the pre-pool gradient from (dP, argmax)
