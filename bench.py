@@ -259,7 +259,10 @@ def main():
            'h2d_prefetch': main_res['h2d_prefetch'],
            'dist': dict(dist_info, **main_res['dist_extra']),
            'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
-                           'frames/s (BASELINE.md B), fp32 P100'}
+                           'frames/s (BASELINE.md B), fp32 P100',
+           # the ratio sets this learner-only synthetic number against the
+           # paper's end-to-end system (actors + learner, shallow model)
+           'vs_baseline_kind': 'learner-only vs paper end-to-end'}
     if extra is not None:
       cfg['bf16'] = {'value': round(fps(extra), 1),
                      'ms_per_step': round(1000 * extra['dt'] / args.steps, 3),

@@ -40,9 +40,10 @@ def main():
           ('valu/mfma', 'SQ_INSTS_VALU', 'SQ_INSTS_MFMA'),
           ('lds/mfma', 'SQ_INSTS_LDS', 'SQ_INSTS_MFMA'),
           ('conf/lds', 'SQ_LDS_BANK_CONFLICT', 'SQ_INSTS_LDS'),
-          ('waves', 'SQ_LEVEL_WAVES', 'SQ_BUSY_CYCLES')]
+          ('waves', 'SQ_LEVEL_WAVES', 'SQ_BUSY_CYCLES'),
+          ('mfmaB', 'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_BUSY_CYCLES')]
   print('%-44s' % 'kernel' + ''.join('%10s' % c[0] for c in cols) +
-        '%10s' % 'fetchMB')
+        '%10s%10s' % ('fetchMB', 'writeMB'))
   for k in sorted(agg):
     d = agg[k]
     row = '%-44s' % k[:44]
@@ -51,6 +52,9 @@ def main():
     n = max(1, len([x for x in disp[k] if 'pmc3' in x[0]]))
     row += '%10.0f' % (d.get('FETCH_SIZE', 0) / n / 1024) if d.get(
         'FETCH_SIZE') else '%10s' % '-'
+    n = max(1, len([x for x in disp[k] if 'pmc4' in x[0]]))
+    row += '%10.0f' % (d.get('WRITE_SIZE', 0) / n / 1024) if d.get(
+        'WRITE_SIZE') else '%10s' % '-'
     print(row)
 
 
