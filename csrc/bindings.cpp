@@ -313,6 +313,7 @@ void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
 void register_conv_ops(pybind11::module& m);     // conv_bindings.cpp
 void register_learner_ops(pybind11::module& m);  // learner_bindings.cpp
 void register_conv_f32_ops(pybind11::module& m); // conv_f32_bindings.cpp
+void register_board_server(pybind11::module& m); // board_server.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "scalable_agent_amd gfx950 HIP kernels";
@@ -344,4 +345,5 @@ PYBIND11_MODULE(_C, m) {
   register_conv_ops(m);
   register_learner_ops(m);
   register_conv_f32_ops(m);
+  register_board_server(m);
 }

@@ -18,6 +18,9 @@ inference on the GPU (a second GPU context per group) or, with
     ONE captured graph over all rows (torso, core, heads + Gumbel sampler; the
     LSTM state of every row resident on the device, updated only where the
     mask is set) -> D2H of each ready slot's outputs -> state 2 + futex wake
+    On a GPU with the HIP backend the loop is a C++ thread
+    (csrc/board_server.cpp, no Python and no GIL per batch); the graphs are
+    captured here first.  SA_BOARD_NATIVE=0 keeps the Python thread.
 
 Replaces the reference's per-request dynamic batching (experiment.py:534-546
 + batcher.cc) for process actors: the "batch" is every slot that is ready
@@ -26,6 +29,7 @@ when the server looks, the batch shape is fixed (no padding buckets).
 
 import logging
 import mmap
+import os
 import threading
 import time
 
@@ -179,10 +183,24 @@ class BoardServer(object):
     self.mask_dev = torch.zeros(b.R, 1, device=dev)
     self._graphs = {}
     self._thread = None
+    self._native = None
     self._stop = False
     self.error = None
-    self.batches = 0
-    self.rows_served = 0
+    self._batches = 0
+    self._rows = 0
+
+  @property
+  def batches(self):
+    return self._batches + (self._native.batches() if self._native else 0)
+
+  @property
+  def rows_served(self):
+    return self._rows + (self._native.rows_served() if self._native else 0)
+
+  @property
+  def native(self):
+    """True when the serving loop is the C++ thread."""
+    return self._native is not None
 
   def _body(self, has_instr):
     torch = self.torch
@@ -265,8 +283,8 @@ class BoardServer(object):
     for s in ready:
       native.atomic_store_u32(b.state_addr(s), RESPONSE)
       native.futex_wake(b.state_addr(s))
-    self.batches += 1
-    self.rows_served += rows
+    self._batches += 1
+    self._rows += rows
     return True
 
   # ------------------------------------------------------------ thread
@@ -279,17 +297,53 @@ class BoardServer(object):
       log.exception('inference server failed')
       self.board.close()
 
+  def _native_ok(self):
+    # the graphs' sampler must keep its state on the device (PhiloxStream of
+    # the HIP backend): a torch.Generator needs CUDAGraph.replay()'s host
+    # prologue, which a C++ hipGraphLaunch does not run
+    return (self.use_graph and self.pinned and
+            os.environ.get('SA_BOARD_NATIVE', '1') != '0' and
+            getattr(self.model.agent, 'backend', '') == 'hip')
+
+  def _start_native(self):
+    from .. import ops
+    b, m = self.board, self.model
+    variants = (False, True) if m.use_instruction else (False,)
+    for v in variants:  # every graph the loop may launch, captured up front
+      if v not in self._graphs:
+        self.prepare(has_instr=v)
+    exe = {v: g.raw_cuda_graph_exec() for v, g in self._graphs.items()}
+    instr_off = [o for n, _, _, o, _ in b.in_fields if n == 'instr_len'][0]
+    self._native = ops.ext().NativeBoardServer(
+        b.base, b.HDR, b.in_bytes, b.slot_out_bytes, b.S, b.M, instr_off,
+        self.in_dev.data_ptr(), self.out_dev.data_ptr(),
+        self.mask_dev.data_ptr(), self.mask_host.data_ptr(),
+        m.stream.cuda_stream, exe.get(False, 0),
+        exe.get(True, 0) if m.use_instruction else 0,
+        m.device.index if m.device.index is not None else
+        self.torch.cuda.current_device())
+    self._native.start()
+
   def start(self):
+    if self._native_ok():
+      self._start_native()
+      return
     self._thread = threading.Thread(target=self._run, daemon=True,
                                     name='inference-board-server')
     self._thread.start()
 
   def check(self):
+    if self._native is not None and self.error is None:
+      err = self._native.error()
+      if err:
+        self.error = err
     if self.error is not None:
       raise RuntimeError('inference server failed: %r' % (self.error,))
 
   def stop(self):
     self._stop = True
     native.futex_wake(self.board.seq_addr)
+    if self._native is not None:
+      self._native.stop()
     if self._thread is not None:
       self._thread.join(timeout=10)

@@ -1,0 +1,115 @@
+"""Native (C++) inference-board serving thread (csrc/board_server.cpp)
+against the Python server loop (runtime/inference_board.py): the same
+captured graph answers a request bit-identically through either loop, and
+the C++ thread serves forked CPU workers end to end (row counts, untouched
+state of rows that never asked, close on stop)."""
+
+import multiprocessing as mp
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from scalable_agent_amd.inference import InferenceModel
+from scalable_agent_amd.models import Agent
+from scalable_agent_amd.runtime import native
+from scalable_agent_amd.runtime.inference_board import (
+    REQUEST, RESPONSE, BoardClient, BoardServer, InferenceBoard)
+
+pytestmark = pytest.mark.gpu
+
+SHAPE = (24, 32, 3)
+
+
+def _model(cuda, instr=False):
+  agent = Agent(9, torso='deep', frame_shape=SHAPE, seed=2, backend='hip')
+  return InferenceModel(agent, cuda, use_instruction=instr, seed=1)
+
+
+def _fill(board, slot, rows, seed):
+  rng = np.random.RandomState(seed)
+  cl = BoardClient(board, slot, rows)
+  cl.inputs['frame'][:] = rng.randint(0, 256, cl.inputs['frame'].shape)
+  cl.inputs['reward'][:] = rng.randn(rows)
+  cl.inputs['last_action'][:] = rng.randint(0, 9, rows)
+  cl.inputs['done'][:] = False
+  return cl
+
+
+def test_native_loop_matches_python_loop(cuda):
+  board = InferenceBoard(3, 4, SHAPE, 9)
+  server = BoardServer(_model(cuda), board)
+  assert server._native_ok()
+  server.prepare(has_instr=False)
+  cl = _fill(board, 1, 3, seed=5)
+  outs = []
+  for loop in ('python', 'native'):
+    server.c.zero_()
+    server.h.zero_()
+    native.atomic_store_u32(board.state_addr(1), REQUEST)
+    if loop == 'python':
+      assert server.serve_once(timeout_ms=10)
+    else:
+      from scalable_agent_amd import ops
+      b, m = board, server.model
+      off = [o for n, _, _, o, _ in b.in_fields if n == 'instr_len'][0]
+      ns = ops.ext().NativeBoardServer(
+          b.base, b.HDR, b.in_bytes, b.slot_out_bytes, b.S, b.M, off,
+          server.in_dev.data_ptr(), server.out_dev.data_ptr(),
+          server.mask_dev.data_ptr(), server.mask_host.data_ptr(),
+          m.stream.cuda_stream, server._graphs[False].raw_cuda_graph_exec(),
+          0, cuda.index or 0)
+      assert ns.serve_once(10) and ns.rows_served() == 3
+    assert board.state(1) == RESPONSE
+    _, logits, baseline, c, h = [x.copy() for x in cl.wait()]
+    outs.append((logits, baseline, c, h, server.c.cpu().clone()))
+  for a, b in zip(outs[0], outs[1]):
+    assert np.array_equal(np.asarray(a), np.asarray(b))
+  # rows of slots that did not ask keep a zero state; slot 1's rows moved
+  st = outs[1][4]
+  assert float(st[0:4].abs().sum()) == 0.0 and float(st[8:].abs().sum()) == 0.0
+  assert float(st[4:7].abs().sum()) > 0.0 and float(st[7].abs().sum()) == 0.0
+  board.close()
+
+
+def _worker(board, slot, rows, n_steps, seed):
+  import os
+  cl = BoardClient(board, slot, rows)
+  rng = np.random.RandomState(seed)
+  for _ in range(n_steps):
+    cl.inputs['frame'][:] = rng.randint(0, 256, cl.inputs['frame'].shape)
+    cl.inputs['done'][:] = False
+    cl.launch()
+    a, lg, b, c, h = cl.wait()
+    assert a.shape == (rows,) and np.all((a >= 0) & (a < 9))
+    assert np.all(np.isfinite(lg)) and np.all(np.isfinite(c))
+  os._exit(0)
+
+
+def test_native_thread_serves_forked_workers(cuda):
+  board = InferenceBoard(4, 8, SHAPE, 9)
+  # the forked workers only use the shared board and futexes, never HIP
+  ctx = mp.get_context('fork')
+  procs = [ctx.Process(target=_worker, args=(board, s, r, 20, s))
+           for s, r in ((0, 8), (1, 5), (3, 2))]
+  for p in procs:
+    p.start()
+  server = BoardServer(_model(cuda), board)
+  server.start()
+  assert server.native
+  deadline = time.time() + 60
+  while any(p.is_alive() for p in procs) and time.time() < deadline:
+    server.check()
+    time.sleep(0.01)
+  for p in procs:
+    p.join(10)
+    assert p.exitcode == 0
+  server.check()
+  assert server.rows_served == 20 * (8 + 5 + 2)
+  assert server.batches >= 20
+  server.stop()
+  st = server.c.cpu()
+  assert float(st[16:24].abs().sum()) == 0.0  # slot 2 never asked
+  assert float(st[8 + 5:16].abs().sum()) == 0.0  # slot 1's unused rows
+  board.close()
