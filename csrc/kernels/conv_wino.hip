@@ -835,8 +835,13 @@ struct WinoBwdArgs {
   int relu_x;        // wgrad operand = relu(x)
 };
 
-template <int C, int RT, int MAXC, int KD>
-__global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
+// WWG: the weight gradient in Winograd form too (dL/dU = sum_tiles V(x) .*
+// Z(dY), dW = G^T P G, as wino_wgrad_kernel): waves 0-3 run the dgrad groups
+// only, waves 4-7 four k-steps of 4 tiles each, 256 instead of 576 weight-
+// gradient MFMAs per range.  One workgroup per CU (LDS) either way, so the
+// WWG instance may use up to 256 VGPRs.
+template <int C, int RT, int MAXC, int KD, bool WWG = false>
+__global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   constexpr int NW = 8, NTH = 512;
   constexpr int PP = C + 4;
   constexpr int C4 = C / 4;
@@ -844,7 +849,9 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   constexpr int NG = RT / 16;          // dgrad tasks (16-tile groups)
   constexpr int USTR = 4 * C * 4;      // floats per xi in U_s (one ci block)
   static_assert(C == 16, "fused backward: 16 channels (LDS)");
-  static_assert(NG == 4 && RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0, "work split");
+  static_assert(NG == 4, "four dgrad groups");
+  static_assert(WWG ? (RT % 16 == 0) : (RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0),
+                "work split");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Wl = 2 * a.TX + 2;
   const int rowstr = Wl * PP;
@@ -930,9 +937,10 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   __syncthreads();
   prefetch();
 
-  f4 wacc[9];
+  constexpr int NACC = WWG ? 16 : 9;  // Winograd xi (4 i + bc) or direct taps
+  f4 wacc[NACC];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) wacc[k] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < NACC; ++k) wacc[k] = f4{0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
 
   for (;;) {
@@ -1057,9 +1065,58 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
         }
     }
 
-    // ---- weight gradient: k-step = one tile (lane group g = its pixel g);
-    // the operands of four k-steps are loaded before their MFMAs
-    {
+    if constexpr (WWG) {
+      // ---- Winograd weight gradient: waves 4-7, k-step = 4 tiles (lane
+      // group g = tile 4 st + g), lane c16 = input channel of V and output
+      // channel of Z; acc[4 i + bc] += V[i][bc] (x) Z[i][bc]
+      if (wave >= 4) {
+        for (int st = wave - 4; st < RT / 4; st += 4) {
+          int base = tile_s[4 * st + g];
+          const bool valid = base >= 0;
+          base = valid ? base : 0;
+          const float* dp = d_s + base + rowstr + PP + c16;
+          float y00 = dp[0], y01 = dp[PP], y10 = dp[rowstr], y11 = dp[rowstr + PP];
+          if (!valid) y00 = y01 = y10 = y11 = 0.f;
+          dbacc += (y00 + y01) + (y10 + y11);
+          f4 zf[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float r0, r1;
+            if (i == 0) { r0 = y00; r1 = y01; }
+            else if (i == 1) { r0 = y00 + y10; r1 = y01 + y11; }
+            else if (i == 2) { r0 = y00 - y10; r1 = y01 - y11; }
+            else { r0 = -y10; r1 = -y11; }
+            zf[i] = f4{r0, r0 + r1, r0 - r1, -r1};
+          }
+          const float* xp = x_s + base + c16;
+          float d[4][4];
+#pragma unroll
+          for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx) {
+              const float v = xp[dy * rowstr + dx * PP];
+              d[dy][dx] = a.relu_x ? fmaxf(v, 0.f) : v;
+            }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float sq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (i == 0) sq[q] = d[0][q] - d[2][q];
+              else if (i == 1) sq[q] = d[1][q] + d[2][q];
+              else if (i == 2) sq[q] = d[2][q] - d[1][q];
+              else sq[q] = d[1][q] - d[3][q];
+            }
+            float V[4] = {sq[0] - sq[2], sq[1] + sq[2], sq[2] - sq[1], sq[1] - sq[3]};
+            if (!valid) V[0] = V[1] = V[2] = V[3] = 0.f;
+#pragma unroll
+            for (int bc = 0; bc < 4; ++bc) wacc[4 * i + bc] = mfma4(V[bc], zf[i][bc], wacc[4 * i + bc]);
+          }
+        }
+      }
+    } else {
+      // ---- weight gradient: k-step = one tile (lane group g = its pixel g);
+      // the operands of four k-steps are loaded before their MFMAs
       constexpr int REST = (RT - 4 * KD) / 4;  // k-steps per wave 4..7
       const int k0 = wave < 4 ? wave * KD : 4 * KD + (wave - 4) * REST;
       const int k1 = wave < 4 ? k0 + KD : k0 + REST;
@@ -1093,6 +1150,52 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
     if (r >= a.nranges) break;
   }
 
+  if constexpr (WWG) {
+    // ---- P = sum of waves 4-7 (fixed order), then dW = G^T P G per
+    // (ci, co) into this workgroup's slot (wino_wgrad_kernel's epilogue)
+    __syncthreads();
+    float* P = smem;                 // [16 xi][C ci][C co]
+    float* dB = smem + 16 * C * C;   // [C]
+    for (int k = 4; k < NW; ++k) {
+      if (wave == k) {
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float* pp = P + (xi * C + 4 * g + q) * C + c16;
+            *pp = (k == 4 ? 0.f : *pp) + wacc[xi][q];
+          }
+        float v = dbacc;
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (g == 0) dB[c16] = (k == 4 ? 0.f : dB[c16]) + v;
+      }
+      __syncthreads();
+    }
+    float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * C;
+    for (int e = threadIdx.x; e < C * C; e += NTH) {
+      const int ci = e / C, co = e - (e / C) * C;
+      float pm[4][4];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) pm[xi >> 2][xi & 3] = P[(xi * C + ci) * C + co];
+      float t[3][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        t[0][b] = pm[0][b] + 0.5f * (pm[1][b] + pm[2][b]);
+        t[1][b] = 0.5f * (pm[1][b] - pm[2][b]);
+        t[2][b] = 0.5f * (pm[1][b] + pm[2][b]) + pm[3][b];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        slot[((3 * i + 0) * C + ci) * C + co] = t[i][0] + 0.5f * (t[i][1] + t[i][2]);
+        slot[((3 * i + 1) * C + ci) * C + co] = 0.5f * (t[i][1] - t[i][2]);
+        slot[((3 * i + 2) * C + ci) * C + co] = 0.5f * (t[i][1] + t[i][2]) + t[i][3];
+      }
+    }
+    for (int co = threadIdx.x; co < C; co += NTH) slot[9 * C * C + co] = dB[co];
+    return;
+  }
+
   // ---- weight-gradient partials of the workgroup (fixed wave order)
   __syncthreads();
   float* red = smem;  // [9 * C + 1][C]
@@ -1120,7 +1223,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   for (int e = threadIdx.x; e < (9 * C + 1) * C; e += NTH) slot[e] = red[e];
 }
 
-template <int C, int RT, int MAXC, int KD>
+template <int C, int RT, int MAXC, int KD, bool WWG = false>
 bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
                   float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
                   float* dw, float* db, hipStream_t s) {
@@ -1150,7 +1253,7 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
-  auto kern = wino_bwd_fused_kernel<C, RT, MAXC, KD>;
+  auto kern = wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
   wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
@@ -1229,6 +1332,9 @@ bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, cons
                            float* out, int relu_x, int N, int H, int W, int C, float* ws,
                            int64_t ws_floats, float* dw, float* db, hipStream_t s) {
   static const int kd = env_int("SA_FUSED_BWD_KD", 4);
+  static const int wwg = env_int("SA_FUSED_BWD_WWG", 1);
+  if (C == 16 && wwg)
+    return run_wino_bwd<16, 64, 5, 0, true>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
   if (C == 16) {
     if (kd == 0) return run_wino_bwd<16, 64, 5, 0>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     if (kd == 8) return run_wino_bwd<16, 64, 5, 8>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
