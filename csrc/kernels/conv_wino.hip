@@ -1223,6 +1223,414 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
   for (int e = threadIdx.x; e < (9 * C + 1) * C; e += NTH) slot[e] = red[e];
 }
 
+// The 32-channel residual convs (18x24 and 9x12): the same single pass with
+// both gradients in Winograd form.  LDS holds U (64 KB) and the dY / x rows
+// of a 32-tile range (<= 90 KB at 18x24; a 64-tile range does not fit next
+// to U).  Waves 0-3 run the four data-gradient tasks (2 groups of 16 tiles x
+// 2 dX-channel blocks, 128 MFMAs each), waves 4-7 the weight gradient: wave
+// 4 + i owns B^T row i (xi = 4 i .. 4 i + 3) for all (ci block, co block)
+// pairs over the range's 8 k-steps (also 128 MFMAs).  Each workgroup walks a
+// CONTIGUOUS run of ranges, so the halo rows a range shares with the previous
+// one come from this CU's L2 instead of being refetched by another XCD.
+template <int RT, int MAXC>
+__global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a) {
+  constexpr int C = 32, NW = 8, NTH = 512;
+  constexpr int PP = C + 4;
+  constexpr int C4 = C / 4, LC4 = 3;
+  constexpr int NB = C / 16;
+  constexpr int NG = RT / 16;
+  constexpr int USTR = NB * 4 * C * 4;  // floats per xi in U_s
+  static_assert(NG * NB == 4, "four data-gradient tasks");
+  static_assert(MAXC <= 32, "stager mask");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Wl = 2 * a.TX + 2;
+  const int rowstr = Wl * PP;
+  float* U_s = smem;                         // [16 xi][NB][4 g][C][4]
+  float* d_s = U_s + 16 * C * C;             // dY rows [maxrows][Wl][PP]
+  float* x_s = d_s + a.maxrows * rowstr;     // x rows, same geometry
+  int* tab_s = reinterpret_cast<int*>(x_s + a.maxrows * rowstr);  // [maxrows]
+  int* tile_s = tab_s + a.maxrows;                                // [RT]
+
+  // U = G g' G^T of the flipped / transposed weights (the dgrad conv)
+  for (int e = threadIdx.x; e < C * C; e += NTH) {
+    const int co = e % C, ci = e / C;  // ci = dY channel, co = dX channel
+    float gk[3][3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[(((2 - ky) * 3 + (2 - kx)) * C + co) * C + ci];
+    float t[4][3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      t[0][kx] = gk[0][kx];
+      t[1][kx] = 0.5f * ((gk[0][kx] + gk[1][kx]) + gk[2][kx]);
+      t[2][kx] = 0.5f * ((gk[0][kx] - gk[1][kx]) + gk[2][kx]);
+      t[3][kx] = gk[2][kx];
+    }
+    const int b = ci >> 4, gq = (ci >> 2) & 3, v = ci & 3;
+#pragma unroll
+    for (int ra = 0; ra < 4; ++ra) {
+      const float u[4] = {t[ra][0], 0.5f * ((t[ra][0] + t[ra][1]) + t[ra][2]),
+                          0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        U_s[(4 * ra + rb) * USTR + ((b * 4 + gq) * C + co) * 4 + v] = u[rb];
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+
+  WinoArgs ga{};
+  ga.NT = a.NT; ga.TX = a.TX; ga.TY = a.TY; ga.rTX = a.rTX; ga.rTY = a.rTY;
+  // this workgroup's contiguous run of ranges (G <= nranges: never empty)
+  const int r_end = static_cast<int>((static_cast<int64_t>(blockIdx.x) + 1) * a.nranges / gridDim.x);
+  int r = static_cast<int>(static_cast<int64_t>(blockIdx.x) * a.nranges / gridDim.x);
+  if (r >= r_end) return;
+
+  int sl_L[MAXC], sl_o[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4 - 1), pix = e >> LC4;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sl_L[k] = L < a.maxrows ? L : -1;
+    sl_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * C + 4 * ch : -1;
+  }
+  auto build_tab = [&](int rr) {
+    const RangeGeom gm = range_geom(ga, rr, RT);
+    const int L = threadIdx.x;
+    if (L < a.maxrows) {
+      int v = -1;
+      if (L < gm.rows) {
+        const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
+        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
+        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W * C;
+      }
+      tab_s[L] = v;
+    }
+  };
+  f4 sd[MAXC], sx[MAXC];
+  uint32_t ok = 0;
+  auto prefetch = [&]() {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
+      const bool in = rb >= 0 && sl_o[k] >= 0;
+      const int off = in ? rb + sl_o[k] : 0;
+      sd[k] = *reinterpret_cast<const f4*>(a.dy + off);
+      sx[k] = *reinterpret_cast<const f4*>(a.x + off);
+      m |= static_cast<uint32_t>(in) << k;
+    }
+    ok = m;
+  };
+  build_tab(r);
+  __syncthreads();
+  prefetch();
+
+  // Commit the prefetched range to LDS, build its tile table and the next
+  // range's row table, start the next prefetch.  Both wave roles run it
+  // once per range (same barrier count); the roles are separate loops so
+  // the weight-gradient accumulators are not live in the data-gradient
+  // code (one loop with both would need > 256 VGPRs).
+  auto advance = [&]() {
+    __syncthreads();  // U_s written / the previous range's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      if (sl_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        const bool in = (ok >> k) & 1u;
+        f4 vd = sd[k], vx = sx[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          vd[q] = in ? vd[q] : 0.f;
+          vx[q] = in ? vx[q] : 0.f;
+        }
+        const int o = (e >> LC4) * PP + 4 * (e & (C4 - 1));
+        *reinterpret_cast<f4*>(d_s + o) = vd;
+        *reinterpret_cast<f4*>(x_s + o) = vx;
+      }
+    }
+    const int cur = r;
+    ++r;
+    const RangeGeom gm = range_geom(ga, cur, RT);
+    if (threadIdx.x < RT) {
+      const int t = gm.t0 + threadIdx.x;
+      int v = -1;
+      if (t < gm.t1) {
+        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
+        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int p = n - gm.n0;
+        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        v = ((offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx) * PP;
+      }
+      tile_s[threadIdx.x] = v;
+    }
+    if (r < r_end) build_tab(r);
+    __syncthreads();
+    if (r < r_end) prefetch();  // in flight under the MFMAs below
+    return gm;
+  };
+
+  const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform role
+  if (wv < 4) {
+    // ---- data gradient: task = (16-tile group grp, dX-channel block cb)
+    const int grp = wv % NG, cb = wv / NG;
+    for (;;) {
+      const RangeGeom gm = advance();
+      if (gm.t0 + 16 * grp < gm.t1) {
+        int t = gm.t0 + 16 * grp + c16;
+        const bool valid = t < gm.t1;
+        if (!valid) t = gm.t0;
+        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
+        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int base = tile_s[valid ? 16 * grp + c16 : 0];
+        const int co = 16 * cb + 4 * g;  // this lane's 4 dX channels
+        f4 addv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+          const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
+          const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + co : 0;
+          addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+        f4 acc[16];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float* dp = d_s + base + 16 * b + 4 * g;
+          f4 d[16];
+#pragma unroll
+          for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx)
+              d[4 * dy + dx] = *reinterpret_cast<const f4*>(dp + dy * rowstr + dx * PP);
+          f4 sv[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            sv[q] = d[q] - d[8 + q];
+            sv[4 + q] = d[4 + q] + d[8 + q];
+            sv[8 + q] = d[8 + q] - d[4 + q];
+            sv[12 + q] = d[4 + q] - d[12 + q];
+          }
+          f4 V[16];
+#pragma unroll
+          for (int ra = 0; ra < 4; ++ra) {
+            V[4 * ra + 0] = sv[4 * ra + 0] - sv[4 * ra + 2];
+            V[4 * ra + 1] = sv[4 * ra + 1] + sv[4 * ra + 2];
+            V[4 * ra + 2] = sv[4 * ra + 2] - sv[4 * ra + 1];
+            V[4 * ra + 3] = sv[4 * ra + 1] - sv[4 * ra + 3];
+          }
+          const float* up = U_s + ((b * 4 + g) * C + 16 * cb + c16) * 4;
+#pragma unroll
+          for (int xp2 = 0; xp2 < 8; ++xp2) {
+            const f4 u0 = *reinterpret_cast<const f4*>(up + (2 * xp2) * USTR);
+            const f4 u1 = *reinterpret_cast<const f4*>(up + (2 * xp2 + 1) * USTR);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              acc[2 * xp2] = mfma4(u0[v], V[2 * xp2][v], acc[2 * xp2]);
+              acc[2 * xp2 + 1] = mfma4(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1]);
+            }
+          }
+        }
+        f4 tt[4][2];
+#pragma unroll
+        for (int ra = 0; ra < 4; ++ra) {
+          tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
+          tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+        }
+        f4 Y[4];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
+          Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+        }
+        const float* xm = x_s + base + co;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) {
+            const int oy = 2 * ty + dy, ox = 2 * tx + dx;
+            if (!valid || oy >= a.H || ox >= a.W) continue;
+            const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + co;
+            const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rowstr + (dx + 1) * PP);
+            f4 v = Y[2 * dy + dx];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
+            v += addv[2 * dy + dx];
+            *reinterpret_cast<f4*>(a.out + o) = v;
+          }
+      }
+      if (r >= r_end) break;
+    }
+    __syncthreads();  // the loop's LDS reads are done (P overwrites U)
+    __syncthreads();  // P written by waves 4-7
+  } else {
+    // ---- Winograd weight gradient, B^T row AR of this wave: k-step = 4
+    // tiles (lane group g = tile 4 st + g); lane c16 = input channel of V
+    // and output channel of Z within their 16-channel blocks
+    f4 wacc[4][NB][NB];  // [bc][ci block][co block]
+#pragma unroll
+    for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int b2 = 0; b2 < NB; ++b2) wacc[bc][b][b2] = f4{0.f, 0.f, 0.f, 0.f};
+    float dbacc[NB] = {0.f, 0.f};
+    auto run = [&](auto ARc) {
+      constexpr int AR = decltype(ARc)::value;
+      for (;;) {
+        advance();
+        for (int st = 0; st < RT / 4; ++st) {
+          int base = tile_s[4 * st + g];
+          const bool valid = base >= 0;
+          base = valid ? base : 0;
+          f4 zf[NB];
+#pragma unroll
+          for (int b2 = 0; b2 < NB; ++b2) {
+            const float* dp = d_s + base + rowstr + PP + 16 * b2 + c16;
+            float y00 = dp[0], y01 = dp[PP], y10 = dp[rowstr], y11 = dp[rowstr + PP];
+            if (!valid) y00 = y01 = y10 = y11 = 0.f;
+            if constexpr (AR == 0) dbacc[b2] += (y00 + y01) + (y10 + y11);
+            float r0, r1;
+            if constexpr (AR == 0) { r0 = y00; r1 = y01; }
+            else if constexpr (AR == 1) { r0 = y00 + y10; r1 = y01 + y11; }
+            else if constexpr (AR == 2) { r0 = y00 - y10; r1 = y01 - y11; }
+            else { r0 = -y10; r1 = -y11; }
+            zf[b2] = f4{r0, r0 + r1, r0 - r1, -r1};
+          }
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const float* xp = x_s + base + 16 * b + c16;
+            // the two patch rows B^T row AR combines
+            constexpr int RA = AR == 0 ? 0 : (AR == 3 ? 1 : 1);
+            constexpr int RB = AR == 0 ? 2 : (AR == 3 ? 3 : 2);
+            float ra[4], rb[4];
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx) {
+              float u = xp[RA * rowstr + dx * PP], w = xp[RB * rowstr + dx * PP];
+              if (a.relu_x) {
+                u = fmaxf(u, 0.f);
+                w = fmaxf(w, 0.f);
+              }
+              ra[dx] = u;
+              rb[dx] = w;
+            }
+            float sq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if constexpr (AR == 0) sq[q] = ra[q] - rb[q];       // d0 - d2
+              else if constexpr (AR == 1) sq[q] = ra[q] + rb[q];  // d1 + d2
+              else if constexpr (AR == 2) sq[q] = rb[q] - ra[q];  // d2 - d1
+              else sq[q] = ra[q] - rb[q];                          // d1 - d3
+            }
+            const float V[4] = {sq[0] - sq[2], sq[1] + sq[2], sq[2] - sq[1], sq[1] - sq[3]};
+#pragma unroll
+            for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+              for (int b2 = 0; b2 < NB; ++b2)
+                wacc[bc][b][b2] = mfma4(V[bc], zf[b2][bc], wacc[bc][b][b2]);
+          }
+        }
+        if (r >= r_end) break;
+      }
+    };
+    if (wv == 4) run(std::integral_constant<int, 0>{});
+    else if (wv == 5) run(std::integral_constant<int, 1>{});
+    else if (wv == 6) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 3>{});
+
+    // ---- P[xi][ci][co] (disjoint xi rows per wave); dW = G^T P G below
+    __syncthreads();  // the loop's LDS reads are done (P overwrites U)
+    float* P = smem;                 // [16 xi][C ci][C co]
+    float* dB = smem + 16 * C * C;   // [C]
+    const int ar = wv - 4;
+#pragma unroll
+    for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int b2 = 0; b2 < NB; ++b2)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            P[((4 * ar + bc) * C + 16 * b + 4 * g + q) * C + 16 * b2 + c16] = wacc[bc][b][b2][q];
+    if (ar == 0) {
+#pragma unroll
+      for (int b2 = 0; b2 < NB; ++b2) {
+        float v = dbacc[b2];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (g == 0) dB[16 * b2 + c16] = v;
+      }
+    }
+    __syncthreads();
+  }
+  // per (ci, co) into this workgroup's slot (wino_wgrad_kernel's epilogue)
+  const float* P = smem;
+  const float* dB = smem + 16 * C * C;
+  float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * C;
+  for (int e = threadIdx.x; e < C * C; e += NTH) {
+    const int ci = e / C, co = e - (e / C) * C;
+    float pm[4][4];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) pm[xi >> 2][xi & 3] = P[(xi * C + ci) * C + co];
+    float t[3][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      t[0][b] = pm[0][b] + 0.5f * (pm[1][b] + pm[2][b]);
+      t[1][b] = 0.5f * (pm[1][b] - pm[2][b]);
+      t[2][b] = 0.5f * (pm[1][b] + pm[2][b]) + pm[3][b];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      slot[((3 * i + 0) * C + ci) * C + co] = t[i][0] + 0.5f * (t[i][1] + t[i][2]);
+      slot[((3 * i + 1) * C + ci) * C + co] = 0.5f * (t[i][1] - t[i][2]);
+      slot[((3 * i + 2) * C + ci) * C + co] = 0.5f * (t[i][1] + t[i][2]) + t[i][3];
+    }
+  }
+  for (int co = threadIdx.x; co < C; co += NTH) slot[9 * C * C + co] = dB[co];
+}
+
+template <int RT, int MAXC>
+bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float* add,
+                    float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
+                    float* dw, float* db, hipStream_t s) {
+  constexpr int C = 32;
+  const int TY = (H + 1) / 2, TX = (W + 1) / 2;
+  const int64_t NT = static_cast<int64_t>(N) * TY * TX;
+  if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
+  if (static_cast<int64_t>(N) * H * W * C >= (int64_t(1) << 31)) return false;
+  const int per_img = TY * TX;
+  const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
+  if (maxparts > kMaxParts) return false;
+  const int Wl = 2 * TX + 2;
+  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  if (maxrows * Wl * (C / 4) > MAXC * 512 || maxrows > 512) return false;
+  const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * Wl * (C + 4)) +
+                       sizeof(int) * (maxrows + RT);
+  if (bytes > 160 * 1024) return false;
+  const int rows16 = ((9 * C + 16) / 16) * 16;
+  const int nranges = static_cast<int>((NT + RT - 1) / RT);
+  const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * C);
+  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  if (G < 1) return false;
+  WinoBwdArgs a{};
+  a.dy = dy; a.w = w; a.x = x; a.add = add; a.out = out; a.part = ws;
+  a.N = N; a.H = H; a.W = W;
+  a.TY = TY; a.TX = TX; a.NT = static_cast<int>(NT); a.nranges = nranges;
+  a.maxrows = maxrows; a.rows16 = rows16;
+  a.rTX = 1.f / static_cast<float>(TX);
+  a.rTY = 1.f / static_cast<float>(TY);
+  a.relu_x = relu_x;
+  auto kern = wino_bwd_fused32_kernel<RT, MAXC>;
+  allow_lds_w(kern, bytes);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
+  wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
+  return true;
+}
+
 template <int C, int RT, int MAXC, int KD, bool WWG = false>
 bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
                   float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
@@ -1340,6 +1748,9 @@ bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, cons
     if (kd == 8) return run_wino_bwd<16, 64, 5, 8>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     return run_wino_bwd<16, 64, 5, 4>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
   }
+  static const int f32c = env_int("SA_FUSED_BWD32", 1);
+  if (C == 32 && f32c)
+    return run_wino_bwd32<32, 5>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
   return false;
 }
 

@@ -231,7 +231,9 @@ bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int ld
                      int ldb, bool ta, bool tb, bool ones_row, int splits, float* part,
                      const GemmEpilogue& ep, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return false;
-  if (lda % 4 || ldb % 4 || K % 4) return false;
+  // K quads are read as f4 only where K is an operand's column index
+  // (!ta: A[m][k], tb: B[n][k]); op(A) = A^T with B[k][n] reads K by rows
+  if (lda % 4 || ldb % 4 || (K % 4 && (!ta || tb))) return false;
   if (ones_row && ep.colsum == nullptr) return false;
   if (splits > 1 && part == nullptr) return false;
   Args a{};

@@ -213,7 +213,8 @@ void gemm_f32(at::Tensor A, at::Tensor B, bool ta, bool tb, at::Tensor C,
   const int64_t Kb = tb ? B.size(1) : B.size(0), N = tb ? B.size(0) : B.size(1);
   TORCH_CHECK(K == Kb, "gemm_f32: inner dimensions ", K, " vs ", Kb);
   TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "gemm_f32: C must be [M, >= N]");
-  TORCH_CHECK(K % 4 == 0, "gemm_f32: K must be a multiple of 4");
+  TORCH_CHECK(K % 4 == 0 || (ta && !tb),
+              "gemm_f32: K must be a multiple of 4 unless op(A) = A^T and op(B) = B");
   sa::GemmEpilogue ep{};
   ep.C = C.data_ptr<float>();
   ep.ldc = C.stride(0);

@@ -358,3 +358,40 @@ def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
   C.cf32_conv_wgrad(x.to(cuda), dy.to(cuda), 1, 1, 1, True, dw, db)
   assert rel_err(dw, rw) <= TOL
   assert rel_err(db, rb) <= TOL
+
+
+@pytest.mark.parametrize('N,H,W,Cc', [(256, 36, 48, 16), (256, 18, 24, 32), (256, 9, 12, 32),
+                                      (5, 11, 11, 16), (5, 11, 11, 32)])
+@pytest.mark.parametrize('relu_x,use_add', [(False, False), (True, True)])
+def test_conv_bwd_fused(cuda, N, H, W, Cc, relu_x, use_add):
+  """The residual-conv backward in one pass (conv_wino.hip
+  wino_bwd_fused_kernel for 16 channels, wino_bwd_fused32_kernel for 32):
+  dX = dgrad(dY, W) * (x > 0) [+ add], dW += relu?(x)^T dY, db += sum dY,
+  against float64 - at N = 256 every persistent workgroup walks many ranges
+  (contiguous range runs, cross-range prefetch, image boundaries inside a
+  range), and 11x11 exercises odd sizes (partial 2x2 tiles)."""
+  C = _C()
+  g = torch.Generator().manual_seed(N * H + Cc)
+  x = torch.randn(N, H, W, Cc, generator=g)
+  w = torch.randn(3, 3, Cc, Cc, generator=g) / (9 * Cc) ** 0.5
+  dy = torch.randn(N, H, W, Cc, generator=g)
+  add = torch.randn(N, H, W, Cc, generator=g)
+  x64 = x.double().requires_grad_(True)
+  xin = x64.clamp(min=0) if relu_x else x64
+  w64 = w.double().requires_grad_(True)
+  b64 = torch.zeros(Cc, dtype=torch.float64, requires_grad=True)
+  _, gw, gb = torch.autograd.grad(layers.conv2d_same_nhwc(xin, w64, b64, 1),
+                                  (x64, w64, b64), dy.double())
+  x2 = x.double().requires_grad_(True)
+  (gx,) = torch.autograd.grad(layers.conv2d_same_nhwc(x2, w.double(), None, 1), x2,
+                              dy.double())
+  ref = torch.where(x.double() > 0, gx, torch.zeros_like(gx))
+  if use_add:
+    ref = ref + add.double()
+  dw = torch.zeros(3, 3, Cc, Cc, device=cuda)
+  db = torch.zeros(Cc, device=cuda)
+  dx = C.cf32_conv_bwd_fused(dy.to(cuda), w.to(cuda), x.to(cuda), relu_x, dw, db,
+                             add=add.to(cuda) if use_add else None)
+  assert rel_err(dx, ref) <= TOL
+  assert rel_err(dw, gw) <= TOL
+  assert rel_err(db, gb) <= TOL

@@ -105,3 +105,20 @@ def test_gemm_f32_deterministic(cuda):
     _C().gemm_f32(X, dh, True, False, dw, accumulate=True, colsum=db)
     outs.append((dw, db))
   assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('M,N,K', [(256, 1024, 14), (272, 1024, 707), (256, 256, 3233)])
+def test_gemm_f32_weight_grad_any_k(cuda, M, N, K):
+  """op(A) = A^T, op(B) = B (the weight-gradient form, K = T*B rows) takes
+  any K: a data-parallel rank's B*(T+1) need not be a multiple of 4 (two
+  ranks of the 4-row dp_check batch: 7 * 2 = 14); the split-K tail chunk is
+  row-masked."""
+  g = torch.Generator().manual_seed(M + N + K)
+  A = torch.randn(K, M, generator=g)
+  B = torch.randn(K, N, generator=g)
+  ref = A.double().t() @ B.double()
+  C = torch.zeros(M, N, device=cuda)
+  db = torch.zeros(N, device=cuda)
+  _C().gemm_f32(A.to(cuda), B.to(cuda), True, False, C, accumulate=True, colsum=db)
+  assert _rel(C, ref) <= 2e-6
+  assert _rel(db, B.double().sum(0)) <= 2e-6
