@@ -264,14 +264,15 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
   check_launch("cf32_conv_wgrad");
 }
 
-// Backward of a 3x3/1 SAME conv whose input x is also the data gradient's
-// ReLU mask (the deep torso's residual convs): returns dX = dgrad(dy, w) *
-// (x > 0) [+ add] and accumulates dw += relu?(x)^T dy, db += sum dy.  One
-// fused pass (dY and x read once) where a kernel covers the shape, else the
+// Backward of a 3x3/1 SAME conv: returns dX = dgrad(dy, w) [* (x > 0) when
+// mask: the deep torso's residual convs, whose input is also the data
+// gradient's ReLU mask] [+ add] and accumulates dw += relu?(x)^T dy, db +=
+// sum dy.  One fused pass (dY and x read once) where a kernel covers the
+// shape (residual convs, the stage heads' 16 -> 32 and 32 -> 32), else the
 // separate data-gradient and weight-gradient kernels.
 at::Tensor conv_bwd_fused(at::Tensor dy, at::Tensor w, at::Tensor x, bool relu_x,
                           at::Tensor dw, c10::optional<at::Tensor> db,
-                          c10::optional<at::Tensor> add) {
+                          c10::optional<at::Tensor> add, bool mask) {
   check_nhwc(dy, "dy");
   check_nhwc(x, "x");
   check_w(w);
@@ -290,22 +291,23 @@ at::Tensor conv_bwd_fused(at::Tensor dy, at::Tensor w, at::Tensor x, bool relu_x
                 "db");
     dbp = db->data_ptr<float>();
   }
-  const int C = x.size(3);
-  if (w.size(2) == w.size(3) && dy.sizes() == x.sizes() && sa::cf32::wino_bwd_fused_enabled()) {
-    const int64_t wsf = sa::cf32::wgrad_workspace_floats(3, C, C);
+  const int C = x.size(3), Cy = dy.size(3);
+  if (sa::cf32::wino_bwd_fused_enabled()) {
+    const int64_t wsf = sa::cf32::wgrad_workspace_floats(3, C, Cy);
     auto ws = at::empty({wsf}, dy.options());
     if (sa::cf32::wino_bwd_fused_launch(dy.data_ptr<float>(), w.data_ptr<float>(),
                                         x.data_ptr<float>(), addp, dx.data_ptr<float>(),
-                                        relu_x ? 1 : 0, x.size(0), x.size(1), x.size(2), C,
-                                        ws.data_ptr<float>(), wsf, dw.data_ptr<float>(), dbp,
-                                        stream())) {
+                                        relu_x ? 1 : 0, mask ? 1 : 0, x.size(0), x.size(1),
+                                        x.size(2), C, Cy, ws.data_ptr<float>(), wsf,
+                                        dw.data_ptr<float>(), dbp, stream())) {
       check_launch("cf32_conv_bwd_fused");
       return dx;
     }
   }
-  // separate kernels: weight gradient, then the masked data gradient
+  // separate kernels: weight gradient, then the (masked) data gradient
   conv_wgrad(x, dy, 1, 1, 1, relu_x, dw, db, c10::nullopt, 0, 0);
-  return conv_dgrad(dy, w, 1, 1, 1, x.size(1), x.size(2), x, add, c10::nullopt, 0, 0);
+  return conv_dgrad(dy, w, 1, 1, 1, x.size(1), x.size(2),
+                    mask ? c10::optional<at::Tensor>(x) : c10::nullopt, add, c10::nullopt, 0, 0);
 }
 
 // Fused stage head: maxpool3x3/2(conv3x3/1(x) + b) -> {pooled, argmax}
@@ -403,7 +405,8 @@ void register_conv_f32_ops(pybind11::module& m) {
         arg("relu_in"), arg("dw"), arg("db") = pybind11::none(),
         arg("pool_arg") = pybind11::none(), arg("pool_pbh") = 0, arg("pool_pbw") = 0);
   m.def("cf32_conv_bwd_fused", &conv_bwd_fused, arg("dy"), arg("w"), arg("x"), arg("relu_x"),
-        arg("dw"), arg("db") = pybind11::none(), arg("add") = pybind11::none());
+        arg("dw"), arg("db") = pybind11::none(), arg("add") = pybind11::none(),
+        arg("mask") = true);
   m.def("cf32_conv_pool_fwd", &conv_pool_fwd);
   m.def("cf32_maxpool_fwd", &maxpool_fwd);
   m.def("cf32_maxpool_bwd", &maxpool_bwd);

@@ -88,15 +88,16 @@ bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
 // the same fixed-order slot reduction as the direct kernel.
 bool wino_wgrad_enabled();
 bool wino_wgrad_launch(const WgradArgs& a, float* ws, hipStream_t s);
-// Fused backward of a 3x3/1 SAME conv whose input x is the data gradient's
-// ReLU mask (the deep torso's residual convs): dX = dgrad(dY) * (x > 0)
-// [+ add]; dW += sum relu?(x) (x) dY, db += sum dY (accumulated); dY and x
-// read once.  `ws` holds >= ws_floats floats of slot workspace.  False when
-// the shape is not covered (then nothing ran).
+// Fused backward of a 3x3/1 SAME conv (x: C channels, dY: Cy): dX =
+// dgrad(dY) [* (x > 0) when mask_x: the residual convs, whose input is the
+// mask] [+ add]; dW += sum relu?(x) (x) dY, db += sum dY (accumulated); dY
+// and x read once.  `ws` holds >= ws_floats floats of slot workspace.
+// False when the shape is not covered (then nothing ran).
 bool wino_bwd_fused_enabled();
 bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, const float* add,
-                           float* out, int relu_x, int N, int H, int W, int C, float* ws,
-                           int64_t ws_floats, float* dw, float* db, hipStream_t s);
+                           float* out, int relu_x, int mask_x, int N, int H, int W, int C,
+                           int Cy, float* ws, int64_t ws_floats, float* dw, float* db,
+                           hipStream_t s);
 // Fixed-order sum of G slot partials [G][rows16][Cout] (rows tap*Cin + ci,
 // row 9*Cin = bias) accumulated into dW (HWIO 3x3) / db.
 void wgrad_reduce_slots(const float* part, int G, int rows16, int Cout, int Cin, float* dw,

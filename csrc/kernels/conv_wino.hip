@@ -69,7 +69,28 @@ struct WinoArgs {
   int maxrows;  // LDS row capacity (>= rows of every range)
   int ablate;  // measurement knob (SA_WINO_ABLATE): 1 no tasks, 2 no global
                // loads, 4 no LDS commit, 8 no stores
+  int runs;    // 1: each workgroup walks a contiguous run of ranges (halo rows
+               // shared with the previous range hit this CU's L2), 0: strided
 };
+
+// Range walk of a persistent workgroup: a contiguous run [r, end) with step
+// 1, or every gridDim.x-th range from blockIdx.x.
+struct RangeWalk {
+  int r, end, step;
+};
+__device__ __forceinline__ RangeWalk range_walk(int nranges, int runs) {
+  RangeWalk w;
+  if (runs) {
+    w.r = static_cast<int>(static_cast<int64_t>(blockIdx.x) * nranges / gridDim.x);
+    w.end = static_cast<int>((static_cast<int64_t>(blockIdx.x) + 1) * nranges / gridDim.x);
+    w.step = 1;
+  } else {
+    w.r = blockIdx.x;
+    w.end = nranges;
+    w.step = gridDim.x;
+  }
+  return w;
+}
 
 // Rows staged for a range: image part p (image n0 + p) contributes input
 // rows 2 tya_p - 1 .. 2 tyb_p + 2 at LDS rows off_p ...; a tile (n, ty) of
@@ -165,8 +186,9 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   const int Wl = 2 * a.TX + 2;
   const int rowstr = Wl * PP;
 
-  int r = blockIdx.x;
-  if (r >= a.nranges) return;  // uniform: the whole workgroup leaves
+  const RangeWalk rw = range_walk(a.nranges, a.runs);
+  int r = rw.r;
+  if (r >= rw.end) return;  // uniform: the whole workgroup leaves
 
   // ---- register prefetch of a range's input rows.  Thread k-slot e of a
   // range always stages LDS element e = (row L, column, channel quad): the
@@ -237,10 +259,10 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       }
     }
     const int cur = r;
-    r += gridDim.x;
-    if (r < a.nranges) build_tab(r);
+    r += rw.step;
+    if (r < rw.end) build_tab(r);
     __syncthreads();
-    if (r < a.nranges) prefetch();  // in flight under the MFMAs below
+    if (r < rw.end) prefetch();  // in flight under the MFMAs below
     const RangeGeom gm = range_geom(a, cur, RT);
 
     for (int task = (a.ablate & 1) ? NTASK : wave; task < NTASK; task += NW) {
@@ -367,7 +389,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
           }
       }
     }
-    if (r >= a.nranges) break;
+    if (r >= rw.end) break;
   }
 }
 
@@ -424,6 +446,8 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   a.maxrows = maxrows;
   static const int ablate = env_int("SA_WINO_ABLATE", 0);
   a.ablate = ablate;
+  static const int runs = env_int("SA_WINO_RUNS", 1);
+  a.runs = runs;
   const int per_cu = std::max(1, std::min(WPS * 4 / NW, static_cast<int>((160 * 1024) / (bytes + 256))));
   static const int occ_env = env_int("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
@@ -833,6 +857,9 @@ struct WinoBwdArgs {
   int TY, TX, NT, nranges, maxrows, rows16;
   float rTX, rTY;
   int relu_x;        // wgrad operand = relu(x)
+  int mask_x = 1;    // dX masked by (x > 0) (fused32 kernel; the 16-channel one always masks)
+  int ablate = 0;    // measurement knob (SA_FUSED_ABLATE): 1 no pair wait, 2 no dgrad, 4 no wgrad
+  int runs = 1;      // contiguous range runs (wino_bwd_fused_kernel; fused32 always)
 };
 
 // WWG: the weight gradient in Winograd form too (dL/dU = sum_tiles V(x) .*
@@ -840,7 +867,7 @@ struct WinoBwdArgs {
 // only, waves 4-7 four k-steps of 4 tiles each, 256 instead of 576 weight-
 // gradient MFMAs per range.  One workgroup per CU (LDS) either way, so the
 // WWG instance may use up to 256 VGPRs.
-template <int C, int RT, int MAXC, int KD, bool WWG = false>
+template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false>
 __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   constexpr int NW = 8, NTH = 512;
   constexpr int PP = C + 4;
@@ -891,8 +918,9 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
 
   WinoArgs ga{};
   ga.NT = a.NT; ga.TX = a.TX; ga.TY = a.TY; ga.rTX = a.rTX; ga.rTY = a.rTY;
-  int r = blockIdx.x;
-  if (r >= a.nranges) return;
+  const RangeWalk rw = range_walk(a.nranges, a.runs);
+  int r = rw.r;
+  if (r >= rw.end) return;
 
   // staging slots: element e of both images = (row L, col, quad)
   int sl_L[MAXC], sl_o[MAXC];
@@ -962,7 +990,7 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       }
     }
     const int cur = r;
-    r += gridDim.x;
+    r += rw.step;
     const RangeGeom gm = range_geom(ga, cur, RT);
     // tile table of this range: LDS offset of each tile's patch origin
     if (threadIdx.x < RT) {
@@ -977,9 +1005,9 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       }
       tile_s[threadIdx.x] = v;
     }
-    if (r < a.nranges) build_tab(r);
+    if (r < rw.end) build_tab(r);
     __syncthreads();
-    if (r < a.nranges) prefetch();
+    if (r < rw.end) prefetch();
 
     // ---- data gradient: waves 0..3, one 16-tile group each
     if (wave < NG && gm.t0 + 16 * wave < gm.t1) {
@@ -1095,7 +1123,7 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
 #pragma unroll
             for (int dx = 0; dx < 4; ++dx) {
               const float v = xp[dy * rowstr + dx * PP];
-              d[dy][dx] = a.relu_x ? fmaxf(v, 0.f) : v;
+              d[dy][dx] = RELU ? fmaxf(v, 0.f) : v;
             }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -1141,13 +1169,13 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
           dbacc += bv[u];
 #pragma unroll
           for (int tap = 0; tap < 9; ++tap) {
-            const float v = a.relu_x ? fmaxf(av[u][tap], 0.f) : av[u][tap];
+            const float v = RELU ? fmaxf(av[u][tap], 0.f) : av[u][tap];
             wacc[tap] = mfma4(v, bv[u], wacc[tap]);
           }
         }
       }
     }
-    if (r >= a.nranges) break;
+    if (r >= rw.end) break;
   }
 
   if constexpr (WWG) {
@@ -1223,42 +1251,58 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
   for (int e = threadIdx.x; e < (9 * C + 1) * C; e += NTH) slot[e] = red[e];
 }
 
-// The 32-channel residual convs (18x24 and 9x12): the same single pass with
-// both gradients in Winograd form.  LDS holds U (64 KB) and the dY / x rows
-// of a 32-tile range (<= 90 KB at 18x24; a 64-tile range does not fit next
-// to U).  Waves 0-3 run the four data-gradient tasks (2 groups of 16 tiles x
-// 2 dX-channel blocks, 128 MFMAs each), waves 4-7 the weight gradient: wave
-// 4 + i owns B^T row i (xi = 4 i .. 4 i + 3) for all (ci block, co block)
-// pairs over the range's 8 k-steps (also 128 MFMAs).  Each workgroup walks a
-// CONTIGUOUS run of ranges, so the halo rows a range shares with the previous
-// one come from this CU's L2 instead of being refetched by another XCD.
-template <int RT, int MAXC>
+// The 32-channel convs (res32 at 18x24 and 9x12, the stage-2 head 32 -> 32)
+// and the stage-1 head (16 -> 32 at 36x48): the same single pass with both
+// gradients in Winograd form, for x with CX channels and dY with CY.  LDS
+// holds U (16 CX CY floats) and the dY / x rows of a 32-tile range (a 64-
+// tile range does not fit next to U).  Waves 0-3 run the data gradient,
+// waves 4-7 the weight gradient: wave 4 + i owns B^T row i (xi = 4 i ..
+// 4 i + 3) for all (ci block, co block) pairs over the range's 8 k-steps.
+// Data-gradient tasks are (16-tile group, dX-channel block); with only two
+// of them (CX = 16) each is split over a wave pair by dY-channel block, and
+// the odd wave hands its partial output transform (A^T M A is linear in M)
+// to the even one through LDS (workgroup-scope release/acquire flag).  Each
+// wave role runs 64 (CX = 16) or 128 MFMAs per range.  mask_x = 0 (stage
+// heads: their input is the previous stage's raw output) skips the ReLU
+// mask.  Each workgroup walks a CONTIGUOUS run of ranges, so the halo rows
+// a range shares with the previous one come from this CU's L2 instead of
+// being refetched by another XCD.
+template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK>
 __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a) {
-  constexpr int C = 32, NW = 8, NTH = 512;
-  constexpr int PP = C + 4;
-  constexpr int C4 = C / 4, LC4 = 3;
-  constexpr int NB = C / 16;
+  constexpr int NW = 8, NTH = 512;
+  constexpr int PPX = CX + 4, PPY = CY + 4;  // odd 16-B units per pixel
+  constexpr int C4X = CX / 4, C4Y = CY / 4;
+  constexpr int LC4X = C4X == 4 ? 2 : 3, LC4Y = C4Y == 4 ? 2 : 3;
+  constexpr int NBX = CX / 16, NBY = CY / 16;
   constexpr int NG = RT / 16;
-  constexpr int USTR = NB * 4 * C * 4;  // floats per xi in U_s
-  static_assert(NG * NB == 4, "four data-gradient tasks");
-  static_assert(MAXC <= 32, "stager mask");
+  constexpr int NTASK = NG * NBX;            // (group, dX-channel block)
+  constexpr int DSPLIT = 4 / NTASK;          // waves per task (dY blocks)
+  constexpr int NBT = NBY / DSPLIT;          // dY blocks per wave
+  constexpr int USTR = NBY * 4 * CX * 4;     // floats per xi in U_s
+  static_assert(NTASK * DSPLIT == 4 && NBT * DSPLIT == NBY, "four data-gradient waves");
+  static_assert(C4X == 4 || C4X == 8, "CX");
+  static_assert(C4Y == 4 || C4Y == 8, "CY");
+  static_assert(MAXCX <= 32 && MAXCY <= 32, "stager masks");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int Wl = 2 * a.TX + 2;
-  const int rowstr = Wl * PP;
-  float* U_s = smem;                         // [16 xi][NB][4 g][C][4]
-  float* d_s = U_s + 16 * C * C;             // dY rows [maxrows][Wl][PP]
-  float* x_s = d_s + a.maxrows * rowstr;     // x rows, same geometry
-  int* tab_s = reinterpret_cast<int*>(x_s + a.maxrows * rowstr);  // [maxrows]
-  int* tile_s = tab_s + a.maxrows;                                // [RT]
+  const int rsx = Wl * PPX, rsy = Wl * PPY;
+  float* U_s = smem;                         // [16 xi][NBY][4 g][CX][4]
+  float* d_s = U_s + 16 * CX * CY;           // dY rows [maxrows][Wl][PPY]
+  float* x_s = d_s + a.maxrows * rsy;        // x rows [maxrows][Wl][PPX]
+  f4* ybuf = reinterpret_cast<f4*>(x_s + a.maxrows * rsx);  // [2 pairs][4][64] (DSPLIT 2)
+  int* flag_s = reinterpret_cast<int*>(ybuf + (DSPLIT == 2 ? 2 * 4 * 64 : 0));  // [2]
+  int* tab_s = flag_s + 2;                   // [maxrows]
+  int* tile_s = tab_s + a.maxrows;           // [RT] patch-origin pixel (row * Wl + col)
 
-  // U = G g' G^T of the flipped / transposed weights (the dgrad conv)
-  for (int e = threadIdx.x; e < C * C; e += NTH) {
-    const int co = e % C, ci = e / C;  // ci = dY channel, co = dX channel
+  // U = G g' G^T of the flipped / transposed weights (the dgrad conv);
+  // forward weights HWIO [3][3][CX][CY]
+  for (int e = threadIdx.x; e < CX * CY; e += NTH) {
+    const int co = e % CX, ci = e / CX;  // ci = dY channel, co = dX channel
     float gk[3][3];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[(((2 - ky) * 3 + (2 - kx)) * C + co) * C + ci];
+      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[(((2 - ky) * 3 + (2 - kx)) * CX + co) * CY + ci];
     float t[4][3];
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
@@ -1274,9 +1318,10 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
                           0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
-        U_s[(4 * ra + rb) * USTR + ((b * 4 + gq) * C + co) * 4 + v] = u[rb];
+        U_s[(4 * ra + rb) * USTR + ((b * 4 + gq) * CX + co) * 4 + v] = u[rb];
     }
   }
+  if (threadIdx.x < 2) flag_s[threadIdx.x] = 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
 
@@ -1287,16 +1332,26 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   int r = static_cast<int>(static_cast<int64_t>(blockIdx.x) * a.nranges / gridDim.x);
   if (r >= r_end) return;
 
-  int sl_L[MAXC], sl_o[MAXC];
+  // staging slots: element e = (row L, col, quad) of the dY image and of x
+  int sy_L[MAXCY], sy_o[MAXCY], sx_L[MAXCX], sx_o[MAXCX];
 #pragma unroll
-  for (int k = 0; k < MAXC; ++k) {
+  for (int k = 0; k < MAXCY; ++k) {
     const int e = threadIdx.x + k * NTH;
-    const int ch = e & (C4 - 1), pix = e >> LC4;
+    const int ch = e & (C4Y - 1), pix = e >> LC4Y;
     const int L = pix / Wl, col = pix - L * Wl;
-    sl_L[k] = L < a.maxrows ? L : -1;
-    sl_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * C + 4 * ch : -1;
+    sy_L[k] = L < a.maxrows ? L : -1;
+    sy_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * CY + 4 * ch : -1;
   }
-  auto build_tab = [&](int rr) {
+#pragma unroll
+  for (int k = 0; k < MAXCX; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4X - 1), pix = e >> LC4X;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sx_L[k] = L < a.maxrows ? L : -1;
+    sx_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * CX + 4 * ch : -1;
+  }
+  // row table: global PIXEL index (n H + y) W of LDS row L, or -1
+  auto build_tab = [&](int rr) __attribute__((always_inline)) {
     const RangeGeom gm = range_geom(ga, rr, RT);
     const int L = threadIdx.x;
     if (L < a.maxrows) {
@@ -1305,25 +1360,32 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
         const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
         const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
         const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
-        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W * C;
+        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W;
       }
       tab_s[L] = v;
     }
   };
-  f4 sd[MAXC], sx[MAXC];
-  uint32_t ok = 0;
-  auto prefetch = [&]() {
+  f4 sy[MAXCY], sx[MAXCX];
+  uint32_t oky = 0, okx = 0;
+  auto prefetch = [&]() __attribute__((always_inline)) {
     uint32_t m = 0;
 #pragma unroll
-    for (int k = 0; k < MAXC; ++k) {
-      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
-      const bool in = rb >= 0 && sl_o[k] >= 0;
-      const int off = in ? rb + sl_o[k] : 0;
-      sd[k] = *reinterpret_cast<const f4*>(a.dy + off);
-      sx[k] = *reinterpret_cast<const f4*>(a.x + off);
+    for (int k = 0; k < MAXCY; ++k) {
+      const int rb = sy_L[k] >= 0 ? tab_s[sy_L[k]] : -1;
+      const bool in = rb >= 0 && sy_o[k] >= 0;
+      sy[k] = *reinterpret_cast<const f4*>(a.dy + (in ? rb * CY + sy_o[k] : 0));
       m |= static_cast<uint32_t>(in) << k;
     }
-    ok = m;
+    oky = m;
+    m = 0;
+#pragma unroll
+    for (int k = 0; k < MAXCX; ++k) {
+      const int rb = sx_L[k] >= 0 ? tab_s[sx_L[k]] : -1;
+      const bool in = rb >= 0 && sx_o[k] >= 0;
+      sx[k] = *reinterpret_cast<const f4*>(a.x + (in ? rb * CX + sx_o[k] : 0));
+      m |= static_cast<uint32_t>(in) << k;
+    }
+    okx = m;
   };
   build_tab(r);
   __syncthreads();
@@ -1334,22 +1396,28 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   // once per range (same barrier count); the roles are separate loops so
   // the weight-gradient accumulators are not live in the data-gradient
   // code (one loop with both would need > 256 VGPRs).
-  auto advance = [&]() {
+  auto advance = [&]() __attribute__((always_inline)) {
     __syncthreads();  // U_s written / the previous range's LDS reads are done
 #pragma unroll
-    for (int k = 0; k < MAXC; ++k) {
-      if (sl_L[k] >= 0) {
+    for (int k = 0; k < MAXCY; ++k) {
+      if (sy_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
-        const bool in = (ok >> k) & 1u;
-        f4 vd = sd[k], vx = sx[k];
+        const bool in = (oky >> k) & 1u;
+        f4 v = sy[k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          vd[q] = in ? vd[q] : 0.f;
-          vx[q] = in ? vx[q] : 0.f;
-        }
-        const int o = (e >> LC4) * PP + 4 * (e & (C4 - 1));
-        *reinterpret_cast<f4*>(d_s + o) = vd;
-        *reinterpret_cast<f4*>(x_s + o) = vx;
+        for (int q = 0; q < 4; ++q) v[q] = in ? v[q] : 0.f;
+        *reinterpret_cast<f4*>(d_s + (e >> LC4Y) * PPY + 4 * (e & (C4Y - 1))) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXCX; ++k) {
+      if (sx_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        const bool in = (okx >> k) & 1u;
+        f4 v = sx[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = in ? v[q] : 0.f;
+        *reinterpret_cast<f4*>(x_s + (e >> LC4X) * PPX + 4 * (e & (C4X - 1))) = v;
       }
     }
     const int cur = r;
@@ -1363,7 +1431,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
         const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
         const int p = n - gm.n0;
         const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
-        v = ((offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx) * PP;
+        v = (offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx;
       }
       tile_s[threadIdx.x] = v;
     }
@@ -1375,38 +1443,46 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 
   const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform role
   if (wv < 4) {
-    // ---- data gradient: task = (16-tile group grp, dX-channel block cb)
-    const int grp = wv % NG, cb = wv / NG;
+    // ---- data gradient: task = (16-tile group grp, dX-channel block cb),
+    // this wave's dY blocks [yb0, yb0 + NBT)
+    const int task = wv / DSPLIT, half = wv % DSPLIT;
+    const int grp = task % NG, cb = task / NG;
+    const int yb0 = half * NBT;
+    int it = 0;
     for (;;) {
       const RangeGeom gm = advance();
-      if (gm.t0 + 16 * grp < gm.t1) {
+      ++it;
+      if (gm.t0 + 16 * grp < gm.t1 && !(a.ablate & 2)) {
         int t = gm.t0 + 16 * grp + c16;
         const bool valid = t < gm.t1;
         if (!valid) t = gm.t0;
         const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
         const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
-        const int base = tile_s[valid ? 16 * grp + c16 : 0];
+        const int bpx = tile_s[valid ? 16 * grp + c16 : 0];
         const int co = 16 * cb + 4 * g;  // this lane's 4 dX channels
         f4 addv[4];
+        if (half == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-          const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
-          const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + co : 0;
-          addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
+          for (int q = 0; q < 4; ++q) {
+            const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+            const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
+            const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * CX + co : 0;
+            addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
+          }
         }
         f4 acc[16];
 #pragma unroll
         for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          const float* dp = d_s + base + 16 * b + 4 * g;
+        for (int bb = 0; bb < NBT; ++bb) {
+          const int b = yb0 + bb;
+          const float* dp = d_s + bpx * PPY + 16 * b + 4 * g;
           f4 d[16];
 #pragma unroll
           for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
             for (int dx = 0; dx < 4; ++dx)
-              d[4 * dy + dx] = *reinterpret_cast<const f4*>(dp + dy * rowstr + dx * PP);
+              d[4 * dy + dx] = *reinterpret_cast<const f4*>(dp + dy * rsy + dx * PPY);
           f4 sv[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -1423,7 +1499,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
             V[4 * ra + 2] = sv[4 * ra + 2] - sv[4 * ra + 1];
             V[4 * ra + 3] = sv[4 * ra + 1] - sv[4 * ra + 3];
           }
-          const float* up = U_s + ((b * 4 + g) * C + 16 * cb + c16) * 4;
+          const float* up = U_s + ((b * 4 + g) * CX + 16 * cb + c16) * 4;
 #pragma unroll
           for (int xp2 = 0; xp2 < 8; ++xp2) {
             const f4 u0 = *reinterpret_cast<const f4*>(up + (2 * xp2) * USTR);
@@ -1447,21 +1523,40 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
           Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
           Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
         }
-        const float* xm = x_s + base + co;
+        if constexpr (DSPLIT == 2) {
+          f4* yb = ybuf + task * 4 * 64 + lane;
+          if (half == 1) {
+            // hand the partial Y to the even wave of the pair
 #pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
+            for (int q = 0; q < 4; ++q) yb[q * 64] = Y[q];
+            __hip_atomic_store(flag_s + task, it, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            while (!(a.ablate & 1) &&
+                   __hip_atomic_load(flag_s + task, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it)
+              __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-          for (int dx = 0; dx < 2; ++dx) {
-            const int oy = 2 * ty + dy, ox = 2 * tx + dx;
-            if (!valid || oy >= a.H || ox >= a.W) continue;
-            const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + co;
-            const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rowstr + (dx + 1) * PP);
-            f4 v = Y[2 * dy + dx];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
-            v += addv[2 * dy + dx];
-            *reinterpret_cast<f4*>(a.out + o) = v;
+            for (int q = 0; q < 4; ++q) Y[q] += yb[q * 64];
           }
+        }
+        if (half == 0) {
+          const float* xm = x_s + bpx * PPX + co;
+#pragma unroll
+          for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+              const int oy = 2 * ty + dy, ox = 2 * tx + dx;
+              if (!valid || oy >= a.H || ox >= a.W) continue;
+              const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * CX + co;
+              f4 v = Y[2 * dy + dx];
+              if constexpr (MASK) {
+                const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rsx + (dx + 1) * PPX);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
+              }
+              v += addv[2 * dy + dx];
+              *reinterpret_cast<f4*>(a.out + o) = v;
+            }
+        }
       }
       if (r >= r_end) break;
     }
@@ -1471,27 +1566,29 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     // ---- Winograd weight gradient, B^T row AR of this wave: k-step = 4
     // tiles (lane group g = tile 4 st + g); lane c16 = input channel of V
     // and output channel of Z within their 16-channel blocks
-    f4 wacc[4][NB][NB];  // [bc][ci block][co block]
+    f4 wacc[4][NBX][NBY];  // [bc][x block][dY block]
 #pragma unroll
     for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NBX; ++b)
 #pragma unroll
-        for (int b2 = 0; b2 < NB; ++b2) wacc[bc][b][b2] = f4{0.f, 0.f, 0.f, 0.f};
-    float dbacc[NB] = {0.f, 0.f};
-    auto run = [&](auto ARc) {
+        for (int b2 = 0; b2 < NBY; ++b2) wacc[bc][b][b2] = f4{0.f, 0.f, 0.f, 0.f};
+    float dbacc[NBY];
+#pragma unroll
+    for (int b2 = 0; b2 < NBY; ++b2) dbacc[b2] = 0.f;
+    auto run = [&](auto ARc) __attribute__((always_inline)) {
       constexpr int AR = decltype(ARc)::value;
       for (;;) {
         advance();
-        for (int st = 0; st < RT / 4; ++st) {
-          int base = tile_s[4 * st + g];
-          const bool valid = base >= 0;
-          base = valid ? base : 0;
-          f4 zf[NB];
+        for (int st = 0; st < ((a.ablate & 4) ? 0 : RT / 4); ++st) {
+          int bpx = tile_s[4 * st + g];
+          const bool valid = bpx >= 0;
+          bpx = valid ? bpx : 0;
+          f4 zf[NBY];
 #pragma unroll
-          for (int b2 = 0; b2 < NB; ++b2) {
-            const float* dp = d_s + base + rowstr + PP + 16 * b2 + c16;
-            float y00 = dp[0], y01 = dp[PP], y10 = dp[rowstr], y11 = dp[rowstr + PP];
+          for (int b2 = 0; b2 < NBY; ++b2) {
+            const float* dp = d_s + bpx * PPY + rsy + PPY + 16 * b2 + c16;
+            float y00 = dp[0], y01 = dp[PPY], y10 = dp[rsy], y11 = dp[rsy + PPY];
             if (!valid) y00 = y01 = y10 = y11 = 0.f;
             if constexpr (AR == 0) dbacc[b2] += (y00 + y01) + (y10 + y11);
             float r0, r1;
@@ -1502,16 +1599,16 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
             zf[b2] = f4{r0, r0 + r1, r0 - r1, -r1};
           }
 #pragma unroll
-          for (int b = 0; b < NB; ++b) {
-            const float* xp = x_s + base + 16 * b + c16;
+          for (int b = 0; b < NBX; ++b) {
+            const float* xp = x_s + bpx * PPX + 16 * b + c16;
             // the two patch rows B^T row AR combines
-            constexpr int RA = AR == 0 ? 0 : (AR == 3 ? 1 : 1);
-            constexpr int RB = AR == 0 ? 2 : (AR == 3 ? 3 : 2);
+            constexpr int RA = AR == 0 ? 0 : 1;
+            constexpr int RB = AR == 3 ? 3 : 2;
             float ra[4], rb[4];
 #pragma unroll
             for (int dx = 0; dx < 4; ++dx) {
-              float u = xp[RA * rowstr + dx * PP], w = xp[RB * rowstr + dx * PP];
-              if (a.relu_x) {
+              float u = xp[RA * rsx + dx * PPX], w = xp[RB * rsx + dx * PPX];
+              if constexpr (RELU) {
                 u = fmaxf(u, 0.f);
                 w = fmaxf(w, 0.f);
               }
@@ -1530,7 +1627,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 #pragma unroll
             for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
-              for (int b2 = 0; b2 < NB; ++b2)
+              for (int b2 = 0; b2 < NBY; ++b2)
                 wacc[bc][b][b2] = mfma4(V[bc], zf[b2][bc], wacc[bc][b][b2]);
           }
         }
@@ -1544,21 +1641,21 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 
     // ---- P[xi][ci][co] (disjoint xi rows per wave); dW = G^T P G below
     __syncthreads();  // the loop's LDS reads are done (P overwrites U)
-    float* P = smem;                 // [16 xi][C ci][C co]
-    float* dB = smem + 16 * C * C;   // [C]
+    float* P = smem;                   // [16 xi][CX ci][CY co]
+    float* dB = smem + 16 * CX * CY;   // [CY]
     const int ar = wv - 4;
 #pragma unroll
     for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+      for (int b = 0; b < NBX; ++b)
 #pragma unroll
-        for (int b2 = 0; b2 < NB; ++b2)
+        for (int b2 = 0; b2 < NBY; ++b2)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            P[((4 * ar + bc) * C + 16 * b + 4 * g + q) * C + 16 * b2 + c16] = wacc[bc][b][b2][q];
+            P[((4 * ar + bc) * CX + 16 * b + 4 * g + q) * CY + 16 * b2 + c16] = wacc[bc][b][b2][q];
     if (ar == 0) {
 #pragma unroll
-      for (int b2 = 0; b2 < NB; ++b2) {
+      for (int b2 = 0; b2 < NBY; ++b2) {
         float v = dbacc[b2];
         v += __shfl_xor(v, 16);
         v += __shfl_xor(v, 32);
@@ -1569,13 +1666,13 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   }
   // per (ci, co) into this workgroup's slot (wino_wgrad_kernel's epilogue)
   const float* P = smem;
-  const float* dB = smem + 16 * C * C;
-  float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * C;
-  for (int e = threadIdx.x; e < C * C; e += NTH) {
-    const int ci = e / C, co = e - (e / C) * C;
+  const float* dB = smem + 16 * CX * CY;
+  float* slot = a.part + static_cast<int64_t>(blockIdx.x) * a.rows16 * CY;
+  for (int e = threadIdx.x; e < CX * CY; e += NTH) {
+    const int ci = e / CY, co = e - (e / CY) * CY;
     float pm[4][4];
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) pm[xi >> 2][xi & 3] = P[(xi * C + ci) * C + co];
+    for (int xi = 0; xi < 16; ++xi) pm[xi >> 2][xi & 3] = P[(xi * CX + ci) * CY + co];
     float t[3][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -1585,35 +1682,38 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      slot[((3 * i + 0) * C + ci) * C + co] = t[i][0] + 0.5f * (t[i][1] + t[i][2]);
-      slot[((3 * i + 1) * C + ci) * C + co] = 0.5f * (t[i][1] - t[i][2]);
-      slot[((3 * i + 2) * C + ci) * C + co] = 0.5f * (t[i][1] + t[i][2]) + t[i][3];
+      slot[((3 * i + 0) * CX + ci) * CY + co] = t[i][0] + 0.5f * (t[i][1] + t[i][2]);
+      slot[((3 * i + 1) * CX + ci) * CY + co] = 0.5f * (t[i][1] - t[i][2]);
+      slot[((3 * i + 2) * CX + ci) * CY + co] = 0.5f * (t[i][1] + t[i][2]) + t[i][3];
     }
   }
-  for (int co = threadIdx.x; co < C; co += NTH) slot[9 * C * C + co] = dB[co];
+  for (int co = threadIdx.x; co < CY; co += NTH) slot[9 * CX * CY + co] = dB[co];
 }
 
-template <int RT, int MAXC>
-bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float* add,
-                    float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
-                    float* dw, float* db, hipStream_t s) {
-  constexpr int C = 32;
+template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK>
+bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const float* add,
+                    float* out, int relu_x, int mask_x, int N, int H, int W, float* ws,
+                    int64_t ws_floats, float* dw, float* db, hipStream_t s) {
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
-  if (static_cast<int64_t>(N) * H * W * C >= (int64_t(1) << 31)) return false;
+  if (static_cast<int64_t>(N) * H * W * CY >= (int64_t(1) << 31)) return false;
   const int per_img = TY * TX;
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
   const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
-  if (maxrows * Wl * (C / 4) > MAXC * 512 || maxrows > 512) return false;
-  const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * Wl * (C + 4)) +
-                       sizeof(int) * (maxrows + RT);
+  if (maxrows * Wl * (CY / 4) > MAXCY * 512 || maxrows * Wl * (CX / 4) > MAXCX * 512 ||
+      maxrows > 512)
+    return false;
+  constexpr int NTASK = (RT / 16) * (CX / 16);
+  const size_t ybytes = NTASK == 2 ? sizeof(float) * 2 * 4 * 64 * 4 : 0;
+  const size_t bytes = sizeof(float) * (16 * CX * CY + static_cast<size_t>(maxrows) * Wl * (CX + CY + 8)) +
+                       ybytes + sizeof(int) * (2 + maxrows + RT);
   if (bytes > 160 * 1024) return false;
-  const int rows16 = ((9 * C + 16) / 16) * 16;
+  const int rows16 = ((9 * CX + 16) / 16) * 16;
   const int nranges = static_cast<int>((NT + RT - 1) / RT);
-  const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * C);
+  const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * CY);
   const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
   if (G < 1) return false;
   WinoBwdArgs a{};
@@ -1624,11 +1724,34 @@ bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
-  auto kern = wino_bwd_fused32_kernel<RT, MAXC>;
+  a.mask_x = mask_x;
+  static const int ablate = env_int("SA_FUSED_ABLATE", 0);
+  a.ablate = ablate;
+  auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
-  wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
+  wgrad_reduce_slots(ws, G, rows16, CY, CX, dw, db, s);
   return true;
+}
+
+// relu_x / mask_x are compile-time in the kernel (the wgrad waves' ReLU on
+// every x operand was a select per value); the residual convs use (1, 1)
+// and (0, 1), the stage heads (0, 0)
+template <int CX, int CY, int RT, int MAXCX, int MAXCY>
+bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float* add,
+                    float* out, int relu_x, int mask_x, int N, int H, int W, float* ws,
+                    int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+  if (relu_x && mask_x)
+    return run_wino_bwd32_t<CX, CY, RT, MAXCX, MAXCY, true, true>(
+        dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
+  if (mask_x)
+    return run_wino_bwd32_t<CX, CY, RT, MAXCX, MAXCY, false, true>(
+        dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
+  if (relu_x)
+    return run_wino_bwd32_t<CX, CY, RT, MAXCX, MAXCY, true, false>(
+        dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
+  return run_wino_bwd32_t<CX, CY, RT, MAXCX, MAXCY, false, false>(
+      dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
 }
 
 template <int C, int RT, int MAXC, int KD, bool WWG = false>
@@ -1661,7 +1784,10 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
-  auto kern = wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG>;
+  static const int runs = env_int("SA_WINO_RUNS", 1);
+  a.runs = runs;
+  auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true>
+                     : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
   wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
@@ -1737,20 +1863,26 @@ bool wino_bwd_fused_enabled() {
 }
 
 bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, const float* add,
-                           float* out, int relu_x, int N, int H, int W, int C, float* ws,
-                           int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+                           float* out, int relu_x, int mask_x, int N, int H, int W, int C,
+                           int Cy, float* ws, int64_t ws_floats, float* dw, float* db,
+                           hipStream_t s) {
   static const int kd = env_int("SA_FUSED_BWD_KD", 4);
   static const int wwg = env_int("SA_FUSED_BWD_WWG", 1);
-  if (C == 16 && wwg)
-    return run_wino_bwd<16, 64, 5, 0, true>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
-  if (C == 16) {
+  if (C == 16 && Cy == 16 && mask_x) {
+    if (wwg)
+      return run_wino_bwd<16, 64, 5, 0, true>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     if (kd == 0) return run_wino_bwd<16, 64, 5, 0>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     if (kd == 8) return run_wino_bwd<16, 64, 5, 8>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     return run_wino_bwd<16, 64, 5, 4>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
   }
   static const int f32c = env_int("SA_FUSED_BWD32", 1);
-  if (C == 32 && f32c)
-    return run_wino_bwd32<32, 5>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
+  if (!f32c) return false;
+  if (C == 32 && Cy == 32)
+    return run_wino_bwd32<32, 32, 32, 5, 5>(dy, w, x, add, out, relu_x, mask_x, N, H, W, ws,
+                                            ws_floats, dw, db, s);
+  if (C == 16 && Cy == 32)
+    return run_wino_bwd32<16, 32, 32, 4, 8>(dy, w, x, add, out, relu_x, mask_x, N, H, W, ws,
+                                            ws_floats, dw, db, s);
   return false;
 }
 

@@ -218,6 +218,13 @@ class _DeepTorsoF32(torch.autograd.Function):
       if DEBUG_TAPE is not None:
         DEBUG_TAPE[('dpool', s)] = dy.clone()
         DEBUG_TAPE[('dconv', s)] = dconv.clone()
+      if s > 0 and gw is gv[pb]:
+        # stage head (16 -> 32 / 32 -> 32): data + weight gradient in one
+        # pass over (dconv, stage input); the input is the previous stage's
+        # raw output, so no ReLU mask
+        dy = C.cf32_conv_bwd_fused(dconv, params[pb], stage_in, False, gw, gv[pb + 1],
+                                   mask=False)
+        continue
       C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gw, gv[pb + 1])
       if gw is not gv[pb]:
         gv[pb].add_(gw[:, :, :gv[pb].shape[2]])

@@ -360,38 +360,45 @@ def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
   assert rel_err(db, rb) <= TOL
 
 
-@pytest.mark.parametrize('N,H,W,Cc', [(256, 36, 48, 16), (256, 18, 24, 32), (256, 9, 12, 32),
-                                      (5, 11, 11, 16), (5, 11, 11, 32)])
+@pytest.mark.parametrize('N,H,W,Cx,Cy,mask', [
+    (256, 36, 48, 16, 16, True), (256, 18, 24, 32, 32, True), (256, 9, 12, 32, 32, True),
+    (5, 11, 11, 16, 16, True), (5, 11, 11, 32, 32, True),
+    (256, 36, 48, 16, 32, False), (256, 18, 24, 32, 32, False), (5, 11, 11, 16, 32, False),
+    (7, 42, 42, 16, 32, False), (3, 36, 64, 16, 32, False)])
 @pytest.mark.parametrize('relu_x,use_add', [(False, False), (True, True)])
-def test_conv_bwd_fused(cuda, N, H, W, Cc, relu_x, use_add):
-  """The residual-conv backward in one pass (conv_wino.hip
-  wino_bwd_fused_kernel for 16 channels, wino_bwd_fused32_kernel for 32):
-  dX = dgrad(dY, W) * (x > 0) [+ add], dW += relu?(x)^T dY, db += sum dY,
-  against float64 - at N = 256 every persistent workgroup walks many ranges
-  (contiguous range runs, cross-range prefetch, image boundaries inside a
-  range), and 11x11 exercises odd sizes (partial 2x2 tiles)."""
+def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
+  """A 3x3/1 conv's backward in one pass (conv_wino.hip
+  wino_bwd_fused_kernel for the 16-channel residual convs,
+  wino_bwd_fused32_kernel for 32 -> 32 and the 16 -> 32 stage head, whose
+  data gradient splits each task over a wave pair and hands the partial
+  output transform through LDS): dX = dgrad(dY, W) [* (x > 0)] [+ add],
+  dW += relu?(x)^T dY, db += sum dY, against float64.  At N = 256 every
+  persistent workgroup walks many ranges (contiguous range runs, cross-range
+  prefetch, image boundaries inside a range); 11x11 / 42x42 exercise odd
+  tile counts and partial 2x2 tiles; 36x64 (Doom) falls back to the
+  separate kernels."""
   C = _C()
-  g = torch.Generator().manual_seed(N * H + Cc)
-  x = torch.randn(N, H, W, Cc, generator=g)
-  w = torch.randn(3, 3, Cc, Cc, generator=g) / (9 * Cc) ** 0.5
-  dy = torch.randn(N, H, W, Cc, generator=g)
-  add = torch.randn(N, H, W, Cc, generator=g)
+  g = torch.Generator().manual_seed(N * H + Cx + Cy)
+  x = torch.randn(N, H, W, Cx, generator=g)
+  w = torch.randn(3, 3, Cx, Cy, generator=g) / (9 * Cx) ** 0.5
+  dy = torch.randn(N, H, W, Cy, generator=g)
+  add = torch.randn(N, H, W, Cx, generator=g)
   x64 = x.double().requires_grad_(True)
   xin = x64.clamp(min=0) if relu_x else x64
   w64 = w.double().requires_grad_(True)
-  b64 = torch.zeros(Cc, dtype=torch.float64, requires_grad=True)
+  b64 = torch.zeros(Cy, dtype=torch.float64, requires_grad=True)
   _, gw, gb = torch.autograd.grad(layers.conv2d_same_nhwc(xin, w64, b64, 1),
                                   (x64, w64, b64), dy.double())
   x2 = x.double().requires_grad_(True)
   (gx,) = torch.autograd.grad(layers.conv2d_same_nhwc(x2, w.double(), None, 1), x2,
                               dy.double())
-  ref = torch.where(x.double() > 0, gx, torch.zeros_like(gx))
+  ref = torch.where(x.double() > 0, gx, torch.zeros_like(gx)) if mask else gx
   if use_add:
     ref = ref + add.double()
-  dw = torch.zeros(3, 3, Cc, Cc, device=cuda)
-  db = torch.zeros(Cc, device=cuda)
+  dw = torch.zeros(3, 3, Cx, Cy, device=cuda)
+  db = torch.zeros(Cy, device=cuda)
   dx = C.cf32_conv_bwd_fused(dy.to(cuda), w.to(cuda), x.to(cuda), relu_x, dw, db,
-                             add=add.to(cuda) if use_add else None)
+                             add=add.to(cuda) if use_add else None, mask=mask)
   assert rel_err(dx, ref) <= TOL
   assert rel_err(dw, gw) <= TOL
   assert rel_err(db, gb) <= TOL

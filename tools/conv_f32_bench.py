@@ -63,21 +63,25 @@ for name, H, W, Ci, Co, K, S, pt, pl, u8 in LAYERS:
     line += ' | dgrad %8.1f us %6.1f TF' % (td, flop / td / 1e6)
   print(line, flush=True)
 # residual-conv backward: fused (one pass) vs separate wgrad + masked dgrad
-for name, H, W, Cc in [('res16 36x48', 36, 48, 16), ('res32 18x24', 18, 24, 32),
-                       ('res32 9x12', 9, 12, 32)]:
-  if ONLY and ONLY not in name and ONLY != 'bwd':
+# (stage heads: 16 -> 32 and 32 -> 32 without mask / skip, relu_x off)
+for name, H, W, Cc, Cy, res in [('res16 36x48', 36, 48, 16, 16, True),
+                                ('res32 18x24', 18, 24, 32, 32, True),
+                                ('res32 9x12', 9, 12, 32, 32, True),
+                                ('head conv2 16->32 36x48', 36, 48, 16, 32, False),
+                                ('head conv3 32->32 18x24', 18, 24, 32, 32, False)]:
+  if ONLY and ONLY not in name and ONLY not in ('bwd', 'deep'):
     continue
   x = torch.randn(N, H, W, Cc, device=dev)
-  w = torch.randn(3, 3, Cc, Cc, device=dev) * 0.1
-  dy = torch.randn(N, H, W, Cc, device=dev)
-  add = torch.randn(N, H, W, Cc, device=dev)
+  w = torch.randn(3, 3, Cc, Cy, device=dev) * 0.1
+  dy = torch.randn(N, H, W, Cy, device=dev)
+  add = torch.randn(N, H, W, Cc, device=dev) if res else None
   dw = torch.zeros_like(w)
-  db = torch.zeros(Cc, device=dev)
-  tf = timeit(lambda: C.cf32_conv_bwd_fused(dy, w, x, True, dw, db, add=add))
+  db = torch.zeros(Cy, device=dev)
+  tf = timeit(lambda: C.cf32_conv_bwd_fused(dy, w, x, res, dw, db, add=add, mask=res))
 
   def sep():
-    C.cf32_conv_wgrad(x, dy, 1, 1, 1, True, dw, db)
-    C.cf32_conv_dgrad(dy, w, 1, 1, 1, H, W, mask=x, add=add)
+    C.cf32_conv_wgrad(x, dy, 1, 1, 1, res, dw, db)
+    C.cf32_conv_dgrad(dy, w, 1, 1, 1, H, W, mask=x if res else None, add=add)
   ts = timeit(sep)
   print('%-26s bwd fused %8.1f us | separate wgrad+dgrad %8.1f us' % (name, tf, ts),
         flush=True)
