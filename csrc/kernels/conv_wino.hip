@@ -48,6 +48,22 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// 16-B loads through a buffer descriptor: an offset at or past the buffer's
+// end returns zeros (the hardware range check), so a stager's padding and
+// out-of-image elements need no select when they are committed to LDS, and
+// the per-lane address is a 32-bit byte offset.  Launchers refuse tensors
+// of >= 4 GB.
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p, int64_t floats) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0,
+                                           static_cast<int>(static_cast<uint32_t>(floats * 4)),
+                                           0x00020000);
+}
+__device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
+
 // x / d for 0 <= x < 2^22, 1 <= d <= 2^10 (exact: (x + 0.5) / d lies at
 // least 0.5 / d from an integer, far above the fp32 product's error)
 __device__ __forceinline__ int fdivi(int x, float rd) {
@@ -125,9 +141,17 @@ __device__ __forceinline__ RangeGeom range_geom(const WinoArgs& a, int r, int RT
   return g;
 }
 
-template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
+// FL: compile-time epilogue / stager flags (bit 0 ReLU on the input, 1 ReLU
+// on the output, 2 mask, 3 residual add, 4 bias), or -1 = read them from
+// the arguments (a runtime ReLU is a max + select per staged value)
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
 __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
+  const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
+  const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
+  const bool f_mask = FL < 0 ? a.mask != nullptr : (FL & 4) != 0;
+  const bool f_add = FL < 0 ? a.add != nullptr : (FL & 8) != 0;
+  const bool f_bias = FL < 0 ? a.bias != nullptr : (FL & 16) != 0;
   constexpr int PP = CIN + 4;  // pixel pitch: 16-B units odd -> b128 patch reads conflict-free
   constexpr int C4 = CIN / 4;
   constexpr int LC4 = C4 == 4 ? 2 : 3;
@@ -226,17 +250,14 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     }
   };
   f4 stg[MAXC];
-  uint32_t stg_ok = 0;
-  auto prefetch = [&]() {  // reads tab_s
-    uint32_t ok = 0;
+  const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * a.H * a.W * CIN);
+  auto prefetch = [&]() __attribute__((always_inline)) {  // reads tab_s
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
       const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
       const bool in = rb >= 0 && sl_x[k] >= 0 && !(a.ablate & 2);
-      stg[k] = *reinterpret_cast<const f4*>(a.src + (in ? rb + sl_x[k] : 0));
-      ok |= static_cast<uint32_t>(in) << k;
+      stg[k] = bload(srcr, in ? static_cast<uint32_t>(rb + sl_x[k]) * 4u : kOOB);
     }
-    stg_ok = ok;
   };
   build_tab(r);
   __syncthreads();
@@ -248,12 +269,10 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     for (int k = 0; k < MAXC; ++k) {
       if (sl_L[k] >= 0 && !(a.ablate & 4)) {
         const int e = threadIdx.x + k * NTH;
-        f4 v = stg[k];
-        const bool in = (stg_ok >> k) & 1u;
+        f4 v = stg[k];  // zero where out of the image (range check)
+        if (f_relu_in) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float x = in ? v[q] : 0.f;
-          v[q] = a.relu_in ? fmaxf(x, 0.f) : x;
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
         }
         *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = v;
       }
@@ -291,9 +310,9 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
           const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT +
                                      co0 + 16 * h + 4 * g
                                : 0;
-          pm[h][q] = (a.mask != nullptr && in) ? *reinterpret_cast<const f4*>(a.mask + o)
+          pm[h][q] = (f_mask && in) ? *reinterpret_cast<const f4*>(a.mask + o)
                                                : f4{1.f, 1.f, 1.f, 1.f};
-          pa[h][q] = (a.add != nullptr && in) ? *reinterpret_cast<const f4*>(a.add + o)
+          pa[h][q] = (f_add && in) ? *reinterpret_cast<const f4*>(a.add + o)
                                               : f4{0.f, 0.f, 0.f, 0.f};
         }
 
@@ -356,7 +375,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       for (int h = 0; h < NH; ++h) {
         const int co = co0 + 16 * h + 4 * g;
         f4 bv = {0.f, 0.f, 0.f, 0.f};
-        if (a.bias != nullptr) bv = *reinterpret_cast<const f4*>(a.bias + co);
+        if (f_bias) bv = *reinterpret_cast<const f4*>(a.bias + co);
         f4 tt[4][2];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
@@ -381,7 +400,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = m[k] > 0.f ? v[k] : 0.f;
             v += pa[h][2 * dy + dx];
-            if (a.relu_out) {
+            if (f_relu_out) {
 #pragma unroll
               for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.f);
             }
@@ -408,7 +427,7 @@ int env_int(const char* name, int def) {
   return (e && *e) ? std::atoi(e) : def;
 }
 
-template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
 bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   const int H = c.Ho, W = c.Wo;
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
@@ -425,7 +444,7 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   const size_t bytes = sizeof(float) * (16 * CIN * COUT +
                                         static_cast<size_t>(maxrows) * Wl * (CIN + 4) +
                                         maxrows);
-  if (static_cast<int64_t>(c.N) * H * W * CIN >= (int64_t(1) << 31) || maxrows > 64 * NW)
+  if (static_cast<int64_t>(c.N) * H * W * CIN * 4 > kMaxBufBytes || maxrows > 64 * NW)
     return false;
   if (bytes > 160 * 1024) return false;
   WinoArgs a{};
@@ -452,10 +471,28 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   static const int occ_env = env_int("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
   const int G = std::max(1, std::min(a.nranges, 256 * occ));
-  auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS>;
+  auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS, FL>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), bytes, s, a);
   return true;
+}
+
+// The deep torso's forward flag sets get compile-time instances: residual
+// conv 1 (ReLU in + out, bias) = 19, conv 2 (skip add, bias [, ReLU out for
+// the torso's last]) = 24 / 26, stage head (bias) = 16; anything else the
+// runtime-flag instance
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
+bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
+  const int fl = (c.relu_in ? 1 : 0) | (c.relu_out ? 2 : 0) | (c.mask ? 4 : 0) |
+                 (c.add ? 8 : 0) | (c.bias ? 16 : 0);
+  static const int on = env_int("SA_WINO_FL", 0);  // measured: 10.85 (on) vs 10.77 ms/step (off)
+  if (on && !flip) {
+    if (fl == 19) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 19>(c, flip, s);
+    if (fl == 24) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 24>(c, flip, s);
+    if (fl == 26) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 26>(c, flip, s);
+    if (fl == 16) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 16>(c, flip, s);
+  }
+  return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
 
 
@@ -947,19 +984,17 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
     }
   };
   f4 sd[MAXC], sx[MAXC];
-  uint32_t ok = 0;
-  auto prefetch = [&]() {
-    uint32_t m = 0;
+  const int64_t nfl = static_cast<int64_t>(a.N) * a.H * a.W * C;
+  const auto dyr = buf_rsrc(a.dy, nfl), xr = buf_rsrc(a.x, nfl);
+  auto prefetch = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
       const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
       const bool in = rb >= 0 && sl_o[k] >= 0;
-      const int off = in ? rb + sl_o[k] : 0;
-      sd[k] = *reinterpret_cast<const f4*>(a.dy + off);
-      sx[k] = *reinterpret_cast<const f4*>(a.x + off);
-      m |= static_cast<uint32_t>(in) << k;
+      const uint32_t off = in ? static_cast<uint32_t>(rb + sl_o[k]) * 4u : kOOB;
+      sd[k] = bload(dyr, off);
+      sx[k] = bload(xr, off);
     }
-    ok = m;
   };
   build_tab(r);
   __syncthreads();
@@ -977,13 +1012,7 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
     for (int k = 0; k < MAXC; ++k) {
       if (sl_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
-        const bool in = (ok >> k) & 1u;
-        f4 vd = sd[k], vx = sx[k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          vd[q] = in ? vd[q] : 0.f;
-          vx[q] = in ? vx[q] : 0.f;
-        }
+        const f4 vd = sd[k], vx = sx[k];  // zero where out of the image
         const int o = (e >> LC4) * PP + 4 * (e & (C4 - 1));
         *reinterpret_cast<f4*>(d_s + o) = vd;
         *reinterpret_cast<f4*>(x_s + o) = vx;
@@ -1366,26 +1395,21 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     }
   };
   f4 sy[MAXCY], sx[MAXCX];
-  uint32_t oky = 0, okx = 0;
+  const int64_t npx = static_cast<int64_t>(a.N) * a.H * a.W;
+  const auto dyr = buf_rsrc(a.dy, npx * CY), xr = buf_rsrc(a.x, npx * CX);
   auto prefetch = [&]() __attribute__((always_inline)) {
-    uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < MAXCY; ++k) {
       const int rb = sy_L[k] >= 0 ? tab_s[sy_L[k]] : -1;
       const bool in = rb >= 0 && sy_o[k] >= 0;
-      sy[k] = *reinterpret_cast<const f4*>(a.dy + (in ? rb * CY + sy_o[k] : 0));
-      m |= static_cast<uint32_t>(in) << k;
+      sy[k] = bload(dyr, in ? static_cast<uint32_t>(rb * CY + sy_o[k]) * 4u : kOOB);
     }
-    oky = m;
-    m = 0;
 #pragma unroll
     for (int k = 0; k < MAXCX; ++k) {
       const int rb = sx_L[k] >= 0 ? tab_s[sx_L[k]] : -1;
       const bool in = rb >= 0 && sx_o[k] >= 0;
-      sx[k] = *reinterpret_cast<const f4*>(a.x + (in ? rb * CX + sx_o[k] : 0));
-      m |= static_cast<uint32_t>(in) << k;
+      sx[k] = bload(xr, in ? static_cast<uint32_t>(rb * CX + sx_o[k]) * 4u : kOOB);
     }
-    okx = m;
   };
   build_tab(r);
   __syncthreads();
@@ -1402,10 +1426,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     for (int k = 0; k < MAXCY; ++k) {
       if (sy_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
-        const bool in = (oky >> k) & 1u;
-        f4 v = sy[k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = in ? v[q] : 0.f;
+        const f4 v = sy[k];  // zero where out of the image
         *reinterpret_cast<f4*>(d_s + (e >> LC4Y) * PPY + 4 * (e & (C4Y - 1))) = v;
       }
     }
@@ -1413,10 +1434,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     for (int k = 0; k < MAXCX; ++k) {
       if (sx_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
-        const bool in = (okx >> k) & 1u;
-        f4 v = sx[k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = in ? v[q] : 0.f;
+        const f4 v = sx[k];  // zero where out of the image
         *reinterpret_cast<f4*>(x_s + (e >> LC4X) * PPX + 4 * (e & (C4X - 1))) = v;
       }
     }
@@ -1697,7 +1715,7 @@ bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const flo
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
-  if (static_cast<int64_t>(N) * H * W * CY >= (int64_t(1) << 31)) return false;
+  if (static_cast<int64_t>(N) * H * W * CY * 4 > kMaxBufBytes) return false;
   const int per_img = TY * TX;
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
@@ -1761,7 +1779,7 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
-  if (static_cast<int64_t>(N) * H * W * C >= (int64_t(1) << 31)) return false;
+  if (static_cast<int64_t>(N) * H * W * C * 4 > kMaxBufBytes) return false;
   const int per_img = TY * TX;
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
@@ -1810,10 +1828,10 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
   const int cin = c.Cs, cout = c.Cout;
   // SA_WINO_CFG: alternative instances for measurement sweeps
   static const int cfg = env_int("SA_WINO_CFG", 0);
-  if (cin == 16 && cout == 16) return run_wino<16, 16, 1, 4, 64, 10, 2>(c, flip, s);
+  if (cin == 16 && cout == 16) return run_wino_fl<16, 16, 1, 4, 64, 10, 2>(c, flip, s);
   if (cin == 16 && cout == 32) {
     if (cfg == 1) return run_wino<16, 32, 2, 4, 64, 10, 1>(c, flip, s);
-    return run_wino<16, 32, 1, 8, 64, 5, 2>(c, flip, s);
+    return run_wino_fl<16, 32, 1, 8, 64, 5, 2>(c, flip, s);
   }
   // 32 -> 16 (the stage-1 head's data gradient at 36x48): one workgroup of
   // four waves per CU (LDS) measured slower than the direct kernel
@@ -1821,7 +1839,7 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
   if (cin == 32 && cout == 16 && cfg == 2) return run_wino<32, 16, 1, 4, 64, 19, 1>(c, flip, s);
   if (cin == 32 && cout == 32) {
     if (cfg == 1) return run_wino<32, 32, 2, 4, 64, 15, 1>(c, flip, s);
-    return run_wino<32, 32, 1, 8, 64, 8, 2>(c, flip, s);
+    return run_wino_fl<32, 32, 1, 8, 64, 8, 2>(c, flip, s);
   }
   return false;
 }
