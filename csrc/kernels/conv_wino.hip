@@ -1886,6 +1886,10 @@ bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, cons
                            hipStream_t s) {
   static const int kd = env_int("SA_FUSED_BWD_KD", 4);
   static const int wwg = env_int("SA_FUSED_BWD_WWG", 1);
+  static const int v2 = env_int("SA_FUSED16_V2", 0);
+  if (C == 16 && Cy == 16 && (v2 || !mask_x))
+    return run_wino_bwd32<16, 16, 64, 5, 5>(dy, w, x, add, out, relu_x, mask_x, N, H, W, ws,
+                                            ws_floats, dw, db, s);
   if (C == 16 && Cy == 16 && mask_x) {
     if (wwg)
       return run_wino_bwd<16, 64, 5, 0, true>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);

@@ -364,6 +364,7 @@ def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
     (256, 36, 48, 16, 16, True), (256, 18, 24, 32, 32, True), (256, 9, 12, 32, 32, True),
     (5, 11, 11, 16, 16, True), (5, 11, 11, 32, 32, True),
     (256, 36, 48, 16, 32, False), (256, 18, 24, 32, 32, False), (5, 11, 11, 16, 32, False),
+    (256, 36, 48, 16, 16, False),
     (7, 42, 42, 16, 32, False), (3, 36, 64, 16, 32, False)])
 @pytest.mark.parametrize('relu_x,use_add', [(False, False), (True, True)])
 def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
