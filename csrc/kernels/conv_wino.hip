@@ -64,6 +64,14 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
 }
 constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
 
+// Weight-gradient k-step: lane group g reads tile 4 st + kperm(g), order
+// {0, 2, 1, 3}.  Adjacent tiles sit 2 pixels apart in LDS (8 banks for a
+// 36-float pitch, 40 for 20), so the natural order put lane groups 0/1 (and
+// 2/3), which one ds_read_b32 half-wave serves together, on overlapping
+// banks; tiles 0 and 2 (1 and 3) are 16 banks apart at both pitches.  Which
+// tile feeds which MFMA k slot does not change the sum over tiles.
+__device__ __forceinline__ int kperm(int g) { return ((g & 1) << 1) | (g >> 1); }
+
 // x / d for 0 <= x < 2^22, 1 <= d <= 2^10 (exact: (x + 0.5) / d lies at
 // least 0.5 / d from an integer, far above the fp32 product's error)
 __device__ __forceinline__ int fdivi(int x, float rd) {
@@ -299,22 +307,28 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       const float* xp = x_s + (base * Wl + 2 * tx) * PP + 4 * g;
       const float* up = U_s + (g * COUT + co0 + c16) * 4;
       // epilogue operands (mask / residual) of the 4 outputs: global loads
-      // issued before the MFMAs, so their latency hides under them
+      // issued before the MFMAs, so their latency hides under them - or,
+      // at >= 3 waves per SIMD (register cap 168), after them (other waves
+      // cover the latency)
+      constexpr bool kLateEpi = WPS >= 3;
       f4 pm[NH][4], pa[NH][4];
+      auto load_epi = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int h = 0; h < NH; ++h)
+        for (int h = 0; h < NH; ++h)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-          const bool in = valid && oy < a.H && ox < a.W;
-          const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT +
-                                     co0 + 16 * h + 4 * g
-                               : 0;
-          pm[h][q] = (f_mask && in) ? *reinterpret_cast<const f4*>(a.mask + o)
-                                               : f4{1.f, 1.f, 1.f, 1.f};
-          pa[h][q] = (f_add && in) ? *reinterpret_cast<const f4*>(a.add + o)
-                                              : f4{0.f, 0.f, 0.f, 0.f};
-        }
+          for (int q = 0; q < 4; ++q) {
+            const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
+            const bool in = valid && oy < a.H && ox < a.W;
+            const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT +
+                                       co0 + 16 * h + 4 * g
+                                 : 0;
+            pm[h][q] = (f_mask && in) ? *reinterpret_cast<const f4*>(a.mask + o)
+                                      : f4{1.f, 1.f, 1.f, 1.f};
+            pa[h][q] = (f_add && in) ? *reinterpret_cast<const f4*>(a.add + o)
+                                     : f4{0.f, 0.f, 0.f, 0.f};
+          }
+      };
+      if constexpr (!kLateEpi) load_epi();
 
       f4 acc[NH][16];
 #pragma unroll
@@ -371,6 +385,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       }
 
       // ---- output transform Y = A^T M A and the fused epilogue
+      if constexpr (kLateEpi) load_epi();
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int co = co0 + 16 * h + 4 * g;
@@ -437,8 +452,10 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
-  // staged rows <= 2 (tile rows spanned) + 2 (images touched)
-  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  // staged rows <= 2 (tile rows spanned) + 2 (images touched); exactly
+  // 2 RT / TX + 2 when every range is whole tile rows of one image
+  int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  if (RT % TX == 0 && per_img % RT == 0) maxrows = 2 * (RT / TX) + 2;
   if (static_cast<int64_t>(maxrows) * Wl * (CIN / 4) > static_cast<int64_t>(MAXC) * 64 * NW)
     return false;
   const size_t bytes = sizeof(float) * (16 * CIN * COUT +
@@ -689,7 +706,7 @@ __global__ __launch_bounds__(256, 1) void wino_wgrad_kernel(WinoWgArgs a) {
     auto run = [&](auto XGc) {
       constexpr int XG = decltype(XGc)::value;
       for (int st = kq; st < NSTEP; st += KS) {
-        const int tt = 4 * st + g;
+        const int tt = 4 * st + kperm(g);
         int xb = tile_s[2 * tt], db = tile_s[2 * tt + 1];
         const bool valid = xb >= 0;
         xb = valid ? xb : 0;
@@ -1128,7 +1145,7 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       // channel of Z; acc[4 i + bc] += V[i][bc] (x) Z[i][bc]
       if (wave >= 4) {
         for (int st = wave - 4; st < RT / 4; st += 4) {
-          int base = tile_s[4 * st + g];
+          int base = tile_s[4 * st + kperm(g)];
           const bool valid = base >= 0;
           base = valid ? base : 0;
           const float* dp = d_s + base + rowstr + PP + c16;
@@ -1599,7 +1616,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
       for (;;) {
         advance();
         for (int st = 0; st < ((a.ablate & 4) ? 0 : RT / 4); ++st) {
-          int bpx = tile_s[4 * st + g];
+          int bpx = tile_s[4 * st + kperm(g)];
           const bool valid = bpx >= 0;
           bpx = valid ? bpx : 0;
           f4 zf[NBY];
@@ -1828,7 +1845,19 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
   const int cin = c.Cs, cout = c.Cout;
   // SA_WINO_CFG: alternative instances for measurement sweeps
   static const int cfg = env_int("SA_WINO_CFG", 0);
-  if (cin == 16 && cout == 16) return run_wino_fl<16, 16, 1, 4, 64, 10, 2>(c, flip, s);
+  if (cin == 16 && cout == 16) {
+    // 3-wave workgroups over 48-tile ranges: at 36x48 every range is two
+    // whole tile rows of one image (6 staged rows, 40 KB of LDS), so four
+    // workgroups (three waves per SIMD) fit on a CU
+    static const int w3 = env_int("SA_WINO16_3W", 0);
+    if (w3 && !flip) {
+      const int fl = (c.relu_in ? 1 : 0) | (c.relu_out ? 2 : 0) | (c.mask ? 4 : 0) |
+                     (c.add ? 8 : 0) | (c.bias ? 16 : 0);
+      if (fl == 19 && run_wino<16, 16, 1, 3, 48, 7, 3, 19>(c, flip, s)) return true;
+      if (fl == 24 && run_wino<16, 16, 1, 3, 48, 7, 3, 24>(c, flip, s)) return true;
+    }
+    return run_wino_fl<16, 16, 1, 4, 64, 10, 2>(c, flip, s);
+  }
   if (cin == 16 && cout == 32) {
     if (cfg == 1) return run_wino<16, 32, 2, 4, 64, 10, 1>(c, flip, s);
     return run_wino_fl<16, 32, 1, 8, 64, 5, 2>(c, flip, s);

@@ -18,12 +18,13 @@
 //     experiment.py:191-198 is never a separate kernel.
 //
 // Tiling: 64 x 64 output tile per 256-thread workgroup (2 x 2 waves of one
-// 32 x 32 MFMA accumulator each), K in steps of 16 staged through a double-
-// buffered LDS image [row][k] (pitch 20 floats: conflict-free 16-B reads)
-// with the next step's global loads in flight under the current MFMAs.  The
-// k order inside a step is permuted (MFMA s uses k = 8 h + s for lane half
-// h) on both operands, so each lane reads its 8 k values of a step with two
-// ds_read_b128.  Large-K products (the weight gradients, K = T*B = 3232)
+// 32 x 32 MFMA accumulator each), K in steps of 32 staged through a double-
+// buffered LDS image [row][k] (pitch 36 floats: conflict-free 16-B reads)
+// with the next step's global loads in flight under the current 16 MFMAs
+// (steps of 16 left ~0.25 us of MFMA work to cover each step's loads).  The
+// k order inside a step is permuted (MFMA (c, s) uses k = 16 h + 4 c + s for
+// lane half h) on both operands, so each lane reads its 16 k values of a
+// step with four ds_read_b128.  Large-K products (the weight gradients, K = T*B = 3232)
 // split K over grid.z into per-split partial slabs that one reduction
 // kernel sums in split order: deterministic, no float atomics.
 #include "gemm_f32.h"
@@ -36,7 +37,7 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 64, BN = 64, BK = 16, PK = 20;
+constexpr int BM = 64, BN = 64, BK = 32, PK = BK + 4;  // pitch: odd 16-B units
 
 struct Args {
   const float* A;
@@ -80,65 +81,73 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
   const int Mr = a.M + a.ones_row;
   const int kbeg = blockIdx.z * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
+  constexpr int KQ = BK / 16;  // f4 per thread and operand per K step
 
-  // global -> register staging of one K step (one f4 per thread and operand)
-  f4 ra, rb;
-  auto load = [&](int k0) {
-    f4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
-    if (!a.ta) {  // A[m][k]: thread = (m, k quad)
-      const int m = m0 + (t >> 2), k = k0 + 4 * (t & 3);
-      if (m < a.M && k < kend)
-        va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(m) * a.lda + k);
-      else if (m == a.M && a.ones_row && k < kend)
-        va = f4{1.f, 1.f, 1.f, 1.f};
-    } else {  // A[k][m]: thread = (k, m quad)
-      const int k = k0 + (t >> 4), m = m0 + 4 * (t & 15);
-      if (k < kend) {
-        if (m + 3 < a.M) {
-          va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(k) * a.lda + m);
-        } else {
+  // global -> register staging of one K step (KQ f4 per thread and operand)
+  f4 ra[KQ], rb[KQ];
+  auto load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (m + q < a.M) va[q] = a.A[static_cast<int64_t>(k) * a.lda + m + q];
-            else if (m + q == a.M && a.ones_row) va[q] = 1.f;
+    for (int j = 0; j < KQ; ++j) {
+      f4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+      if (!a.ta) {  // A[m][k]: thread = (m, k quad)
+        const int m = m0 + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
+        if (m < a.M && k < kend)
+          va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(m) * a.lda + k);
+        else if (m == a.M && a.ones_row && k < kend)
+          va = f4{1.f, 1.f, 1.f, 1.f};
+      } else {  // A[k][m]: thread = (k, m quad)
+        const int k = k0 + (t >> 4) + 16 * j, m = m0 + 4 * (t & 15);
+        if (k < kend) {
+          if (m + 3 < a.M) {
+            va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(k) * a.lda + m);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (m + q < a.M) va[q] = a.A[static_cast<int64_t>(k) * a.lda + m + q];
+              else if (m + q == a.M && a.ones_row) va[q] = 1.f;
+            }
           }
         }
       }
+      if (!a.tb) {  // B[k][n]: thread = (k, n quad)
+        const int k = k0 + (t >> 4) + 16 * j, n = n0 + 4 * (t & 15);
+        if (k < kend && n < a.N)
+          vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(k) * a.ldb + n);
+      } else {  // B[n][k]: thread = (n, k quad)
+        const int n = n0 + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
+        if (n < a.N && k < kend)
+          vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(n) * a.ldb + k);
+      }
+      ra[j] = va;
+      rb[j] = vb;
     }
-    if (!a.tb) {  // B[k][n]: thread = (k, n quad)
-      const int k = k0 + (t >> 4), n = n0 + 4 * (t & 15);
-      if (k < kend && n < a.N)
-        vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(k) * a.ldb + n);
-    } else {  // B[n][k]: thread = (n, k quad)
-      const int n = n0 + (t >> 2), k = k0 + 4 * (t & 3);
-      if (n < a.N && k < kend)
-        vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(n) * a.ldb + k);
-    }
-    ra = va;
-    rb = vb;
   };
-  auto commit = [&](int buf) {
-    if (!a.ta) {
-      *reinterpret_cast<f4*>(&As[buf][(t >> 2) * PK + 4 * (t & 3)]) = ra;
-    } else {
-      const int k = t >> 4, m = 4 * (t & 15);
+  auto commit = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[q];
-    }
-    if (!a.tb) {
-      const int k = t >> 4, n = 4 * (t & 15);
+    for (int j = 0; j < KQ; ++j) {
+      if (!a.ta) {
+        *reinterpret_cast<f4*>(&As[buf][(t >> 2) * PK + 4 * (t & 3) + 16 * j]) = ra[j];
+      } else {
+        const int k = (t >> 4) + 16 * j, m = 4 * (t & 15);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Bs[buf][(n + q) * PK + k] = rb[q];
-    } else {
-      *reinterpret_cast<f4*>(&Bs[buf][(t >> 2) * PK + 4 * (t & 3)]) = rb;
+        for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[j][q];
+      }
+      if (!a.tb) {
+        const int k = (t >> 4) + 16 * j, n = 4 * (t & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bs[buf][(n + q) * PK + k] = rb[j][q];
+      } else {
+        *reinterpret_cast<f4*>(&Bs[buf][(t >> 2) * PK + 4 * (t & 3) + 16 * j]) = rb[j];
+      }
     }
   };
 
   f16v acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  const int arow = (wm * 32 + l32) * PK + 8 * h;
-  const int brow = (wn * 32 + l32) * PK + 8 * h;
+  // lane half h consumes k = (BK / 2) h + s in MFMA s of a step
+  const int arow = (wm * 32 + l32) * PK + (BK / 2) * h;
+  const int brow = (wn * 32 + l32) * PK + (BK / 2) * h;
   int buf = 0;
   if (kbeg < kend) {
     load(kbeg);
@@ -148,16 +157,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     const bool more = k0 + BK < kend;
     if (more) load(k0 + BK);  // in flight under the MFMAs
-    const f4 a0 = *reinterpret_cast<const f4*>(&As[buf][arow]);
-    const f4 a1 = *reinterpret_cast<const f4*>(&As[buf][arow + 4]);
-    const f4 b0 = *reinterpret_cast<const f4*>(&Bs[buf][brow]);
-    const f4 b1 = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc, 0, 0, 0);
+    for (int c = 0; c < BK / 8; ++c) {
+      const f4 av = *reinterpret_cast<const f4*>(&As[buf][arow + 4 * c]);
+      const f4 bv = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4 * c]);
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc, 0, 0, 0);
+      for (int s = 0; s < 4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+    }
     if (more) {
       commit(buf ^ 1);
       __syncthreads();

@@ -403,3 +403,28 @@ def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
   assert rel_err(dx, ref) <= TOL
   assert rel_err(dw, gw) <= TOL
   assert rel_err(db, gb) <= TOL
+
+
+@pytest.mark.parametrize('H,W,C', [(36, 48, 16), (18, 24, 32), (11, 11, 16)])
+@pytest.mark.parametrize('block_conv', [1, 2])
+def test_residual_block_forward_flags(cuda, H, W, C, block_conv):
+  """The two forward flag sets of a residual block at N = 160 frames: conv 1
+  = ReLU on the input + ReLU on the output + bias, conv 2 = bias + skip add
+  (the sets that have compile-time kernel instances, conv_wino.hip)."""
+  Cmod = _C()
+  N = 160
+  g = torch.Generator().manual_seed(H * C + block_conv)
+  x = torch.randn(N, H, W, C, generator=g)
+  w = torch.randn(3, 3, C, C, generator=g) / (9 * C) ** 0.5
+  b = torch.randn(C, generator=g) * 0.1
+  if block_conv == 1:
+    ref = layers.conv2d_same_nhwc(x.double().clamp(min=0), w.double(), b.double(), 1)
+    ref = ref.clamp(min=0)
+    y = Cmod.cf32_conv_fwd(x.to(cuda), w.to(cuda), b.to(cuda), 1, 1, 1, H, W,
+                           relu_in=True, relu_out=True)
+  else:
+    add = torch.randn(N, H, W, C, generator=g)
+    ref = layers.conv2d_same_nhwc(x.double(), w.double(), b.double(), 1) + add.double()
+    y = Cmod.cf32_conv_fwd(x.to(cuda), w.to(cuda), b.to(cuda), 1, 1, 1, H, W,
+                           add=add.to(cuda))
+  assert rel_err(y, ref) <= TOL
