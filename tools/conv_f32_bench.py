@@ -83,8 +83,9 @@ for name, H, W, Cc, Cy, res in [('res16 36x48', 36, 48, 16, 16, True),
     C.cf32_conv_wgrad(x, dy, 1, 1, 1, res, dw, db)
     C.cf32_conv_dgrad(dy, w, 1, 1, 1, H, W, mask=x if res else None, add=add)
   ts = timeit(sep)
-  print('%-26s bwd fused %8.1f us | separate wgrad+dgrad %8.1f us' % (name, tf, ts),
-        flush=True)
+  bflop = 2 * 2.0 * N * H * W * 9 * Cc * Cy  # dgrad + wgrad, direct-conv FLOPs
+  print('%-26s bwd fused %8.1f us %6.1f TF | separate wgrad+dgrad %8.1f us %6.1f TF' % (
+      name, tf, bflop / tf / 1e6, ts, bflop / ts / 1e6), flush=True)
 if ONLY:
   sys.exit(0)
 xp = torch.randn(N, 72, 96, 16, device=dev)
