@@ -1,0 +1,6 @@
+bash tools/gpu_session.sh \
+ "fused|300|python -u -m pytest tests/test_conv_f32_gpu.py -k 'bwd_fused or many_tiles or residual_block' -x -q --timeout 200 --timeout-method thread" \
+ "bench|200|python bench.py" \
+ "benchskip|200|SA_BENCH_SKIP_H2D=1 python bench.py" \
+ "layers|200|python tools/conv_f32_bench.py 3232 10 bwd" \
+ "bench1|200|python bench.py"
