@@ -967,6 +967,10 @@ static_assert(pw_pitch(96) == 101 && pw_pitch(84) == 101 && pw_pitch(3) == 5, "p
 // x: the fp32 4-channel image, or (u8_cs > 0) the uint8 frames themselves
 // with u8_cs <= 4 channels, scaled by 1/255 on the way into LDS (the same
 // tf.to_float(frame) / 255 as the forward, experiment.py:153-155)
+// U8: the image is uint8 with u8_cs channels (x / 255 at staging), else the
+// 4-channel fp32 image.  Compile-time: the runtime source switch cost the
+// fp32 path 226 -> 334 us per call.
+template <bool U8>
 __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
     const void* __restrict__ xsrc, int u8_cs, const float* __restrict__ dP,
     const uint8_t* __restrict__ arg, int H, int W, int Hp, int Wp, int pbh, int pbw,
@@ -1011,7 +1015,7 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
       f4 v = {0.f, 0.f, 0.f, 0.f};
       if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
         const int64_t pix = (static_cast<int64_t>(n) * H + yy) * W + xx;
-        if (u8_cs > 0) {
+        if constexpr (U8) {
           const uint8_t* p = xu + pix * u8_cs;
           v[0] = static_cast<float>(p[0]) / 255.f;
           if (u8_cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
@@ -1487,10 +1491,17 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, int u8_cs, hipStream_t
   const int G = std::min(ntiles, slots);
   const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
                                       sizeof(float) * 4 * 37 * 16);
-  allow_lds(pool_wgrad_kernel, lds);
-  hipLaunchKernelGGL(pool_wgrad_kernel, dim3(G), dim3(kThreads), lds, s, a.src,
-                     u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,
-                     ntiles, ws);
+  if (u8_cs > 0) {
+    allow_lds(pool_wgrad_kernel<true>, lds);
+    hipLaunchKernelGGL(pool_wgrad_kernel<true>, dim3(G), dim3(kThreads), lds, s, a.src,
+                       u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,
+                       ntiles, ws);
+  } else {
+    allow_lds(pool_wgrad_kernel<false>, lds);
+    hipLaunchKernelGGL(pool_wgrad_kernel<false>, dim3(G), dim3(kThreads), lds, s, a.src,
+                       u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,
+                       ntiles, ws);
+  }
   wgrad_reduce(ws, G, 1, 48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db, s);
   return true;
 }
