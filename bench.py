@@ -245,6 +245,8 @@ def main():
     device = torch.device(args.device)
   if device.type == 'cuda':
     torch.cuda.set_device(device)
+    # the H2D prefetch stream is the process's first stream (see measure)
+    _COPY_STREAMS.setdefault(device, torch.cuda.Stream(device))
 
   backend = args.backend
   if backend == 'auto':

@@ -163,8 +163,8 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
 // columns of dG) in [4H/16 w, 4H/16 (w+1)).  dh_rec = dG_{t+1} W_h^T.
 // dg_pk_in/out: dG in MFMA-operand order [row tile][wave][mt][s][lane];
 // wt: W_h^T packed [H/16][wave][s][lane] (lane <-> unit l&15, n = 4s+(l>>4)).
-template <int H, int RW = 32>
-__global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
+template <int H, int RW = 32, int NW = 16>
+__global__ __launch_bounds__(64 * NW) void lstm_bwd_step_kernel(
     const float* __restrict__ dh_out_t, const float* __restrict__ dg_pk_in,
     const uint8_t* __restrict__ done_next, const uint8_t* __restrict__ done_t,
     const float* __restrict__ wt, const float* __restrict__ acts_t,
@@ -173,7 +173,6 @@ __global__ __launch_bounds__(1024) void lstm_bwd_step_kernel(
     float* __restrict__ dg_t, float* __restrict__ dg_pk_out,
     __hip_bfloat16* __restrict__ dg16_t, int B, int xpack) {
   const float* dg_next = dg_pk_in;
-  constexpr int NW = 16;
   constexpr int NWID = 4 * H / NW;  // n per wave
   constexpr int NS = NWID / 4;
   __shared__ f4v red[NW][2][64];
@@ -352,6 +351,20 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
   const int xp = g_xpack;
   dim3 grid(H / 16 * xp, (B + 31) / 32);
   __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
+  static const bool w8 = [] {
+    const char* e = std::getenv("SA_LSTM_BWD_W8");
+    return e && std::atoi(e) == 1;
+  }();
+  if (H == 256 && g_rows16 && w8) {
+    // 8 waves of 128 gate columns each (the packed W_h^T layout is the same:
+    // each wave's slice is contiguous); the packed dG layout is private to
+    // this kernel's own step-to-step hand-off
+    dim3 grid16(H / 16 * xp, (B + 15) / 16);
+    hipLaunchKernelGGL((lstm_bwd_step_kernel<256, 16, 8>), grid16, dim3(512), 0, stream,
+                       dh_out_t, dg_pk_in, done_next, done_t, wt, acts_t, c_t,
+                       c_prev, dcarry_in, dcarry_out, dg_t, dg_pk_out, d16, B, xp);
+    return;
+  }
   if (H == 256 && g_rows16) {
     dim3 grid16(H / 16 * xp, (B + 15) / 16);
     hipLaunchKernelGGL((lstm_bwd_step_kernel<256, 16>), grid16, dim3(1024), 0, stream,
