@@ -30,6 +30,7 @@
 #include "gemm_f32.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sa {
 namespace {
@@ -70,45 +71,54 @@ __device__ __forceinline__ void store_aug(const GemmEpilogue& e, int m, int j) {
   e.C[static_cast<int64_t>(m) * e.ldc + e.aug_c0 + j] = v;
 }
 
+// RM: 32-row MFMA blocks per wave (workgroup tile (64 RM) x 64): RM = 2 for
+// the tall learner GEMMs (M = T*B = 3232) reuses each B fragment twice
+template <int RM>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
-  __shared__ __attribute__((aligned(16))) float As[2][BM * PK];
+  constexpr int BMt = BM * RM;
+  __shared__ __attribute__((aligned(16))) float As[2][BMt * PK];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * PK];
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int h = lane >> 5, l32 = lane & 31;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = blockIdx.x * BMt, n0 = blockIdx.y * BN;
   const int Mr = a.M + a.ones_row;
   const int kbeg = blockIdx.z * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
-  constexpr int KQ = BK / 16;  // f4 per thread and operand per K step
+  constexpr int KQ = BK / 16;  // f4 per thread and operand per K step and 64 rows
 
-  // global -> register staging of one K step (KQ f4 per thread and operand)
-  f4 ra[KQ], rb[KQ];
+  // global -> register staging of one K step
+  f4 ra[RM][KQ], rb[KQ];
   auto load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < KQ; ++j) {
-      f4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
-      if (!a.ta) {  // A[m][k]: thread = (m, k quad)
-        const int m = m0 + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
-        if (m < a.M && k < kend)
-          va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(m) * a.lda + k);
-        else if (m == a.M && a.ones_row && k < kend)
-          va = f4{1.f, 1.f, 1.f, 1.f};
-      } else {  // A[k][m]: thread = (k, m quad)
-        const int k = k0 + (t >> 4) + 16 * j, m = m0 + 4 * (t & 15);
-        if (k < kend) {
-          if (m + 3 < a.M) {
-            va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(k) * a.lda + m);
-          } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (m + q < a.M) va[q] = a.A[static_cast<int64_t>(k) * a.lda + m + q];
-              else if (m + q == a.M && a.ones_row) va[q] = 1.f;
+      for (int r = 0; r < RM; ++r) {
+        f4 va = {0.f, 0.f, 0.f, 0.f};
+        if (!a.ta) {  // A[m][k]: thread = (m, k quad)
+          const int m = m0 + 64 * r + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
+          if (m < a.M && k < kend)
+            va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(m) * a.lda + k);
+          else if (m == a.M && a.ones_row && k < kend)
+            va = f4{1.f, 1.f, 1.f, 1.f};
+        } else {  // A[k][m]: thread = (k, m quad)
+          const int k = k0 + (t >> 4) + 16 * j, m = m0 + 64 * r + 4 * (t & 15);
+          if (k < kend) {
+            if (m + 3 < a.M) {
+              va = *reinterpret_cast<const f4*>(a.A + static_cast<int64_t>(k) * a.lda + m);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                if (m + q < a.M) va[q] = a.A[static_cast<int64_t>(k) * a.lda + m + q];
+                else if (m + q == a.M && a.ones_row) va[q] = 1.f;
+              }
             }
           }
         }
+        ra[r][j] = va;
       }
+      f4 vb = {0.f, 0.f, 0.f, 0.f};
       if (!a.tb) {  // B[k][n]: thread = (k, n quad)
         const int k = k0 + (t >> 4) + 16 * j, n = n0 + 4 * (t & 15);
         if (k < kend && n < a.N)
@@ -118,19 +128,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
         if (n < a.N && k < kend)
           vb = *reinterpret_cast<const f4*>(a.B + static_cast<int64_t>(n) * a.ldb + k);
       }
-      ra[j] = va;
       rb[j] = vb;
     }
   };
   auto commit = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < KQ; ++j) {
-      if (!a.ta) {
-        *reinterpret_cast<f4*>(&As[buf][(t >> 2) * PK + 4 * (t & 3) + 16 * j]) = ra[j];
-      } else {
-        const int k = (t >> 4) + 16 * j, m = 4 * (t & 15);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[j][q];
+      for (int r = 0; r < RM; ++r) {
+        if (!a.ta) {
+          *reinterpret_cast<f4*>(&As[buf][(64 * r + (t >> 2)) * PK + 4 * (t & 3) + 16 * j]) =
+              ra[r][j];
+        } else {
+          const int k = (t >> 4) + 16 * j, m = 64 * r + 4 * (t & 15);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[r][j][q];
+        }
       }
       if (!a.tb) {
         const int k = (t >> 4) + 16 * j, n = 4 * (t & 15);
@@ -142,11 +155,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
     }
   };
 
-  f16v acc;
+  f16v acc[RM];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  // lane half h consumes k = (BK / 2) h + s in MFMA s of a step
-  const int arow = (wm * 32 + l32) * PK + (BK / 2) * h;
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+  // wave rows: 32-row blocks wm * 32 RM + 32 r; lane half h consumes
+  // k = (BK / 2) h + s in MFMA s of a step
+  const int arow = (wm * 32 * RM + l32) * PK + (BK / 2) * h;
   const int brow = (wn * 32 + l32) * PK + (BK / 2) * h;
   int buf = 0;
   if (kbeg < kend) {
@@ -159,11 +175,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
     if (more) load(k0 + BK);  // in flight under the MFMAs
 #pragma unroll
     for (int c = 0; c < BK / 8; ++c) {
-      const f4 av = *reinterpret_cast<const f4*>(&As[buf][arow + 4 * c]);
       const f4 bv = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4 * c]);
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc, 0, 0, 0);
+      for (int r = 0; r < RM; ++r) {
+        const f4 av = *reinterpret_cast<const f4*>(&As[buf][arow + 32 * r * PK + 4 * c]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[r], 0, 0, 0);
+      }
     }
     if (more) {
       commit(buf ^ 1);
@@ -172,27 +191,31 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
     }
   }
 
-  // D[i][j]: j = lane & 31, i = (r & 3) + 8 (r >> 2) + 4 h
+  // D[i][j]: j = lane & 31, i = (e & 3) + 8 (e >> 2) + 4 h
   const int n = n0 + wn * 32 + l32;
   if (a.splits > 1) {
     float* p = a.part + static_cast<int64_t>(blockIdx.z) * Mr * a.N;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (m < Mr && n < a.N) p[static_cast<int64_t>(m) * a.N + n] = acc[r];
-    }
+    for (int r = 0; r < RM; ++r)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * 32 * RM + 32 * r + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m < Mr && n < a.N) p[static_cast<int64_t>(m) * a.N + n] = acc[r][e];
+      }
     return;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (n >= a.N) continue;
-    if (m < a.M) store_out(a.ep, m, n, acc[r]);
-    else if (m == a.M && a.ones_row) a.ep.colsum[n] += acc[r];
-  }
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = m0 + wm * 32 * RM + 32 * r + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (n >= a.N) continue;
+      if (m < a.M) store_out(a.ep, m, n, acc[r][e]);
+      else if (m == a.M && a.ones_row) a.ep.colsum[n] += acc[r][e];
+    }
   if (a.ep.aug_c0 > 0 && blockIdx.y == 0) {
     const int naug = a.ep.ldc - a.ep.aug_c0;
-    for (int e = t; e < BM * naug; e += 256) {
+    for (int e = t; e < BMt * naug; e += 256) {
       const int m = m0 + e / naug;
       if (m < a.M) store_aug(a.ep, m, e % naug);
     }
@@ -226,8 +249,21 @@ int64_t gemm_f32_part_floats(int M, int N, int K, int ones_row, int splits) {
   return splits > 1 ? static_cast<int64_t>(splits) * (M + ones_row) * N : 0;
 }
 
+// 128-row workgroup tiles (RM = 2) for tall products are opt-in
+// (SA_GEMM_RM=2 for M + ones_row >= 1024): the learner step measured 10.61 -
+// 10.63 ms with them against 10.51 ms with 64-row tiles (fewer workgroups
+// per GEMM on 256 CUs, 55 KB of LDS each)
+static int gemm_rm(int Mr) {
+  static const int force = [] {
+    const char* e = std::getenv("SA_GEMM_RM");
+    return e ? std::atoi(e) : 1;
+  }();
+  return force == 2 && Mr >= 1024 ? 2 : 1;
+}
+
 int gemm_f32_splits(int M, int N, int K, int ones_row) {
-  const int tiles = ((M + ones_row + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int bm = BM * gemm_rm(M + ones_row);
+  const int tiles = ((M + ones_row + bm - 1) / bm) * ((N + BN - 1) / BN);
   int s = 1;
   // enough workgroups to fill 256 CUs twice over, each K chunk >= 128
   while (tiles * s < 512 && K / (2 * s) >= 128 && s < 16) s *= 2;
@@ -253,8 +289,12 @@ bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int ld
   a.part = part;
   a.ep = ep;
   const int Mr = M + (ones_row ? 1 : 0);
-  dim3 grid((Mr + BM - 1) / BM, (N + BN - 1) / BN, a.splits);
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, stream, a);
+  const int rm = gemm_rm(Mr);
+  dim3 grid((Mr + BM * rm - 1) / (BM * rm), (N + BN - 1) / BN, a.splits);
+  if (rm == 2)
+    hipLaunchKernelGGL(gemm_f32_kernel<2>, grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_f32_kernel<1>, grid, dim3(256), 0, stream, a);
   if (a.splits > 1) {
     const int64_t total = static_cast<int64_t>(Mr) * N;
     const int64_t aug = ep.aug_c0 > 0 ? static_cast<int64_t>(M) * (ep.ldc - ep.aug_c0) : 0;
