@@ -1575,8 +1575,13 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
             for (int q = 0; q < 4; ++q) yb[q * 64] = Y[q];
             __hip_atomic_store(flag_s + task, it, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
-            while (!(a.ablate & 1) &&
-                   __hip_atomic_load(flag_s + task, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != it)
+            // bounded wait (~30 ms): the partner wave always publishes
+            // (same task, same group condition), but a kernel must never be
+            // able to spin forever
+            for (int spin = 0; !(a.ablate & 1) && spin < (1 << 20) &&
+                               __hip_atomic_load(flag_s + task, __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP) != it;
+                 ++spin)
               __builtin_amdgcn_s_sleep(1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) Y[q] += yb[q * 64];
@@ -1867,6 +1872,8 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
     // 3-wave workgroups over 48-tile ranges: at 36x48 every range is two
     // whole tile rows of one image (6 staged rows, 40 KB of LDS), so four
     // workgroups (three waves per SIMD) fit on a CU
+    // SA_WINO_CFG=3: 8 waves over 128-tile ranges (one workgroup per CU)
+    if (cfg == 3 && run_wino<16, 16, 1, 8, 128, 7, 2>(c, flip, s)) return true;
     static const int w3 = env_int("SA_WINO16_3W", 0);
     if (w3 && !flip) {
       const int fl = (c.relu_in ? 1 : 0) | (c.relu_out ? 2 : 0) | (c.mask ? 4 : 0) |
