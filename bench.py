@@ -20,7 +20,13 @@ re-unroll, V-trace, loss, backward, gradient all-reduce, RMSProp with
 on-device LR decay, frame-counter increment.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16]
-(multi-GPU: launched by torch.distributed.run, one rank per GPU).
+
+Multi-GPU: either launched by torch.distributed.run (one rank per GPU, the
+env carries RANK/WORLD_SIZE/...), or plain `python bench.py --gpus N`: then
+this process is only a launcher - it never imports torch or touches a GPU -
+and starts N fresh rank processes itself (the reference's N-process local
+cluster, experiment.py:497-512, minus gRPC), relays rank 0's JSON line and
+exits non-zero if any rank fails or overruns its time limit.
 """
 
 import argparse
@@ -30,7 +36,84 @@ import os
 import sys
 import time
 
-import torch
+
+def _self_launch(argv):
+  """`--gpus N` (N>1) with no WORLD_SIZE in the env: run N ranks as child
+  processes of this (GPU-free) launcher.  Returns the exit code."""
+  import signal
+  import socket
+  import subprocess
+  ap = argparse.ArgumentParser(add_help=False)
+  ap.add_argument('--gpus', type=int, default=1)
+  known, _ = ap.parse_known_args(argv)
+  n = known.gpus
+  s = socket.socket()
+  s.bind(('127.0.0.1', 0))
+  port = s.getsockname()[1]
+  s.close()
+  limit = float(os.environ.get('SA_BENCH_TIMEOUT_S', '1500'))
+  procs = []
+  for r in range(n):
+    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), GROUP_RANK='0',
+               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    # rank 0 owns stdout (the one JSON line); the others' stdout is dropped
+    procs.append(subprocess.Popen(
+        [sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+        stdout=None if r == 0 else subprocess.DEVNULL,
+        start_new_session=True))
+
+  def kill_all():
+    for p in procs:
+      if p.poll() is None:
+        try:
+          os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+          pass
+    for p in procs:
+      p.wait()
+
+  t0 = time.time()
+  last_note = t0
+  while True:
+    codes = [p.poll() for p in procs]
+    bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+    if bad:
+      r, c = bad[0]
+      sys.stderr.write('bench.py launcher: rank %d exited with %d; stopping '
+                       'the other ranks\n' % (r, c))
+      kill_all()
+      return c if c > 0 else 1
+    if all(c == 0 for c in codes):
+      return 0
+    now = time.time()
+    if now - t0 > limit:
+      sys.stderr.write('bench.py launcher: ranks still running after %.0f s; '
+                       'killing them\n' % limit)
+      kill_all()
+      return 124
+    if now - last_note > 60:
+      last_note = now
+      sys.stderr.write('bench.py launcher: %d/%d ranks running (%.0f s)\n' %
+                       (sum(c is None for c in codes), n, now - t0))
+      sys.stderr.flush()
+    time.sleep(0.2)
+
+
+def _wants_self_launch(argv):
+  if 'WORLD_SIZE' in os.environ:
+    return False
+  ap = argparse.ArgumentParser(add_help=False)
+  ap.add_argument('--gpus', type=int, default=1)
+  known, _ = ap.parse_known_args(argv)
+  return known.gpus > 1
+
+
+if __name__ == '__main__' and _wants_self_launch(sys.argv[1:]):
+  sys.exit(_self_launch(sys.argv[1:]))
+
+import torch  # noqa: E402  (after the launcher: it must not load torch)
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -97,7 +180,12 @@ def measure(args, dtype, device, backend, rank, world):
       # one captured graph per staging slot (static input addresses)
       for sl in slots:
         learner.capture(sl, clone=False)
-        graphs.append((learner._graph, learner._static_in, learner._static_loss))
+        # split mode (world>1): the torso-feature tensors live in this
+        # slot's graph pool; keeping them per slot stops the next capture
+        # from freeing them (experiment.py keeps them the same way)
+        graphs.append((learner._graph, learner._static_in,
+                       learner._static_loss,
+                       getattr(learner, '_graph_keep', None)))
     slot_free = [torch.cuda.Event(), torch.cuda.Event()]
     slot_ready = [torch.cuda.Event(), torch.cuda.Event()]
     for e in slot_ready + slot_free:
@@ -126,7 +214,8 @@ def measure(args, dtype, device, backend, rank, world):
     j = (k + 1) % 2
     comp.wait_event(slot_ready[i])
     if use_graph:
-      learner._graph, learner._static_in, learner._static_loss = graphs[i]
+      (learner._graph, learner._static_in, learner._static_loss,
+       learner._graph_keep) = graphs[i]
       loss = learner.graph_step()
     else:
       loss = learner.step(slots[i])
@@ -231,10 +320,8 @@ def main():
                                torch.cuda.device_count())
   rank, world, local = parallel.init_distributed()
   if args.gpus != world:
-    raise SystemExit(
-        'bench.py: --gpus %d but WORLD_SIZE=%d; launch N>1 GPUs with '
-        '`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`'
-        % (args.gpus, world))
+    raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' %
+                     (args.gpus, world))
   if args.device == 'auto':
     # one-card rehearsal (SA_DIST_BACKEND): ranks share the visible GPUs
     if torch.cuda.is_available():

@@ -310,6 +310,15 @@ void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
 
 }  // namespace
 
+namespace sa {
+unsigned* device_error_words() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return reinterpret_cast<unsigned*>(
+      lstm_err_word(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(d))).data_ptr<int>());
+}
+}  // namespace sa
+
 void register_conv_ops(pybind11::module& m);     // conv_bindings.cpp
 void register_learner_ops(pybind11::module& m);  // learner_bindings.cpp
 void register_conv_f32_ops(pybind11::module& m); // conv_f32_bindings.cpp

@@ -412,4 +412,5 @@ void register_conv_f32_ops(pybind11::module& m) {
   m.def("cf32_maxpool_bwd", &maxpool_bwd);
   m.def("cf32_relu_mask_", &relu_mask_);
   m.def("cf32_frames_f32", &frames_f32);
+  m.def("cf32_wino_fault", [](int v) { return sa::cf32::conv_wino_fault(v); });
 }

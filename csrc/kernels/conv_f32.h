@@ -15,6 +15,12 @@
 #include <cstdint>
 
 namespace sa {
+
+// The current device's sticky error words, int32[4] zero-initialised device
+// memory (bindings.cpp): [0] the LSTM recurrence's timeout word, [1] the
+// conv kernels' hand-off timeout word.  The RMSProp guard consumes both.
+unsigned* device_error_words();
+
 namespace cf32 {
 
 // kSrcPoolGrad: the source is the gradient of a 3x3/2 SAME max-pool's
@@ -82,6 +88,10 @@ struct WgradArgs {
 // 16/32 channels in and out (forward and data gradient); false when the
 // shape is not covered.  SA_F32_WINO=0 disables it (direct implicit GEMM).
 bool wino_enabled();
+
+// Fault injection (tests): 1 = every bounded intra-workgroup hand-off wait of
+// the fused Winograd backward reports a timeout.  Returns the old setting.
+int conv_wino_fault(int v);
 bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
 // Winograd weight gradient (3x3/1 SAME, 16/32 channels; SA_F32_WINO_WG=0
 // disables): per-workgroup partials in the wgrad slot layout of `ws`, then

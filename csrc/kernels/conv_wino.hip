@@ -41,8 +41,20 @@ namespace cf32 {
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int kMaxParts = 4;  // images one range may touch
+
+// Measurement knobs (SA_WINO_ABLATE / SA_FUSED_ABLATE: drop parts of a
+// kernel's work to time the rest) exist only in builds with
+// -DSA_MEASURE_KNOBS=1; in production builds every knob test folds to false,
+// so no environment variable can remove a synchronisation or a store.
+#ifndef SA_MEASURE_KNOBS
+#define SA_MEASURE_KNOBS 0
+#endif
+__device__ __forceinline__ bool knob(int v, int bit) {
+  return SA_MEASURE_KNOBS && (v & bit) != 0;
+}
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -271,7 +283,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
       const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
-      const bool in = rb >= 0 && sl_x[k] >= 0 && !(a.ablate & 2);
+      const bool in = rb >= 0 && sl_x[k] >= 0 && !knob(a.ablate, 2);
       stg[k] = bload(srcr, in ? static_cast<uint32_t>(rb + sl_x[k]) * 4u : kOOB);
     }
   };
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     __syncthreads();  // U_s written / the previous range's patch reads done
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
-      if (sl_L[k] >= 0 && !(a.ablate & 4)) {
+      if (sl_L[k] >= 0 && !knob(a.ablate, 4)) {
         const int e = threadIdx.x + k * NTH;
         f4 v = stg[k];  // zero where out of the image (range check)
         if (f_relu_in) {
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     if (r < rw.end) prefetch();  // in flight under the MFMAs below
     const RangeGeom gm = range_geom(a, cur, RT);
 
-    for (int task = (a.ablate & 1) ? NTASK : wave; task < NTASK; task += NW) {
+    for (int task = knob(a.ablate, 1) ? NTASK : wave; task < NTASK; task += NW) {
       const int grp = task % NG, sl = task / NG;
       if (gm.t0 + 16 * grp >= gm.t1) continue;  // empty group (batch tail)
       const int co0 = sl * 16 * NH;
@@ -416,7 +428,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
           for (int dx = 0; dx < 2; ++dx) {
             const int oy = 2 * ty + dy, ox = 2 * tx + dx;
-            if (!valid || oy >= a.H || ox >= a.W || (a.ablate & 8)) continue;
+            if (!valid || oy >= a.H || ox >= a.W || knob(a.ablate, 8)) continue;
             const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT + co;
             f4 v = Y[2 * dy + dx] + bv;
             const f4 m = pm[h][2 * dy + dx];
@@ -449,6 +461,8 @@ int env_int(const char* name, int def) {
   const char* e = std::getenv(name);
   return (e && *e) ? std::atoi(e) : def;
 }
+
+int g_wino_fault = 0;  // conv_wino_fault(): tests of the fail-loud hand-off
 
 template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
 bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
@@ -488,7 +502,7 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   a.wcin = c.wcin; a.wcout = c.wcout; a.flip = flip ? 1 : 0;
   a.relu_in = c.relu_in; a.relu_out = c.relu_out;
   a.maxrows = maxrows;
-  static const int ablate = env_int("SA_WINO_ABLATE", 0);
+  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_WINO_ABLATE", 0) : 0;
   a.ablate = ablate;
   static const int runs = env_int("SA_WINO_RUNS", 1);
   a.runs = runs;
@@ -920,8 +934,11 @@ struct WinoBwdArgs {
   float rTX, rTY;
   int relu_x;        // wgrad operand = relu(x)
   int mask_x = 1;    // dX masked by (x > 0) (fused32 kernel; the 16-channel one always masks)
-  int ablate = 0;    // measurement knob (SA_FUSED_ABLATE): 1 no pair wait, 2 no dgrad, 4 no wgrad
+  int ablate = 0;    // measurement knob (SA_FUSED_ABLATE, SA_MEASURE_KNOBS builds only):
+                     // 2 no dgrad, 4 no wgrad
   int runs = 1;      // contiguous range runs (wino_bwd_fused_kernel; fused32 always)
+  unsigned* err = nullptr;  // the device's sticky conv error word (rmsprop.hip guard)
+  int fault = 0;     // fault injection: every hand-off wait reports a timeout
 };
 
 // WWG: the weight gradient in Winograd form too (dL/dU = sum_tiles V(x) .*
@@ -1496,7 +1513,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     for (;;) {
       const RangeGeom gm = advance();
       ++it;
-      if (gm.t0 + 16 * grp < gm.t1 && !(a.ablate & 2)) {
+      if (gm.t0 + 16 * grp < gm.t1 && !knob(a.ablate, 2)) {
         int t = gm.t0 + 16 * grp + c16;
         const bool valid = t < gm.t1;
         if (!valid) t = gm.t0;
@@ -1577,14 +1594,28 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
           } else {
             // bounded wait (~30 ms): the partner wave always publishes
             // (same task, same group condition), but a kernel must never be
-            // able to spin forever
-            for (int spin = 0; !(a.ablate & 1) && spin < (1 << 20) &&
-                               __hip_atomic_load(flag_s + task, __ATOMIC_ACQUIRE,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP) != it;
-                 ++spin)
-              __builtin_amdgcn_s_sleep(1);
+            // able to spin forever.  A wait that expires fails LOUD: the
+            // sticky error word makes the RMSProp guard skip this step's
+            // update and count it (learner health 'conv_timeouts'), instead
+            // of adding a stale partial into dX.
+            bool got = false;
+            if (!a.fault) {
+              for (int spin = 0; spin < (1 << 20); ++spin) {
+                if (__hip_atomic_load(flag_s + task, __ATOMIC_ACQUIRE,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP) == it) {
+                  got = true;
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+            }
+            if (got) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) Y[q] += yb[q * 64];
+              for (int q = 0; q < 4; ++q) Y[q] += yb[q * 64];
+            } else {
+              __hip_atomic_store((gu32*)(a.err), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
         }
         if (half == 0) {
@@ -1630,7 +1661,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     auto kloop = [&](auto ARc, auto FULLc) __attribute__((always_inline)) {
       constexpr int AR = decltype(ARc)::value;
       constexpr bool FULL = decltype(FULLc)::value;
-        for (int st = 0; st < ((a.ablate & 4) ? 0 : RT / 4); ++st) {
+        for (int st = 0; st < (knob(a.ablate, 4) ? 0 : RT / 4); ++st) {
           int bpx = tile_s[4 * st + kperm(g)];
           const bool valid = FULL || bpx >= 0;
           bpx = valid ? bpx : 0;
@@ -1783,8 +1814,10 @@ bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const flo
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
   a.mask_x = mask_x;
-  static const int ablate = env_int("SA_FUSED_ABLATE", 0);
+  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_FUSED_ABLATE", 0) : 0;
   a.ablate = ablate;
+  a.err = device_error_words() + 1;
+  a.fault = g_wino_fault;
   auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
@@ -1853,6 +1886,12 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
 }
 
 }  // namespace
+
+int conv_wino_fault(int v) {
+  const int old = g_wino_fault;
+  if (v == 0 || v == 1) g_wino_fault = v;
+  return old;
+}
 
 bool wino_enabled() {
   static const bool on = env_int("SA_F32_WINO", 1) != 0;

@@ -5,13 +5,15 @@
 //   mom = momentum * mom + lr * g / sqrt(ms + eps)
 //   w  -= mom
 //
-// Step guard (optional), int32[4] = {flag, skipped, lstm_timeouts, -}: a
-// check kernel ORs "some gradient is NaN/inf" (bit 0) into guard[0] (zeroed
-// by a memset node each step) and, when given the recurrence's sticky
-// timeout word (lstm_gang.hip / lstm_persistent.hip: a workgroup of the
-// cooperative unroll could not co-reside and the unroll was abandoned, so
-// its activations/gradients are stale), consumes it: bit 1, guard[2] += 1,
-// word reset.  The update kernel then leaves every parameter and slot
+// Step guard (optional), int32[4] = {flag, skipped, lstm_timeouts,
+// conv_timeouts}: a check kernel ORs "some gradient is NaN/inf" (bit 0) into
+// guard[0] (zeroed by a memset node each step) and, when given the device's
+// sticky error words (err[0]: the recurrence, lstm_gang.hip /
+// lstm_persistent.hip - a workgroup of the cooperative unroll could not
+// co-reside and the unroll was abandoned; err[1]: a bounded intra-workgroup
+// hand-off wait of the fused Winograd backward expired, conv_wino.hip - in
+// both cases activations/gradients are stale), consumes them: bit 1,
+// guard[2] / guard[3] += 1, words reset.  The update kernel then leaves every parameter and slot
 // untouched and counts the skipped step in guard[1].  One extra 8-MB read
 // per step, no host synchronisation; the host reads the counters lazily.
 //
@@ -24,16 +26,20 @@
 namespace sa {
 namespace {
 
+typedef __attribute__((address_space(1))) unsigned gu32;
+
 __global__ __launch_bounds__(256) void finite_check_kernel(
     const float4* __restrict__ g, int64_t n4, int* __restrict__ guard,
     unsigned* __restrict__ lstm_err) {
-  if (lstm_err != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
-    const unsigned e = __hip_atomic_load(lstm_err, __ATOMIC_RELAXED,
+  if (lstm_err != nullptr && blockIdx.x == 0 && threadIdx.x < 2) {
+    // lane 0: the recurrence's word, lane 1: the conv backward's word
+    gu32* ew = (gu32*)(lstm_err + threadIdx.x);
+    const unsigned e = __hip_atomic_load(ew, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     if (e != 0u) {
       atomicOr(guard, 2);
-      atomicAdd(guard + 2, 1);
-      __hip_atomic_store(lstm_err, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(guard + 2 + threadIdx.x, 1);
+      __hip_atomic_store(ew, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;

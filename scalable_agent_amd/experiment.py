@@ -786,8 +786,9 @@ def train(flags):
         if health['skipped_updates'] > reported_skips:
           # loud, not fatal: the guard already dropped those updates
           log.warning('learner dropped %d update(s) so far (%d LSTM unroll '
-                      'timeout(s), rest non-finite gradients)',
-                      health['skipped_updates'], health['lstm_timeouts'])
+                      'timeout(s), %d conv hand-off timeout(s), rest '
+                      'non-finite gradients)', health['skipped_updates'],
+                      health['lstm_timeouts'], health['conv_timeouts'])
           reported_skips = health['skipped_updates']
       if saver is not None:
         saver.maybe_save()

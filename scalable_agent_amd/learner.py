@@ -324,11 +324,14 @@ class Learner:
     return self._static_loss
 
   def health(self):
-    """{'skipped_updates', 'lstm_timeouts'} since construction (one device
-    read): updates the step guard dropped (non-finite gradients or an
-    abandoned LSTM unroll) and how many of them were LSTM timeouts."""
-    skipped, timeouts = self.opt.health()
-    return {'skipped_updates': skipped, 'lstm_timeouts': timeouts}
+    """{'skipped_updates', 'lstm_timeouts', 'conv_timeouts'} since
+    construction (one device read): updates the step guard dropped
+    (non-finite gradients, an abandoned LSTM unroll or an expired hand-off
+    wait in the fused conv backward) and how many were LSTM / conv
+    timeouts."""
+    skipped, timeouts, conv_timeouts = self.opt.health()
+    return {'skipped_updates': skipped, 'lstm_timeouts': timeouts,
+            'conv_timeouts': conv_timeouts}
 
   # ------------------------------------------------------------ state
   def state_dict(self):

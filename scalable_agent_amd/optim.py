@@ -103,10 +103,11 @@ class RMSProp:
     if use_hip is None:
       use_hip = dev.type == 'cuda'
     self.use_hip = use_hip
-    # (flag, skipped steps, lstm timeouts, -): a step with NaN/inf gradients
-    # or an abandoned cooperative LSTM unroll (lstm_err: the recurrence's
-    # sticky timeout word) leaves the parameters and slots untouched
-    # (SURVEY §5.3 failure detection).
+    # (flag, skipped steps, lstm timeouts, conv timeouts): a step with NaN/inf
+    # gradients, an abandoned cooperative LSTM unroll or an expired conv
+    # hand-off wait (lstm_err: the device's sticky error words, [0] the
+    # recurrence's, [1] the fused conv backward's) leaves the parameters and
+    # slots untouched (SURVEY §5.3 failure detection).
     self.skip_nonfinite = skip_nonfinite
     self.lstm_err = lstm_err if skip_nonfinite else None
     self.guard = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -120,9 +121,9 @@ class RMSProp:
     return int(self.guard[2].item())
 
   def health(self):
-    """(skipped steps, lstm timeouts) with one device read."""
+    """(skipped steps, lstm timeouts, conv timeouts) with one device read."""
     g = self.guard.tolist()
-    return int(g[1]), int(g[2])
+    return int(g[1]), int(g[2]), int(g[3])
 
   def step(self, frames):
     """frames: int64 0-d tensor on the param device (read-only here)."""

@@ -48,7 +48,8 @@ def test_two_ranks_match_one_rank_with_the_whole_batch(cuda, tmp_path, dtype, to
   assert a['world'] == 1 and b['world'] == 2
   g1, g2 = a['grads'].double(), b['grads'].double()
   assert ((g2 - g1).norm() / g1.norm()).item() <= tol
-  assert b['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
+  assert b['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0,
+                                'conv_timeouts': 0}
   # the RMSProp update built from them agrees too
   assert torch.allclose(a['params'], b['params'], rtol=0, atol=atol)
 

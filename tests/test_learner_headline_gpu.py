@@ -39,5 +39,6 @@ def test_fp32_learner_step_at_headline_shape(cuda, torso):
     worst = min(worst, (cos, name))
     assert cos >= 0.9999, (name, cos)
   print('%s: worst gradient cosine %.7f (%s)' % (torso, worst[0], worst[1]))
-  assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
+  assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0,
+                                'conv_timeouts': 0}
   assert torch.isfinite(hip['p1']).all()

@@ -105,7 +105,8 @@ def test_fp32_hip_learner_step_matches_torch(cuda, torso, aseed, bseed):
   hip = _step('hip', torso, torch.float32, cuda, **kw)
   worst = _compare(ref, hip, cos_min=0.999999, rel_max=1e-4)
   print('fp32 %s worst relative gradient error %.3g (%s)' % (torso, worst[0], worst[1]))
-  assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0}
+  assert hip['health'] == {'skipped_updates': 0, 'lstm_timeouts': 0,
+                                'conv_timeouts': 0}
 
 
 # (agent seed, batch seed) whose float64 forward has no pool near-tie /
@@ -168,7 +169,8 @@ def test_gang_lstm_timeout_skips_update(cuda):
     learner.step(batch)
     torch.cuda.synchronize()
     assert torch.equal(learner.flat.params, p0), 'stale-gradient update applied'
-    assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 1}
+    assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 1,
+                                'conv_timeouts': 0}
   finally:
     lstm_ops.set_gang_fault(prev_fault)
   try:
@@ -177,6 +179,35 @@ def test_gang_lstm_timeout_skips_update(cuda):
     learner.step(batch)
     torch.cuda.synchronize()
     assert not torch.equal(learner.flat.params, p0)
-    assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 1}
+    assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 1,
+                                'conv_timeouts': 0}
   finally:
     lstm_ops.set_gang(prev_gang)
+
+
+def test_conv_handoff_timeout_skips_update(cuda):
+  """The fused Winograd backward's bounded LDS hand-off wait (the 16->32
+  stage head, conv_wino.hip) fails loud: with the fault injected every wait
+  'expires', the sticky conv error word is set, the RMSProp guard skips the
+  update and counts it as a conv timeout; the next healthy step applies."""
+  from scalable_agent_amd.ops import _ext
+  flags = flags_lib.default_flags(batch_size=4, unroll_length=8, torso='deep')
+  agent = Agent(9, torso='deep', seed=3, backend='hip',
+                compute_dtype=torch.float32)
+  learner = Learner(agent, flags, cuda)
+  batch = batch_to_device(make_synthetic_batch(4, 8, (72, 96, 3), 9, seed=4), cuda)
+  prev = _ext.ext().cf32_wino_fault(1)
+  try:
+    p0 = learner.flat.params.clone()
+    learner.step(batch)
+    torch.cuda.synchronize()
+    assert torch.equal(learner.flat.params, p0), 'stale-gradient update applied'
+    assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 0,
+                                'conv_timeouts': 1}
+  finally:
+    _ext.ext().cf32_wino_fault(prev)
+  learner.step(batch)
+  torch.cuda.synchronize()
+  assert not torch.equal(learner.flat.params, p0)
+  assert learner.health() == {'skipped_updates': 1, 'lstm_timeouts': 0,
+                              'conv_timeouts': 1}
