@@ -62,7 +62,9 @@ __global__ __launch_bounds__(256) void lang_lstm_fwd_kernel(
   const int er = tid >> 4, eq = tid & 15;
   const int erow = r0 + er;
   const bool eok = erow < N;
-  const int elen = eok ? static_cast<int>(lengths[erow]) : 0;
+  // lengths past the word dimension are clamped (the output is the last
+  // step's h, as in the forward and backward of the torch path)
+  const int elen = eok ? static_cast<int>(min<int64_t>(max<int64_t>(lengths[erow], 0), L)) : 0;
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   for (int e = tid; e < kRows * (kH + 4); e += 256) (&h_s[0][0])[e] = 0.f;
   // B-operand row of this lane
@@ -157,7 +159,9 @@ __global__ __launch_bounds__(256) void lang_lstm_bwd_kernel(
   const int er = tid >> 4, eq = tid & 15;
   const int erow = r0 + er;
   const bool eok = erow < N;
-  const int elen = eok ? static_cast<int>(lengths[erow]) : 0;
+  // lengths past the word dimension are clamped (the output is the last
+  // step's h, as in the forward and backward of the torch path)
+  const int elen = eok ? static_cast<int>(min<int64_t>(max<int64_t>(lengths[erow], 0), L)) : 0;
   float dcar[4] = {0.f, 0.f, 0.f, 0.f};
   float dout_v[4] = {0.f, 0.f, 0.f, 0.f};
   if (eok)

@@ -413,13 +413,18 @@ def train(flags):
 
   rank, world, local_rank = parallel.world_info()
   numa = getattr(flags, 'numa_affinity', 'auto')
-  if numa == 'on' or (numa == 'auto' and (
-      flags.device.startswith('cuda') or
-      (flags.device == 'auto' and torch.cuda.device_count() > 0))):
+  on_gpu = flags.device.startswith('cuda') or (
+      flags.device == 'auto' and torch.cuda.device_count() > 0)
+  local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+  if numa == 'on' or (numa == 'auto' and on_gpu and
+                      parallel.auto_pin_wanted(local_world)):
     # before the actor processes fork and before any pinned allocation:
     # the rank's host-side data path lives next to its GPU (sysfs only, the
-    # GPU is not initialised yet)
-    parallel.pin_to_gpu_numa(local_rank)
+    # GPU is not initialised yet; device_count() does not initialise it).
+    # 'auto' pins only when this node's ranks cover every socket: the
+    # forked actors inherit the mask, and a lone rank would otherwise leave
+    # them half of a 2-socket machine.
+    parallel.pin_to_gpu_numa(local_rank % max(1, torch.cuda.device_count()))
   # many actor threads share the GIL with the learner thread: a short switch
   # interval bounds how long the learner waits for it between GPU launches
   sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))

@@ -32,14 +32,14 @@ class _LanguageLSTM(torch.autograd.Function):
     L, N, G = dg.shape
     (gemb, gk, gb), direct = grad_sink.sinks([embed, kernel, bias])
     xh2, dg2 = xh.view(L * N, xh.shape[2]), dg.view(L * N, G)
-    if (L * N) % 4 == 0:
-      C.gemm_f32(xh2, dg2, True, False, gk, accumulate=True, colsum=gb)
-    else:  # tiny test shapes (the GEMM takes K % 4 == 0)
-      gk.add_(xh2.t() @ dg2)
-      gb.add_(dg2.sum(0))
+    # the A^T B form takes any K (= L * N)
+    C.gemm_f32(xh2, dg2, True, False, gk, accumulate=True, colsum=gb)
     # embedding rows: scatter-add of dx over the word ids (steps past an
-    # instruction's length carry dx = 0)
+    # instruction's length carry dx = 0); out-of-range ids read row 0 in the
+    # forward kernel, so their gradient goes to row 0 too
     flat = ids.t().reshape(-1)  # [L*N] in the kernel's (t, n) order
+    flat = torch.where((flat >= 0) & (flat < embed.shape[0]), flat,
+                       torch.zeros_like(flat))
     dx2 = dx.view(L * N, dx.shape[2])
     if torch.are_deterministic_algorithms_enabled():
       onehot = torch.nn.functional.one_hot(flat, embed.shape[0]).to(dx2.dtype)

@@ -11,4 +11,4 @@ under the reference's sum losses.
 from .dist import (init_distributed, GradientSynchronizer, broadcast_params,
                    param_checksum_consistent, world_info, cleanup,
                    backend_info)
-from .affinity import pin_to_gpu_numa, gpu_numa_node
+from .affinity import auto_pin_wanted, gpu_numa_node, pin_to_gpu_numa

@@ -5,8 +5,9 @@ learner thread, H2D feeder and pinned trajectory slabs live on the other
 socket pays a cross-socket hop on every ~67 MB/step batch copy and on every
 kernel launch.  `pin_to_gpu_numa` restricts the calling process (and every
 process it forks afterwards: actor groups, env workers) to the CPUs of the
-NUMA node of the rank's GPU, in process and without re-executing anything,
-so it must run BEFORE the first pinned allocation and before the actor
+NUMA node of the rank's GPU (under `--numa_affinity auto` only when the
+node's ranks cover every socket, `auto_pin_wanted`), in process and without
+re-executing anything, so it must run BEFORE the first pinned allocation and before the actor
 processes are forked (the slabs' pages are first-touched by those
 processes).
 
@@ -73,16 +74,51 @@ def gpu_pci_addresses(root='/sys'):
 
 def visible_index(local_rank, env=None):
   """Physical GPU index of logical device `local_rank` under the
-  *_VISIBLE_DEVICES masks (ROCR first, then HIP / CUDA, as the runtime)."""
+  *_VISIBLE_DEVICES masks, applied like the runtime does: the HIP-level
+  mask (HIP_VISIBLE_DEVICES, or CUDA_VISIBLE_DEVICES when HIP's is unset -
+  HIP honours only one of them) indexes the devices ROCr exposes, and
+  ROCR_VISIBLE_DEVICES (applied first, at the ROCr level) maps those to
+  physical devices."""
   env = os.environ if env is None else env
-  idx = local_rank
-  for var in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
+
+  def ids(var):
     spec = env.get(var)
-    if spec:
-      ids = [int(x) for x in spec.split(',') if x.strip().isdigit()]
-      if idx < len(ids):
-        idx = ids[idx]
+    if not spec:
+      return None
+    return [int(x) for x in spec.split(',') if x.strip().isdigit()]
+
+  idx = local_rank
+  hip = ids('HIP_VISIBLE_DEVICES')
+  if hip is None:
+    hip = ids('CUDA_VISIBLE_DEVICES')
+  if hip is not None and idx < len(hip):
+    idx = hip[idx]
+  rocr = ids('ROCR_VISIBLE_DEVICES')
+  if rocr is not None and idx < len(rocr):
+    idx = rocr[idx]
   return idx
+
+
+def numa_node_count(root='/sys'):
+  """Number of NUMA nodes with CPUs (1 when unknown)."""
+  base = os.path.join(root, 'devices/system/node')
+  try:
+    names = [n for n in os.listdir(base)
+             if n.startswith('node') and n[4:].isdigit()]
+  except OSError:
+    return 1
+  n = sum(1 for name in names
+          if parse_cpulist(_read(os.path.join(base, name, 'cpulist'))))
+  return max(1, n)
+
+
+def auto_pin_wanted(local_world, root='/sys'):
+  """'auto' NUMA pinning policy: pin a rank (and the actor / env processes
+  it forks, which inherit the mask) to its GPU's node only when the node's
+  ranks together cover every socket.  A single rank on a 2-socket box would
+  otherwise confine every CPU-bound actor to half of the machine."""
+  nodes = numa_node_count(root)
+  return nodes > 1 and local_world >= nodes
 
 
 def gpu_numa_node(local_rank, root='/sys', env=None):

@@ -66,3 +66,26 @@ def test_pin_applies_in_process(tmp_path):
   avail = sorted(os.sched_getaffinity(0) & {0, 1, 2, 3})
   if avail and avail != sorted(os.sched_getaffinity(0)):
     assert r[0] == 0 and aff == avail
+
+
+def test_visible_masks_like_the_runtime():
+  # HIP honours HIP_VISIBLE_DEVICES OR CUDA_VISIBLE_DEVICES (HIP first), not
+  # both; ROCR_VISIBLE_DEVICES maps the HIP-level index to a physical one
+  vi = affinity.visible_index
+  assert vi(0, {'HIP_VISIBLE_DEVICES': '1,0', 'CUDA_VISIBLE_DEVICES': '1,0'}) == 1
+  assert vi(1, {'HIP_VISIBLE_DEVICES': '1,0', 'CUDA_VISIBLE_DEVICES': '1,0'}) == 0
+  assert vi(0, {'CUDA_VISIBLE_DEVICES': '2,3'}) == 2
+  assert vi(0, {'HIP_VISIBLE_DEVICES': '1', 'ROCR_VISIBLE_DEVICES': '4,6'}) == 6
+  assert vi(1, {'ROCR_VISIBLE_DEVICES': '4,6'}) == 6
+  assert vi(3, {}) == 3
+
+
+def test_auto_pin_only_when_ranks_cover_every_socket(tmp_path):
+  _fake_sysfs(tmp_path, [(0x05, 0), (0x85, 1)])
+  root = str(tmp_path)
+  assert affinity.numa_node_count(root) == 2
+  assert not affinity.auto_pin_wanted(1, root)   # lone rank: actors keep both sockets
+  assert affinity.auto_pin_wanted(2, root)
+  assert affinity.auto_pin_wanted(8, root)
+  assert affinity.numa_node_count(str(tmp_path / 'missing')) == 1
+  assert not affinity.auto_pin_wanted(8, str(tmp_path / 'missing'))

@@ -57,3 +57,31 @@ def test_instruction_encoding_routes_to_fused_kernel(cuda):
   g.replay()
   torch.cuda.synchronize()
   assert torch.isfinite(out).all()
+
+
+def test_language_lstm_clamps_lengths_and_ids(cuda):
+  """A length past the word dimension is clamped to L (the output is the
+  last step's h, never uninitialised memory) and an out-of-range word id
+  reads - and gets the gradient of - embedding row 0, in the forward and
+  the backward alike."""
+  from scalable_agent_amd import ops
+  N, L = 40, 6
+  g = torch.Generator().manual_seed(5)
+  ids = torch.randint(1, 1000, (N, L), generator=g)
+  lengths = torch.randint(0, 2 * L, (N,), generator=g)
+  ids_bad = ids.clone()
+  ids_bad[::3, 1] = 5000
+  ids_bad[1::3, 2] = -7
+  ids_ok = torch.where((ids_bad >= 0) & (ids_bad < 1000), ids_bad, 0)
+  w = torch.randn(N, 64, generator=g)
+  outs, grads = [], []
+  for i, l in ((ids_bad, lengths), (ids_ok, lengths.clamp(max=L))):
+    agent = Agent(9, torso='shallow', seed=3, backend='hip').to(cuda)
+    out = ops.language_lstm(i.to(cuda), l.to(cuda), agent.embed,
+                            agent.language_lstm_kernel, agent.language_lstm_bias)
+    (out * w.to(cuda)).sum().backward()
+    outs.append(out.detach())
+    grads.append(agent.embed.grad.clone())
+  assert torch.isfinite(outs[0]).all()
+  assert torch.equal(outs[0], outs[1])
+  assert torch.allclose(grads[0], grads[1], rtol=0, atol=1e-6)
