@@ -136,13 +136,15 @@ def measure(args, dtype, device, backend, rank, world):
   Returns a dict of per-rank results (dt is the MAX over ranks)."""
   flags = flags_lib.default_flags(
       batch_size=args.batch_size, unroll_length=args.unroll_length,
-      torso=args.torso, dtype=dtype, height=args.height, width=args.width)
+      torso=args.torso, dtype=dtype, height=args.height, width=args.width,
+      popart=args.popart > 0)
   num_actions = 9
   frame_shape = (args.height, args.width, args.channels)
   cdt = torch.bfloat16 if dtype == 'bf16' else torch.float32
   agent = Agent(num_actions, torso=args.torso, frame_shape=frame_shape,
                 seed=flags.seed, backend=backend, compute_dtype=cdt,
-                pipeline_chunks=args.pipeline_chunks)
+                pipeline_chunks=args.pipeline_chunks,
+                num_value_heads=max(1, args.popart))
   learner = Learner(agent, flags, device, world_size=world)
   if world > 1:
     parallel.broadcast_params(learner.flat.params)
@@ -157,6 +159,12 @@ def measure(args, dtype, device, backend, rank, world):
     host_batches = [add_synthetic_instructions(hb, agent.embed.shape[0],
                                                seed=77 + i)
                     for i, hb in enumerate(host_batches)]
+  if args.popart > 0:
+    # DMLab-30-style multi-task batch: a task (value head) per batch column
+    g = torch.Generator().manual_seed(5 + rank)
+    host_batches = [hb._replace(level_name=torch.randint(
+        0, args.popart, (args.batch_size,), generator=g))
+                    for hb in host_batches]
   cuda = device.type == 'cuda'
   use_graph = bool(args.graph) and cuda
   graphs = []
@@ -306,6 +314,9 @@ def main():
   ap.add_argument('--instructions', type=int, default=0,
                  help='1: DMLab-style batches with instruction strings '
                       '(language LSTM in the core input).')
+  ap.add_argument('--popart', type=int, default=0,
+                  help='K > 0: multi-task PopArt learner with K value heads '
+                       '(DMLab-30: 30), random task per batch column')
   ap.add_argument('--graph', type=int, default=1)
   ap.add_argument('--device', default='auto')
   ap.add_argument('--pipeline_chunks', type=int, default=1,
@@ -365,6 +376,7 @@ def main():
            'learner_health': main_res['health'],
            'pipeline_chunks': args.pipeline_chunks,
            'instructions': bool(args.instructions),
+           'popart_tasks': args.popart,
            'host_enqueue_ms_per_step': round(
                1000 * main_res['enqueue_s'] / args.steps, 3),
            'h2d_prefetch': main_res['h2d_prefetch'],

@@ -121,6 +121,17 @@ void lstm_bwd_gang_launch(const float* dh_out, const uint8_t* done, const void* 
 // header).  core [T+1,B,256]; behaviour/actions/rewards/done point at row 1
 // of the [T+1,B,...] batch tensors; dlogits [T,B,A], dvalues [T,B];
 // partial [B*3] scratch; ticket: zero-initialised persistent counter.
+// Multi-task value heads (PopArt): task [B] int64 head index per batch
+// column (null: one head), K heads (wb [256, K], bb [K]); mu / nu [K] the
+// PopArt first / second moments (null: no normalisation); vs_out [T, B] the
+// de-normalised V-trace targets (null: not written).
+struct HeadTasks {
+  const int64_t* task = nullptr;
+  int K = 1;
+  const float* mu = nullptr;
+  const float* nu = nullptr;
+  float* vs_out = nullptr;
+};
 size_t learner_head_fwd_smem(int T, int A);
 void learner_head_fwd_launch(const float* core, const float* wp, const float* bp,
                              const float* wb, const float* bb,
@@ -130,18 +141,20 @@ void learner_head_fwd_launch(const float* core, const float* wp, const float* bp
                              float clip_rho, float clip_pg_rho,
                              float baseline_cost, float entropy_cost,
                              float* dlogits, float* dvalues, float* partial,
-                             unsigned* ticket, float* loss, hipStream_t stream);
-// dcore [N1,256] = g (dlogits Wp^T + dv Wb^T) (rows >= Ng zero); heads'
-// gradients accumulated into gwp [256,A], gbp [A], gwb [256], gbb through
-// per-row-chunk slots `part` (learner_head_bwd_part_floats) summed in a fixed
-// order (bitwise reproducible).
-int64_t learner_head_bwd_part_floats(int N1, int A);
+                             unsigned* ticket, float* loss, const HeadTasks& tk,
+                             hipStream_t stream);
+// dcore [N1,256] = g (dlogits Wp^T + dv Wb[:, task]^T) (rows >= Ng zero;
+// row r = t B + b reads head task[r % B], task null = head 0); heads'
+// gradients accumulated into gwp [256,A], gbp [A], gwb [256,K], gbb [K]
+// through per-row-chunk slots `part` (learner_head_bwd_part_floats) summed in
+// a fixed order (bitwise reproducible).  A + K <= 64.
+int64_t learner_head_bwd_part_floats(int N1, int A, int K);
 void learner_head_bwd_launch(const float* gscale, const float* core,
                              const float* dlogits, const float* dvalues,
                              const float* wp, const float* wb, int N1, int Ng,
-                             int A, float* dcore, float* gwp, float* gbp,
-                             float* gwb, float* gbb, float* part,
-                             hipStream_t stream);
+                             int A, int B, const int64_t* task, int K, float* dcore,
+                             float* gwp, float* gbp, float* gwb, float* gbb,
+                             float* part, hipStream_t stream);
 // h_aug (bf16 [N, ld]) <- [h (bf16 [N, c0]), clip(r), one_hot(a), 0...]
 void core_aug_fwd_launch(void* h_aug, const void* h, const float* rewards,
                          const int64_t* actions, int N, int ld, int c0,

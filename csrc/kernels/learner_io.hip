@@ -10,9 +10,16 @@
 //                      along time inside the workgroup), the four loss sums
 //                      finished by the last workgroup to arrive (ticket) in a
 //                      fixed order, so the loss is deterministic.
-//  * learner_head_bwd  dcore = g (dlogits W_p^T + dv W_b^T) and the heads'
-//                      weight/bias gradients (fp32 atomics into the learner's
-//                      flat gradient buffer), g = the incoming loss gradient.
+//                      Multi-task PopArt (Hessel et al. 2019; the learner's
+//                      popart.py): K value heads, batch column b reads head
+//                      task[b]; V-trace runs on the de-normalised values
+//                      sigma n + mu, the baseline error is (vs - mu) / sigma - n
+//                      and the policy-gradient advantage is divided by sigma;
+//                      the targets vs go out for the statistics update.
+//  * learner_head_bwd  dcore = g (dlogits W_p^T + dv W_b[:, task]^T) and the
+//                      heads' weight/bias gradients (per-row-chunk slots
+//                      summed in a fixed order), g = the incoming loss
+//                      gradient.
 //  * core_aug_fwd      [clip(r), one_hot(a), 0...] columns next to the torso
 //                      output, so the core-input concat (experiment.py:185-198)
 //                      and the x W_x projection are ONE GEMM.
@@ -64,6 +71,9 @@ namespace {
 #endif
 
 constexpr int kHeadThreads = 1024;
+// PopArt sigma bounds (popart.py SIGMA_MIN / SIGMA_MAX)
+constexpr float kPopArtSigmaMin = 1e-4f;
+constexpr float kPopArtSigmaMax = 1e6f;
 constexpr int kHeadWaves = kHeadThreads / 64;
 constexpr int kMaxA = 31;      // A + 1 head outputs <= 32
 
@@ -90,7 +100,7 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
     int clip_mode, float clip_rho, float clip_pg_rho, float baseline_cost,
     float entropy_cost, float* __restrict__ dlogits, float* __restrict__ dvalues,
     float* __restrict__ partial, unsigned* __restrict__ ticket,
-    float* __restrict__ loss) {
+    float* __restrict__ loss, HeadTasks tk) {
   constexpr int H = 256;
   extern __shared__ float smem[];
   const int A1 = A + 1;
@@ -112,6 +122,15 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  // this column's value head and its PopArt statistics (identity without)
+  const int kt = tk.task != nullptr ? static_cast<int>(tk.task[b]) : 0;
+  float sig = 1.f, mu = 0.f;
+  if (tk.mu != nullptr) {
+    mu = tk.mu[kt];
+    const float var = fmaxf(tk.nu[kt] - mu * mu, kPopArtSigmaMin * kPopArtSigmaMin);
+    sig = fminf(fmaxf(sqrtf(var), kPopArtSigmaMin), kPopArtSigmaMax);
+  }
+  const float rsig = 1.f / sig;
 
   HEAD_TRACE(0);
   // ---- prologue: every load of the column issued before any is consumed
@@ -131,7 +150,7 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
     const int c = 16 * ct + arow;
-    bias[ct] = c < A ? bp[c] : (c == A ? bb[0] : 0.f);
+    bias[ct] = c < A ? bp[c] : (c == A ? bb[kt] : 0.f);
   }
   // (register-staged: every load below is issued before the first LDS store)
   constexpr int WPT = H * MAXC / kHeadThreads;
@@ -140,7 +159,7 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
   for (int j = 0; j < WPT; ++j) {
     const int i = tid + j * kHeadThreads;
     const int k = i / MAXC, c = i - k * MAXC;
-    wv[j] = c < A ? wp[k * A + c] : (c == A ? wb[k] : 0.f);
+    wv[j] = c < A ? wp[k * A + c] : (c == A ? wb[k * tk.K + kt] : 0.f);
   }
   constexpr int BPT = 2;  // behaviour logits per thread staged in registers
   float bv[BPT];
@@ -239,8 +258,8 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
     const float log_mu = zb[a] - mb - __logf(sb);
     const float rho = __expf(log_pi - log_mu);
     const float disc = disc_s[t];
-    const float v = zt[A];
-    const float v1 = lv_s[(t + 1) * A1 + A];
+    const float v = sig * zt[A] + mu;  // de-normalised (PopArt) values
+    const float v1 = sig * lv_s[(t + 1) * A1 + A] + mu;
     a_s[t] = disc * fminf(1.0f, rho);
     d_s[t] = fminf(clip_rho, rho) * (r_s[t] + disc * v1 - v);
     p_s[t] = fminf(clip_pg_rho, rho);
@@ -278,9 +297,9 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
   if (lane < 63) acc = scan_b[tid + 1] + scan_a[tid + 1] * acc;
   for (int t = t1 - 1; t >= t0; --t) {
     acc = d_s[t] + a_s[t] * acc;
-    vs_s[t] = acc + lv_s[t * A1 + A];
+    vs_s[t] = acc + (sig * lv_s[t * A1 + A] + mu);
   }
-  if (tid == 0) vs_s[T] = lv_s[T * A1 + A];  // bootstrap
+  if (tid == 0) vs_s[T] = sig * lv_s[T * A1 + A] + mu;  // bootstrap
   __syncthreads();
   HEAD_TRACE(5);
 
@@ -291,9 +310,14 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
     const float* zt = lv_s + t * A1;
     float* dz = dlogits + idx * A;
     const int a = act_s[t];
-    const float v = zt[A];
+    const float n = zt[A];
+    const float v = sig * n + mu;
     const float vs = vs_s[t];
-    const float pg_adv = p_s[t] * (r_s[t] + disc_s[t] * vs_s[t + 1] - v);
+    // PopArt: advantages in normalised units, baseline error against the
+    // normalised target (sig = 1, mu = 0: the plain IMPALA loss, bitwise)
+    const float pg_adv = p_s[t] * (r_s[t] + disc_s[t] * vs_s[t + 1] - v) * rsig;
+    const float err = (vs - mu) * rsig - n;
+    if (tk.vs_out != nullptr) tk.vs_out[idx] = vs;
     float m = -INFINITY;
     for (int j = 0; j < A; ++j) m = fmaxf(m, zt[j]);
     float s = 0.f;
@@ -309,9 +333,9 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
       const float p = __expf(lp);
       dz[j] = (p - (j == a ? 1.f : 0.f)) * pg_adv + entropy_cost * p * (lp + Hn);
     }
-    dvalues[idx] = -baseline_cost * (vs - v);
+    dvalues[idx] = -baseline_cost * err;
     l_pg += (lse - zt[a]) * pg_adv;
-    l_bl += 0.5f * (vs - v) * (vs - v);
+    l_bl += 0.5f * err * err;
     l_ent -= Hn;
   }
   l_pg = wave_sum(l_pg);
@@ -361,64 +385,76 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
   HEAD_TRACE(8);
 }
 
-// dcore [N1, H] = g (dlogits W_p^T + dv W_b^T) (rows >= Ng get zero), and
-// g core^T [dlogits | dv] and its column sums accumulated into the heads'
-// fp32 gradients.  Block = 16 hidden units x a chunk of kBwdRows rows
-// (thread = (unit kk, row lane rl), kBwdRows / 16 rows per thread, all core
-// and dlogits loads of the chunk in flight at once); the 16 row lanes are
-// reduced in registers/LDS, then ONE atomic per (unit, output) per block.
-constexpr int kBwdRows = 256;
-constexpr int kBwdRowsPerThread = kBwdRows / 16;
+// dcore [N1, H] = g (dlogits W_p^T + dv W_b[:, task]^T) (rows >= Ng get
+// zero), and g core^T [dlogits | dv routed to the row's value head] and its
+// column sums into per-row-chunk slots.  Columns: c < A policy, A + k value
+// head k (K heads; row r = t B + b reads head task[b]).  Block = 16 hidden
+// units x a chunk of ROWS rows (thread = (unit kk, row lane rl), ROWS / 16
+// rows per thread, all core and dlogits loads of the chunk in flight at
+// once); the 16 row lanes are reduced in registers/LDS, then one slot value
+// per (unit, output) per block.
+template <int MAXC>
+constexpr int head_bwd_rows() { return MAXC <= 32 ? 256 : 128; }
 
 template <int MAXC>
 __global__ __launch_bounds__(256) void learner_head_bwd_kernel(
     const float* __restrict__ gscale, const float* __restrict__ core,
     const float* __restrict__ dlogits, const float* __restrict__ dvalues,
     const float* __restrict__ wp, const float* __restrict__ wb, int N1, int Ng,
-    int A, float* __restrict__ dcore, float* __restrict__ part) {
+    int A, int B, const int64_t* __restrict__ task, int K,
+    float* __restrict__ dcore, float* __restrict__ part) {
   constexpr int H = 256;
-  __shared__ float dl_s[kBwdRows][MAXC];
+  constexpr int ROWS = head_bwd_rows<MAXC>();
+  constexpr int RPT = ROWS / 16;
+  __shared__ float dl_s[ROWS][MAXC];
   __shared__ float red_s[4][16][MAXC];
   const int tid = threadIdx.x;
   const int kk = tid & 15, rl = tid >> 4;
   const int k = blockIdx.x * 16 + kk;
-  const int r0 = blockIdx.y * kBwdRows;
-  const int rows = min(kBwdRows, N1 - r0);
-  const int A1 = A + 1;
+  const int r0 = blockIdx.y * ROWS;
+  const int rows = min(ROWS, N1 - r0);
+  const int A1 = A + K;
   // prologue: this thread's core values, the chunk's dlogits, the weights
-  float x[kBwdRowsPerThread];
+  float x[RPT];
 #pragma unroll
-  for (int i = 0; i < kBwdRowsPerThread; ++i) {
+  for (int i = 0; i < RPT; ++i) {
     const int rr = rl + 16 * i;
     x[i] = rr < rows ? core[static_cast<int64_t>(r0 + rr) * H + k] : 0.f;
   }
   const float g = gscale ? *gscale : 1.f;
-  // dlogits/dv of the chunk: MAXC values per thread, all loads in flight
-  float dv_r[MAXC];
+  // dlogits / dv of the chunk: MAXC values per thread, all loads in flight;
+  // a row's dv sits in its value head's column, the other heads get 0
+  float dv_r[ROWS * MAXC / 256];
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
+  for (int j = 0; j < ROWS * MAXC / 256; ++j) {
     const int i = tid + 256 * j;
     const int rr = i / MAXC, c = i - rr * MAXC;
     const int r = r0 + rr;
     float v = 0.f;
-    if (rr < rows && r < Ng && c < A1)
-      v = c < A ? dlogits[static_cast<int64_t>(r) * A + c] : dvalues[r];
+    if (rr < rows && r < Ng && c < A1) {
+      if (c < A) {
+        v = dlogits[static_cast<int64_t>(r) * A + c];
+      } else {
+        const int kt = task != nullptr ? static_cast<int>(task[r % B]) : 0;
+        v = (c - A == kt) ? dvalues[r] : 0.f;
+      }
+    }
     dv_r[j] = v;
   }
 #pragma unroll
-  for (int j = 0; j < MAXC; ++j) {
+  for (int j = 0; j < ROWS * MAXC / 256; ++j) {
     const int i = tid + 256 * j;
     dl_s[i / MAXC][i % MAXC] = dv_r[j];
   }
   float w[MAXC], acc[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    w[c] = c < A ? wp[k * A + c] : (c == A ? wb[k] : 0.f);
+    w[c] = c < A ? wp[k * A + c] : (c < A1 ? wb[k * K + (c - A)] : 0.f);
     acc[c] = 0.f;
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kBwdRowsPerThread; ++i) {
+  for (int i = 0; i < RPT; ++i) {
     const int rr = rl + 16 * i;
     if (rr < rows) {
       float d = 0.f;
@@ -464,12 +500,12 @@ __global__ __launch_bounds__(256) void learner_head_bwd_kernel(
   }
 }
 
-// Fixed-order sum of the head-gradient slots into gwp [256, A], gwb [256],
-// gbp [A], gbb [1].
+// Fixed-order sum of the head-gradient slots into gwp [256, A], gwb [256, K],
+// gbp [A], gbb [K].
 __global__ __launch_bounds__(256) void head_grad_reduce_kernel(
-    const float* __restrict__ part, int S, int A, float* __restrict__ gwp,
+    const float* __restrict__ part, int S, int A, int K, float* __restrict__ gwp,
     float* __restrict__ gbp, float* __restrict__ gwb, float* __restrict__ gbb) {
-  const int A1 = A + 1;
+  const int A1 = A + K;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= 257 * A1) return;
   float v = 0.f;
@@ -477,11 +513,11 @@ __global__ __launch_bounds__(256) void head_grad_reduce_kernel(
   if (e < 256 * A1) {
     const int ku = e / A1, c = e - ku * A1;
     if (c < A) gwp[ku * A + c] += v;
-    else gwb[ku] += v;
+    else gwb[ku * K + (c - A)] += v;
   } else {
     const int c = e - 256 * A1;
     if (c < A) gbp[c] += v;
-    else gbb[0] += v;
+    else gbb[c - A] += v;
   }
 }
 
@@ -639,7 +675,8 @@ void learner_head_fwd_launch(const float* core, const float* wp, const float* bp
                              float clip_rho, float clip_pg_rho,
                              float baseline_cost, float entropy_cost,
                              float* dlogits, float* dvalues, float* partial,
-                             unsigned* ticket, float* loss, hipStream_t stream) {
+                             unsigned* ticket, float* loss, const HeadTasks& tk,
+                             hipStream_t stream) {
   const size_t smem = learner_head_fwd_smem(T, A);
   auto k16 = learner_head_fwd_kernel<16>;
   auto k32 = learner_head_fwd_kernel<kMaxA + 1>;
@@ -652,30 +689,41 @@ void learner_head_fwd_launch(const float* core, const float* wp, const float* bp
                      bp, wb, bb, behaviour, actions, rewards, done, T, B, A,
                      discounting, clip_mode, clip_rho, clip_pg_rho,
                      baseline_cost, entropy_cost, dlogits, dvalues, partial,
-                     ticket, loss);
+                     ticket, loss, tk);
 }
 
-int64_t learner_head_bwd_part_floats(int N1, int A) {
-  return static_cast<int64_t>((N1 + kBwdRows - 1) / kBwdRows) * 257 * (A + 1);
+int head_bwd_maxc(int A1) { return A1 <= 16 ? 16 : (A1 <= 32 ? 32 : 64); }
+int head_bwd_rows_for(int A1) {
+  return head_bwd_maxc(A1) <= 32 ? head_bwd_rows<32>() : head_bwd_rows<64>();
+}
+
+int64_t learner_head_bwd_part_floats(int N1, int A, int K) {
+  const int rows = head_bwd_rows_for(A + K);
+  return static_cast<int64_t>((N1 + rows - 1) / rows) * 257 * (A + K);
 }
 
 void learner_head_bwd_launch(const float* gscale, const float* core,
                              const float* dlogits, const float* dvalues,
                              const float* wp, const float* wb, int N1, int Ng,
-                             int A, float* dcore, float* gwp, float* gbp,
-                             float* gwb, float* gbb, float* part,
-                             hipStream_t stream) {
-  const dim3 grid(256 / 16, (N1 + kBwdRows - 1) / kBwdRows);
-  if (A + 1 <= 16)
+                             int A, int B, const int64_t* task, int K, float* dcore,
+                             float* gwp, float* gbp, float* gwb, float* gbb,
+                             float* part, hipStream_t stream) {
+  const int A1 = A + K, maxc = head_bwd_maxc(A1), rows = head_bwd_rows_for(A1);
+  const dim3 grid(256 / 16, (N1 + rows - 1) / rows);
+  if (maxc == 16)
     hipLaunchKernelGGL(learner_head_bwd_kernel<16>, grid, dim3(256), 0, stream,
-                       gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, dcore,
-                       part);
-  else
-    hipLaunchKernelGGL(learner_head_bwd_kernel<kMaxA + 1>, grid, dim3(256), 0,
-                       stream, gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A,
+                       gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, B, task, K,
                        dcore, part);
-  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3((257 * (A + 1) + 255) / 256),
-                     dim3(256), 0, stream, part, static_cast<int>(grid.y), A, gwp,
+  else if (maxc == 32)
+    hipLaunchKernelGGL(learner_head_bwd_kernel<32>, grid, dim3(256), 0, stream,
+                       gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, B, task, K,
+                       dcore, part);
+  else
+    hipLaunchKernelGGL(learner_head_bwd_kernel<64>, grid, dim3(256), 0, stream,
+                       gscale, core, dlogits, dvalues, wp, wb, N1, Ng, A, B, task, K,
+                       dcore, part);
+  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3((257 * A1 + 255) / 256),
+                     dim3(256), 0, stream, part, static_cast<int>(grid.y), A, K, gwp,
                      gbp, gwb, gbb);
 }
 

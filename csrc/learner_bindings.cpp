@@ -24,12 +24,17 @@ const uint8_t* mask_ptr(const at::Tensor& t) {
 
 // core [T1,B,256]; behaviour [T1,B,A]; actions/rewards/done [T1,B] (full
 // batch tensors: the kernel reads rows 1..T).  ticket: persistent int32[1],
-// zero between launches.  -> {loss[4], dlogits [T,B,A], dvalues [T,B]}
+// zero between launches.  Multi-task value heads: wb [256, K], bb [K] with
+// task [B] (int64 head per batch column; required when K > 1); PopArt:
+// mu / nu [K] statistics (both or neither), want_vs returns the V-trace
+// targets.  -> {loss[4], dlogits [T,B,A], dvalues [T,B][, vs [T,B]]}
 std::vector<at::Tensor> learner_head_fwd(
     at::Tensor core, at::Tensor wp, at::Tensor bp, at::Tensor wb, at::Tensor bb,
     at::Tensor behaviour, at::Tensor actions, at::Tensor rewards, at::Tensor done,
     at::Tensor ticket, double discounting, int64_t clip_mode, double clip_rho,
-    double clip_pg_rho, double baseline_cost, double entropy_cost) {
+    double clip_pg_rho, double baseline_cost, double entropy_cost,
+    c10::optional<at::Tensor> task, c10::optional<at::Tensor> mu,
+    c10::optional<at::Tensor> nu, bool want_vs) {
   LB_CHECK(core); LB_CHECK(wp); LB_CHECK(bp); LB_CHECK(wb); LB_CHECK(bb);
   LB_CHECK(behaviour); LB_CHECK(actions); LB_CHECK(rewards); LB_CHECK(done);
   LB_CHECK(ticket);
@@ -43,18 +48,40 @@ std::vector<at::Tensor> learner_head_fwd(
   TORCH_CHECK(T >= 1, "need T >= 1");
   TORCH_CHECK(wp.dim() == 2 && wp.size(0) == 256, "policy w must be [256,A]");
   TORCH_CHECK(A >= 1 && A + 1 <= 32, "1 <= num_actions <= 31");
-  TORCH_CHECK(bp.numel() == A && wb.numel() == 256 && bb.numel() == 1,
-              "one value head");
+  TORCH_CHECK(wb.numel() % 256 == 0, "value w must be [256, K]");
+  const int K = wb.numel() / 256;
+  TORCH_CHECK(bp.numel() == A && bb.numel() == K && K >= 1 && A + K <= 64,
+              "value heads: b [K], A + K <= 64");
+  TORCH_CHECK(K == 1 || task.has_value(), "K > 1 value heads need the task ids");
+  TORCH_CHECK(mu.has_value() == nu.has_value(), "PopArt needs mu and nu");
   TORCH_CHECK(behaviour.numel() == (int64_t)T1 * B * A, "behaviour logits shape");
   TORCH_CHECK(actions.numel() == (int64_t)T1 * B && rewards.numel() == (int64_t)T1 * B &&
               done.numel() == (int64_t)T1 * B, "[T+1,B] shape mismatch");
   TORCH_CHECK(sa::learner_head_fwd_smem(T, A) <= 160 * 1024, "unroll too long");
+  sa::HeadTasks tk;
+  tk.K = K;
+  if (task.has_value()) {
+    LB_CHECK(*task);
+    TORCH_CHECK(task->scalar_type() == at::kLong && task->numel() == B, "task ids [B] int64");
+    tk.task = task->data_ptr<int64_t>();
+  }
+  if (mu.has_value()) {
+    LB_CHECK(*mu); LB_CHECK(*nu); LB_F32(*mu); LB_F32(*nu);
+    TORCH_CHECK(mu->numel() == K && nu->numel() == K, "PopArt statistics [K]");
+    tk.mu = mu->data_ptr<float>();
+    tk.nu = nu->data_ptr<float>();
+  }
   const c10::DeviceGuard guard(core.device());
   auto f32 = core.options();
   auto loss = at::empty({4}, f32);
   auto dlogits = at::empty({T, B, A}, f32);
   auto dvalues = at::empty({T, B}, f32);
   auto partial = at::empty({B * 3}, f32);
+  at::Tensor vs;
+  if (want_vs) {
+    vs = at::empty({T, B}, f32);
+    tk.vs_out = vs.data_ptr<float>();
+  }
   sa::learner_head_fwd_launch(
       core.data_ptr<float>(), wp.data_ptr<float>(), bp.data_ptr<float>(),
       wb.data_ptr<float>(), bb.data_ptr<float>(),
@@ -64,31 +91,42 @@ std::vector<at::Tensor> learner_head_fwd(
       (float)clip_rho, (float)clip_pg_rho, (float)baseline_cost,
       (float)entropy_cost, dlogits.data_ptr<float>(), dvalues.data_ptr<float>(),
       partial.data_ptr<float>(), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
-      loss.data_ptr<float>(), stream());
+      loss.data_ptr<float>(), tk, stream());
+  if (want_vs) return {loss, dlogits, dvalues, vs};
   return {loss, dlogits, dvalues};
 }
 
 // -> dcore [T1,B,256]; the heads' gradients are ACCUMULATED into gwp/gbp/gwb/gbb
+// (gwb [256, K], gbb [K]; task [B] selects each column's value head)
 at::Tensor learner_head_bwd(at::Tensor gscale, at::Tensor core, at::Tensor dlogits,
                             at::Tensor dvalues, at::Tensor wp, at::Tensor wb,
                             at::Tensor gwp, at::Tensor gbp, at::Tensor gwb,
-                            at::Tensor gbb) {
+                            at::Tensor gbb, c10::optional<at::Tensor> task) {
   LB_CHECK(gscale); LB_CHECK(core); LB_CHECK(dlogits); LB_CHECK(dvalues);
   LB_CHECK(wp); LB_CHECK(wb); LB_CHECK(gwp); LB_CHECK(gbp); LB_CHECK(gwb);
   LB_CHECK(gbb);
   LB_F32(gscale); LB_F32(core); LB_F32(dlogits); LB_F32(dvalues); LB_F32(gwp);
   LB_F32(gbp); LB_F32(gwb); LB_F32(gbb);
   const int T1 = core.size(0), B = core.size(1), A = wp.size(1);
+  const int K = wb.numel() / 256;
+  TORCH_CHECK(wb.numel() == 256 * K && K >= 1 && A + K <= 64, "value heads");
+  TORCH_CHECK(K == 1 || task.has_value(), "K > 1 value heads need the task ids");
   TORCH_CHECK(dlogits.numel() == (int64_t)(T1 - 1) * B * A, "dlogits shape");
   TORCH_CHECK(gwp.numel() == wp.numel() && gbp.numel() == A &&
-              gwb.numel() == 256 && gbb.numel() == 1, "gradient sink shapes");
+              gwb.numel() == 256 * K && gbb.numel() == K, "gradient sink shapes");
+  const int64_t* tp = nullptr;
+  if (task.has_value()) {
+    LB_CHECK(*task);
+    TORCH_CHECK(task->scalar_type() == at::kLong && task->numel() == B, "task ids [B] int64");
+    tp = task->data_ptr<int64_t>();
+  }
   const c10::DeviceGuard guard(core.device());
   auto dcore = at::empty_like(core);
-  auto part = at::empty({sa::learner_head_bwd_part_floats(T1 * B, A)}, core.options());
+  auto part = at::empty({sa::learner_head_bwd_part_floats(T1 * B, A, K)}, core.options());
   sa::learner_head_bwd_launch(
       gscale.data_ptr<float>(), core.data_ptr<float>(), dlogits.data_ptr<float>(),
       dvalues.data_ptr<float>(), wp.data_ptr<float>(), wb.data_ptr<float>(),
-      T1 * B, (T1 - 1) * B, A, dcore.data_ptr<float>(), gwp.data_ptr<float>(),
+      T1 * B, (T1 - 1) * B, A, B, tp, K, dcore.data_ptr<float>(), gwp.data_ptr<float>(),
       gbp.data_ptr<float>(), gwb.data_ptr<float>(), gbb.data_ptr<float>(),
       part.data_ptr<float>(), stream());
   return dcore;
@@ -311,8 +349,18 @@ std::vector<at::Tensor> lang_lstm_bwd(at::Tensor lengths, at::Tensor kernel, at:
 }  // namespace
 
 void register_learner_ops(pybind11::module& m) {
-  m.def("learner_head_fwd", &learner_head_fwd);
-  m.def("learner_head_bwd", &learner_head_bwd);
+  m.def("learner_head_fwd", &learner_head_fwd, pybind11::arg("core"), pybind11::arg("wp"),
+        pybind11::arg("bp"), pybind11::arg("wb"), pybind11::arg("bb"),
+        pybind11::arg("behaviour"), pybind11::arg("actions"), pybind11::arg("rewards"),
+        pybind11::arg("done"), pybind11::arg("ticket"), pybind11::arg("discounting"),
+        pybind11::arg("clip_mode"), pybind11::arg("clip_rho"), pybind11::arg("clip_pg_rho"),
+        pybind11::arg("baseline_cost"), pybind11::arg("entropy_cost"),
+        pybind11::arg("task") = pybind11::none(), pybind11::arg("mu") = pybind11::none(),
+        pybind11::arg("nu") = pybind11::none(), pybind11::arg("want_vs") = false);
+  m.def("learner_head_bwd", &learner_head_bwd, pybind11::arg("gscale"), pybind11::arg("core"),
+        pybind11::arg("dlogits"), pybind11::arg("dvalues"), pybind11::arg("wp"),
+        pybind11::arg("wb"), pybind11::arg("gwp"), pybind11::arg("gbp"), pybind11::arg("gwb"),
+        pybind11::arg("gbb"), pybind11::arg("task") = pybind11::none());
   m.def("core_aug_fwd", &core_aug_fwd);
   m.def("lang_lstm_fwd", &lang_lstm_fwd);
   m.def("lang_lstm_bwd", &lang_lstm_bwd);

@@ -41,9 +41,13 @@ def compute_loss(agent, data, flags, use_fused=False, popart=None,
   env_outputs = data.env_outputs
   agent_outputs = data.agent_outputs
   instr = env_outputs.observation[1]
-  if (use_fused and popart is None and agent.num_value_heads == 1 and
-      agent.fused_core_ready(instr)):
-    # HIP learner path: fused core + fused heads/V-trace/loss; same math
+  task_ids = data.level_name if popart is not None else None
+  if (use_fused and agent.fused_core_ready(instr) and
+      agent.num_actions + agent.num_value_heads <= 64 and
+      (agent.num_value_heads == 1 or task_ids is not None)):
+    # HIP learner path: fused core + fused heads/V-trace/loss; same math.
+    # PopArt (multi-task heads, de-normalised V-trace, normalised baseline
+    # error and advantages) runs inside the same kernels.
     from . import ops
     core_out, _ = agent.unroll_core(agent_outputs.action, env_outputs,
                                     data.agent_state)
@@ -52,8 +56,9 @@ def compute_loss(agent, data, flags, use_fused=False, popart=None,
         agent.baseline_b, agent_outputs.policy_logits, agent_outputs.action,
         env_outputs.reward, env_outputs.done, discounting=flags.discounting,
         reward_clipping=flags.reward_clipping,
-        baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost)
-  task_ids = data.level_name if popart is not None else None
+        baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost,
+        task_ids=task_ids, popart=popart,
+        aux=aux if popart is not None else None)
   learner_outputs, _ = agent.unroll(agent_outputs.action, env_outputs,
                                     data.agent_state, sample=False,
                                     task_ids=task_ids)

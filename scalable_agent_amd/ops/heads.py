@@ -9,7 +9,10 @@ the heads for all T+1 steps, V-trace, the loss sums and the analytic
 gradients w.r.t. the logits/values.  Backward: ONE kernel (learner_head_bwd)
 scales them by the incoming loss gradient, maps them through the heads
 (dcore) and accumulates the heads' weight/bias gradients (ops.grad_sink).
-Single value head only (PopArt multi-head runs the generic path).
+Multi-task PopArt (K value heads, per-column task index, de-normalised
+V-trace, normalised baseline error and scaled advantages) runs in the same
+two kernels; the PopArt statistics update stays a few device tensor ops
+(popart.py).
 """
 
 import torch
@@ -34,12 +37,17 @@ class _HeadsVTraceLoss(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, core, wp, bp, wb, bb, behaviour, actions, rewards, done,
-              cfg):
-    loss, dl, dv = ext().learner_head_fwd(
+              cfg, task, mu, nu, aux):
+    outs = ext().learner_head_fwd(
         core, wp, bp, wb.reshape(-1), bb.reshape(-1), behaviour, actions,
         rewards, done, _ticket(core.device), cfg['discounting'],
         _CLIP[cfg['reward_clipping']], 1.0, 1.0, cfg['baseline_cost'],
-        cfg['entropy_cost'])
+        cfg['entropy_cost'], task=task, mu=mu, nu=nu,
+        want_vs=aux is not None)
+    loss, dl, dv = outs[:3]
+    if aux is not None:
+      aux['targets'] = outs[3]
+    ctx.task = task
     ctx.save_for_backward(core, dl, dv, wp, bp, wb, bb)
     return loss[0]
 
@@ -49,26 +57,37 @@ class _HeadsVTraceLoss(torch.autograd.Function):
     (gwp, gbp, gwb, gbb), direct = grad_sink.sinks([wp, bp, wb, bb])
     gs = g.reshape(1).to(torch.float32).contiguous()
     dcore = ext().learner_head_bwd(gs, core, dl, dv, wp, wb.reshape(-1), gwp,
-                                   gbp, gwb.view(-1), gbb.view(-1))
+                                   gbp, gwb.view(-1), gbb.view(-1),
+                                   task=ctx.task)
     return (dcore,) + grad_sink.returned((gwp, gbp, gwb, gbb), direct) + (
-        None,) * 5
+        None,) * 9
 
 
 def heads_vtrace_loss(core_out, policy_w, policy_b, baseline_w, baseline_b,
                       behaviour_logits, actions, rewards, done, discounting,
-                      reward_clipping, baseline_cost, entropy_cost):
+                      reward_clipping, baseline_cost, entropy_cost,
+                      task_ids=None, popart=None, aux=None):
   """core_out [T+1,B,256] f32 from the learner unroll; behaviour_logits /
   actions / rewards / done: the FULL [T+1,B,...] batch tensors (rows 1..T
-  are used, as in experiment.py:360-375).  Returns the total loss (sum)."""
+  are used, as in experiment.py:360-375).  Returns the total loss (sum).
+
+  Multi-task value heads: baseline_w [256, K], baseline_b [K] and task_ids
+  [B] (the head of each batch column).  popart: a PopArt whose mu / nu
+  de-normalise the values inside the kernel (popart.py); aux: a dict that
+  receives 'targets' = the V-trace targets vs [T, B] for its update."""
   cfg = dict(discounting=float(discounting), reward_clipping=reward_clipping,
              baseline_cost=float(baseline_cost),
              entropy_cost=float(entropy_cost))
+  task = None if task_ids is None else task_ids.to(torch.int64).contiguous()
+  mu = nu = None
+  if popart is not None:
+    mu, nu = popart.mu, popart.nu
   return _HeadsVTraceLoss.apply(
       core_out.contiguous(), policy_w, policy_b, baseline_w, baseline_b,
       behaviour_logits.to(torch.float32).contiguous(),
       actions.to(torch.int64).contiguous(),
       rewards.to(torch.float32).contiguous(),
-      done.to(torch.bool).contiguous(), cfg)
+      done.to(torch.bool).contiguous(), cfg, task, mu, nu, aux)
 
 
 class PhiloxStream(object):

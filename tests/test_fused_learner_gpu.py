@@ -85,6 +85,103 @@ def test_heads_vtrace_loss_matches_reference(cuda, T, B, A, clip):
     torch.testing.assert_close(t.grad, 1.0 + 0.5 * g, rtol=1e-3, atol=1e-4)
 
 
+def _ref_popart_loss(core, wp, bp, wb, bb, beh, act, rew, done, task, popart,
+                     bc, ec):
+  """compute_loss's generic PopArt path (learner.py) on given core outputs."""
+  logits = core @ wp + bp
+  values_all = core @ wb + bb                      # [T1, B, K]
+  idx = task.view(1, -1, 1).expand(values_all.shape[0], -1, 1)
+  n = values_all.gather(-1, idx).squeeze(-1)       # normalised values
+  sigma, mu = popart.stats_for(task)
+  sigma, mu = sigma.to(core.dtype), mu.to(core.dtype)
+  values = n[:-1] * sigma + mu
+  boot = n[-1] * sigma + mu
+  discounts = (~done[1:]).to(core.dtype) * 0.99
+  vt = vtrace_lib.from_logits(
+      behaviour_policy_logits=beh[1:], target_policy_logits=logits[:-1],
+      actions=act[1:], discounts=discounts,
+      rewards=losses_lib.clip_rewards(rew[1:], 'abs_one'), values=values,
+      bootstrap_value=boot)
+  err = (vt.vs - mu) / sigma - n[:-1]
+  total = losses_lib.compute_policy_gradient_loss(
+      logits[:-1], act[1:], vt.pg_advantages / sigma)
+  total = total + bc * losses_lib.compute_baseline_loss(err)
+  return total + ec * losses_lib.compute_entropy_loss(logits[:-1]), vt.vs
+
+
+@pytest.mark.parametrize('T,B,K', [(100, 32, 30), (9, 5, 3)])
+def test_heads_vtrace_loss_popart_matches_reference(cuda, T, B, K):
+  """Multi-task PopArt in the fused head kernels (K value heads, the task
+  column of each batch column, de-normalised V-trace, normalised baseline
+  error and advantages) against the generic torch path in float64."""
+  from scalable_agent_amd.popart import PopArt
+  ops = _ops()
+  torch.manual_seed(5)
+  T1, A = T + 1, 9
+  pa = PopArt(K, device=cuda)
+  pa.mu.copy_(torch.randn(K, device=cuda) * 3)
+  pa.nu.copy_(pa.mu * pa.mu + torch.rand(K, device=cuda) * 20 + 0.5)
+  core = torch.randn(T1, B, 256, device=cuda)
+  wp = torch.randn(256, A, device=cuda) * 0.05
+  bp = torch.randn(A, device=cuda) * 0.1
+  wb = torch.randn(256, K, device=cuda) * 0.05
+  bb = torch.randn(K, device=cuda) * 0.1
+  beh = torch.randn(T1, B, A, device=cuda)
+  act = torch.randint(0, A, (T1, B), device=cuda)
+  rew = torch.randn(T1, B, device=cuda) * 2
+  done = torch.rand(T1, B, device=cuda) < 0.05
+  task = torch.randint(0, K, (B,), device=cuda)
+  leaves64 = [t.double().requires_grad_() for t in (core, wp, bp, wb, bb)]
+  ref, vs_ref = _ref_popart_loss(*leaves64, beh.double(), act, rew.double(),
+                                 done, task, pa, 0.5, 0.01)
+  (2.0 * ref).backward()
+  leaves = [t.clone().requires_grad_() for t in (core, wp, bp, wb, bb)]
+  aux = {}
+  loss = ops.heads_vtrace_loss(*leaves, beh, act, rew, done, 0.99, 'abs_one',
+                               0.5, 0.01, task_ids=task, popart=pa, aux=aux)
+  torch.testing.assert_close(loss.double(), ref.detach(), rtol=1e-4, atol=1e-3)
+  torch.testing.assert_close(aux['targets'].double(), vs_ref, rtol=1e-4, atol=1e-4)
+  (2.0 * loss).backward()
+  for t, r in zip(leaves, leaves64):
+    g, gr = t.grad.double(), r.grad
+    assert ((g - gr).norm() / gr.norm().clamp_min(1e-30)).item() <= 1e-4
+  # only the heads the batch uses get a value-head gradient
+  unused = torch.ones(K, dtype=torch.bool, device=cuda)
+  unused[task] = False
+  assert torch.all(leaves[3].grad[:, unused] == 0)
+  assert torch.all(leaves[4].grad[unused] == 0)
+
+
+def test_popart_learner_uses_fused_heads(cuda):
+  """A --popart HIP learner step runs the fused head kernels (no torch
+  V-trace) and keeps PopArt's statistics and preserved outputs updating."""
+  flags = flags_lib.default_flags(batch_size=4, unroll_length=8, torso='deep',
+                                  popart=True)
+  agent = Agent(9, torso='deep', seed=1, backend='hip', num_value_heads=5)
+  learner = Learner(agent, flags, cuda)
+  batch = make_synthetic_batch(4, 8, (72, 96, 3), 9, seed=3)
+  batch = batch._replace(level_name=torch.tensor([0, 3, 3, 1]))
+  batch = batch_to_device(batch, cuda)
+  calls = []
+  from scalable_agent_amd.ops import heads as heads_mod
+  orig = heads_mod.heads_vtrace_loss
+  import scalable_agent_amd.ops as ops_pkg
+  def spy(*a, **k):
+    calls.append(k.get('popart') is not None)
+    return orig(*a, **k)
+  ops_pkg.heads_vtrace_loss = spy
+  try:
+    mu0 = learner.popart.mu.clone()
+    loss = learner.step(batch)
+    torch.cuda.synchronize()
+  finally:
+    ops_pkg.heads_vtrace_loss = orig
+  assert calls == [True]
+  assert torch.isfinite(loss).item()
+  changed = (learner.popart.mu != mu0).cpu()
+  assert changed.tolist() == [True, True, False, True, False]
+
+
 def _ref_lstm(x, done, c, h, kernel, bias):
   F_in = x.shape[-1]
   kx, kh = kernel[:F_in], kernel[F_in:]
