@@ -41,8 +41,10 @@ float* ptr_or_null(const at::Tensor& t) { return t.defined() ? t.data_ptr<float>
 std::vector<at::Tensor> conv1_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
                                        int64_t pb_h, int64_t pb_w) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kByte &&
-              x.dim() == 4 && x.size(3) == 3, "frames must be uint8 NHWC C=3");
-  check_w(w, b, 3, 16);
+              x.dim() == 4 && (x.size(3) == 3 || x.size(3) == 4),
+              "frames must be uint8 NHWC with C = 3 or 4");
+  const int64_t C = x.size(3);
+  check_w(w, b, C, 16);
   const c10::DeviceGuard g(x.device());
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
   const int64_t Hp = (H + 1) / 2, Wo = (W + 1) / 2;
@@ -50,7 +52,7 @@ std::vector<at::Tensor> conv1_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
   auto arg = at::empty({N, Hp, Wo, 16}, x.options());
   sa::conv::conv1_pool_fwd_launch(x.data_ptr<uint8_t>(), w.data_ptr<float>(),
                                   b.data_ptr<float>(), pooled.data_ptr(),
-                                  arg.data_ptr<uint8_t>(), N, H, W, pb_h, pb_w,
+                                  arg.data_ptr<uint8_t>(), N, H, W, C, pb_h, pb_w,
                                   stream());
   return {pooled, arg};
 }
@@ -170,19 +172,20 @@ c10::optional<at::Tensor> pool_conv_bwd(at::Tensor dP, at::Tensor arg, at::Tenso
 
 void conv1_pool_bwd(at::Tensor dP, at::Tensor arg, at::Tensor x, at::Tensor dw,
                     at::Tensor db, int64_t pb_h, int64_t pb_w) {
-  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3 &&
-              x.is_contiguous(), "frames");
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 &&
+              (x.size(3) == 3 || x.size(3) == 4) && x.is_contiguous(), "frames");
+  const int64_t C = x.size(3);
   check_act(dP, "dP", 16);
   TORCH_CHECK(arg.sizes() == dP.sizes() && arg.scalar_type() == at::kByte, "argmax");
   TORCH_CHECK(dP.size(1) == (x.size(1) + 1) / 2 && dP.size(2) == (x.size(2) + 1) / 2,
               "pooled shape");
-  check_grad(dw, db, 3, 16);
+  check_grad(dw, db, C, 16);
   const c10::DeviceGuard g(x.device());
-  auto part = wgrad_part(dw, 3, 16, true);
+  auto part = wgrad_part(dw, C, 16, true);
   sa::conv::conv1_pool_bwd_launch(dP.data_ptr(), arg.data_ptr<uint8_t>(),
                                   x.data_ptr<uint8_t>(), dw.data_ptr<float>(),
                                   db.data_ptr<float>(), x.size(0), x.size(1),
-                                  x.size(2), pb_h, pb_w, stream(), ptr_or_null(part));
+                                  x.size(2), C, pb_h, pb_w, stream(), ptr_or_null(part));
 }
 
 }  // namespace

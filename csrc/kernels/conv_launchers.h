@@ -14,9 +14,10 @@ int res_conv_rows(int H, int W);
 // -1 for an unknown key.
 int conv_tune_set(const char* key, int value);
 
+// C = 3 (RGB) or 4 (stacked Atari frames) uint8 channels per pixel.
 void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                            void* pooled, uint8_t* argmax, int N, int H, int W,
-                           int pb_h, int pb_w, hipStream_t s);
+                           int C, int pb_h, int pb_w, hipStream_t s);
 void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
                           void* pooled, uint8_t* argmax, int N, int H, int W,
                           int CIN, int COUT, int pb_h, int pb_w, hipStream_t s);
@@ -39,7 +40,7 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
                           hipStream_t s, float* part = nullptr);
 void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
-                           int H, int W, int pb_h, int pb_w, hipStream_t s,
+                           int H, int W, int C, int pb_h, int pb_w, hipStream_t s,
                            float* part = nullptr);
 // Deterministic mode (conv_tune("deterministic", 1)): the wgrad launches
 // above take a slot workspace of this many floats (0 = mode off) and add the

@@ -739,14 +739,16 @@ struct SpanStager {
   }
 };
 
-// uint8 RGB frame rows, staged as groups of 4 pixels (12 bytes = 3 dwords)
-// per lane: when the rows are dword aligned (W % 4 == 0, the usual frame
-// widths) a group is three dword loads; otherwise it falls back to bytes.
+// uint8 frame rows (CPX = 3 RGB channels or 4 stacked Atari frames per
+// pixel), staged as groups of 4 pixels (4 CPX bytes = CPX dwords) per lane:
+// when the rows are dword aligned (W % 4 == 0, or CPX == 4) a group is CPX
+// dword loads; otherwise it falls back to bytes.
 constexpr int kU8Groups = 2;  // 4-pixel groups per lane per tile
 
-template <int NG>
+template <int NG, int CPX>
 struct U8Stager {
-  uint32_t v[3 * NG];
+  static_assert(CPX == 3 || CPX == 4, "frame channels");
+  uint32_t v[CPX * NG];
   int npix;   // pixels in the (clipped) row span
   int row0;   // first staged row (tile coordinates)
   int nrows;  // staged image rows
@@ -756,36 +758,37 @@ struct U8Stager {
     row0 = rlo - r_begin;
     nrows = rhi > rlo ? rhi - rlo : 0;
     npix = nrows * W;
-    const uint8_t* base = src + (static_cast<int64_t>(n) * H + rlo) * W * 3;
+    const uint8_t* base = src + (static_cast<int64_t>(n) * H + rlo) * W * CPX;
     const bool aligned =
-        ((W & 3) | (reinterpret_cast<uintptr_t>(src) & 3)) == 0;
+        (((CPX == 4 ? 0 : W) & 3) | (reinterpret_cast<uintptr_t>(src) & 3)) == 0;
 #pragma unroll
     for (int k = 0; k < NG; ++k) {
       const int g = threadIdx.x + k * kThreads;
-      v[3 * k] = v[3 * k + 1] = v[3 * k + 2] = 0;
+#pragma unroll
+      for (int j = 0; j < CPX; ++j) v[CPX * k + j] = 0;
       if (4 * g < npix) {
-        if (aligned) {
-          const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base) + 3 * g;
-          v[3 * k] = b32[0];
-          v[3 * k + 1] = b32[1];
-          v[3 * k + 2] = b32[2];
+        if (aligned && 4 * g + 4 <= npix) {
+          const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base) + CPX * g;
+#pragma unroll
+          for (int j = 0; j < CPX; ++j) v[CPX * k + j] = b32[j];
         } else {
 #pragma unroll
-          for (int b = 0; b < 12; ++b)
-            if (12 * g + b < 3 * npix)
-              v[3 * k + b / 4] |= static_cast<uint32_t>(base[12 * g + b]) << (8 * (b % 4));
+          for (int b = 0; b < 4 * CPX; ++b)
+            if (4 * CPX * g + b < CPX * npix)
+              v[CPX * k + b / 4] |= static_cast<uint32_t>(base[4 * CPX * g + b]) << (8 * (b % 4));
         }
       }
     }
   }
 };
 
-// Staged uint8 rows -> bf16x4 halo tile [rows][W+2][4] (channel 3 and halo
-// zero); `pad` extra zero pixels follow the tile (MFMA reads may run 3 pixels
-// past the last row into weights-zero columns).  Every LDS pixel is written
-// exactly once (data, halo or zero row), so no barrier is needed inside.
-template <int NG>
-__device__ __forceinline__ void commit_x4(const U8Stager<NG>& st, bf16_t* x4,
+// Staged uint8 rows -> bf16x4 halo tile [rows][W+2][4] (channel 3 zero for
+// RGB frames; halo zero); `pad` extra zero pixels follow the tile (MFMA reads
+// may run 3 pixels past the last row into weights-zero columns).  Every LDS
+// pixel is written exactly once (data, halo or zero row), so no barrier is
+// needed inside.
+template <int NG, int CPX>
+__device__ __forceinline__ void commit_x4(const U8Stager<NG, CPX>& st, bf16_t* x4,
                                           int W, int rows, int pad) {
   const int Wp = W + 2;
   uint2* px4 = reinterpret_cast<uint2*>(x4);
@@ -808,15 +811,16 @@ __device__ __forceinline__ void commit_x4(const U8Stager<NG>& st, bf16_t* x4,
       const int p = 4 * g + j;
       if (p < st.npix) {
         const int rr = p / W, c = p - rr * W;
-        uint32_t ch[3];
+        uint32_t ch[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int ci = 0; ci < 3; ++ci) {
-          const int b = 3 * j + ci;  // byte within the 12-byte group
+        for (int ci = 0; ci < CPX; ++ci) {
+          const int b = CPX * j + ci;  // byte within the 4 CPX-byte group
           // byte values are exact in bf16: take the top half of the fp32
           ch[ci] = __float_as_uint(static_cast<float>(
-                       (st.v[3 * k + b / 4] >> (8 * (b % 4))) & 0xFF)) >> 16;
+                       (st.v[CPX * k + b / 4] >> (8 * (b % 4))) & 0xFF)) >> 16;
         }
-        px4[(st.row0 + rr) * Wp + c + 1] = make_uint2(ch[0] | (ch[1] << 16), ch[2]);
+        px4[(st.row0 + rr) * Wp + c + 1] =
+            make_uint2(ch[0] | (ch[1] << 16), ch[2] | (ch[3] << 16));
       }
     }
   }
@@ -1073,8 +1077,9 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
 // First layer: the uint8 frame tile is staged as bf16x4 pixels (raw byte
 // values are exact in bf16; 1/255 is folded into the weights).  With 4 values
 // per pixel, one 16x16x16 MFMA covers a whole kernel row (kx = 0..2 plus a
-// zero-weight kx = 3, ci = 0..3): 3 MFMAs and 3 ds_read_b64 per 16 pixels.
-template <int HC, int WC, int RC>
+// zero-weight kx = 3, ci = 0..3): 3 MFMAs and 3 ds_read_b64 per 16 pixels,
+// for RGB (CPX = 3, ci = 3 zero-weight) and 4-frame stacks (CPX = 4) alike.
+template <int CPX, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     const uint8_t* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, bf16_t* __restrict__ pooled,
@@ -1091,15 +1096,15 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
   for (int e = threadIdx.x; e < 3 * 16 * 16; e += blockDim.x) {
     const int ky = e / 256, co = (e / 16) % 16, k = e % 16;
     const int kx = k / 4, ci = k % 4;
-    w_s[e] = (kx < 3 && ci < 3)
-                 ? f2bf(w[((ky * 3 + kx) * 3 + ci) * COUT + co] * (1.0f / 255.0f))
+    w_s[e] = (kx < 3 && ci < CPX)
+                 ? f2bf(w[((ky * 3 + kx) * CPX + ci) * COUT + co] * (1.0f / 255.0f))
                  : 0;
   }
   const int lane = lane_id();
   const int wave = wave_id();
   const int tpi = (Hp + Rp - 1) / Rp;
   const int ntiles = N * tpi;
-  U8Stager<kU8Groups> sx;
+  U8Stager<kU8Groups, CPX> sx;
   auto issue = [&](int t) {
     const int n = t / tpi, i0 = (t - n * tpi) * Rp, Rpv = min(Rp, Hp - i0);
     sx.issue(x, n, H, W, 2 * i0 - pb_h - 1, 2 * Rpv + 3);
@@ -1383,8 +1388,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 // First-layer weight gradient on the bf16x4 frame tile: for each kernel row
 // ky, D[m = 4 kx + ci][co] += X4[p + (ky-1, kx-1)][ci] dY[p][co]; the A tile
 // (4 pixels x 16 contiguous values = kx 0..3 x ci 0..3) and dY both come from
-// transposed LDS reads.  Scaled by 1/255 at the flush.
-template <int HC, int WC, int RC>
+// transposed LDS reads.  Scaled by 1/255 at the flush.  CPX input channels
+// (3 RGB, 4 stacked frames).
+template <int CPX, int HC, int WC, int RC>
 __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     const bf16_t* __restrict__ dP, const uint8_t* __restrict__ argmax,
     const uint8_t* __restrict__ x, float* __restrict__ dw,
@@ -1412,7 +1418,7 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
   ones[0] = ones[1] = ones[2] = ones[3] = 0x3F80;
   const int tpi = (H + R - 1) / R;
   const int ntiles = N * tpi;
-  U8Stager<kU8Groups> sx;
+  U8Stager<kU8Groups, CPX> sx;
   SpanStager<NREG> sp, sg;
   const int prow_bytes = Wo * COUT;
   auto issue = [&](int t) {
@@ -1467,22 +1473,22 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
   // deterministic mode: one slot per WAVE (27*16 + 16 floats), reduced in a
   // fixed order by slot_reduce_kernel; otherwise float atomics
   float* slot = part ? part + (static_cast<int64_t>(blockIdx.x) * kWaves + wave) *
-                                  (27 * COUT + COUT)
+                                  (9 * CPX * COUT + COUT)
                      : nullptr;
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kx = lane >> 4, ci = i;
-      if (kx < 3 && ci < 3) {
-        const int o = ((ky * 3 + kx) * 3 + ci) * COUT + sub;
+      if (kx < 3 && ci < CPX) {
+        const int o = ((ky * 3 + kx) * CPX + ci) * COUT + sub;
         const float v = accw[ky][i] * (1.0f / 255.0f);
         if (slot) slot[o] = v;
         else atomicAdd(dw + o, v);
       }
     }
   if ((lane >> 4) == 0) {
-    if (slot) slot[27 * COUT + sub] = accb[0];
+    if (slot) slot[9 * CPX * COUT + sub] = accb[0];
     else atomicAdd(db + sub, accb[0]);
   }
 }
@@ -1843,7 +1849,7 @@ void conv_pool_fwd_launch(const void* x, const float* w, const float* b,
 
 void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
                            void* pooled, uint8_t* argmax, int N, int H, int W,
-                           int pb_h, int pb_w, hipStream_t s) {
+                           int C, int pb_h, int pb_w, hipStream_t s) {
   const int Hp = (H + 1) / 2;
   const int Rp = rows_conv1_fwd(H, W, g_tune.px_conv1_fwd);
   require_fit(((2 * Rp + 3) * W + 3) / 4 <= kU8Groups * kThreads, "conv1_pool_fwd");
@@ -1853,9 +1859,13 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
   const int grid = grid_for(ntiles, smem, g_tune.cap_fwd);
   auto P = static_cast<bf16_t*>(pooled);
   const int xcd = g_tune.xcd | (g_tune.ablate << 8);
+  require_fit(C == 3 || C == 4, "conv1_pool_fwd: 3 or 4 frame channels");
   with_geo<kConv1, RowsConv1Fwd>(H, W, Rp, [&](auto h, auto ww, auto r) {
-    auto k = conv1_pool_fwd_kernel<decltype(h)::value, decltype(ww)::value,
-                                   decltype(r)::value>;
+    auto k3 = conv1_pool_fwd_kernel<3, decltype(h)::value, decltype(ww)::value,
+                                    decltype(r)::value>;
+    auto k4 = conv1_pool_fwd_kernel<4, decltype(h)::value, decltype(ww)::value,
+                                    decltype(r)::value>;
+    auto k = C == 4 ? k4 : k3;
     set_smem(k, smem);
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, x, w, b, P,
                        argmax, N, H, W, Rp, pb_h, pb_w, xcd);
@@ -1866,7 +1876,7 @@ void conv1_pool_fwd_launch(const uint8_t* x, const float* w, const float* b,
 // when off); the slots are summed by slot_reduce_kernel after the launch.
 int64_t wgrad_part_floats(int cin, int cout, bool conv1) {
   if (!g_tune.deterministic) return 0;
-  const int64_t nel = conv1 ? 27 * 16 + 16 : 9 * cin * cout + cout;
+  const int64_t nel = conv1 ? 9 * cin * 16 + 16 : 9 * cin * cout + cout;
   const int64_t slots = static_cast<int64_t>(num_cus()) *
                         std::max(1, std::max(g_tune.cap_bwd, 1)) * (conv1 ? kWaves : 1);
   return slots * nel;
@@ -1970,7 +1980,7 @@ void pool_conv_bwd_launch(const void* dP, const uint8_t* argmax, const void* x,
 
 void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
                            const uint8_t* x, float* dw, float* db, int N,
-                           int H, int W, int pb_h, int pb_w, hipStream_t s,
+                           int H, int W, int C, int pb_h, int pb_w, hipStream_t s,
                            float* part) {
   const int Wo = (W + 1) / 2;
   const int R = rows_conv1_bwd(H, W, g_tune.px_conv1_bwd);
@@ -1985,14 +1995,19 @@ void conv1_pool_bwd_launch(const void* dP, const uint8_t* argmax,
   const int grid = grid_for(ntiles, smem, g_tune.cap_bwd);
   auto DP = static_cast<const bf16_t*>(dP);
   const int xcd = g_tune.xcd | (g_tune.ablate << 8);
+  require_fit(C == 3 || C == 4, "conv1_pool_bwd: 3 or 4 frame channels");
   with_geo<kConv1, RowsConv1Bwd>(H, W, R, [&](auto h, auto ww, auto r) {
-    auto k = conv1_pool_bwd_kernel<decltype(h)::value, decltype(ww)::value,
-                                   decltype(r)::value>;
+    auto k3 = conv1_pool_bwd_kernel<3, decltype(h)::value, decltype(ww)::value,
+                                    decltype(r)::value>;
+    auto k4 = conv1_pool_bwd_kernel<4, decltype(h)::value, decltype(ww)::value,
+                                    decltype(r)::value>;
+    auto k = C == 4 ? k4 : k3;
     set_smem(k, smem);
     hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), smem, s, DP, argmax, x,
                        dw, db, N, H, W, R, pb_h, pb_w, xcd, part);
   });
-  if (part) reduce_slots(part, grid * kWaves, 27 * 16 + 16, 27 * 16, dw, db, s);
+  if (part)
+    reduce_slots(part, grid * kWaves, 9 * C * 16 + 16, 9 * C * 16, dw, db, s);
 }
 
 }  // namespace conv

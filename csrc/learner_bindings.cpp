@@ -7,6 +7,7 @@
 
 #include "kernels/launchers.h"
 #include "kernels/gemm_f32.h"
+#include "kernels/gemm_bf16.h"
 
 namespace {
 
@@ -297,6 +298,79 @@ void gemm_f32(at::Tensor A, at::Tensor B, bool ta, bool tb, at::Tensor C,
 }
 
 
+// C[:, :N] (+)= op(A) op(B) over bf16 A / B (fp32 accumulate), the fused
+// epilogue of kernels/gemm_bf16.h: C fp32 or bf16, mask bf16.  Same
+// conventions as gemm_f32 (row slices of wider matrices; op(A) = A^T when
+// ta, A is [K, M]; op(B) = B^T when tb, B is [N, K]).
+void gemm_bf16(at::Tensor A, at::Tensor B, bool ta, bool tb, at::Tensor C,
+               c10::optional<at::Tensor> bias, c10::optional<at::Tensor> mask, bool relu,
+               bool accumulate, c10::optional<at::Tensor> colsum,
+               c10::optional<at::Tensor> aug_reward, c10::optional<at::Tensor> aug_action) {
+  auto rm = [](const at::Tensor& t, const char* n, bool want_bf16) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.stride(1) == 1, n,
+                " must be a row-major GPU matrix");
+    TORCH_CHECK(!want_bf16 || t.scalar_type() == at::kBFloat16, n, " must be bf16");
+    TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, n,
+                " rows must be 16-byte aligned");
+  };
+  rm(A, "A", true); rm(B, "B", true);
+  TORCH_CHECK(C.is_cuda() && C.dim() == 2 && C.stride(1) == 1 &&
+              (C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16),
+              "C must be a row-major fp32 / bf16 GPU matrix");
+  const int64_t M = ta ? A.size(1) : A.size(0), K = ta ? A.size(0) : A.size(1);
+  const int64_t Kb = tb ? B.size(1) : B.size(0), N = tb ? B.size(0) : B.size(1);
+  TORCH_CHECK(K == Kb, "gemm_bf16: inner dimensions ", K, " vs ", Kb);
+  TORCH_CHECK(C.size(0) == M && C.size(1) >= N, "gemm_bf16: C must be [M, >= N]");
+  TORCH_CHECK(K % 8 == 0 || (ta && !tb),
+              "gemm_bf16: K must be a multiple of 8 unless op(A) = A^T and op(B) = B");
+  sa::GemmBf16Epilogue ep{};
+  ep.C = C.data_ptr();
+  ep.ldc = C.stride(0);
+  ep.c_bf16 = C.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(!(accumulate && ep.c_bf16), "gemm_bf16: accumulate needs an fp32 C");
+  if (bias.has_value() && bias->defined()) {
+    LB_CHECK(*bias); LB_F32(*bias);
+    TORCH_CHECK(bias->numel() == N, "bias size");
+    ep.bias = bias->data_ptr<float>();
+  }
+  if (mask.has_value() && mask->defined()) {
+    rm(*mask, "mask", true);
+    TORCH_CHECK(mask->size(0) == M && mask->size(1) >= N, "mask shape");
+    ep.mask = reinterpret_cast<const uint16_t*>(mask->data_ptr());
+    ep.ldm = mask->stride(0);
+  }
+  ep.relu = relu;
+  ep.accumulate = accumulate;
+  const bool ones = colsum.has_value() && colsum->defined();
+  if (ones) {
+    LB_CHECK(*colsum); LB_F32(*colsum);
+    TORCH_CHECK(colsum->numel() == N, "colsum size");
+    ep.colsum = colsum->data_ptr<float>();
+  }
+  if (aug_reward.has_value() && aug_reward->defined()) {
+    TORCH_CHECK(aug_action.has_value() && aug_action->defined(), "aug needs actions");
+    LB_CHECK(*aug_reward); LB_F32(*aug_reward); LB_CHECK(*aug_action);
+    TORCH_CHECK(aug_action->scalar_type() == at::kLong, "actions must be int64");
+    TORCH_CHECK(aug_reward->numel() == M && aug_action->numel() == M, "aug rows");
+    TORCH_CHECK(C.size(1) > N && C.size(1) == C.stride(0), "aug: C must be [M, ld > N]");
+    ep.aug_reward = aug_reward->data_ptr<float>();
+    ep.aug_action = aug_action->data_ptr<int64_t>();
+    ep.aug_c0 = N;
+  }
+  const c10::DeviceGuard guard(A.device());
+  const int splits = sa::gemm_bf16_splits(M, N, K, ones);
+  at::Tensor part;
+  if (splits > 1)
+    part = at::empty({sa::gemm_bf16_part_floats(M, N, K, ones, splits)},
+                     A.options().dtype(at::kFloat));
+  TORCH_CHECK(sa::gemm_bf16_launch(reinterpret_cast<const uint16_t*>(A.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(B.data_ptr()), M, N, K,
+                                   A.stride(0), B.stride(0), ta, tb, ones, splits,
+                                   splits > 1 ? part.data_ptr<float>() : nullptr, ep,
+                                   stream()),
+              "gemm_bf16: launch refused");
+}
+
 // Instruction encoder: ids [N, L] int64, lengths [N] int64, embed [V, 20],
 // kernel [84, 256], bias [256] -> {out [N, 64], acts, cs, xh} (saved for the
 // backward).
@@ -365,6 +439,12 @@ void register_learner_ops(pybind11::module& m) {
   m.def("lang_lstm_fwd", &lang_lstm_fwd);
   m.def("lang_lstm_bwd", &lang_lstm_bwd);
   m.def("gemm_f32", &gemm_f32, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("ta"),
+        pybind11::arg("tb"), pybind11::arg("C"), pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("mask") = pybind11::none(), pybind11::arg("relu") = false,
+        pybind11::arg("accumulate") = false, pybind11::arg("colsum") = pybind11::none(),
+        pybind11::arg("aug_reward") = pybind11::none(),
+        pybind11::arg("aug_action") = pybind11::none());
+  m.def("gemm_bf16", &gemm_bf16, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("ta"),
         pybind11::arg("tb"), pybind11::arg("C"), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("relu") = false,
         pybind11::arg("accumulate") = false, pybind11::arg("colsum") = pybind11::none(),

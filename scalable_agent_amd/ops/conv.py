@@ -28,10 +28,11 @@ FUSED_BLOCK = os.environ.get('SA_FUSED_BLOCK', '0') == '1'
 
 
 def supports(agent):
-  """Shapes the fused bf16 kernels cover: the deep ResNet on uint8 RGB
-  frames (conv1 is specialised for C=3; other inputs take the fp32
-  kernels, ops/conv_f32.py)."""
-  return agent.torso_kind == 'deep' and agent.frame_shape[2] == 3
+  """Shapes the fused bf16 kernels cover: the deep ResNet on uint8 frames
+  with 3 (RGB: DMLab, Doom) or 4 (stacked Atari frames, BASELINE config #2)
+  channels - conv1 packs a pixel's channels into one bf16x4 MFMA operand;
+  other inputs take the fp32 kernels, ops/conv_f32.py."""
+  return agent.torso_kind == 'deep' and agent.frame_shape[2] in (3, 4)
 
 
 def _pool_pads(h, w):

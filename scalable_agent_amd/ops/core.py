@@ -5,27 +5,31 @@ Reference: experiment.py:185-198 (Linear(256)+ReLU on the flattened conv
 features; concat [torso, clip(reward, -1, 1), one_hot(last_action),
 instruction]) and :228-235 (LSTMBlockCell(256) unrolled with done-reset).
 
-Forward (one autograd node: 4 launches + the recurrence):
-  h      = relu(feats W_fc + b_fc)              hipBLASLt bf16, bias+ReLU epilogue
-  h_aug  = [h, clip(r), one_hot(a), instr|0]   core_aug_fwd (+ the 64
-                                               language-LSTM columns on
-                                               instruction levels; without
-                                               instructions they are zero
-                                               and their W_x rows drop out)
-  xw     = h_aug W_x[:K] + b_lstm               hipBLASLt bf16 in, fp32 out
-  hs, cs = LSTM recurrence                      lstm.hip fwd steps (fp32)
+Forward (one autograd node: 2 GEMM launches + the recurrence):
+  h_aug  = [relu(feats W_fc + b_fc),           ONE bf16 MFMA GEMM (gemm_bf16:
+            clip(r), one_hot(a), instr|0]      bias + ReLU + the core-input
+                                               columns in its epilogue; the
+                                               64 language-LSTM columns are
+                                               copied in on instruction
+                                               levels, else they are zero and
+                                               their W_x rows drop out)
+  xw     = h_aug W_x[:K] + b_lstm               gemm_bf16, fp32 out
+  hs, cs = LSTM recurrence                      lstm.hip / lstm_gang.hip
 Backward:
-  dG (fp32 + bf16)                              lstm.hip bwd steps
-  dW_h  += hpm^T dG        dW_x[:K] += h_aug^T dG        db_lstm += colsum dG
-  dh     = dG W_x[:256]^T ; dh *= (h > 0) ; db_fc += colsum dh
-  dfeats = dh W_fc^T       dW_fc += feats^T dh
+  dG (fp32 + bf16)                              LSTM bwd steps
+  dh     = (dG W_x[:256]^T) * (h > 0)           gemm_bf16 (mask epilogue)
+  dfeats = dh W_fc^T                            gemm_bf16
+  dW_h  += hpm^T dG                             gemm_f32 (exact fp32)
+  dW_x[:K] += h_aug^T dG ; db_lstm += colsum dG gemm_bf16 (split-K) + colsum
+  dW_fc += feats^T dh ; db_fc += 1^T dh         ONE gemm_bf16 (ones row)
 Weight gradients accumulate straight into the learner's flat fp32 gradient
 buffer inside grad_sink.direct_grads(), and inside
 grad_sink.overlap_weight_grads() the four weight-gradient products run on a
 side stream concurrently with the conv-torso backward; the pad rows of W_x[:K] past the
 one-hot (the first instruction rows) meet all-zero h_aug columns, so they
-receive exactly 0.  GEMMs are plain library GEMMs (hipBLASLt); the glue
-kernels are in csrc/kernels/learner_io.hip.
+receive exactly 0.  Every GEMM is a hand-written MFMA kernel (no vendor
+GEMM library on either path); the glue kernels are in
+csrc/kernels/learner_io.hip.
 """
 
 import contextlib
@@ -58,22 +62,25 @@ class _CoreLSTM(torch.autograd.Function):
     assert kernel.shape[0] == f_in + CORE
     bf = torch.bfloat16
     w16_fc = w_fc.to(bf)
-    h = torch._addmm_activation(b_fc.to(bf), feats, w16_fc)
     if instr_enc is None:
       # the instruction columns are all zero: their W_x rows drop out
       K = ld = aug_width(num_actions)
     else:
       # the 64 language-LSTM columns join the core input (experiment.py:
-      # 191-198); rows padded to 16 columns, the product uses the f_in first
-      K, ld = f_in, (f_in + 15) // 16 * 16
-    assert K <= f_in
-    wx16 = kernel[:K].to(bf)
-    # reward clipping of the core input is always abs_one (experiment.py:194)
-    h_aug = C.core_aug_fwd(h, rewards, actions, ld, 0)
-    del h
+      # 191-198); K padded to 16 with zero columns (the matching kernel rows
+      # - W_h's first rows - meet zeros: no effect)
+      K = ld = (f_in + 15) // 16 * 16
+    # h_aug = [relu(feats W_fc + b_fc), clip(r), one_hot(a), 0...] in bf16:
+    # ONE hand-written bf16 MFMA GEMM (bias + ReLU + the core-input columns
+    # in its epilogue)
+    h_aug = torch.empty(N, ld, dtype=bf, device=feats.device)
+    C.gemm_bf16(feats, w16_fc, False, False, h_aug, bias=b_fc, relu=True,
+                aug_reward=rewards, aug_action=actions)
     if instr_enc is not None:
       h_aug[:, c_instr:f_in].copy_(instr_enc)
-    xw = torch.addmm(bias, h_aug[:, :K], wx16, out_dtype=torch.float32)
+    wx16 = kernel[:K].to(bf)
+    xw = torch.empty(N, 4 * CORE, dtype=torch.float32, device=feats.device)
+    C.gemm_bf16(h_aug, wx16, False, False, xw, bias=bias)
     mode = C.lstm_mode(CORE, B, T, False)  # bf16 path: the gang may run
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
                                        kernel[f_in:], mode)
@@ -103,35 +110,40 @@ class _CoreLSTM(torch.autograd.Function):
     (gwfc, gbfc, gk, gb), direct = grad_sink.sinks([w_fc, b_fc, kernel, bias])
     dg2 = dg.view(N, G)
     dg16_2 = dg16.view(N, G)
-    f32 = torch.float32
+    dev = dg.device
+    bf = torch.bfloat16
     # critical path: dfeats feeds the conv-torso backward
-    dh = torch.mm(dg16_2, wx16[:CORE].t())                          # [N,256]
-    C.relu_bwd_colsum_(dh, h_aug[:, :CORE], gbfc)                   # b_fc
-    dfeats = torch.mm(dh, w16_fc.t())
+    dh = torch.empty(N, CORE, dtype=bf, device=dev)
+    C.gemm_bf16(dg16_2, wx16[:CORE], False, True, dh,
+                mask=h_aug[:, :CORE])                               # (h > 0)
+    dfeats = torch.empty_like(feats)
+    C.gemm_bf16(dh, w16_fc, False, True, dfeats)
     # weight gradients only: on a side stream next to the torso backward
     # when they accumulate into the learner's sinks (grad_sink overlap)
-    side = grad_sink.side_stream(dg.device) if all(direct) else None
+    side = grad_sink.side_stream(dev) if all(direct) else None
     if side is not None:
-      side.wait_stream(torch.cuda.current_stream(dg.device))
+      side.wait_stream(torch.cuda.current_stream(dev))
       for t in (hpm, dg, dg16, h_aug, feats, dh):
         t.record_stream(side)
     with torch.cuda.stream(side) if side is not None else _nullctx():
-      gk[f_in:].addmm_(hpm.view(N, CORE).t(), dg2)                  # W_h
-      gxk = gk[:K]
-      torch.addmm(gxk, h_aug[:, :K].t(), dg16_2, out_dtype=f32,
-                  out=gxk)                                          # W_x rows
+      C.gemm_f32(hpm.view(N, CORE), dg2, True, False, gk[f_in:],
+                 accumulate=True)                                   # W_h (fp32)
+      C.gemm_bf16(h_aug[:, :K], dg16_2, True, False, gk[:K],
+                  accumulate=True)                                  # W_x rows
       C.colsum_f32_(dg2, gb)                                        # b_lstm
-      torch.addmm(gwfc, feats.t(), dh, out_dtype=f32, out=gwfc)     # W_fc
+      C.gemm_bf16(feats, dh, True, False, gwfc, accumulate=True,
+                  colsum=gbfc)                                      # W_fc, b_fc
     dh0 = None
     if ctx.needs_input_grad[8]:
-      keep0 = (done_u8[0] == 0).to(f32).unsqueeze(-1)
+      keep0 = (done_u8[0] == 0).to(torch.float32).unsqueeze(-1)
       dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
     if not ctx.needs_input_grad[7]:
       dc0 = None
     d_instr = None
     if ctx.has_instr and ctx.needs_input_grad[11]:
       # into the language LSTM: dG W_x[instruction rows]^T
-      d_instr = torch.mm(dg16_2, wx16[ctx.c_instr:f_in].t(), out_dtype=f32)
+      d_instr = torch.empty(N, 64, dtype=torch.float32, device=dev)
+      C.gemm_bf16(dg16_2, wx16[ctx.c_instr:f_in], False, True, d_instr)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
     return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
             d_instr)

@@ -217,17 +217,21 @@ def test_torso_f32_matches_float64(cuda, torso, shape, fseed):
     assert rel_err(p.grad, P[k].grad) <= 5 * TOL, k
 
 
-def test_bf16_agent_non_rgb_takes_fp32_kernels(cuda):
-  """Shapes the fused bf16 kernels do not cover (Atari 4-channel stack)
-  run the exact-fp32 kernels instead of failing or leaving the GPU path."""
+def test_bf16_agent_atari_stack_takes_bf16_kernels(cuda):
+  """The Atari 4-channel stack (BASELINE config #2) runs the fused bf16
+  torso at bf16 (conv1 takes C = 3 or 4 uint8 channels); other channel
+  counts take the exact-fp32 kernels instead of failing."""
   from scalable_agent_amd.models import Agent
   from scalable_agent_amd.models.agent import torso_precision
   agent = Agent(6, torso='deep', frame_shape=(84, 84, 4), seed=1, backend='hip',
                 compute_dtype=torch.bfloat16).to(cuda)
-  assert torso_precision(agent) == 'fp32'
+  assert torso_precision(agent) == 'bf16'
   frames = torch.randint(0, 256, (4, 84, 84, 4), dtype=torch.uint8, device=cuda)
   feats = agent.conv_features(frames)
   assert feats.shape == (4, 11 * 11 * 32) and torch.isfinite(feats).all()
+  gray = Agent(6, torso='deep', frame_shape=(84, 84, 1), seed=1, backend='hip',
+               compute_dtype=torch.bfloat16).to(cuda)
+  assert torso_precision(gray) == 'fp32'
 
 
 @pytest.mark.parametrize('N,H,W,Cin,Cout,u8', [

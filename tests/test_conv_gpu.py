@@ -104,12 +104,13 @@ def test_conv_pool_fwd(cuda, CIN, COUT, H, W):
   close(picked, pooled.float(), 1e-2)
 
 
-@pytest.mark.parametrize('H,W', [(72, 96), (20, 26)])
-def test_conv1_pool_fwd(cuda, H, W):
+@pytest.mark.parametrize('H,W,C', [(72, 96, 3), (20, 26, 3), (84, 84, 4),
+                                   (21, 19, 4)])
+def test_conv1_pool_fwd(cuda, H, W, C):
   torch.manual_seed(2)
   N = 3
-  frames = torch.randint(0, 256, (N, H, W, 3), device=cuda, dtype=torch.uint8)
-  w = torch.randn(3, 3, 3, 16, device=cuda) * 0.2
+  frames = torch.randint(0, 256, (N, H, W, C), device=cuda, dtype=torch.uint8)
+  w = torch.randn(3, 3, C, 16, device=cuda) * 0.2
   b = torch.randn(16, device=cuda) * 0.1
   pb_h, pb_w = pads(H, W)
   pooled, arg = _C().conv1_pool_fwd(frames, w, b, pb_h, pb_w)
@@ -170,17 +171,18 @@ def test_pool_conv_bwd(cuda, CIN, COUT, H, W):
   close(db, br.grad, 1e-3)
 
 
-@pytest.mark.parametrize('H,W', [(72, 96), (20, 26)])
-def test_conv1_pool_bwd(cuda, H, W):
+@pytest.mark.parametrize('H,W,C', [(72, 96, 3), (20, 26, 3), (84, 84, 4),
+                                   (21, 19, 4)])
+def test_conv1_pool_bwd(cuda, H, W, C):
   torch.manual_seed(5)
   N = 2
-  frames = torch.randint(0, 256, (N, H, W, 3), device=cuda, dtype=torch.uint8)
-  w = torch.randn(3, 3, 3, 16, device=cuda) * 0.2
+  frames = torch.randint(0, 256, (N, H, W, C), device=cuda, dtype=torch.uint8)
+  w = torch.randn(3, 3, C, 16, device=cuda) * 0.2
   b = torch.randn(16, device=cuda) * 0.1
   pb_h, pb_w = pads(H, W)
   pooled, arg = _C().conv1_pool_fwd(frames, w, b, pb_h, pb_w)
   dP = torch.randn_like(pooled.float()).to(torch.bfloat16)
-  dw = torch.zeros(3, 3, 3, 16, device=cuda)
+  dw = torch.zeros(3, 3, C, 16, device=cuda)
   db = torch.zeros(16, device=cuda)
   _C().conv1_pool_bwd(dP, arg, frames, dw, db, pb_h, pb_w)
   dY = bf(scatter_pool_grad(dP, arg, H, W, pb_h, pb_w))
@@ -197,17 +199,21 @@ def _cos(a, b):
   return float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-12))
 
 
-def test_deep_torso_matches_fp32_reference(cuda):
+@pytest.mark.parametrize('shape', [(72, 96, 3), (84, 84, 4)])
+def test_deep_torso_matches_fp32_reference(cuda, shape):
   """Whole torso fwd+bwd: the HIP bf16 path must track the fp32 oracle at
-  least as well as PyTorch's own bf16 path (MIOpen) does."""
+  least as well as PyTorch's own bf16 path (MIOpen) does - on DMLab RGB
+  frames and on Atari 84x84 4-frame stacks (BASELINE config #2)."""
   from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.models.agent import torso_precision
   torch.manual_seed(6)
-  mk = lambda **kw: Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=3,
+  mk = lambda **kw: Agent(9, torso='deep', frame_shape=shape, seed=3,
                           **kw).to(cuda)
   ref = mk()
   tbf = mk(compute_dtype=torch.bfloat16)
   hip = mk(backend='hip', compute_dtype=torch.bfloat16)
-  frames = torch.randint(0, 256, (6, 72, 96, 3), device=cuda, dtype=torch.uint8)
+  assert torso_precision(hip) == 'bf16'
+  frames = torch.randint(0, 256, (6,) + shape, device=cuda, dtype=torch.uint8)
   feats = [m.conv_features(frames) for m in (ref, tbf, hip)]
   assert feats[2].shape == feats[0].shape
   assert _cos(feats[2], feats[0]) > 0.999

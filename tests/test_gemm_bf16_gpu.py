@@ -1,0 +1,156 @@
+"""bf16-operand MFMA GEMM (csrc/kernels/gemm_bf16.hip) vs a float64 oracle
+on the same bf16-rounded operands.
+
+Every learner product of the fused bf16 core (ops/core.py _CoreLSTM): the
+torso FC with bias + ReLU + the core-input columns written as bf16
+(reference experiment.py:185-198), the LSTM input projection (fp32 out),
+the masked data gradients (bf16 out) and the split-K weight gradients with
+the ones-row bias gradient, at the learner's shapes (N = 3232) and at
+ragged small shapes.  fp32 accumulation of exact bf16 products: the error
+bound is the fp32 accumulation's plus one bf16 rounding for bf16 outputs.
+"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+bf = torch.bfloat16
+
+
+def _C():
+  from scalable_agent_amd import ops
+  return ops.ext()
+
+
+def _rel(a, ref):
+  a = a.detach().double().cpu()
+  ref = ref.detach().double().cpu()
+  return (a - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+
+
+def _op(t, tr):
+  return t.t() if tr else t
+
+
+def _rnd(g, *shape):
+  return torch.randn(*shape, generator=g).to(bf)
+
+
+@pytest.mark.parametrize('M,N,K', [(3232, 256, 3456), (3232, 1024, 272),
+                                   (3232, 256, 1024), (3232, 3456, 256),
+                                   (272, 1024, 3232), (3456, 256, 3232),
+                                   (36, 44, 24), (8, 4, 8), (101, 70, 136)])
+@pytest.mark.parametrize('ta,tb', [(False, False), (False, True), (True, False)])
+def test_gemm_bf16_plain(cuda, M, N, K, ta, tb):
+  if M * N * K > 4e9 and (ta, tb) != (False, False):
+    pytest.skip('one layout per large shape is enough')
+  g = torch.Generator().manual_seed(M + N + K)
+  A = _rnd(g, *((K, M) if ta else (M, K)))
+  B = _rnd(g, *((N, K) if tb else (K, N)))
+  ref = _op(A.double(), ta) @ _op(B.double(), tb)
+  C = torch.empty(M, N, device=cuda)
+  _C().gemm_bf16(A.to(cuda), B.to(cuda), ta, tb, C)
+  assert _rel(C, ref) <= 3e-6
+  C16 = torch.empty(M, N, device=cuda, dtype=bf)
+  _C().gemm_bf16(A.to(cuda), B.to(cuda), ta, tb, C16)
+  assert _rel(C16, ref) <= 8e-3
+
+
+def test_gemm_bf16_fc_epilogue(cuda):
+  """h_aug = [relu(feats W + b), clip(r), one_hot(a), 0...] in bf16."""
+  g = torch.Generator().manual_seed(1)
+  M, K, N, ld, A_ = 3232, 3456, 256, 272, 9
+  x = torch.randn(M, K, generator=g).clamp(min=0).to(bf)
+  w = (torch.randn(K, N, generator=g) / K ** 0.5).to(bf)
+  b = torch.randn(N, generator=g)
+  r = torch.randn(M, generator=g) * 3
+  a = torch.randint(0, A_, (M,), generator=g)
+  ref = torch.zeros(M, ld, dtype=torch.float64)
+  ref[:, :N] = (x.double() @ w.double() + b.double()).clamp(min=0)
+  ref[:, N] = r.double().clamp(-1, 1)
+  ref[torch.arange(M), N + 1 + a] = 1.0
+  out = torch.full((M, ld), float('nan'), device=cuda).to(bf)
+  _C().gemm_bf16(x.to(cuda), w.to(cuda), False, False, out, bias=b.to(cuda),
+                 relu=True, aug_reward=r.to(cuda), aug_action=a.to(cuda))
+  assert _rel(out[:, :N], ref[:, :N]) <= 8e-3
+  assert torch.equal(out[:, N:].cpu().double(), ref[:, N:].to(bf).double())
+
+
+def test_gemm_bf16_masked_and_weight_grads(cuda):
+  """dh = (dG W^T) * (h > 0) in bf16 and dW += X^T dh, db += colsum(dh)."""
+  g = torch.Generator().manual_seed(2)
+  M, K, N = 3232, 1024, 256
+  dG = _rnd(g, M, K)
+  W = (torch.randn(N, K, generator=g) / K ** 0.5).to(bf)
+  h = _rnd(g, M, 272)
+  dh_ref = (dG.double() @ W.double().t()) * (h[:, :N].double() > 0)
+  dh = torch.empty(M, N, device=cuda, dtype=bf)
+  hc = h.to(cuda)
+  _C().gemm_bf16(dG.to(cuda), W.to(cuda), False, True, dh, mask=hc[:, :N])
+  assert _rel(dh, dh_ref) <= 8e-3
+  assert torch.all((dh.cpu() == 0) | (h[:, :N] > 0))
+  X = torch.randn(M, 3456, generator=g).clamp(min=0).to(bf)
+  dw0 = torch.randn(3456, N, generator=g)
+  db0 = torch.randn(N, generator=g)
+  dw, db = dw0.to(cuda), db0.to(cuda)
+  _C().gemm_bf16(X.to(cuda), dh, True, False, dw, accumulate=True, colsum=db)
+  dhd = dh.double().cpu()
+  assert _rel(dw, dw0.double() + X.double().t() @ dhd) <= 3e-6
+  assert _rel(db, db0.double() + dhd.sum(0)) <= 3e-6
+  # a column slice of a wider matrix as the transposed A operand
+  dwx = torch.zeros(272, K, device=cuda)
+  _C().gemm_bf16(hc[:, :272], dG.to(cuda), True, False, dwx, accumulate=True)
+  assert _rel(dwx, h.double().t() @ dG.double()) <= 3e-6
+
+
+def test_gemm_bf16_deterministic(cuda):
+  g = torch.Generator().manual_seed(3)
+  X = _rnd(g, 3232, 3456).to(cuda)
+  dh = _rnd(g, 3232, 256).to(cuda)
+  outs = []
+  for _ in range(2):
+    dw = torch.zeros(3456, 256, device=cuda)
+    db = torch.zeros(256, device=cuda)
+    _C().gemm_bf16(X, dh, True, False, dw, accumulate=True, colsum=db)
+    outs.append((dw, db))
+  assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('M,N,K', [(256, 1024, 14), (272, 1024, 707), (256, 256, 3233)])
+def test_gemm_bf16_weight_grad_any_k(cuda, M, N, K):
+  """The weight-gradient form (op(A) = A^T, op(B) = B) takes any K."""
+  g = torch.Generator().manual_seed(M + N + K)
+  A = _rnd(g, K, M)
+  B = _rnd(g, K, N)
+  ref = A.double().t() @ B.double()
+  C = torch.zeros(M, N, device=cuda)
+  db = torch.zeros(N, device=cuda)
+  _C().gemm_bf16(A.to(cuda), B.to(cuda), True, False, C, accumulate=True, colsum=db)
+  assert _rel(C, ref) <= 3e-6
+  assert _rel(db, B.double().sum(0)) <= 3e-6
+
+
+def test_bf16_core_runs_no_library_gemm(cuda):
+  """The bf16 fused core's forward and backward launch only hand-written
+  kernels: no hipBLASLt / rocBLAS GEMM (torch.mm / addmm / matmul) runs."""
+  from scalable_agent_amd import ops
+  T, B, A = 6, 4, 9
+  N, Fd = T * B, 3456
+  f_in = 256 + 1 + A + 64
+  feats = torch.randn(N, Fd, device=cuda).relu().to(bf).requires_grad_()
+  w_fc = (torch.randn(Fd, 256, device=cuda) * 0.02).requires_grad_()
+  b_fc = torch.zeros(256, device=cuda, requires_grad=True)
+  kernel = (torch.randn(f_in + 256, 1024, device=cuda) * 0.05).requires_grad_()
+  bias = torch.zeros(1024, device=cuda, requires_grad=True)
+  rew = torch.randn(N, device=cuda)
+  act = torch.randint(0, A, (N,), device=cuda)
+  done = torch.zeros(T, B, dtype=torch.bool, device=cuda)
+  st = (torch.zeros(B, 256, device=cuda), torch.zeros(B, 256, device=cuda))
+  with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+    hs, _ = ops.core_lstm(feats, w_fc, b_fc, kernel, bias, rew, act, done, st, A)
+    hs.sum().backward()
+  names = {e.name for e in prof.events()}
+  lib = {n for n in names if n in ('aten::mm', 'aten::addmm', 'aten::matmul',
+                                   'aten::_addmm_activation', 'aten::bmm')}
+  assert not lib, lib
