@@ -31,7 +31,7 @@ const uint8_t* u8ptr(const at::Tensor& t) {
 void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
              at::Tensor frames, double lr0, double total_frames, double decay,
              double momentum, double eps, c10::optional<at::Tensor> guard,
-             c10::optional<at::Tensor> lstm_err) {
+             c10::optional<at::Tensor> lstm_err, double gscale) {
   SA_CHECK(w); SA_CHECK(g); SA_CHECK(ms); SA_CHECK(mom); SA_CHECK_CUDA(frames);
   SA_CHECK_F32(w); SA_CHECK_F32(g); SA_CHECK_F32(ms); SA_CHECK_F32(mom);
   TORCH_CHECK(frames.scalar_type() == at::kLong, "frames must be int64");
@@ -57,7 +57,7 @@ void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
                      ms.data_ptr<float>(), mom.data_ptr<float>(),
                      frames.data_ptr<int64_t>(), w.numel(), (float)lr0,
                      total_frames, (float)decay, (float)momentum, (float)eps,
-                     gp, ep, cur_stream());
+                     (float)gscale, gp, ep, cur_stream());
 }
 
 std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
@@ -331,7 +331,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("lr0"), pybind11::arg("total_frames"),
         pybind11::arg("decay"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("guard") = pybind11::none(),
-        pybind11::arg("lstm_err") = pybind11::none());
+        pybind11::arg("lstm_err") = pybind11::none(), pybind11::arg("gscale") = 1.0);
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd, pybind11::arg("xw"), pybind11::arg("done"),
         pybind11::arg("c0"), pybind11::arg("h0"), pybind11::arg("w_h"),

@@ -14,7 +14,7 @@ namespace sa {
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, int* guard, unsigned* lstm_err,
+                    float eps, float gscale, int* guard, unsigned* lstm_err,
                     hipStream_t stream);
 
 // ---- vtrace_loss.hip -------------------------------------------------------

@@ -1,6 +1,8 @@
 // Fused TF-semantics RMSProp over the flat parameter buffer.
 //
 //   lr  = lr0 * (1 - min(frames, F) / F)          (polynomial_decay, power 1)
+//   g   = gscale * grad                             (1, or 1/world for the
+//                                                    data-parallel mean)
 //   ms  = ms + (g*g - ms) * (1 - decay)             (ms initialised to 1.0)
 //   mom = momentum * mom + lr * g / sqrt(ms + eps)
 //   w  -= mom
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
     float4* __restrict__ ms, float4* __restrict__ mom,
     const int64_t* __restrict__ frames, int64_t n4, float lr0,
     double total_frames, float one_minus_decay, float momentum, float eps,
-    int* __restrict__ guard) {
+    float gscale, int* __restrict__ guard) {
   if (guard != nullptr && *guard) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(guard + 1, 1);
     return;
@@ -68,6 +70,7 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
        i < n4; i += stride) {
     float4 gv = g[i];
+    gv.x *= gscale; gv.y *= gscale; gv.z *= gscale; gv.w *= gscale;
     float4 m = ms[i];
     float4 mo = mom[i];
     float4 wv = w[i];
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,
                     double total_frames, float decay, float momentum,
-                    float eps, int* guard, unsigned* lstm_err,
+                    float eps, float gscale, int* guard, unsigned* lstm_err,
                     hipStream_t stream) {
   const int64_t n4 = n / 4;  // FlatParams pads every tensor to 64 elements
   const int threads = 256;
@@ -106,7 +109,7 @@ void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                      reinterpret_cast<const float4*>(g),
                      reinterpret_cast<float4*>(ms),
                      reinterpret_cast<float4*>(mom), frames, n4, lr0,
-                     total_frames, 1.0f - decay, momentum, eps, guard);
+                     total_frames, 1.0f - decay, momentum, eps, gscale, guard);
 }
 
 }  // namespace sa

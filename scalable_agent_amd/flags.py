@@ -76,6 +76,11 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
                  help='sum: N learners x B == one learner with N*B (reference '
                       'losses are sums).')
+  p.add_argument('--grad_scale', type=float, default=1.0,
+                 help='Multiplies the (all-reduced) gradient inside the '
+                      'RMSProp update; a single learner with batch N*B and '
+                      'grad_scale 1/N reproduces N learners with '
+                      '--grad_reduce=mean (DP-semantics experiments).')
   p.add_argument('--grad_overlap', type=_str2bool, default=True,
                  help='Data-parallel: all-reduce the heads/core/FC gradients '
                       'while the conv-torso backward runs (two-phase '

@@ -143,11 +143,16 @@ class Learner:
       # counted) instead of applying gradients of stale activations
       from .ops import lstm as lstm_ops
       lstm_err = lstm_ops.persistent_error_word(self.device)
+    # data-parallel mean: the 1/world factor is folded into the update
+    # (the all-reduce itself always sums)
+    grad_scale = float(getattr(flags, 'grad_scale', 1.0))
+    if world_size > 1 and getattr(flags, 'grad_reduce', 'sum') == 'mean':
+      grad_scale /= world_size
     self.opt = RMSProp(self.flat, flags.learning_rate, flags.decay,
                        flags.momentum, flags.epsilon,
                        flags.total_environment_frames, use_hip=use_hip,
                        skip_nonfinite=getattr(flags, 'skip_nonfinite', True),
-                       lstm_err=lstm_err)
+                       lstm_err=lstm_err, grad_scale=grad_scale)
     self.frames = torch.zeros((), dtype=torch.int64, device=self.device)
     self.world_size = world_size
     self.pg = process_group
@@ -177,7 +182,7 @@ class Learner:
     if world_size > 1:
       from .parallel import GradientSynchronizer
       self.grad_sync = GradientSynchronizer(self.flat, process_group,
-                                            reduce=flags.grad_reduce)
+                                            reduce='sum')
       off = self._torso_offset()
       if getattr(flags, 'grad_overlap', True) and off is not None:
         self.grad_sync.set_split(off)

@@ -4,8 +4,10 @@ from ._ext import ext, check_cuda
 
 
 def rmsprop_step(params, grads, ms, mom, frames, lr0, total_frames, decay,
-                 momentum, epsilon, guard=None, lstm_err=None):
+                 momentum, epsilon, guard=None, lstm_err=None, grad_scale=1.0):
   """In-place update of the flat buffers; lr decays with the device counter.
+  grad_scale multiplies the gradient inside the update (1/world: the
+  data-parallel mean without a separate pass over the buffer).
 
   guard: optional int32[4] device tensor (flag, skipped, lstm_timeouts,
   conv_timeouts): when given, a step whose gradients contain a NaN/inf is
@@ -17,4 +19,4 @@ def rmsprop_step(params, grads, ms, mom, frames, lr0, total_frames, decay,
   check_cuda(params, grads, ms, mom, frames)
   ext().rmsprop(params, grads, ms, mom, frames, float(lr0),
                 float(total_frames), float(decay), float(momentum),
-                float(epsilon), guard, lstm_err)
+                float(epsilon), guard, lstm_err, float(grad_scale))

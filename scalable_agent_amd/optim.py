@@ -90,8 +90,11 @@ class RMSProp:
 
   def __init__(self, flat: FlatParams, learning_rate, decay=0.99, momentum=0.,
                epsilon=0.1, total_frames=int(1e9), use_hip=None,
-               skip_nonfinite=True, lstm_err=None):
+               skip_nonfinite=True, lstm_err=None, grad_scale=1.0):
     self.flat = flat
+    # the step uses grad_scale * grad (data-parallel mean: 1 / world, folded
+    # into the update instead of a separate pass over the gradient buffer)
+    self.grad_scale = float(grad_scale)
     self.lr0 = float(learning_rate)
     self.decay = float(decay)
     self.momentum = float(momentum)
@@ -133,9 +136,11 @@ class RMSProp:
                        frames, self.lr0, self.total_frames, self.decay,
                        self.momentum, self.epsilon,
                        self.guard if self.skip_nonfinite else None,
-                       self.lstm_err)
+                       self.lstm_err, self.grad_scale)
       return
     g = self.flat.grads
+    if self.grad_scale != 1.0:
+      g = g * self.grad_scale
     if self.skip_nonfinite and not bool(torch.isfinite(g).all()):
       self.guard[1] += 1
       return

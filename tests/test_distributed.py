@@ -43,14 +43,14 @@ def _slice_batch(batch, lo, hi):
           baseline=sl_time(out.agent_outputs.baseline)))
 
 
-def _worker(rank, world, port, result_path, overlap=True):
+def _worker(rank, world, port, result_path, overlap=True, reduce='sum'):
   os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                     MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
   from scalable_agent_amd import parallel
   parallel.init_distributed(backend='gloo')
   torch.manual_seed(0)
   f = flags_lib.default_flags(batch_size=B // world, unroll_length=T,
-                              torso='shallow', grad_reduce='sum',
+                              torso='shallow', grad_reduce=reduce,
                               grad_overlap=overlap)
   agent = Agent(9, torso='shallow', frame_shape=SHAPE, seed=rank + 10)
   learner = Learner(agent, f, 'cpu', world_size=world)
@@ -85,3 +85,30 @@ def test_dp_sum_equals_single_learner_with_full_batch(tmp_path, overlap):
   assert dp['frames'] == int(learner.frames)
   torch.testing.assert_close(dp['params'], learner.flat.params, rtol=1e-4,
                              atol=1e-6)
+
+
+def test_dp_mean_equals_single_learner_with_grad_scale(tmp_path):
+  """--grad_reduce=mean (the 1/world folded into the RMSProp update) over N
+  learners x B == one learner with N*B and --grad_scale 1/N: the single-GPU
+  stand-in used to pick the data-parallel default
+  (profiles/r4_learning_dp_equiv.md)."""
+  path = str(tmp_path / 'dp_mean.pt')
+  mp.spawn(_worker, args=(2, _free_port(), path, True, 'mean'), nprocs=2,
+           join=True)
+  dp = torch.load(path, weights_only=True)
+  torch.manual_seed(0)
+  f = flags_lib.default_flags(batch_size=B, unroll_length=T, torso='shallow',
+                              grad_scale=0.5)
+  agent = Agent(9, torso='shallow', frame_shape=SHAPE, seed=10)
+  learner = Learner(agent, f, 'cpu')
+  full = make_synthetic_batch(B, T, SHAPE, 9, seed=7)
+  learner.step(full)
+  learner.step(full)
+  torch.testing.assert_close(dp['params'], learner.flat.params, rtol=1e-4,
+                             atol=1e-6)
+  # and it is NOT the sum semantics
+  f2 = flags_lib.default_flags(batch_size=B, unroll_length=T, torso='shallow')
+  ref = Learner(Agent(9, torso='shallow', frame_shape=SHAPE, seed=10), f2, 'cpu')
+  ref.step(full)
+  ref.step(full)
+  assert not torch.allclose(dp['params'], ref.flat.params, rtol=1e-4, atol=1e-6)

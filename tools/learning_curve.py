@@ -26,7 +26,7 @@ from scalable_agent_amd import flags as flags_lib  # noqa: E402
 def run(level, backend, frames, dtype, torso='shallow', episode_length=20,
         num_actors=16, batch_size=8, unroll_length=20, height=36, width=48,
         learning_rate=0.0006, seed=1, logdir=None, log_every_frames=10 ** 9,
-        entropy_cost=0.003):
+        entropy_cost=0.003, grad_scale=1.0):
   logdir = logdir or tempfile.mkdtemp(prefix='sa_learn_')
   fl = flags_lib.default_flags(
       level_name=level, env='synthetic', backend=backend, dtype=dtype,
@@ -34,7 +34,8 @@ def run(level, backend, frames, dtype, torso='shallow', episode_length=20,
       batch_size=batch_size, unroll_length=unroll_length, height=height,
       width=width, synthetic_episode_length=episode_length,
       num_action_repeats=1, learning_rate=learning_rate, seed=seed,
-      entropy_cost=entropy_cost, logdir=logdir, save_summaries_secs=0,
+      entropy_cost=entropy_cost, grad_scale=grad_scale, logdir=logdir,
+      save_summaries_secs=0,
       save_checkpoint_secs=1e9, log_every_frames=log_every_frames)
   t0 = time.time()
   experiment.train(fl)
@@ -80,6 +81,9 @@ def main():
   ap.add_argument('--learning_rate', type=float, default=0.0006)
   ap.add_argument('--log_every_frames', type=int, default=10 ** 9)
   ap.add_argument('--entropy_cost', type=float, default=0.003)
+  # data-parallel semantics on one GPU: batch N*B with grad_scale 1 (N
+  # learners, --grad_reduce=sum) or 1/N (--grad_reduce=mean)
+  ap.add_argument('--grad_scale', type=float, default=1.0)
   args = ap.parse_args()
   logging.basicConfig(level=logging.INFO, stream=sys.stdout)
   res = run(args.level, args.backend, args.frames, args.dtype, torso=args.torso,
@@ -88,8 +92,9 @@ def main():
             height=args.height, width=args.width,
             learning_rate=args.learning_rate,
             log_every_frames=args.log_every_frames,
-            entropy_cost=args.entropy_cost)
+            entropy_cost=args.entropy_cost, grad_scale=args.grad_scale)
   res.update(learning_rate=args.learning_rate, entropy_cost=args.entropy_cost,
+             grad_scale=args.grad_scale,
              height=args.height, width=args.width, batch_size=args.batch_size,
              unroll_length=args.unroll_length, num_actors=args.num_actors)
   line = json.dumps(res)
