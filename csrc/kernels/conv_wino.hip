@@ -76,6 +76,37 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
 }
 constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
 
+// Packed-fp32 transform arithmetic (SA_WINO_PK=1 experiment builds): the
+// Winograd input / output transforms as v_pk_add_f32 pairs (2 lanes of a
+// float4 per instruction) instead of 4 scalar v_add/v_sub_f32.  The default
+// build keeps the scalar forms: measured in profiles/experiments.md
+// (round 4) and priced as an anti-lever beside MFMAs in MI355X_MICROARCH.md.
+#ifndef SA_WINO_PK
+#define SA_WINO_PK 0
+#endif
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 lo2(f4 a) { return __builtin_shufflevector(a, a, 0, 1); }
+__device__ __forceinline__ f2 hi2(f4 a) { return __builtin_shufflevector(a, a, 2, 3); }
+__device__ __forceinline__ f4 cat2(f2 a, f2 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3); }
+__device__ __forceinline__ f2 pk_add2(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 pk_sub2(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f4 tadd(f4 a, f4 b) {
+  if constexpr (SA_WINO_PK) return cat2(pk_add2(lo2(a), lo2(b)), pk_add2(hi2(a), hi2(b)));
+  else return a + b;
+}
+__device__ __forceinline__ f4 tsub(f4 a, f4 b) {
+  if constexpr (SA_WINO_PK) return cat2(pk_sub2(lo2(a), lo2(b)), pk_sub2(hi2(a), hi2(b)));
+  else return a - b;
+}
+
 // ReLU as one integer max on the bit pattern (negative floats, -0 and
 // negative NaNs have the sign bit set: signed-int max with 0 gives +0);
 // fmaxf(x, 0) is two instructions under IEEE mode (a canonicalising
@@ -369,18 +400,18 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 s[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          s[q] = d[q] - d[8 + q];
-          s[4 + q] = d[4 + q] + d[8 + q];
-          s[8 + q] = d[8 + q] - d[4 + q];
-          s[12 + q] = d[4 + q] - d[12 + q];
+          s[q] = tsub(d[q], d[8 + q]);
+          s[4 + q] = tadd(d[4 + q], d[8 + q]);
+          s[8 + q] = tsub(d[8 + q], d[4 + q]);
+          s[12 + q] = tsub(d[4 + q], d[12 + q]);
         }
         f4 V[16];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
-          V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
-          V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
-          V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
+          V[4 * ra + 0] = tsub(s[4 * ra + 0], s[4 * ra + 2]);
+          V[4 * ra + 1] = tadd(s[4 * ra + 1], s[4 * ra + 2]);
+          V[4 * ra + 2] = tsub(s[4 * ra + 2], s[4 * ra + 1]);
+          V[4 * ra + 3] = tsub(s[4 * ra + 1], s[4 * ra + 3]);
         }
         // 16 xi x 4 k-steps x NH slices; two xi chains interleaved (the
         // 16x16x4 f32 MFMA's dependent latency is 40 cycles, issue 32)
@@ -414,14 +445,14 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 tt[4][2];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          tt[ra][0] = (acc[h][4 * ra] + acc[h][4 * ra + 1]) + acc[h][4 * ra + 2];
-          tt[ra][1] = (acc[h][4 * ra + 1] - acc[h][4 * ra + 2]) - acc[h][4 * ra + 3];
+          tt[ra][0] = tadd(tadd(acc[h][4 * ra], acc[h][4 * ra + 1]), acc[h][4 * ra + 2]);
+          tt[ra][1] = tsub(tsub(acc[h][4 * ra + 1], acc[h][4 * ra + 2]), acc[h][4 * ra + 3]);
         }
         f4 Y[4];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
-          Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+          Y[c] = tadd(tadd(tt[0][c], tt[1][c]), tt[2][c]);
+          Y[2 + c] = tsub(tsub(tt[1][c], tt[2][c]), tt[3][c]);
         }
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy)
@@ -1111,18 +1142,18 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       f4 sv[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        sv[q] = d[q] - d[8 + q];
-        sv[4 + q] = d[4 + q] + d[8 + q];
-        sv[8 + q] = d[8 + q] - d[4 + q];
-        sv[12 + q] = d[4 + q] - d[12 + q];
+        sv[q] = tsub(d[q], d[8 + q]);
+        sv[4 + q] = tadd(d[4 + q], d[8 + q]);
+        sv[8 + q] = tsub(d[8 + q], d[4 + q]);
+        sv[12 + q] = tsub(d[4 + q], d[12 + q]);
       }
       f4 V[16];
 #pragma unroll
       for (int ra = 0; ra < 4; ++ra) {
-        V[4 * ra + 0] = sv[4 * ra + 0] - sv[4 * ra + 2];
-        V[4 * ra + 1] = sv[4 * ra + 1] + sv[4 * ra + 2];
-        V[4 * ra + 2] = sv[4 * ra + 2] - sv[4 * ra + 1];
-        V[4 * ra + 3] = sv[4 * ra + 1] - sv[4 * ra + 3];
+        V[4 * ra + 0] = tsub(sv[4 * ra + 0], sv[4 * ra + 2]);
+        V[4 * ra + 1] = tadd(sv[4 * ra + 1], sv[4 * ra + 2]);
+        V[4 * ra + 2] = tsub(sv[4 * ra + 2], sv[4 * ra + 1]);
+        V[4 * ra + 3] = tsub(sv[4 * ra + 1], sv[4 * ra + 3]);
       }
       const float* up = U_s + (g * C + c16) * 4;
 #pragma unroll
@@ -1138,14 +1169,14 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       f4 tt[4][2];
 #pragma unroll
       for (int ra = 0; ra < 4; ++ra) {
-        tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
-        tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+        tt[ra][0] = tadd(tadd(acc[4 * ra], acc[4 * ra + 1]), acc[4 * ra + 2]);
+        tt[ra][1] = tsub(tsub(acc[4 * ra + 1], acc[4 * ra + 2]), acc[4 * ra + 3]);
       }
       f4 Y[4];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
-        Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+        Y[c] = tadd(tadd(tt[0][c], tt[1][c]), tt[2][c]);
+        Y[2 + c] = tsub(tsub(tt[1][c], tt[2][c]), tt[3][c]);
       }
       const float* xm = x_s + base + 4 * g;
 #pragma unroll
@@ -1547,18 +1578,18 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
           f4 sv[16];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            sv[q] = d[q] - d[8 + q];
-            sv[4 + q] = d[4 + q] + d[8 + q];
-            sv[8 + q] = d[8 + q] - d[4 + q];
-            sv[12 + q] = d[4 + q] - d[12 + q];
+            sv[q] = tsub(d[q], d[8 + q]);
+            sv[4 + q] = tadd(d[4 + q], d[8 + q]);
+            sv[8 + q] = tsub(d[8 + q], d[4 + q]);
+            sv[12 + q] = tsub(d[4 + q], d[12 + q]);
           }
           f4 V[16];
 #pragma unroll
           for (int ra = 0; ra < 4; ++ra) {
-            V[4 * ra + 0] = sv[4 * ra + 0] - sv[4 * ra + 2];
-            V[4 * ra + 1] = sv[4 * ra + 1] + sv[4 * ra + 2];
-            V[4 * ra + 2] = sv[4 * ra + 2] - sv[4 * ra + 1];
-            V[4 * ra + 3] = sv[4 * ra + 1] - sv[4 * ra + 3];
+            V[4 * ra + 0] = tsub(sv[4 * ra + 0], sv[4 * ra + 2]);
+            V[4 * ra + 1] = tadd(sv[4 * ra + 1], sv[4 * ra + 2]);
+            V[4 * ra + 2] = tsub(sv[4 * ra + 2], sv[4 * ra + 1]);
+            V[4 * ra + 3] = tsub(sv[4 * ra + 1], sv[4 * ra + 3]);
           }
           const float* up = U_s + ((b * 4 + g) * CX + 16 * cb + c16) * 4;
 #pragma unroll
@@ -1575,14 +1606,14 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
         f4 tt[4][2];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
-          tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+          tt[ra][0] = tadd(tadd(acc[4 * ra], acc[4 * ra + 1]), acc[4 * ra + 2]);
+          tt[ra][1] = tsub(tsub(acc[4 * ra + 1], acc[4 * ra + 2]), acc[4 * ra + 3]);
         }
         f4 Y[4];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
-          Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+          Y[c] = tadd(tadd(tt[0][c], tt[1][c]), tt[2][c]);
+          Y[2 + c] = tsub(tsub(tt[1][c], tt[2][c]), tt[3][c]);
         }
         if constexpr (DSPLIT == 2) {
           f4* yb = ybuf + task * 4 * 64 + lane;
