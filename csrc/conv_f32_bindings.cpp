@@ -14,6 +14,18 @@
 
 namespace {
 
+// Slot workspaces of the deferred weight-gradient reductions (see
+// wgrad_set_defer): kept alive until cf32_wgrad_flush launches their sums.
+thread_local bool t_defer = false;
+thread_local std::vector<at::Tensor> t_keep;
+
+at::Tensor slot_workspace(int64_t floats, const at::Tensor& like) {
+  auto ws = at::empty({floats}, like.options().dtype(at::kFloat));
+  if (t_defer) t_keep.push_back(ws);
+  return ws;
+}
+
+
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 // A launch that fails (e.g. an LDS request the device refuses) must not
@@ -236,10 +248,10 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
   check_w(dw);
   const int kind = src_kind(x);
   const int64_t K = dw.size(0);
-  TORCH_CHECK(dw.size(2) == x.size(3) && dw.size(3) == dy.size(3), "dw shape");
+  // dw may have fewer input channels than x (RGB weights, 4-channel image)
+  TORCH_CHECK(dw.size(2) <= x.size(3) && dw.size(3) == dy.size(3), "dw shape");
   const c10::DeviceGuard g(x.device());
-  auto ws = at::empty({sa::cf32::wgrad_workspace_floats(K, x.size(3), dy.size(3))},
-                      dy.options());
+  auto ws = slot_workspace(sa::cf32::wgrad_workspace_floats(K, x.size(3), dy.size(3)), dy);
   sa::cf32::WgradArgs a{};
   a.src = x.data_ptr();
   a.dy = dy.data_ptr<float>();
@@ -258,6 +270,7 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, int64_t stride, int64_t pt, int64_t
     a.pool = pool_geom(pool_arg, dy, a.Ho, a.Wo, pool_pbh, pool_pbw);
   }
   a.pt = pt; a.pl = pl; a.relu_in = relu_in;
+  a.dw_cin = dw.size(2);
   TORCH_CHECK(sa::cf32::wgrad_launch(a, K, stride, kind, ws.data_ptr<float>(), stream()),
               "conv_f32 wgrad: no kernel instance for K=", K, " stride=", stride, " Cin=",
               x.size(3), " Cout=", dy.size(3));
@@ -294,7 +307,7 @@ at::Tensor conv_bwd_fused(at::Tensor dy, at::Tensor w, at::Tensor x, bool relu_x
   const int C = x.size(3), Cy = dy.size(3);
   if (sa::cf32::wino_bwd_fused_enabled()) {
     const int64_t wsf = sa::cf32::wgrad_workspace_floats(3, C, Cy);
-    auto ws = at::empty({wsf}, dy.options());
+    auto ws = slot_workspace(wsf, dy);
     if (sa::cf32::wino_bwd_fused_launch(dy.data_ptr<float>(), w.data_ptr<float>(),
                                         x.data_ptr<float>(), addp, dx.data_ptr<float>(),
                                         relu_x ? 1 : 0, mask ? 1 : 0, x.size(0), x.size(1),
@@ -413,4 +426,14 @@ void register_conv_f32_ops(pybind11::module& m) {
   m.def("cf32_relu_mask_", &relu_mask_);
   m.def("cf32_frames_f32", &frames_f32);
   m.def("cf32_wino_fault", [](int v) { return sa::cf32::conv_wino_fault(v); });
+  // deferred weight-gradient reductions: defer(True) ... flush() -> one launch
+  m.def("cf32_wgrad_defer", [](bool on) {
+    t_defer = on;
+    sa::cf32::wgrad_set_defer(on);
+  });
+  m.def("cf32_wgrad_flush", []() {
+    const int n = sa::cf32::wgrad_flush(stream());
+    t_keep.clear();
+    return n;
+  });
 }

@@ -82,12 +82,22 @@ struct WgradArgs {
   int pt, pl;
   int relu_in;
   PoolGeom pool;       // pool.arg != null: dy is dP, (Ho, Wo) pre-pool dims
+  int dw_cin = 0;      // > 0: dw has this many input channels (<= Cin; the
+                       // stage-0 weights of an RGB frame staged as 4 channels)
 };
 
 // Winograd F(2x2,3x3) fp32 path (conv_wino.hip) for 3x3/1 SAME convs with
 // 16/32 channels in and out (forward and data gradient); false when the
 // shape is not covered.  SA_F32_WINO=0 disables it (direct implicit GEMM).
 bool wino_enabled();
+
+// Deferred weight-gradient slot reductions: while on, every fixed-order
+// slot sum (wgrad_reduce / wgrad_reduce_slots) is queued instead of
+// launched, and wgrad_flush launches all queued sums as ONE kernel (the
+// torso backward's ~15 reductions become one launch).  The caller keeps the
+// slot workspaces alive until the flush.  Per host thread.
+void wgrad_set_defer(bool on);
+int wgrad_flush(hipStream_t s);  // -> number of reductions launched
 
 // Fault injection (tests): 1 = every bounded intra-workgroup hand-off wait of
 // the fused Winograd backward reports a timeout.  Returns the old setting.

@@ -24,6 +24,8 @@
 // bitwise reproducible run to run (no float atomics).
 #include "conv_f32.h"
 
+#include <vector>
+
 #include <utility>
 
 #include <algorithm>
@@ -900,13 +902,13 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
 // 16/32-channel layers); slot group sg adds slots sg, sg+16, ... through 8
 // independent accumulators, and the 16 groups are combined in LDS in a fixed
 // tree order, so every run gives the same bits.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+__device__ __forceinline__ void wgrad_reduce_body(
     const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
-    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db, int bid) {
   __shared__ float red[16][17];
   const int per = MT16 * CG;
   const int l = threadIdx.x & 15;
-  const int e = blockIdx.x * 16 + l;
+  const int e = bid * 16 + l;
   const int sg = threadIdx.x >> 4;
   const bool live = e < ngrp * per;
   const int ng = live ? e / per : 0, rem = live ? e - ng * per : 0;
@@ -939,6 +941,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   } else {
     db[co] += s;
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+    const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+  wgrad_reduce_body(part, G, ngrp, MT16, CG, CINP, M, Cin, Cout, dw, db, blockIdx.x);
 }
 
 // ------------------------------------------------- stage-head wgrad (scatter)
@@ -1090,14 +1098,14 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
 // stage-0 scatter wgrad's 768, res16's 2560): block = 4 outputs x 64 slot
 // groups, so the launch still fills the GPU (the 16 x 16 blocks gave the
 // stage-0 reduction 48 workgroups and 38 us).
-__global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(
+__device__ __forceinline__ void wgrad_reduce_narrow_body(
     const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
-    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db, int bid) {
   constexpr int OPB = 4, SG = 256 / OPB;
   __shared__ float red[SG][OPB + 1];
   const int per = MT16 * CG;
   const int l = threadIdx.x % OPB;
-  const int e = blockIdx.x * OPB + l;
+  const int e = bid * OPB + l;
   const int sg = threadIdx.x / OPB;
   const bool live = e < ngrp * per;
   const int ng = live ? e / per : 0, rem = live ? e - ng * per : 0;
@@ -1133,10 +1141,56 @@ __global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(
   }
 }
 
-// launches the fixed-order slot sum (the narrow form for small layers)
+__global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(
+    const float* __restrict__ part, int G, int ngrp, int MT16, int CG, int CINP, int M,
+    int Cin, int Cout, float* __restrict__ dw, float* __restrict__ db) {
+  wgrad_reduce_narrow_body(part, G, ngrp, MT16, CG, CINP, M, Cin, Cout, dw, db, blockIdx.x);
+}
+
+// One queued slot sum (deferred mode) and a batch of them for one launch:
+// block b of the launch works for the job whose [first, first + blocks)
+// range holds b (<= kMaxJobs jobs: a short scan of kernel arguments).
+struct WgJob {
+  const float* part;
+  float* dw;
+  float* db;
+  int G, ngrp, MT16, CG, CINP, M, Cin, Cout;
+  int narrow, blocks;
+};
+constexpr int kMaxJobs = 16;
+struct WgJobs {
+  WgJob job[kMaxJobs];
+  int first[kMaxJobs + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_multi_kernel(WgJobs js) {
+  int j = 0;
+  while (j + 1 < js.n && static_cast<int>(blockIdx.x) >= js.first[j + 1]) ++j;
+  const WgJob& q = js.job[j];
+  const int bid = blockIdx.x - js.first[j];
+  if (q.narrow)
+    wgrad_reduce_narrow_body(q.part, q.G, q.ngrp, q.MT16, q.CG, q.CINP, q.M, q.Cin, q.Cout,
+                             q.dw, q.db, bid);
+  else
+    wgrad_reduce_body(q.part, q.G, q.ngrp, q.MT16, q.CG, q.CINP, q.M, q.Cin, q.Cout, q.dw,
+                      q.db, bid);
+}
+
+thread_local bool t_wg_defer = false;
+thread_local std::vector<WgJob> t_wg_jobs;
+
+// launches the fixed-order slot sum (the narrow form for small layers), or
+// queues it in deferred mode
 void wgrad_reduce(const float* part, int G, int ngrp, int MT16, int CG, int CINP, int M, int Cin,
                   int Cout, float* dw, float* db, hipStream_t s) {
   const int total = ngrp * MT16 * CG;
+  if (t_wg_defer) {
+    WgJob q{part, dw, db, G, ngrp, MT16, CG, CINP, M, Cin, Cout, total < 4096 ? 1 : 0,
+            total < 4096 ? (total + 3) / 4 : (total + 15) / 16};
+    t_wg_jobs.push_back(q);
+    return;
+  }
   if (total < 4096) {
     hipLaunchKernelGGL(wgrad_reduce_narrow_kernel, dim3((total + 3) / 4), dim3(256), 0, s, part,
                        G, ngrp, MT16, CG, CINP, M, Cin, Cout, dw, db);
@@ -1395,7 +1449,8 @@ bool run_wgrad(const WgradArgs& a, float* ws, hipStream_t s) {
   auto kern = conv_wgrad_kernel<CINP, K, S, SRC, NTT, WSM, GATHER>;
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, ngrp), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, ws);
-  wgrad_reduce(ws, G, ngrp, MT * 16, CG, CINP, M, a.Cin, a.Cout, a.dw, a.db, s);
+  wgrad_reduce(ws, G, ngrp, MT * 16, CG, CINP, M, a.dw_cin > 0 ? a.dw_cin : a.Cin, a.Cout,
+               a.dw, a.db, s);
   return true;
 }
 
@@ -1408,6 +1463,26 @@ void wgrad_reduce_slots(const float* part, int G, int rows16, int Cout, int Cin,
 
 // Scatter-form stage-head wgrad from (dP, argmax) (pool_wgrad_kernel): on
 // unless SA_F32_POOL_SCATTER=0 (then the dense-gather MFMA wgrad runs).
+void wgrad_set_defer(bool on) { t_wg_defer = on; }
+
+int wgrad_flush(hipStream_t s) {
+  const int n = static_cast<int>(t_wg_jobs.size());
+  for (int i0 = 0; i0 < n; i0 += kMaxJobs) {
+    WgJobs js{};
+    js.n = std::min(kMaxJobs, n - i0);
+    int blocks = 0;
+    for (int k = 0; k < js.n; ++k) {
+      js.job[k] = t_wg_jobs[i0 + k];
+      js.first[k] = blocks;
+      blocks += js.job[k].blocks;
+    }
+    js.first[js.n] = blocks;
+    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3(blocks), dim3(256), 0, s, js);
+  }
+  t_wg_jobs.clear();
+  return n;
+}
+
 static bool pool_scatter_on() {
   static const bool on = env_knob("SA_F32_POOL_SCATTER", 1) != 0;
   return on;
@@ -1502,7 +1577,7 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, int u8_cs, hipStream_t
                        u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,
                        ntiles, ws);
   }
-  wgrad_reduce(ws, G, 1, 48, 16, 4, 36, a.Cin, a.Cout, a.dw, a.db, s);
+  wgrad_reduce(ws, G, 1, 48, 16, 4, 36, a.dw_cin > 0 ? a.dw_cin : a.Cin, a.Cout, a.dw, a.db, s);
   return true;
 }
 

@@ -76,13 +76,16 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
 }
 constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
 
-// Packed-fp32 transform arithmetic (SA_WINO_PK=1 experiment builds): the
-// Winograd input / output transforms as v_pk_add_f32 pairs (2 lanes of a
-// float4 per instruction) instead of 4 scalar v_add/v_sub_f32.  The default
-// build keeps the scalar forms: measured in profiles/experiments.md
-// (round 4) and priced as an anti-lever beside MFMAs in MI355X_MICROARCH.md.
+// Packed-fp32 transform arithmetic: the Winograd input / output transforms
+// as v_pk_add_f32 pairs (2 lanes of a float4 per instruction) instead of 4
+// scalar v_add/v_sub_f32.  Measured per kernel (profiles/experiments.md,
+// round 4): the 32-channel forward / data-gradient kernel gains 4-5 %, the
+// 16-channel kernels and the fused backward kernels gain nothing or lose
+// (priced as an anti-lever beside MFMAs in MI355X_MICROARCH.md), so
+// SA_WINO_PK = 2 (default) packs only the 32-channel forward; 1 = every
+// kernel, 0 = none (experiment builds).
 #ifndef SA_WINO_PK
-#define SA_WINO_PK 0
+#define SA_WINO_PK 2
 #endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 lo2(f4 a) { return __builtin_shufflevector(a, a, 0, 1); }
@@ -98,12 +101,14 @@ __device__ __forceinline__ f2 pk_sub2(f2 a, f2 b) {
   asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+template <bool PK = SA_WINO_PK == 1>
 __device__ __forceinline__ f4 tadd(f4 a, f4 b) {
-  if constexpr (SA_WINO_PK) return cat2(pk_add2(lo2(a), lo2(b)), pk_add2(hi2(a), hi2(b)));
+  if constexpr (PK) return cat2(pk_add2(lo2(a), lo2(b)), pk_add2(hi2(a), hi2(b)));
   else return a + b;
 }
+template <bool PK = SA_WINO_PK == 1>
 __device__ __forceinline__ f4 tsub(f4 a, f4 b) {
-  if constexpr (SA_WINO_PK) return cat2(pk_sub2(lo2(a), lo2(b)), pk_sub2(hi2(a), hi2(b)));
+  if constexpr (PK) return cat2(pk_sub2(lo2(a), lo2(b)), pk_sub2(hi2(a), hi2(b)));
   else return a - b;
 }
 
@@ -206,6 +211,7 @@ __device__ __forceinline__ RangeGeom range_geom(const WinoArgs& a, int r, int RT
 template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
 __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
+  constexpr bool kPk = SA_WINO_PK == 1 || (SA_WINO_PK == 2 && CIN == 32);
   const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
   const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
   const bool f_mask = FL < 0 ? a.mask != nullptr : (FL & 4) != 0;
@@ -400,18 +406,18 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 s[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          s[q] = tsub(d[q], d[8 + q]);
-          s[4 + q] = tadd(d[4 + q], d[8 + q]);
-          s[8 + q] = tsub(d[8 + q], d[4 + q]);
-          s[12 + q] = tsub(d[4 + q], d[12 + q]);
+          s[q] = tsub<kPk>(d[q], d[8 + q]);
+          s[4 + q] = tadd<kPk>(d[4 + q], d[8 + q]);
+          s[8 + q] = tsub<kPk>(d[8 + q], d[4 + q]);
+          s[12 + q] = tsub<kPk>(d[4 + q], d[12 + q]);
         }
         f4 V[16];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          V[4 * ra + 0] = tsub(s[4 * ra + 0], s[4 * ra + 2]);
-          V[4 * ra + 1] = tadd(s[4 * ra + 1], s[4 * ra + 2]);
-          V[4 * ra + 2] = tsub(s[4 * ra + 2], s[4 * ra + 1]);
-          V[4 * ra + 3] = tsub(s[4 * ra + 1], s[4 * ra + 3]);
+          V[4 * ra + 0] = tsub<kPk>(s[4 * ra + 0], s[4 * ra + 2]);
+          V[4 * ra + 1] = tadd<kPk>(s[4 * ra + 1], s[4 * ra + 2]);
+          V[4 * ra + 2] = tsub<kPk>(s[4 * ra + 2], s[4 * ra + 1]);
+          V[4 * ra + 3] = tsub<kPk>(s[4 * ra + 1], s[4 * ra + 3]);
         }
         // 16 xi x 4 k-steps x NH slices; two xi chains interleaved (the
         // 16x16x4 f32 MFMA's dependent latency is 40 cycles, issue 32)
@@ -445,14 +451,14 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 tt[4][2];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          tt[ra][0] = tadd(tadd(acc[h][4 * ra], acc[h][4 * ra + 1]), acc[h][4 * ra + 2]);
-          tt[ra][1] = tsub(tsub(acc[h][4 * ra + 1], acc[h][4 * ra + 2]), acc[h][4 * ra + 3]);
+          tt[ra][0] = tadd<kPk>(tadd<kPk>(acc[h][4 * ra], acc[h][4 * ra + 1]), acc[h][4 * ra + 2]);
+          tt[ra][1] = tsub<kPk>(tsub<kPk>(acc[h][4 * ra + 1], acc[h][4 * ra + 2]), acc[h][4 * ra + 3]);
         }
         f4 Y[4];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          Y[c] = tadd(tadd(tt[0][c], tt[1][c]), tt[2][c]);
-          Y[2 + c] = tsub(tsub(tt[1][c], tt[2][c]), tt[3][c]);
+          Y[c] = tadd<kPk>(tadd<kPk>(tt[0][c], tt[1][c]), tt[2][c]);
+          Y[2 + c] = tsub<kPk>(tsub<kPk>(tt[1][c], tt[2][c]), tt[3][c]);
         }
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy)

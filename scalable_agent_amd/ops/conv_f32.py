@@ -106,12 +106,8 @@ class _ShallowTorsoF32(torch.autograd.Function):
     C.cf32_relu_mask_(dy, out)
     for i in reversed(range(3)):
       s, pt, pl, H, W = ctx.geoms[i]
-      if i == 0 and gv[0].shape[2] != acts[0].shape[3]:
-        dw4 = torch.zeros(gv[0].shape[:2] + (acts[0].shape[3],) + gv[0].shape[3:],
-                          dtype=torch.float32, device=dy.device)
-        C.cf32_conv_wgrad(acts[0], dy, s, pt, pl, False, dw4, gv[1])
-        gv[0].add_(dw4[:, :, :gv[0].shape[2]])
-        continue
+      # layer 0 on an RGB frame staged as 4 channels: the kernel writes the
+      # 3-channel weight gradient directly (dw_cin)
       C.cf32_conv_wgrad(acts[i], dy, s, pt, pl, False, gv[2 * i], gv[2 * i + 1])
       if i > 0:
         # input of layer i is the ReLU'd output of layer i-1
@@ -177,60 +173,65 @@ class _DeepTorsoF32(torch.autograd.Function):
     dy = grad_out.reshape(out.shape).to(torch.float32).clone(
         memory_format=torch.contiguous_format)
     C.cf32_relu_mask_(dy, out)  # final ReLU of the torso
-    for s in reversed(range(3)):
-      k = 6 * s
-      if DEBUG_TAPE is not None:
-        DEBUG_TAPE[('intact', s)] = [bool(torch.equal(a, b)) for a, b in
-                                     zip(saved, DEBUG_TAPE['saved'])]
-      stage_in, arg = saved[k], saved[k + 1]
-      H, W, h, w_, pbh, pbw = ctx.meta[s]
-      pb = 10 * s
-      for blk in reversed(range(2)):
-        xa, tt = saved[k + 2 + 2 * blk], saved[k + 3 + 2 * blk]
-        i1 = pb + 2 + 4 * blk
-        w1, w2 = params[i1], params[i1 + 2]
-        # one pass per conv: its data gradient (masked by the conv's own
-        # input, + the skip for the block's first conv) and its weight/bias
-        # gradient read dY and the input once (conv_wino.hip fused backward
-        # where it covers the shape, else the separate kernels)
-        dt = C.cf32_conv_bwd_fused(dy, w2, tt, False, gv[i1 + 2], gv[i1 + 3])
-        if DEBUG_TAPE is not None:
-          DEBUG_TAPE[('dy', s, blk)] = dy.clone()
-          DEBUG_TAPE[('dt', s, blk)] = dt.clone()
-        dy = C.cf32_conv_bwd_fused(dt, w1, xa, True, gv[i1], gv[i1 + 1], add=dy)
-      gw = gv[pb]
-      if s == 0 and gw.shape[2] != stage_in.shape[3]:
-        gw = torch.zeros(gw.shape[:2] + (stage_in.shape[3],) + gw.shape[3:],
-                         dtype=torch.float32, device=dy.device)
-      scatter = (s == 0 and POOL_SCATTER and stage_in.shape[3] <= 4
-                 and dy.shape[3] == 16)
-      if s in POOL_GATHER_STAGES or scatter:
-        # the conv kernels gather the pre-pool gradient from (dP, argmax)
-        C.cf32_conv_wgrad(stage_in, dy, 1, 1, 1, False, gw, gv[pb + 1],
-                          pool_arg=arg, pool_pbh=pbh, pool_pbw=pbw)
-        if gw is not gv[pb]:
-          gv[pb].add_(gw[:, :, :gv[pb].shape[2]])
-        if s > 0:
-          dy = C.cf32_conv_dgrad(dy, params[pb], 1, 1, 1, H, W, pool_arg=arg,
-                                 pool_pbh=pbh, pool_pbw=pbw)
-        continue
-      dconv = C.cf32_maxpool_bwd(dy, arg, H, W, pbh, pbw)
-      if DEBUG_TAPE is not None:
-        DEBUG_TAPE[('dpool', s)] = dy.clone()
-        DEBUG_TAPE[('dconv', s)] = dconv.clone()
-      if s > 0 and gw is gv[pb]:
-        # stage head (16 -> 32 / 32 -> 32): data + weight gradient in one
-        # pass over (dconv, stage input); the input is the previous stage's
-        # raw output, so no ReLU mask
-        dy = C.cf32_conv_bwd_fused(dconv, params[pb], stage_in, False, gw, gv[pb + 1],
-                                   mask=False)
-        continue
-      C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gw, gv[pb + 1])
-      if gw is not gv[pb]:
-        gv[pb].add_(gw[:, :, :gv[pb].shape[2]])
-      if s > 0:
-        dy = C.cf32_conv_dgrad(dconv, params[pb], 1, 1, 1, H, W)
+    # the ~15 fixed-order weight-gradient slot sums of this backward are
+    # queued and launched as ONE kernel at the end (cf32_wgrad_flush)
+    C.cf32_wgrad_defer(True)
+    try:
+      _deep_backward(C, ctx, saved, params, gv, dy)
+    finally:
+      C.cf32_wgrad_defer(False)
+      C.cf32_wgrad_flush()
     return (None,) + grad_sink.returned(gv, direct)
+
+
+def _deep_backward(C, ctx, saved, params, gv, dy):
+  """The stage loop of _DeepTorsoF32.backward (reverse stage order)."""
+  for s in reversed(range(3)):
+    k = 6 * s
+    if DEBUG_TAPE is not None:
+      DEBUG_TAPE[('intact', s)] = [bool(torch.equal(a, b)) for a, b in
+                                   zip(saved, DEBUG_TAPE['saved'])]
+    stage_in, arg = saved[k], saved[k + 1]
+    H, W, h, w_, pbh, pbw = ctx.meta[s]
+    pb = 10 * s
+    for blk in reversed(range(2)):
+      xa, tt = saved[k + 2 + 2 * blk], saved[k + 3 + 2 * blk]
+      i1 = pb + 2 + 4 * blk
+      w1, w2 = params[i1], params[i1 + 2]
+      # one pass per conv: its data gradient (masked by the conv's own
+      # input, + the skip for the block's first conv) and its weight/bias
+      # gradient read dY and the input once (conv_wino.hip fused backward
+      # where it covers the shape, else the separate kernels)
+      dt = C.cf32_conv_bwd_fused(dy, w2, tt, False, gv[i1 + 2], gv[i1 + 3])
+      if DEBUG_TAPE is not None:
+        DEBUG_TAPE[('dy', s, blk)] = dy.clone()
+        DEBUG_TAPE[('dt', s, blk)] = dt.clone()
+      dy = C.cf32_conv_bwd_fused(dt, w1, xa, True, gv[i1], gv[i1 + 1], add=dy)
+    # stage 0 on an RGB frame staged as 4 channels: the kernels write
+    # the 3-channel weight gradient directly (dw_cin)
+    gw = gv[pb]
+    scatter = (s == 0 and POOL_SCATTER and stage_in.shape[3] <= 4
+               and dy.shape[3] == 16)
+    if s in POOL_GATHER_STAGES or scatter:
+      # the conv kernels gather the pre-pool gradient from (dP, argmax)
+      C.cf32_conv_wgrad(stage_in, dy, 1, 1, 1, False, gw, gv[pb + 1],
+                        pool_arg=arg, pool_pbh=pbh, pool_pbw=pbw)
+      if s > 0:
+        dy = C.cf32_conv_dgrad(dy, params[pb], 1, 1, 1, H, W, pool_arg=arg,
+                               pool_pbh=pbh, pool_pbw=pbw)
+      continue
+    dconv = C.cf32_maxpool_bwd(dy, arg, H, W, pbh, pbw)
+    if DEBUG_TAPE is not None:
+      DEBUG_TAPE[('dpool', s)] = dy.clone()
+      DEBUG_TAPE[('dconv', s)] = dconv.clone()
+    if s > 0:
+      # stage head (16 -> 32 / 32 -> 32): data + weight gradient in one
+      # pass over (dconv, stage input); the input is the previous stage's
+      # raw output, so no ReLU mask
+      dy = C.cf32_conv_bwd_fused(dconv, params[pb], stage_in, False, gw, gv[pb + 1],
+                                 mask=False)
+      continue
+    C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gw, gv[pb + 1])
 
 
 def _pad_cin(w, c):

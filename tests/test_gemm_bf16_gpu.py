@@ -37,10 +37,20 @@ def _rnd(g, *shape):
   return torch.randn(*shape, generator=g).to(bf)
 
 
+def _padded(t):
+  """t as a row slice of a matrix whose rows are padded to 8 bf16 (16 B),
+  the kernel's row alignment: ragged widths exercise the tile tails."""
+  r, c = t.shape
+  cp = (c + 7) // 8 * 8
+  out = torch.zeros(r, cp, dtype=t.dtype, device=t.device)
+  out[:, :c] = t
+  return out[:, :c]
+
+
 @pytest.mark.parametrize('M,N,K', [(3232, 256, 3456), (3232, 1024, 272),
                                    (3232, 256, 1024), (3232, 3456, 256),
                                    (272, 1024, 3232), (3456, 256, 3232),
-                                   (36, 44, 24), (8, 4, 8), (101, 70, 136)])
+                                   (36, 44, 24), (8, 4, 8), (101, 70, 136), (45, 9, 16)])
 @pytest.mark.parametrize('ta,tb', [(False, False), (False, True), (True, False)])
 def test_gemm_bf16_plain(cuda, M, N, K, ta, tb):
   if M * N * K > 4e9 and (ta, tb) != (False, False):
@@ -50,10 +60,11 @@ def test_gemm_bf16_plain(cuda, M, N, K, ta, tb):
   B = _rnd(g, *((N, K) if tb else (K, N)))
   ref = _op(A.double(), ta) @ _op(B.double(), tb)
   C = torch.empty(M, N, device=cuda)
-  _C().gemm_bf16(A.to(cuda), B.to(cuda), ta, tb, C)
+  Ad, Bd = _padded(A.to(cuda)), _padded(B.to(cuda))
+  _C().gemm_bf16(Ad, Bd, ta, tb, C)
   assert _rel(C, ref) <= 3e-6
   C16 = torch.empty(M, N, device=cuda, dtype=bf)
-  _C().gemm_bf16(A.to(cuda), B.to(cuda), ta, tb, C16)
+  _C().gemm_bf16(Ad, Bd, ta, tb, C16)
   assert _rel(C16, ref) <= 8e-3
 
 
@@ -126,7 +137,8 @@ def test_gemm_bf16_weight_grad_any_k(cuda, M, N, K):
   ref = A.double().t() @ B.double()
   C = torch.zeros(M, N, device=cuda)
   db = torch.zeros(N, device=cuda)
-  _C().gemm_bf16(A.to(cuda), B.to(cuda), True, False, C, accumulate=True, colsum=db)
+  _C().gemm_bf16(_padded(A.to(cuda)), _padded(B.to(cuda)), True, False, C,
+                 accumulate=True, colsum=db)
   assert _rel(C, ref) <= 3e-6
   assert _rel(db, B.double().sum(0)) <= 3e-6
 
