@@ -108,11 +108,15 @@ def build_hip(workers=8, force=False, extra_flags=(), out=None):
   objs = [o for _, o, _ in jobs]
   if (force or not os.path.exists(out) or
       max(os.path.getmtime(o) for o in objs) > os.path.getmtime(out)):
-    cmd = [HIPCC, '-shared', '-fPIC', '-o', out] + objs + [
+    # link to a temporary name and rename: a concurrent reader (a gpurun
+    # snapshot, an importing process) never sees a half-written library
+    tmp_out = out + '.tmp'
+    cmd = [HIPCC, '-shared', '-fPIC', '-o', tmp_out] + objs + [
         '--offload-arch=' + ARCH, '-L' + lib, '-Wl,-rpath,' + lib,
         '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_hip',
         '-ltorch_python', '-lamdhip64']
     _run(cmd)
+    os.replace(tmp_out, out)
     print('  linked', os.path.relpath(out, ROOT), flush=True)
   return out
 
@@ -152,10 +156,12 @@ def build_native(workers=8, force=False, sanitize=None):
   objs = [o for _, o, _ in jobs]
   if (force or not os.path.exists(out) or
       max(os.path.getmtime(o) for o in objs) > os.path.getmtime(out)):
-    cmd = [cxx, '-shared', '-o', out] + objs + ['-pthread', '-lrt']
+    tmp_out = out + '.tmp'  # atomic replace, as build_hip
+    cmd = [cxx, '-shared', '-o', tmp_out] + objs + ['-pthread', '-lrt']
     if sanitize:
       cmd += ['-fsanitize=%s' % sanitize]
     _run(cmd)
+    os.replace(tmp_out, out)
     print('  linked', os.path.relpath(out, ROOT), flush=True)
   return out
 

@@ -561,8 +561,11 @@ template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
 bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   const int fl = (c.relu_in ? 1 : 0) | (c.relu_out ? 2 : 0) | (c.mask ? 4 : 0) |
                  (c.add ? 8 : 0) | (c.bias ? 16 : 0);
-  static const int on = env_int("SA_WINO_FL", 0);  // measured: 10.85 (on) vs 10.77 ms/step (off)
-  if (on && !flip) {
+  // SA_WINO_FL: 1 = every instance (measured 10.85 vs 10.77 ms/step with
+  // none: the 32-channel instances spilled), 2 = the 16-channel-input
+  // instances only (no spill risk at 112 VGPRs), 0 = none
+  static const int on = env_int("SA_WINO_FL", 0);
+  if ((on == 1 || (on == 2 && CIN == 16)) && !flip) {
     if (fl == 19) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 19>(c, flip, s);
     if (fl == 24) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 24>(c, flip, s);
     if (fl == 26) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 26>(c, flip, s);
