@@ -170,8 +170,12 @@ class _DeepTorsoF32(torch.autograd.Function):
     out = t[-ctx.nparams - 1]
     saved = t[:-ctx.nparams - 1]
     gv, direct = grad_sink.sinks(params)
-    dy = grad_out.reshape(out.shape).to(torch.float32).clone(
-        memory_format=torch.contiguous_format)
+    dy = grad_out.reshape(out.shape)
+    if not (getattr(grad_out, '_sa_scratch', False) and
+            dy.dtype == torch.float32 and dy.is_contiguous()):
+      # the incoming gradient is masked in place below: copy unless it is
+      # the fused core's own scratch dfeats buffer (never a caller's tensor)
+      dy = dy.to(torch.float32).clone(memory_format=torch.contiguous_format)
     C.cf32_relu_mask_(dy, out)  # final ReLU of the torso
     # the ~15 fixed-order weight-gradient slot sums of this backward are
     # queued and launched as ONE kernel at the end (cf32_wgrad_flush)

@@ -222,6 +222,7 @@ class _CoreLSTMF32(torch.autograd.Function):
     C.gemm_f32(dg2, kernel[:CORE], False, True, dh, mask=h_aug[:, :CORE])
     dfeats = torch.empty_like(feats)
     C.gemm_f32(dh, w_fc, False, True, dfeats)
+    dfeats._sa_scratch = True  # the torso backward may mask it in place
     C.gemm_f32(hpm.view(N, CORE), dg2, True, False, gk[f_in:],
                accumulate=True)                                     # W_h
     C.gemm_f32(h_aug[:, :K], dg2, True, False, gk[:K], accumulate=True,
@@ -243,6 +244,15 @@ class _CoreLSTMF32(torch.autograd.Function):
             d_instr)
 
 
+def _as_u8(done):
+  """done as a contiguous uint8 tensor: a bool tensor is reinterpreted in
+  place (same 1-byte elements), anything else converted."""
+  done = done.contiguous()
+  if done.dtype == torch.bool:
+    return done.view(torch.uint8)
+  return done.to(torch.uint8)
+
+
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
               num_actions, instr_enc=None):
   """feats [T*B, F] (ReLU'd torso output: bf16 -> the bf16-operand path,
@@ -257,6 +267,6 @@ def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
       rewards.reshape(-1).to(torch.float32).contiguous(),
       actions.reshape(-1).to(torch.int64).contiguous(),
       c0.float().contiguous(), h0.float().contiguous(),
-      done.to(torch.uint8).contiguous(), int(num_actions),
+      _as_u8(done), int(num_actions),
       None if instr_enc is None else instr_enc.float().contiguous())
   return hs, (c_last, hs[-1])
