@@ -986,16 +986,23 @@ struct WinoBwdArgs {
 // only, waves 4-7 four k-steps of 4 tiles each, 256 instead of 576 weight-
 // gradient MFMAs per range.  One workgroup per CU (LDS) either way, so the
 // WWG instance may use up to 256 VGPRs.
-template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false>
-__global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
-  constexpr int NW = 8, NTH = 512;
+// NW waves per workgroup (WWG only, else 8): NW / 2 data-gradient waves (one
+// 16-tile group each) and NW / 2 weight-gradient waves splitting the range's
+// RT / 4 k-steps evenly.  NW = 12 over 96-tile ranges (three waves per SIMD)
+// does not fit: capped at 168 VGPRs the kernel spills 121 (it needs ~256 at
+// two waves per SIMD), so only NW = 8 is instantiated.
+template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
+  constexpr int NTH = 64 * NW;
   constexpr int PP = C + 4;
   constexpr int C4 = C / 4;
   constexpr int LC4 = C4 == 4 ? 2 : 3;
   constexpr int NG = RT / 16;          // dgrad tasks (16-tile groups)
+  constexpr int NWG = NW - NG;         // weight-gradient waves (WWG)
   constexpr int USTR = 4 * C * 4;      // floats per xi in U_s (one ci block)
   static_assert(C == 16, "fused backward: 16 channels (LDS)");
-  static_assert(NG == 4, "four dgrad groups");
+  static_assert(WWG ? (NG == NW / 2 && (RT / 4) % NWG == 0) : (NW == 8 && NG == 4),
+                "one dgrad wave per 16-tile group");
   static_assert(WWG ? (RT % 16 == 0) : (RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0),
                 "work split");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1208,8 +1215,8 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
       // ---- Winograd weight gradient: waves 4-7, k-step = 4 tiles (lane
       // group g = tile 4 st + g), lane c16 = input channel of V and output
       // channel of Z; acc[4 i + bc] += V[i][bc] (x) Z[i][bc]
-      if (wave >= 4) {
-        for (int st = wave - 4; st < RT / 4; st += 4) {
+      if (wave >= NG) {
+        for (int st = wave - NG; st < RT / 4; st += NWG) {
           int base = tile_s[4 * st + kperm(g)];
           const bool valid = base >= 0;
           base = valid ? base : 0;
@@ -1296,19 +1303,19 @@ __global__ __launch_bounds__(512, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBw
     __syncthreads();
     float* P = smem;                 // [16 xi][C ci][C co]
     float* dB = smem + 16 * C * C;   // [C]
-    for (int k = 4; k < NW; ++k) {
+    for (int k = NG; k < NW; ++k) {
       if (wave == k) {
 #pragma unroll
         for (int xi = 0; xi < 16; ++xi)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float* pp = P + (xi * C + 4 * g + q) * C + c16;
-            *pp = (k == 4 ? 0.f : *pp) + wacc[xi][q];
+            *pp = (k == NG ? 0.f : *pp) + wacc[xi][q];
           }
         float v = dbacc;
         v += __shfl_xor(v, 16);
         v += __shfl_xor(v, 32);
-        if (g == 0) dB[c16] = (k == 4 ? 0.f : dB[c16]) + v;
+        if (g == 0) dB[c16] = (k == NG ? 0.f : dB[c16]) + v;
       }
       __syncthreads();
     }
@@ -1885,7 +1892,7 @@ bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float
       dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
 }
 
-template <int C, int RT, int MAXC, int KD, bool WWG = false>
+template <int C, int RT, int MAXC, int KD, bool WWG = false, int NW = 8>
 bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
                   float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
                   float* dw, float* db, hipStream_t s) {
@@ -1898,7 +1905,7 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
   const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
-  if (maxrows * Wl * (C / 4) > MAXC * 512 || maxrows > 512) return false;
+  if (maxrows * Wl * (C / 4) > MAXC * 64 * NW || maxrows > 64 * NW) return false;
   const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * Wl * (C + 4)) +
                        sizeof(int) * (maxrows + RT);
   if (bytes > 160 * 1024) return false;
@@ -1917,10 +1924,10 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   a.relu_x = relu_x;
   static const int runs = env_int("SA_WINO_RUNS", 1);
   a.runs = runs;
-  auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true>
-                     : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false>;
+  auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true, NW>
+                     : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false, NW>;
   allow_lds_w(kern, bytes);
-  hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), bytes, s, a);
   wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
   return true;
 }
