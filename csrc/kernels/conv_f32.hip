@@ -1246,6 +1246,56 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(
       (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
 }
 
+// Pool gradient for even H, W and pad-before 0 (the deep torso's 36x48 and
+// 18x24 pools): thread = (pooled block (i, j), 4 channels) owning the 2x2
+// pre-pool cells (2i + a, 2j + b).  Those cells can only be the argmax of
+// windows (i-1, j-1), (i-1, j), (i, j-1), (i, j); each is loaded once (4
+// dP + 4 code loads instead of 9 of each for the four cells separately) and
+// the sums run in ascending (py, px) order: bitwise maxpool_bwd_kernel.
+// Codes: window (py, px) tap (oy, ox) = oy * 3 + ox.
+__global__ __launch_bounds__(256) void maxpool_bwd_blk_kernel(
+    const float* __restrict__ dy, const uint8_t* __restrict__ arg, float* __restrict__ dx,
+    int N, int Hp, int Wp, int C, int c4_shift) {
+  const unsigned total = static_cast<unsigned>(N) * Hp * (static_cast<unsigned>(Wp) << c4_shift);
+  const unsigned flat = blockIdx.x * 256u + threadIdx.x;
+  if (flat >= total) return;
+  const int c4 = static_cast<int>(flat & ((1u << c4_shift) - 1));
+  const unsigned pix = flat >> c4_shift;  // (n, i, j)
+  const int j = static_cast<int>(pix % static_cast<unsigned>(Wp));
+  const unsigned ni = pix / static_cast<unsigned>(Wp);
+  const int i = static_cast<int>(ni % static_cast<unsigned>(Hp));
+  const int n = static_cast<int>(ni / static_cast<unsigned>(Hp));
+  const int W = 2 * Wp;
+  const int64_t pbase = static_cast<int64_t>(n) * Hp * Wp * C + 4 * c4;
+  // windows: 0 = (i-1, j-1), 1 = (i-1, j), 2 = (i, j-1), 3 = (i, j)
+  f4 g[4];
+  uint32_t cd[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int py = i - 1 + (w >> 1), px = j - 1 + (w & 1);
+    const bool in = py >= 0 && px >= 0;
+    const int64_t o = pbase + static_cast<int64_t>(in ? py * Wp + px : 0) * C;
+    g[w] = in ? *reinterpret_cast<const f4*>(dy + o) : f4{0.f, 0.f, 0.f, 0.f};
+    cd[w] = in ? *reinterpret_cast<const uint32_t*>(arg + o) : 0xFFFFFFFFu;
+  }
+  auto add = [&](f4& acc, int w, uint32_t want) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (((cd[w] >> (8 * r)) & 0xFFu) == want) acc[r] += g[w][r];
+  };
+  f4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c10 = c00, c11 = c00;
+  add(c00, 0, 8); add(c00, 1, 6); add(c00, 2, 2); add(c00, 3, 0);
+  add(c01, 1, 7); add(c01, 3, 1);
+  add(c10, 2, 5); add(c10, 3, 3);
+  add(c11, 3, 4);
+  float* row0 = dx + ((static_cast<int64_t>(n) * 2 * Hp + 2 * i) * W + 2 * j) * C + 4 * c4;
+  float* row1 = row0 + static_cast<int64_t>(W) * C;
+  *reinterpret_cast<f4*>(row0) = c00;
+  *reinterpret_cast<f4*>(row0 + C) = c01;
+  *reinterpret_cast<f4*>(row1) = c10;
+  *reinterpret_cast<f4*>(row1 + C) = c11;
+}
+
 // Pool gradient gather: one grid row = one pre-pool row (n, y); thread = 4
 // channels of one pixel (a flat layout as in maxpool_fwd measured slower here:
 // 0.37 -> 0.41 ms/step), summing the (<= 4) windows whose argmax is this
@@ -1643,6 +1693,15 @@ bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, i
                         int C, int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
   const int sh = c4_shift_of(C);
   if (sh < 0) return false;
+  static const bool blk = env_knob("SA_F32_POOL_BWD_BLK", 1) != 0;
+  if (blk && pb_h == 0 && pb_w == 0 && H == 2 * Hp && W == 2 * Wp) {
+    const int64_t total = static_cast<int64_t>(N) * Hp * (static_cast<int64_t>(Wp) << sh);
+    if (total < (int64_t{1} << 31)) {
+      hipLaunchKernelGGL(maxpool_bwd_blk_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                         dim3(256), 0, s, dy, arg, dx, N, Hp, Wp, C, sh);
+      return true;
+    }
+  }
   const dim3 grid(static_cast<unsigned>(N) * H, ((W << sh) + 255) / 256);
   hipLaunchKernelGGL(maxpool_bwd_kernel, grid, dim3(256), 0, s, dy, arg, dx, N, H, W, C, Hp,
                      Wp, pb_h, pb_w, sh);
