@@ -76,16 +76,16 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
 }
 constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
 
-// Packed-fp32 transform arithmetic: the Winograd input / output transforms
-// as v_pk_add_f32 pairs (2 lanes of a float4 per instruction) instead of 4
-// scalar v_add/v_sub_f32.  Measured per kernel (profiles/experiments.md,
-// round 4): the 32-channel forward / data-gradient kernel gains 4-5 %, the
-// 16-channel kernels and the fused backward kernels gain nothing or lose
-// (priced as an anti-lever beside MFMAs in MI355X_MICROARCH.md), so
-// SA_WINO_PK = 2 (default) packs only the 32-channel forward; 1 = every
-// kernel, 0 = none (experiment builds).
+// Packed-fp32 transform arithmetic (experiment builds, SA_WINO_PK=1): the
+// Winograd input / output transforms as v_pk_add_f32 pairs (2 lanes of a
+// float4 per instruction) instead of 4 scalar v_add/v_sub_f32.  The backend
+// does not select v_pk_add_f32 for <2 x float> arithmetic here (it stays
+// scalar), so the packed form needs inline asm - and the compiler inserts no
+// wait states inside asm: the output transform then reads MFMA accumulators
+// before the MFMAs have written them (the 32-channel forward computed wrong
+// outputs, profiles/experiments.md round 4).  Default 0: scalar everywhere.
 #ifndef SA_WINO_PK
-#define SA_WINO_PK 2
+#define SA_WINO_PK 0
 #endif
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 lo2(f4 a) { return __builtin_shufflevector(a, a, 0, 1); }
@@ -211,7 +211,7 @@ __device__ __forceinline__ RangeGeom range_geom(const WinoArgs& a, int r, int RT
 template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
 __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
-  constexpr bool kPk = SA_WINO_PK == 1 || (SA_WINO_PK == 2 && CIN == 32);
+  constexpr bool kPk = SA_WINO_PK == 1;
   const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
   const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
   const bool f_mask = FL < 0 ? a.mask != nullptr : (FL & 4) != 0;
