@@ -13,6 +13,10 @@ void check_act(const at::Tensor& t, const char* name, int64_t C) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
   TORCH_CHECK(t.dim() == 4 && t.size(3) == C, name, " must be NHWC with C=", C);
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+  // validated sizes (and the largest learner chunk: ops/conv_f32.py
+  // MAX_FRAMES); an oversized call fails here instead of computing garbage
+  TORCH_CHECK(t.numel() * 2 < (int64_t{1} << 32), name, " is ", t.numel() * 2,
+              " bytes: bf16 conv tensors must stay under 4 GB (chunk the frames)");
 }
 void check_w(const at::Tensor& w, const at::Tensor& b, int64_t cin, int64_t cout) {
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == at::kFloat,

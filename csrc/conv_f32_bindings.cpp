@@ -41,9 +41,22 @@ int src_kind(const at::Tensor& x) {
   return sa::cf32::kSrcF32;
 }
 
+// Every activation / gradient tensor these kernels touch stays under 4 GB:
+// the kernels and their tile schedules are validated up to that size (the
+// Winograd stagers address one tensor with 32-bit buffer offsets).  Larger
+// learner batches run the torso in frame chunks (ops/conv_f32.py
+// MAX_FRAMES); an oversized call fails here instead of computing garbage.
+void check_size(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.numel() * static_cast<int64_t>(t.element_size()) < (int64_t{1} << 32), name,
+              " is ", t.numel() * t.element_size(),
+              " bytes: fp32 conv tensors must stay under 4 GB (chunk the frames: "
+              "ops/conv_f32.py MAX_FRAMES)");
+}
+
 void check_nhwc(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, name,
               " must be a contiguous NHWC GPU tensor");
+  check_size(t, name);
 }
 
 const float* opt_f32(const c10::optional<at::Tensor>& t, const at::Tensor& like,
@@ -71,6 +84,7 @@ at::Tensor conv_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, int
   const int64_t Cout = w.size(3);
   const c10::DeviceGuard g(x.device());
   auto y = at::empty({x.size(0), Ho, Wo, Cout}, x.options().dtype(at::kFloat));
+  check_size(y, "y");
   sa::cf32::ConvArgs a{};
   a.src = x.data_ptr();
   a.w = w.data_ptr<float>();
@@ -130,6 +144,7 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
   const int64_t K = w.size(0), Cin = w.size(2);
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, Cin}, dy.options());
+  check_size(dx, "dx");
   static const bool phase = [] {
     const char* e = std::getenv("SA_F32_DGRAD_PHASE");
     return !(e && e[0] == '0');
@@ -334,6 +349,7 @@ std::vector<at::Tensor> conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b, 
   const c10::DeviceGuard g(x.device());
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), Cout = w.size(3);
   auto y = at::empty({N, (H + 1) / 2, (W + 1) / 2, Cout}, x.options().dtype(at::kFloat));
+  check_size(y, "y");
   auto arg = at::empty(y.sizes(), x.options().dtype(at::kByte));
   sa::cf32::ConvArgs a{};
   a.src = x.data_ptr();
@@ -375,6 +391,7 @@ at::Tensor maxpool_bwd(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int6
   TORCH_CHECK(dy.size(1) == (H + 1) / 2 && dy.size(2) == (W + 1) / 2, "pooled shape");
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  check_size(dx, "dx");
   TORCH_CHECK(sa::cf32::maxpool_bwd_launch(dy.data_ptr<float>(), arg.data_ptr<uint8_t>(),
                                            dx.data_ptr<float>(), dy.size(0), H, W,
                                            dy.size(3), dy.size(1), dy.size(2), pb_h, pb_w,
@@ -390,6 +407,7 @@ at::Tensor frames_f32(at::Tensor x) {
               "frames must be uint8 NHWC with 1..4 channels");
   const c10::DeviceGuard g(x.device());
   auto y = at::empty({x.size(0), x.size(1), x.size(2), 4}, x.options().dtype(at::kFloat));
+  check_size(y, "y");
   sa::cf32::frames_f32_launch(x.data_ptr<uint8_t>(), y.data_ptr<float>(),
                               x.size(0) * x.size(1) * x.size(2), x.size(3), stream());
   check_launch("cf32_frames_f32");

@@ -975,7 +975,7 @@ struct WinoBwdArgs {
   int relu_x;        // wgrad operand = relu(x)
   int mask_x = 1;    // dX masked by (x > 0) (fused32 kernel; the 16-channel one always masks)
   int ablate = 0;    // measurement knob (SA_FUSED_ABLATE, SA_MEASURE_KNOBS builds only):
-                     // 2 no dgrad, 4 no wgrad
+                     // 2 no dgrad, 4 no wgrad, 8 no global dY loads (fused32)
   int runs = 1;      // contiguous range runs (wino_bwd_fused_kernel; fused32 always)
   unsigned* err = nullptr;  // the device's sticky conv error word (rmsprop.hip guard)
   int fault = 0;     // fault injection: every hand-off wait reports a timeout
@@ -1491,7 +1491,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 #pragma unroll
     for (int k = 0; k < MAXCY; ++k) {
       const int rb = sy_L[k] >= 0 ? tab_s[sy_L[k]] : -1;
-      const bool in = rb >= 0 && sy_o[k] >= 0;
+      const bool in = rb >= 0 && sy_o[k] >= 0 && !knob(a.ablate, 8);
       sy[k] = bload(dyr, in ? static_cast<uint32_t>(rb * CY + sy_o[k]) * 4u : kOOB);
     }
 #pragma unroll

@@ -73,9 +73,14 @@ def build_parser() -> argparse.ArgumentParser:
                  help='Data-parallel learners (one process per GPU, RCCL '
                       'all-reduce), launched with torch.distributed.run; '
                       '0 = WORLD_SIZE decides, else it must equal WORLD_SIZE.')
-  p.add_argument('--grad_reduce', default='sum', choices=['sum', 'mean'],
-                 help='sum: N learners x B == one learner with N*B (reference '
-                      'losses are sums).')
+  p.add_argument('--grad_reduce', default='mean', choices=['sum', 'mean'],
+                 help='Data-parallel gradient reduction.  mean (default): '
+                      'the all-reduced sum times 1/N, folded into the RMSProp '
+                      'update - each update has the size of one B-column '
+                      'learner\'s.  sum: N learners x B == one learner with '
+                      'N*B under the reference sum losses, which at N=8 does '
+                      'not learn at the reference learning rate '
+                      '(profiles/r4_learning_dp_equiv.md).')
   p.add_argument('--grad_scale', type=float, default=1.0,
                  help='Multiplies the (all-reduced) gradient inside the '
                       'RMSProp update; a single learner with batch N*B and '

@@ -151,16 +151,29 @@ class _DeepTorso(torch.autograd.Function):
 
 
 def torso_forward(agent, frames):
-  """uint8 frames [N,H,W,3] -> relu'd conv features [N, flat] (bf16)."""
+  """uint8 frames [N,H,W,C] (C = 3 or 4) -> relu'd conv features [N, flat]
+  (bf16).  Batches above conv_f32.MAX_FRAMES frames run in equal chunks."""
   if not supports(agent):
     raise NotImplementedError(
-        'bf16 HIP torso: deep ResNet on uint8 RGB frames only (got %r, %r)' %
+        'bf16 HIP torso: deep ResNet on 3/4-channel uint8 frames only (got %r, %r)' %
         (agent.torso_kind, agent.frame_shape))
-  return _DeepTorso.apply(frames, *deep_param_list(agent))
+  from .conv_f32 import _chunked
+  return _chunked(_DeepTorso, frames.contiguous(), deep_param_list(agent))
 
 
 def linear_relu(x, w, b):
-  """Torso FC: relu(x W + b) as a bf16 hipBLASLt GEMM (plain library GEMM)."""
-  y = torch.addmm(b.to(torch.bfloat16), x.to(torch.bfloat16),
-                  w.to(torch.bfloat16))
+  """Torso FC: relu(x W + b) on bf16 operands, fp32 accumulation.  Without
+  autograd (actor inference) it is one hand-written bf16 MFMA GEMM
+  (gemm_bf16.hip, bias + ReLU in the epilogue, fp32 out); the differentiable
+  per-op path (the fused core's test oracle) keeps torch.addmm."""
+  x16 = x.to(torch.bfloat16).contiguous()
+  w16 = w.to(torch.bfloat16).contiguous()
+  if not (torch.is_grad_enabled() and
+          (x.requires_grad or w.requires_grad or b.requires_grad)):
+    out = torch.empty(x16.shape[0], w16.shape[1], device=x.device,
+                      dtype=torch.float32)
+    ext().gemm_bf16(x16, w16, False, False, out,
+                    bias=b.detach().float().contiguous(), relu=True)
+    return out
+  y = torch.addmm(b.to(torch.bfloat16), x16, w16)
   return torch.relu(y).to(torch.float32)

@@ -252,6 +252,27 @@ def shallow_param_list(agent):
   return out
 
 
+# Frames per torso launch sequence.  Larger learner batches (e.g. the
+# single-learner equivalent of 8 data-parallel ranks: B=256, T=100 = 25856
+# frames) run the torso in equal chunks of at most this many frames: the
+# Winograd launchers take < 2^22 tiles (9709 frames at 36x48) and every
+# tensor must stay inside one 4 GB buffer descriptor (36x48x32 fp32 is
+# 221 KB per frame).  Per-frame features are independent of the chunking;
+# the weight gradients of the chunks accumulate into the same sinks.  The
+# headline batch (3232 frames) is one chunk.
+MAX_FRAMES = int(os.environ.get('SA_F32_MAX_FRAMES', '8192'))
+
+
+def _chunked(fn, frames, params):
+  n = frames.shape[0]
+  k = -(-n // max(1, MAX_FRAMES))
+  if k <= 1:
+    return fn.apply(frames, *params)
+  step = -(-n // k)
+  return torch.cat([fn.apply(frames[i:i + step], *params)
+                    for i in range(0, n, step)])
+
+
 def torso_forward_f32(agent, frames):
   """uint8 frames [N,H,W,C] -> ReLU'd conv features [N, flat] (fp32)."""
   if not supports(agent):
@@ -260,10 +281,11 @@ def torso_forward_f32(agent, frames):
         (agent.torso_kind, agent.frame_shape))
   if frames.dtype != torch.uint8:
     raise TypeError('HIP torso expects uint8 frames, got %s' % frames.dtype)
+  frames = frames.contiguous()
   if agent.torso_kind == 'shallow':
-    return _ShallowTorsoF32.apply(frames, *shallow_param_list(agent))
+    return _chunked(_ShallowTorsoF32, frames, shallow_param_list(agent))
   from .conv import deep_param_list
-  return _DeepTorsoF32.apply(frames, *deep_param_list(agent))
+  return _chunked(_DeepTorsoF32, frames, deep_param_list(agent))
 
 
 def linear_relu_f32(x, w, b):

@@ -3,9 +3,12 @@
 The reference has exactly one learner (experiment.py:508).  Here N learners,
 one process per GPU, each consume their own B-sized batches; after backward the
 flat gradient buffer (see optim.FlatParams) is summed (or averaged) with one
-`torch.distributed.all_reduce` — backend "nccl" is RCCL on ROCm.  With
-`--grad_reduce=sum`, N learners x batch B is exactly one learner with batch N*B
-under the reference's sum losses.
+`torch.distributed.all_reduce` — backend "nccl" is RCCL on ROCm.  The default
+`--grad_reduce=mean` scales the summed gradient by 1/N inside the RMSProp
+update (N learners x B == one learner with batch N*B and --grad_scale 1/N);
+`--grad_reduce=sum` is exactly one learner with batch N*B under the
+reference's sum losses, which at N*B = 256 does not learn at the reference
+learning rate (profiles/r4_learning_dp_equiv.md).
 """
 
 from .dist import (init_distributed, GradientSynchronizer, broadcast_params,

@@ -234,6 +234,83 @@ def test_bf16_agent_atari_stack_takes_bf16_kernels(cuda):
   assert torso_precision(gray) == 'fp32'
 
 
+def _torso_run(agent, frames, r, max_frames):
+  """Features and conv-parameter gradients of sum(features * r) with the
+  torso chunked at max_frames frames per launch sequence."""
+  from scalable_agent_amd.ops import conv_f32
+  old = conv_f32.MAX_FRAMES
+  conv_f32.MAX_FRAMES = max_frames
+  try:
+    for p in agent.parameters():
+      p.grad = None
+    f = agent.conv_features(frames)
+    (f.float() * r).sum().backward()
+    return f.detach(), {k: p.grad.clone() for k, p in agent.convnet.items()}
+  finally:
+    conv_f32.MAX_FRAMES = old
+
+
+@pytest.mark.parametrize('torso,dtype', [('deep', torch.float32), ('shallow', torch.float32),
+                                         ('deep', torch.bfloat16)])
+def test_torso_chunking_matches_whole_batch(cuda, torso, dtype):
+  """Large learner batches run the torso in frame chunks (ops/conv_f32.py
+  MAX_FRAMES): per-frame features are bitwise those of one launch sequence,
+  and the chunks' weight gradients add up to the whole batch's."""
+  from scalable_agent_amd.models import Agent
+  agent = Agent(9, torso=torso, frame_shape=(72, 96, 3), seed=3, backend='hip',
+                compute_dtype=dtype).to(cuda)
+  g = torch.Generator(device=cuda).manual_seed(4)
+  frames = torch.randint(0, 256, (150, 72, 96, 3), generator=g, dtype=torch.uint8,
+                         device=cuda)
+  r = torch.randn(150, agent.flat_size, generator=g, device=cuda)
+  f1, g1 = _torso_run(agent, frames, r, 1 << 20)
+  f3, g3 = _torso_run(agent, frames, r, 64)  # 3 chunks of 50 frames
+  assert torch.equal(f1, f3)
+  tol = 1e-5 if dtype == torch.float32 else 2e-3
+  for k in g1:
+    assert rel_err(g3[k], g1[k]) <= tol, k
+
+
+def test_torso_f32_learner_scale_batch(cuda):
+  """The single-learner equivalent of 8 data-parallel ranks (B=256, T=100:
+  25856 frames, past the Winograd launchers' 2^22-tile / 4 GB limits for one
+  launch): 4 chunks of 6464 frames vs 8 chunks of 3232 (the headline batch)
+  - bitwise features, gradients within fp32 summation order - and the first
+  frames against the float64 oracle."""
+  from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.ops import conv_f32
+  agent = Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=5, backend='hip',
+                compute_dtype=torch.float32).to(cuda)
+  N = 256 * 101
+  g = torch.Generator(device=cuda).manual_seed(2)
+  frames = torch.randint(0, 256, (N, 72, 96, 3), generator=g, dtype=torch.uint8,
+                         device=cuda)
+  r = torch.randn(N, agent.flat_size, generator=g, device=cuda)
+  assert -(-N // conv_f32.MAX_FRAMES) == 4
+  fa, ga = _torso_run(agent, frames, r, conv_f32.MAX_FRAMES)
+  fb, gb = _torso_run(agent, frames, r, 3232)
+  assert torch.isfinite(fa).all()
+  assert torch.equal(fa, fb)
+  for k in ga:
+    assert torch.isfinite(ga[k]).all(), k
+    assert rel_err(ga[k], gb[k]) <= 1e-5, k
+  cpu_agent = Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=5)
+  ref, _ = _ref_features(cpu_agent, frames[-2:].cpu())
+  assert rel_err(fa[-2:], ref) <= 1e-4
+
+
+def test_oversized_conv_call_fails_loudly(cuda):
+  """A conv tensor of >= 4 GB (past the validated sizes) raises instead of
+  running: the learner chunks such batches (ops/conv_f32.py MAX_FRAMES)."""
+  C = _C()
+  x = torch.empty(19500, 36, 48, 16, device=cuda)  # 4.3 GB, never written
+  w = torch.zeros(3, 3, 16, 16, device=cuda)
+  b = torch.zeros(16, device=cuda)
+  with pytest.raises(RuntimeError, match='4 GB'):
+    C.cf32_conv_fwd(x, w, b, 1, 1, 1, 36, 48)
+  del x
+
+
 @pytest.mark.parametrize('N,H,W,Cin,Cout,u8', [
     (3, 72, 96, 3, 16, True), (3, 36, 48, 16, 32, False), (3, 18, 24, 32, 32, False),
     (2, 84, 84, 4, 16, True), (2, 42, 42, 16, 32, False), (2, 21, 21, 32, 32, False)])

@@ -112,3 +112,10 @@ def test_dp_mean_equals_single_learner_with_grad_scale(tmp_path):
   ref.step(full)
   ref.step(full)
   assert not torch.allclose(dp['params'], ref.flat.params, rtol=1e-4, atol=1e-6)
+
+
+def test_default_reduction_is_mean():
+  """Data-parallel default (profiles/r4_learning_dp_equiv.md: at the B=256
+  single-learner equivalent of 8 ranks the summed gradient does not learn at
+  the reference learning rate, the 1/N-scaled one does)."""
+  assert flags_lib.default_flags().grad_reduce == 'mean'
