@@ -574,6 +574,377 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
 
+// ------------------------------------------------------- fused stage head
+// Stage-head conv (16 -> 32 channels, 3x3/1 SAME + bias) with the following
+// 3x3/2 SAME max-pool and its argmax fused into the epilogue (reference
+// experiment.py:160-163: conv -> max_pool), so the pre-pool map exists only
+// in LDS.  Needs H % 4 == 0 and a pooled pad-before of 0 (even H, W).  Each
+// range is the tile-row pair (2k, 2k+1) of one image (RT = W tiles: pixel
+// rows 4k..4k+3), one 16-tile x 16-channel task per wave.  The epilogue writes
+// Y + b into an LDS image of those 4 rows (aliasing the staged input rows,
+// which every wave has finished reading); the pool phase (thread = pooled
+// column x channel quad) then stores pooled row 2k (pixel rows 4k..4k+2) and
+// keeps the rows-(4k+2, 4k+3) part of pooled row 2k+1 in registers until
+// the next range - the same workgroup's, since each walks a contiguous run -
+// adds pixel row 4k+4.  A run's first range (k > 0) leaves its top-row part
+// in `side`, the run's last carry is stored as is, and wino_pool_fix_kernel
+// merges those pairs afterwards.  Values and argmax codes are bitwise those
+// of the conv + maxpool_fwd_kernel pair (strict >, taps in row-major window
+// order: the first maximal tap wins).
+struct WinoPoolArgs {
+  WinoArgs c;
+  float* pooled;     // [N, H/2, W/2, 32]
+  uint8_t* arg;      // [N, H/2, W/2, 32] tap codes dy * 3 + dx
+  f4* side_v;        // [G][W/2 * 8] top-row parts of the run-start ranges
+  uint32_t* side_c;  // [G][W/2 * 8] their codes (4 x 8 bits)
+};
+
+template <int RT>
+struct PoolGeo {
+  static constexpr int CIN = 16, COUT = 32;
+  static constexpr int W = RT;              // one tile-row pair = RT tiles
+  static constexpr int NW = RT / 8;         // NG = RT / 16 groups x 2 slices
+  static constexpr int PP = CIN + 4;        // staged pixel pitch (floats)
+  static constexpr int IPP = COUT + 4;      // pre-pool image pixel pitch
+  static constexpr int ROWS = 6;            // staged input rows per range
+  static constexpr int XREG = (ROWS * (W + 2) * PP > 4 * W * IPP) ? ROWS * (W + 2) * PP
+                                                                   : 4 * W * IPP;
+  static constexpr int MAXC = (ROWS * (W + 2) * (CIN / 4) + 64 * NW - 1) / (64 * NW);
+  static constexpr int WP = W / 2;          // pooled width
+  static constexpr size_t bytes = sizeof(float) * (16 * CIN * COUT + XREG + ROWS);
+};
+
+__device__ __forceinline__ void pool_take(f4& best, int (&code)[4], const f4 v, int c) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (v[q] > best[q]) {  // strict: the first maximal tap wins
+      best[q] = v[q];
+      code[q] = c;
+    }
+}
+__device__ __forceinline__ uint32_t pack_codes(const int (&code)[4]) {
+  return static_cast<uint32_t>(code[0]) | (static_cast<uint32_t>(code[1]) << 8) |
+         (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
+}
+
+template <int RT>
+__global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs pa) {
+  using P = PoolGeo<RT>;
+  constexpr int CIN = P::CIN, COUT = P::COUT, W = P::W, NW = P::NW, NTH = 64 * NW;
+  constexpr int PP = P::PP, IPP = P::IPP, MAXC = P::MAXC, WP = P::WP;
+  constexpr int C4 = CIN / 4, LC4 = 2;
+  constexpr int NG = RT / 16;
+  constexpr int USTR = 4 * COUT * 4;  // floats per xi in U_s (one ci block)
+  constexpr int Wl = W + 2, rowstr = Wl * PP;
+  static_assert(NG * (COUT / 16) == NW && RT % 16 == 0 && MAXC <= 32, "shape");
+  const WinoArgs& a = pa.c;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* U_s = smem;                    // [16 xi][4 g][COUT][4]
+  float* x_s = smem + 16 * CIN * COUT;  // staged rows [6][Wl][PP], then the image [4][W][IPP]
+  float* img = x_s;
+  int* tab_s = reinterpret_cast<int*>(x_s + P::XREG);  // [6]
+
+  // U = G g G^T (forward weights HWIO [3][3][16][32])
+  for (int e = threadIdx.x; e < CIN * COUT; e += NTH) {
+    const int co = e % COUT, ci = e / COUT;
+    float gk[3][3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[((ky * 3 + kx) * CIN + ci) * COUT + co];
+    float t[4][3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      t[0][kx] = gk[0][kx];
+      t[1][kx] = 0.5f * ((gk[0][kx] + gk[1][kx]) + gk[2][kx]);
+      t[2][kx] = 0.5f * ((gk[0][kx] - gk[1][kx]) + gk[2][kx]);
+      t[3][kx] = gk[2][kx];
+    }
+    const int gq = (ci >> 2) & 3, v = ci & 3;
+#pragma unroll
+    for (int ra = 0; ra < 4; ++ra) {
+      const float u[4] = {t[ra][0], 0.5f * ((t[ra][0] + t[ra][1]) + t[ra][2]),
+                          0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        U_s[(4 * ra + rb) * USTR + (gq * COUT + co) * 4 + v] = u[rb];
+    }
+  }
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const RangeWalk rw = range_walk(a.nranges, 1);
+  int r = rw.r;
+  if (r >= rw.end) return;  // uniform
+  const int rfirst = r;
+  const int KP = a.TY / 2;  // ranges (tile-row pairs) per image
+  const int Hp = a.H / 2;
+
+  // staging: the generic kernel's register prefetch (row table in LDS)
+  int sl_L[MAXC], sl_x[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4 - 1), pix = e >> LC4;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sl_L[k] = L < P::ROWS ? L : -1;
+    sl_x[k] = (col >= 1 && col <= W) ? (col - 1) * CIN + 4 * ch : -1;
+  }
+  auto build_tab = [&](int rr) {
+    const int n = rr / KP, k = rr - n * KP;
+    const int L = threadIdx.x;
+    if (L < P::ROWS) {
+      const int y = 4 * k - 1 + L;
+      tab_s[L] = (y >= 0 && y < a.H) ? ((n * a.H + y) * W) * CIN : -1;
+    }
+  };
+  f4 stg[MAXC];
+  const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * a.H * W * CIN);
+  auto prefetch = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
+      const bool in = rb >= 0 && sl_x[k] >= 0;
+      stg[k] = bload(srcr, in ? static_cast<uint32_t>(rb + sl_x[k]) * 4u : kOOB);
+    }
+  };
+  build_tab(r);
+  __syncthreads();
+  prefetch();
+
+  // pool-phase thread: pooled column pj, channel quad pq
+  const int pj = threadIdx.x >> 3, pq = threadIdx.x & 7;
+  const bool pooler = threadIdx.x < WP * 8;
+  constexpr float kNegInf = -__builtin_inff();
+  f4 cv = {kNegInf, kNegInf, kNegInf, kNegInf};
+  int cc[4] = {0, 0, 0, 0};
+  bool cvalid = false;
+  int64_t cdst = 0;  // pooled element offset of the carried window
+
+  // this wave's task: 16-tile group grp, 16-channel slice sl
+  const int grp = wave % NG, sl = wave / NG;
+  const int co0 = sl * 16;
+  const int txl = 16 * grp + c16;  // tile within the range = (row txl / (W/2), column)
+  const int tyl = txl / (W / 2), tx = txl - tyl * (W / 2);
+  const float* xp = x_s + (2 * tyl * Wl + 2 * tx) * PP + 4 * g;
+  const float* up = U_s + (g * COUT + co0 + c16) * 4;
+  const f4 bv = *reinterpret_cast<const f4*>(a.bias + co0 + 4 * g);
+
+  for (;;) {
+    __syncthreads();  // U_s written / the previous range's pool reads are done
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      if (sl_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = stg[k];
+      }
+    }
+    const int cur = r;
+    ++r;
+    if (r < rw.end) build_tab(r);
+    __syncthreads();
+    if (r < rw.end) prefetch();  // in flight under the MFMAs below
+
+    f4 acc[16];
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
+    {
+      f4 d[16];
+#pragma unroll
+      for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 4; ++dx)
+          d[4 * dy + dx] = *reinterpret_cast<const f4*>(xp + dy * rowstr + dx * PP);
+      f4 s[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s[q] = d[q] - d[8 + q];
+        s[4 + q] = d[4 + q] + d[8 + q];
+        s[8 + q] = d[8 + q] - d[4 + q];
+        s[12 + q] = d[4 + q] - d[12 + q];
+      }
+      f4 V[16];
+#pragma unroll
+      for (int ra = 0; ra < 4; ++ra) {
+        V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
+        V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
+        V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
+        V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
+      }
+#pragma unroll
+      for (int xp2 = 0; xp2 < 8; ++xp2) {
+        f4 ua[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          ua[q] = *reinterpret_cast<const f4*>(up + (2 * xp2 + q) * USTR);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            acc[2 * xp2 + q] = mfma4(ua[q][v], V[2 * xp2 + q][v], acc[2 * xp2 + q]);
+      }
+    }
+    __syncthreads();  // every wave's patch reads are done: x_s becomes the image
+
+    // output transform Y = A^T M A + b into the pre-pool image
+    {
+      f4 tt[4][2];
+#pragma unroll
+      for (int ra = 0; ra < 4; ++ra) {
+        tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
+        tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+      }
+      f4 Y[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        Y[c] = (tt[0][c] + tt[1][c]) + tt[2][c];
+        Y[2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c];
+      }
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx)
+          *reinterpret_cast<f4*>(img + ((2 * tyl + dy) * W + 2 * tx + dx) * IPP + co0 + 4 * g) =
+              Y[2 * dy + dx] + bv;
+    }
+    __syncthreads();
+
+    // pool phase
+    if (pooler) {
+      const int n = cur / KP, k = cur - n * KP;
+      auto tap = [&](int row, int dx) -> f4 {
+        return *reinterpret_cast<const f4*>(img + (row * W + 2 * pj + dx) * IPP + 4 * pq);
+      };
+      const bool edge = 2 * pj + 2 >= W;  // the window's third column is padding
+      const int64_t orow = static_cast<int64_t>(n) * Hp;
+      // (a) pooled row 2k-1: the carried rows (4k-2, 4k-1) + pixel row 4k
+      if (cvalid || (cur == rfirst && k > 0)) {
+        f4 best = cv;
+        int code[4] = {cc[0], cc[1], cc[2], cc[3]};
+        if (!cvalid) {
+          best = f4{kNegInf, kNegInf, kNegInf, kNegInf};
+          code[0] = code[1] = code[2] = code[3] = 0;
+        }
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          if (dx < 2 || !edge) pool_take(best, code, tap(0, dx), 6 + dx);
+        if (cvalid) {
+          *reinterpret_cast<f4*>(pa.pooled + cdst) = best;
+          *reinterpret_cast<uint32_t*>(pa.arg + cdst) = pack_codes(code);
+        } else {  // the run's first range: the previous workgroup holds rows 4k-2, 4k-1
+          pa.side_v[blockIdx.x * (WP * 8) + threadIdx.x] = best;
+          pa.side_c[blockIdx.x * (WP * 8) + threadIdx.x] = pack_codes(code);
+        }
+      }
+      // (b) pooled row 2k: pixel rows 4k .. 4k+2
+      {
+        f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
+        int code[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            if (dx < 2 || !edge) pool_take(best, code, tap(dy, dx), 3 * dy + dx);
+        const int64_t o = ((orow + 2 * k) * WP + pj) * COUT + 4 * pq;
+        *reinterpret_cast<f4*>(pa.pooled + o) = best;
+        *reinterpret_cast<uint32_t*>(pa.arg + o) = pack_codes(code);
+      }
+      // (c) pooled row 2k+1: pixel rows 4k+2, 4k+3 here, 4k+4 in the next range
+      {
+        f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
+        int code[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+            if (dx < 2 || !edge) pool_take(best, code, tap(2 + dy, dx), 3 * dy + dx);
+        const int64_t o = ((orow + 2 * k + 1) * WP + pj) * COUT + 4 * pq;
+        if (k == KP - 1 || r >= rw.end) {
+          // the image's last pooled row (pixel row 4k+4 is padding), or the
+          // run's last range (the next workgroup's side part is merged by
+          // wino_pool_fix_kernel)
+          *reinterpret_cast<f4*>(pa.pooled + o) = best;
+          *reinterpret_cast<uint32_t*>(pa.arg + o) = pack_codes(code);
+          cvalid = false;
+        } else {
+          cv = best;
+          cc[0] = code[0]; cc[1] = code[1]; cc[2] = code[2]; cc[3] = code[3];
+          cdst = o;
+          cvalid = true;
+        }
+      }
+    }
+    if (r >= rw.end) break;
+  }
+}
+
+// Merges the top-row parts left by each run's first range into the pooled
+// row its predecessor workgroup stored without them (one workgroup per run).
+__global__ __launch_bounds__(256) void wino_pool_fix_kernel(const f4* __restrict__ side_v,
+                                                            const uint32_t* __restrict__ side_c,
+                                                            float* __restrict__ pooled,
+                                                            uint8_t* __restrict__ arg,
+                                                            int nranges, int KP, int Hp, int WP) {
+  const int b = blockIdx.x;
+  const int r = static_cast<int>(static_cast<int64_t>(b) * nranges / gridDim.x);
+  const int n = r / KP, k = r - n * KP;
+  if (k == 0 || static_cast<int>(threadIdx.x) >= WP * 8) return;
+  const int pj = threadIdx.x >> 3, pq = threadIdx.x & 7;
+  const int64_t o = ((static_cast<int64_t>(n) * Hp + 2 * k - 1) * WP + pj) * 32 + 4 * pq;
+  f4 best = *reinterpret_cast<const f4*>(pooled + o);
+  const uint32_t c0 = *reinterpret_cast<const uint32_t*>(arg + o);
+  int code[4] = {static_cast<int>(c0 & 0xFF), static_cast<int>((c0 >> 8) & 0xFF),
+                 static_cast<int>((c0 >> 16) & 0xFF), static_cast<int>(c0 >> 24)};
+  const f4 sv = side_v[b * (WP * 8) + threadIdx.x];
+  const uint32_t sc = side_c[b * (WP * 8) + threadIdx.x];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (sv[q] > best[q]) {
+      best[q] = sv[q];
+      code[q] = static_cast<int>((sc >> (8 * q)) & 0xFF);
+    }
+  *reinterpret_cast<f4*>(pooled + o) = best;
+  *reinterpret_cast<uint32_t*>(arg + o) = pack_codes(code);
+}
+
+template <int RT>
+bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled, uint8_t* arg,
+                   float* side, int64_t side_floats, int N, int H, int W, hipStream_t s) {
+  using P = PoolGeo<RT>;
+  if (W != P::W || H % 4 != 0 || H < 4) return false;
+  const int TY = H / 2, TX = W / 2;
+  const int64_t NT = static_cast<int64_t>(N) * TY * TX;
+  if (NT >= (1 << 22) || static_cast<int64_t>(N) * H * W * P::CIN * 4 > kMaxBufBytes) return false;
+  WinoArgs a{};
+  a.src = x;
+  a.w = w;
+  a.bias = b;
+  a.N = N; a.H = H; a.W = W;
+  a.TY = TY; a.TX = TX; a.NT = static_cast<int>(NT);
+  a.nranges = static_cast<int>(NT / RT);
+  a.rTX = 1.f / static_cast<float>(TX);
+  a.rTY = 1.f / static_cast<float>(TY);
+  a.wcin = P::CIN; a.wcout = P::COUT;
+  a.maxrows = P::ROWS;
+  a.runs = 1;
+  const int per_cu = std::max(1, std::min(3 * 4 / P::NW, static_cast<int>((160 * 1024) / (P::bytes + 256))));
+  const int G = std::max(1, std::min(a.nranges, 256 * per_cu));
+  const int WP = W / 2;
+  if (static_cast<int64_t>(G) * WP * 8 * 5 > side_floats) return false;
+  WinoPoolArgs pa{};
+  pa.c = a;
+  pa.pooled = pooled;
+  pa.arg = arg;
+  pa.side_v = reinterpret_cast<f4*>(side);
+  pa.side_c = reinterpret_cast<uint32_t*>(side + static_cast<int64_t>(G) * WP * 8 * 4);
+  auto kern = wino_conv_pool_kernel<RT>;
+  allow_lds_w(kern, P::bytes);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * P::NW), P::bytes, s, pa);
+  hipLaunchKernelGGL(wino_pool_fix_kernel, dim3(G), dim3(256), 0, s, pa.side_v, pa.side_c,
+                     pooled, arg, a.nranges, TY / 2, TY, WP);
+  return true;
+}
+
 
 // ------------------------------------------------------------ weight grad
 // Winograd F(2x2, 3x3) weight gradient.  With Z = A dY A^T (4x4 per 2x2 dY
@@ -1943,6 +2314,19 @@ int conv_wino_fault(int v) {
 bool wino_enabled() {
   static const bool on = env_int("SA_F32_WINO", 1) != 0;
   return on;
+}
+
+int64_t wino_conv_pool_side_floats(int W) { return int64_t{256} * 3 * (W / 2) * 8 * 5; }
+
+bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float* pooled,
+                           uint8_t* arg, float* side, int64_t side_floats, int N, int H, int W,
+                           hipStream_t s) {
+  static const bool on = env_int("SA_F32_WINO_POOL", 1) != 0;
+  if (!on) return false;
+  if (W == 48) return run_wino_pool<48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+  if (W == 32) return run_wino_pool<32>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+  if (W == 64) return run_wino_pool<64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+  return false;
 }
 
 bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {

@@ -299,15 +299,53 @@ def test_torso_f32_learner_scale_batch(cuda):
   assert rel_err(fa[-2:], ref) <= 1e-4
 
 
+@pytest.mark.parametrize('N,H,W,zero_w', [(256, 36, 48, False), (5, 36, 48, False),
+                                           (3, 16, 32, False), (2, 8, 64, False),
+                                           (7, 36, 48, True)])
+def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w):
+  """The 16 -> 32 stage head with the max-pool in the Winograd epilogue
+  (wino_conv_pool_kernel): pooled values and argmax codes bitwise those of
+  the Winograd conv followed by maxpool_fwd.  N = 256: long contiguous runs
+  per workgroup (the register carry between tile-row pairs); N = 5: one
+  range per workgroup, so every pooled odd row goes through the run-boundary
+  merge; zero weights: every tap ties, the first one must win everywhere."""
+  C = _C()
+  g = torch.Generator().manual_seed(11)
+  x = torch.randn(N, H, W, 16, generator=g).to(cuda)
+  w = (torch.zeros(3, 3, 16, 32) if zero_w else
+       torch.randn(3, 3, 16, 32, generator=g) / 12.0).to(cuda)
+  b = torch.randn(32, generator=g).to(cuda)
+  out = C.cf32_wino_conv_pool_fwd(x, w, b)
+  assert len(out) == 2
+  y, arg = out
+  conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
+  ry, rarg = C.cf32_maxpool_fwd(conv, 0, 0)
+  assert y.shape == ry.shape == (N, H // 2, W // 2, 32)
+  assert torch.equal(y, ry)
+  assert torch.equal(arg, rarg)
+  if zero_w:
+    assert int(arg.max()) == 0
+
+
+def test_wino_conv_pool_declines_other_shapes(cuda):
+  C = _C()
+  x = torch.randn(2, 18, 24, 32, device=cuda)  # stage 2 (32 -> 32): not covered
+  assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 32, 32, device=cuda),
+                                   torch.zeros(32, device=cuda)) == []
+  x = torch.randn(2, 42, 42, 16, device=cuda)  # Atari stage 1 (H % 4 != 0)
+  assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 16, 32, device=cuda),
+                                   torch.zeros(32, device=cuda)) == []
+
+
 def test_oversized_conv_call_fails_loudly(cuda):
   """A conv tensor of >= 4 GB (past the validated sizes) raises instead of
   running: the learner chunks such batches (ops/conv_f32.py MAX_FRAMES)."""
   C = _C()
-  x = torch.empty(19500, 36, 48, 16, device=cuda)  # 4.3 GB, never written
+  x = torch.empty(10000, 72, 96, 16, device=cuda)  # 4.4 GB, never written
   w = torch.zeros(3, 3, 16, 16, device=cuda)
   b = torch.zeros(16, device=cuda)
   with pytest.raises(RuntimeError, match='4 GB'):
-    C.cf32_conv_fwd(x, w, b, 1, 1, 1, 36, 48)
+    C.cf32_conv_fwd(x, w, b, 1, 1, 1, 72, 96)
   del x
 
 
