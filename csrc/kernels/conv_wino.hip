@@ -151,6 +151,8 @@ struct WinoArgs {
                // loads, 4 no LDS commit, 8 no stores
   int runs;    // 1: each workgroup walks a contiguous run of ranges (halo rows
                // shared with the previous range hit this CU's L2), 0: strided
+  int prio;    // SA_WINO_PRIO=1: waves NW/2.. run at s_setprio 1 (static
+               // priority for the second-dispatched half, MI355X_MICROARCH)
 };
 
 // Range walk of a persistent workgroup: a contiguous run [r, end) with step
@@ -278,6 +280,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   const RangeWalk rw = range_walk(a.nranges, a.runs);
   int r = rw.r;
   if (r >= rw.end) return;  // uniform: the whole workgroup leaves
+  if (a.prio && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
   // ---- register prefetch of a range's input rows.  Thread k-slot e of a
   // range always stages LDS element e = (row L, column, channel quad): the
@@ -543,6 +546,8 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   a.ablate = ablate;
   static const int runs = env_int("SA_WINO_RUNS", 1);
   a.runs = runs;
+  static const int prio = env_int("SA_WINO_PRIO", 0);
+  a.prio = prio;
   const int per_cu = std::max(1, std::min(WPS * 4 / NW, static_cast<int>((160 * 1024) / (bytes + 256))));
   static const int occ_env = env_int("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
@@ -1350,6 +1355,8 @@ struct WinoBwdArgs {
   int runs = 1;      // contiguous range runs (wino_bwd_fused_kernel; fused32 always)
   unsigned* err = nullptr;  // the device's sticky conv error word (rmsprop.hip guard)
   int fault = 0;     // fault injection: every hand-off wait reports a timeout
+  int prio = 0;      // SA_FUSED_PRIO: s_setprio 1 for the weight-gradient waves
+                     // (1) or the data-gradient waves (2)
 };
 
 // WWG: the weight gradient in Winograd form too (dL/dU = sum_tiles V(x) .*
@@ -1418,6 +1425,10 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
   const RangeWalk rw = range_walk(a.nranges, a.runs);
   int r = rw.r;
   if (r >= rw.end) return;
+  {
+    const int w0 = __builtin_amdgcn_readfirstlane(wave);
+    if ((a.prio == 1 && w0 >= NW / 2) || (a.prio == 2 && w0 < NW / 2)) __builtin_amdgcn_s_setprio(1);
+  }
 
   // staging slots: element e of both images = (row L, col, quad)
   int sl_L[MAXC], sl_o[MAXC];
@@ -1821,6 +1832,10 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   const int r_end = static_cast<int>((static_cast<int64_t>(blockIdx.x) + 1) * a.nranges / gridDim.x);
   int r = static_cast<int>(static_cast<int64_t>(blockIdx.x) * a.nranges / gridDim.x);
   if (r >= r_end) return;
+  {
+    const int w0 = __builtin_amdgcn_readfirstlane(wave);
+    if ((a.prio == 1 && w0 >= NW / 2) || (a.prio == 2 && w0 < NW / 2)) __builtin_amdgcn_s_setprio(1);
+  }
 
   // staging slots: element e = (row L, col, quad) of the dY image and of x
   int sy_L[MAXCY], sy_o[MAXCY], sx_L[MAXCX], sx_o[MAXCX];
@@ -2236,6 +2251,8 @@ bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const flo
   a.ablate = ablate;
   a.err = device_error_words() + 1;
   a.fault = g_wino_fault;
+  static const int fprio = env_int("SA_FUSED_PRIO", 0);
+  a.prio = fprio;
   auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
@@ -2295,6 +2312,8 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   a.relu_x = relu_x;
   static const int runs = env_int("SA_WINO_RUNS", 1);
   a.runs = runs;
+  static const int fprio = env_int("SA_FUSED_PRIO", 0);
+  a.prio = fprio;
   auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true, NW>
                      : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false, NW>;
   allow_lds_w(kern, bytes);
