@@ -717,9 +717,13 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
   __syncthreads();
   prefetch();
 
-  // pool-phase thread: pooled column pj, channel quad pq
-  const int pj = threadIdx.x >> 3, pq = threadIdx.x & 7;
-  const bool pooler = threadIdx.x < WP * 8;
+  // pool-phase thread: pooled column pj, channel quad pq; the first WP * 8
+  // threads own pooled row 2k (9 taps), the next WP * 8 the odd row 2k+1
+  // (its carried part + 3 taps of the next range, then 6 taps): balanced
+  const int pt = threadIdx.x % (WP * 8);
+  const int pj = pt >> 3, pq = pt & 7;
+  const bool even_row = threadIdx.x < WP * 8;
+  static_assert(2 * WP * 8 == 64 * NW, "two pooled rows x WP columns x 8 quads = the workgroup");
   constexpr float kNegInf = -__builtin_inff();
   f4 cv = {kNegInf, kNegInf, kNegInf, kNegInf};
   int cc[4] = {0, 0, 0, 0};
@@ -753,7 +757,7 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
     f4 acc[16];
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
-    {
+    if (!knob(a.ablate, 1)) {
       f4 d[16];
 #pragma unroll
       for (int dy = 0; dy < 4; ++dy)
@@ -809,13 +813,14 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx)
-          *reinterpret_cast<f4*>(img + ((2 * tyl + dy) * W + 2 * tx + dx) * IPP + co0 + 4 * g) =
-              Y[2 * dy + dx] + bv;
+          if (!knob(a.ablate, 32))
+            *reinterpret_cast<f4*>(img + ((2 * tyl + dy) * W + 2 * tx + dx) * IPP + co0 + 4 * g) =
+                Y[2 * dy + dx] + bv;
     }
     __syncthreads();
 
     // pool phase
-    if (pooler) {
+    if (!knob(a.ablate, 16)) {
       const int n = cur / KP, k = cur - n * KP;
       auto tap = [&](int row, int dx) -> f4 {
         return *reinterpret_cast<const f4*>(img + (row * W + 2 * pj + dx) * IPP + 4 * pq);
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
       const bool edge = 2 * pj + 2 >= W;  // the window's third column is padding
       const int64_t orow = static_cast<int64_t>(n) * Hp;
       // (a) pooled row 2k-1: the carried rows (4k-2, 4k-1) + pixel row 4k
-      if (cvalid || (cur == rfirst && k > 0)) {
+      if (!even_row && (cvalid || (cur == rfirst && k > 0))) {
         f4 best = cv;
         int code[4] = {cc[0], cc[1], cc[2], cc[3]};
         if (!cvalid) {
@@ -837,12 +842,12 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
           *reinterpret_cast<f4*>(pa.pooled + cdst) = best;
           *reinterpret_cast<uint32_t*>(pa.arg + cdst) = pack_codes(code);
         } else {  // the run's first range: the previous workgroup holds rows 4k-2, 4k-1
-          pa.side_v[blockIdx.x * (WP * 8) + threadIdx.x] = best;
-          pa.side_c[blockIdx.x * (WP * 8) + threadIdx.x] = pack_codes(code);
+          pa.side_v[blockIdx.x * (WP * 8) + pt] = best;
+          pa.side_c[blockIdx.x * (WP * 8) + pt] = pack_codes(code);
         }
       }
       // (b) pooled row 2k: pixel rows 4k .. 4k+2
-      {
+      if (even_row) {
         f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
         int code[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -855,7 +860,7 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
         *reinterpret_cast<uint32_t*>(pa.arg + o) = pack_codes(code);
       }
       // (c) pooled row 2k+1: pixel rows 4k+2, 4k+3 here, 4k+4 in the next range
-      {
+      if (!even_row) {
         f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
         int code[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -932,6 +937,8 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   a.wcin = P::CIN; a.wcout = P::COUT;
   a.maxrows = P::ROWS;
   a.runs = 1;
+  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_WINO_ABLATE", 0) : 0;
+  a.ablate = ablate;  // 1 no MFMA tasks, 16 no pool phase, 32 no image writes
   const int per_cu = std::max(1, std::min(3 * 4 / P::NW, static_cast<int>((160 * 1024) / (P::bytes + 256))));
   const int G = std::max(1, std::min(a.nranges, 256 * per_cu));
   const int WP = W / 2;

@@ -86,6 +86,17 @@ for name, H, W, Cc, Cy, res in [('res16 36x48', 36, 48, 16, 16, True),
   bflop = 2 * 2.0 * N * H * W * 9 * Cc * Cy  # dgrad + wgrad, direct-conv FLOPs
   print('%-26s bwd fused %8.1f us %6.1f TF | separate wgrad+dgrad %8.1f us %6.1f TF' % (
       name, tf, bflop / tf / 1e6, ts, bflop / ts / 1e6), flush=True)
+# stage-1 head forward: conv + maxpool_fwd vs the pool fused into the
+# Winograd epilogue (wino_conv_pool_kernel)
+if not ONLY or ONLY in 'head conv2 pool deep':
+  x = torch.randn(N, 36, 48, 16, device=dev)
+  w = torch.randn(3, 3, 16, 32, device=dev) * 0.1
+  b = torch.randn(32, device=dev)
+  tc = timeit(lambda: C.cf32_maxpool_fwd(C.cf32_conv_fwd(x, w, b, 1, 1, 1, 36, 48), 0, 0))
+  tfp = timeit(lambda: C.cf32_wino_conv_pool_fwd(x, w, b))
+  flop = 2.0 * N * 36 * 48 * 9 * 16 * 32
+  print('%-26s fwd+pool: conv + maxpool %8.1f us | fused %8.1f us %6.1f TF' % (
+      'head conv2 16->32 36x48', tc, tfp, flop / tfp / 1e6), flush=True)
 if ONLY:
   sys.exit(0)
 xp = torch.randn(N, 72, 96, 16, device=dev)
