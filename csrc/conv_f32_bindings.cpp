@@ -366,28 +366,34 @@ std::vector<at::Tensor> conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b, 
   return {y, arg};
 }
 
-// Deep stage head 16 -> 32 with the max-pool fused into the Winograd conv
-// (conv_wino.hip wino_conv_pool_kernel): {pooled, argmax}, or {} when the
-// shape is not covered (nothing ran; the caller takes conv + maxpool_fwd)
-std::vector<at::Tensor> wino_conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b) {
+// Deep stage head (16 -> 32, or 4 -> 16 on the stage-0 image) with the
+// max-pool fused into the Winograd conv (conv_wino.hip wino_conv_pool_kernel):
+// {pooled, argmax}, or {} when the shape is not covered (nothing ran; the
+// caller takes the other kernels)
+std::vector<at::Tensor> wino_conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tensor b,
+                                           int64_t stages) {
   check_nhwc(x, "x");
   check_w(w);
   TORCH_CHECK(x.scalar_type() == at::kFloat, "x must be float32");
   TORCH_CHECK(b.scalar_type() == at::kFloat && b.is_contiguous() && b.numel() == w.size(3), "bias");
-  if (w.size(0) != 3 || x.size(3) != 16 || w.size(2) != 16 || w.size(3) != 32) return {};
+  const int64_t Cin = x.size(3), Cout = w.size(3);
+  if (w.size(0) != 3 || w.size(2) != Cin || !((Cin == 16 && Cout == 32) || (Cin == 4 && Cout == 16)))
+    return {};
   const c10::DeviceGuard g(x.device());
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
   if (H % 4 != 0 || W % 2 != 0) return {};
-  auto y = at::empty({N, H / 2, W / 2, 32}, x.options());
+  auto y = at::empty({N, H / 2, W / 2, Cout}, x.options());
   check_size(y, "y");
   auto arg = at::empty(y.sizes(), x.options().dtype(at::kByte));
-  const int64_t sf = sa::cf32::wino_conv_pool_side_floats(static_cast<int>(W));
+  const int64_t sf = sa::cf32::wino_conv_pool_side_floats(static_cast<int>(W), static_cast<int>(Cout));
   auto side = at::empty({sf}, x.options());
   if (!sa::cf32::wino_conv_pool_launch(x.data_ptr<float>(), w.data_ptr<float>(),
                                        b.data_ptr<float>(), y.data_ptr<float>(),
                                        arg.data_ptr<uint8_t>(), side.data_ptr<float>(), sf,
                                        static_cast<int>(N), static_cast<int>(H),
-                                       static_cast<int>(W), stream()))
+                                       static_cast<int>(W), static_cast<int>(Cin),
+                                       static_cast<int>(Cout), static_cast<int>(stages),
+                                       stream()))
     return {};
   check_launch("cf32_wino_conv_pool_fwd");
   return {y, arg};
@@ -466,7 +472,8 @@ void register_conv_f32_ops(pybind11::module& m) {
         arg("dw"), arg("db") = pybind11::none(), arg("add") = pybind11::none(),
         arg("mask") = true);
   m.def("cf32_conv_pool_fwd", &conv_pool_fwd);
-  m.def("cf32_wino_conv_pool_fwd", &wino_conv_pool_fwd);
+  m.def("cf32_wino_conv_pool_fwd", &wino_conv_pool_fwd, arg("x"), arg("w"), arg("b"),
+        arg("stages") = -1);
   m.def("cf32_maxpool_fwd", &maxpool_fwd);
   m.def("cf32_maxpool_bwd", &maxpool_bwd);
   m.def("cf32_relu_mask_", &relu_mask_);

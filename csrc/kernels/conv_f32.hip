@@ -1340,17 +1340,26 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(
 // reference experiment.py:153-155), zero-padded to 4 channels: the torso's
 // first conv then stages one 16-B load per pixel instead of byte loads and
 // divisions in every tile (and its weight gradient reuses the same image).
+// uint8 frames [P pixels][Cs] -> the fp32 x / 255 image [P][4] (zero pad
+// channels).  x / 255 comes from a 256-entry table of the correctly rounded
+// quotients (computed in double: equal to the fp32 IEEE division for every
+// byte), so the image is bitwise torch's / the reference's to_float / 255
+// (experiment.py:153); the compiler's default fp32 division on gfx950 is
+// not correctly rounded.
 __global__ __launch_bounds__(256) void frames_f32_kernel(const uint8_t* __restrict__ x,
                                                          f4* __restrict__ y, int64_t P,
                                                          int Cs) {
+  __shared__ float lut[256];
+  lut[threadIdx.x] = static_cast<float>(static_cast<double>(threadIdx.x) / 255.0);
+  __syncthreads();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < P; i += stride) {
     const uint8_t* p = x + i * Cs;
     f4 v = {0.f, 0.f, 0.f, 0.f};
-    v[0] = static_cast<float>(p[0]) / 255.f;
-    if (Cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
-    if (Cs > 2) v[2] = static_cast<float>(p[2]) / 255.f;
-    if (Cs > 3) v[3] = static_cast<float>(p[3]) / 255.f;
+    v[0] = lut[p[0]];
+    if (Cs > 1) v[1] = lut[p[1]];
+    if (Cs > 2) v[2] = lut[p[2]];
+    if (Cs > 3) v[3] = lut[p[3]];
     y[i] = v;
   }
 }

@@ -579,43 +579,51 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
 
-// ------------------------------------------------------- fused stage head
-// Stage-head conv (16 -> 32 channels, 3x3/1 SAME + bias) with the following
-// 3x3/2 SAME max-pool and its argmax fused into the epilogue (reference
+// ------------------------------------------------------- fused stage heads
+// Deep-torso stage head (3x3/1 SAME conv + bias) with the following 3x3/2
+// SAME max-pool and its argmax fused into the epilogue (reference
 // experiment.py:160-163: conv -> max_pool), so the pre-pool map exists only
-// in LDS.  Needs H % 4 == 0 and a pooled pad-before of 0 (even H, W).  Each
+// in LDS: stage 0 (4-channel fp32 image -> 16, 72x96) and stage 1 (16 -> 32,
+// 36x48).  Needs H % 4 == 0 and a pooled pad-before of 0 (even H, W).  Each
 // range is the tile-row pair (2k, 2k+1) of one image (RT = W tiles: pixel
 // rows 4k..4k+3), one 16-tile x 16-channel task per wave.  The epilogue writes
 // Y + b into an LDS image of those 4 rows (aliasing the staged input rows,
 // which every wave has finished reading); the pool phase (thread = pooled
-// column x channel quad) then stores pooled row 2k (pixel rows 4k..4k+2) and
-// keeps the rows-(4k+2, 4k+3) part of pooled row 2k+1 in registers until
-// the next range - the same workgroup's, since each walks a contiguous run -
-// adds pixel row 4k+4.  A run's first range (k > 0) leaves its top-row part
-// in `side`, the run's last carry is stored as is, and wino_pool_fix_kernel
-// merges those pairs afterwards.  Values and argmax codes are bitwise those
-// of the conv + maxpool_fwd_kernel pair (strict >, taps in row-major window
-// order: the first maximal tap wins).
+// column x channel quad; one half of the workgroup per pooled row) then
+// stores pooled row 2k (pixel rows 4k..4k+2) and keeps the rows-(4k+2, 4k+3)
+// part of pooled row 2k+1 in registers until the next range - the same
+// workgroup's, since each walks a contiguous run - adds pixel row 4k+4.  A
+// run's first range (k > 0) leaves its top-row part in `side`, the run's last
+// carry is stored as is, and wino_pool_fix_kernel merges those pairs
+// afterwards.  Values and argmax codes are bitwise those of the Winograd conv
+// + maxpool_fwd_kernel pair (strict >, taps in row-major window order: the
+// first maximal tap wins).
+//
+// CIN == 4 (stage 0: RGB + a zero channel): the MFMA's k = 4 input channels
+// are the lane groups g, so a lane transforms ONE channel of its tile's 4x4
+// patch (scalar B^T d B) and each xi is one MFMA; CIN == 16 as
+// wino_conv_kernel (4 channels per lane, 4 k-steps per xi).
 struct WinoPoolArgs {
   WinoArgs c;
-  float* pooled;     // [N, H/2, W/2, 32]
-  uint8_t* arg;      // [N, H/2, W/2, 32] tap codes dy * 3 + dx
-  f4* side_v;        // [G][W/2 * 8] top-row parts of the run-start ranges
-  uint32_t* side_c;  // [G][W/2 * 8] their codes (4 x 8 bits)
+  float* pooled;     // [N, H/2, W/2, COUT]
+  uint8_t* arg;      // [N, H/2, W/2, COUT] tap codes dy * 3 + dx
+  f4* side_v;        // [G][W/2 * COUT/4] top-row parts of the run-start ranges
+  uint32_t* side_c;  // [G][W/2 * COUT/4] their codes (4 x 8 bits)
 };
 
-template <int RT>
+template <int CIN_, int COUT_, int RT>
 struct PoolGeo {
-  static constexpr int CIN = 16, COUT = 32;
-  static constexpr int W = RT;              // one tile-row pair = RT tiles
-  static constexpr int NW = RT / 8;         // NG = RT / 16 groups x 2 slices
-  static constexpr int PP = CIN + 4;        // staged pixel pitch (floats)
-  static constexpr int IPP = COUT + 4;      // pre-pool image pixel pitch
-  static constexpr int ROWS = 6;            // staged input rows per range
+  static constexpr int CIN = CIN_, COUT = COUT_;
+  static constexpr int W = RT;                      // one tile-row pair = RT tiles
+  static constexpr int NW = (RT / 16) * (COUT / 16);  // one task per wave
+  static constexpr int PP = CIN == 4 ? 4 : CIN + 4;  // staged pixel pitch (floats)
+  static constexpr int IPP = COUT + 4;               // pre-pool image pixel pitch
+  static constexpr int ROWS = 6;                     // staged input rows per range
   static constexpr int XREG = (ROWS * (W + 2) * PP > 4 * W * IPP) ? ROWS * (W + 2) * PP
                                                                    : 4 * W * IPP;
   static constexpr int MAXC = (ROWS * (W + 2) * (CIN / 4) + 64 * NW - 1) / (64 * NW);
-  static constexpr int WP = W / 2;          // pooled width
+  static constexpr int WP = W / 2;                   // pooled width
+  static constexpr int CQ = COUT / 4;                // channel quads
   static constexpr size_t bytes = sizeof(float) * (16 * CIN * COUT + XREG + ROWS);
 };
 
@@ -632,24 +640,27 @@ __device__ __forceinline__ uint32_t pack_codes(const int (&code)[4]) {
          (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
 }
 
-template <int RT>
-__global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs pa) {
-  using P = PoolGeo<RT>;
-  constexpr int CIN = P::CIN, COUT = P::COUT, W = P::W, NW = P::NW, NTH = 64 * NW;
-  constexpr int PP = P::PP, IPP = P::IPP, MAXC = P::MAXC, WP = P::WP;
-  constexpr int C4 = CIN / 4, LC4 = 2;
+template <int CIN, int COUT, int RT>
+__global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
+    WinoPoolArgs pa) {
+  using P = PoolGeo<CIN, COUT, RT>;
+  constexpr int W = P::W, NW = P::NW, NTH = 64 * NW;
+  constexpr int PP = P::PP, IPP = P::IPP, MAXC = P::MAXC, WP = P::WP, CQ = P::CQ;
+  constexpr int C4 = CIN / 4, LC4 = C4 == 4 ? 2 : 0;
   constexpr int NG = RT / 16;
-  constexpr int USTR = 4 * COUT * 4;  // floats per xi in U_s (one ci block)
   constexpr int Wl = W + 2, rowstr = Wl * PP;
-  static_assert(NG * (COUT / 16) == NW && RT % 16 == 0 && MAXC <= 32, "shape");
+  static_assert(CIN == 4 || CIN == 16, "CIN");
+  static_assert(NW * 64 == 2 * WP * CQ, "two pooled rows x WP columns x CQ quads = the workgroup");
+  static_assert(RT % 16 == 0 && MAXC <= 32, "shape");
   const WinoArgs& a = pa.c;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* U_s = smem;                    // [16 xi][4 g][COUT][4]
+  // U: CIN 16 [16 xi][4 g][COUT][4 v] (f4 A fragments), CIN 4 [16 xi][4 ci][COUT]
+  float* U_s = smem;
   float* x_s = smem + 16 * CIN * COUT;  // staged rows [6][Wl][PP], then the image [4][W][IPP]
   float* img = x_s;
   int* tab_s = reinterpret_cast<int*>(x_s + P::XREG);  // [6]
 
-  // U = G g G^T (forward weights HWIO [3][3][16][32])
+  // U = G g G^T (forward weights HWIO [3][3][CIN][COUT])
   for (int e = threadIdx.x; e < CIN * COUT; e += NTH) {
     const int co = e % COUT, ci = e / COUT;
     float gk[3][3];
@@ -665,14 +676,18 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
       t[2][kx] = 0.5f * ((gk[0][kx] - gk[1][kx]) + gk[2][kx]);
       t[3][kx] = gk[2][kx];
     }
-    const int gq = (ci >> 2) & 3, v = ci & 3;
 #pragma unroll
     for (int ra = 0; ra < 4; ++ra) {
       const float u[4] = {t[ra][0], 0.5f * ((t[ra][0] + t[ra][1]) + t[ra][2]),
                           0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-        U_s[(4 * ra + rb) * USTR + (gq * COUT + co) * 4 + v] = u[rb];
+      for (int rb = 0; rb < 4; ++rb) {
+        const int xi = 4 * ra + rb;
+        if constexpr (CIN == 16)
+          U_s[xi * (16 * COUT) + (((ci >> 2) & 3) * COUT + co) * 4 + (ci & 3)] = u[rb];
+        else
+          U_s[(xi * 4 + ci) * COUT + co] = u[rb];
+      }
     }
   }
 
@@ -717,13 +732,12 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
   __syncthreads();
   prefetch();
 
-  // pool-phase thread: pooled column pj, channel quad pq; the first WP * 8
-  // threads own pooled row 2k (9 taps), the next WP * 8 the odd row 2k+1
-  // (its carried part + 3 taps of the next range, then 6 taps): balanced
-  const int pt = threadIdx.x % (WP * 8);
-  const int pj = pt >> 3, pq = pt & 7;
-  const bool even_row = threadIdx.x < WP * 8;
-  static_assert(2 * WP * 8 == 64 * NW, "two pooled rows x WP columns x 8 quads = the workgroup");
+  // pool-phase thread: pooled column pj, channel quad pq; the first WP * CQ
+  // threads own pooled row 2k (9 taps), the rest the odd row 2k+1 (its
+  // carried part + 3 taps of the next range, then 6 taps): balanced
+  const int pt = threadIdx.x % (WP * CQ);
+  const int pj = pt / CQ, pq = pt % CQ;
+  const bool even_row = threadIdx.x < WP * CQ;
   constexpr float kNegInf = -__builtin_inff();
   f4 cv = {kNegInf, kNegInf, kNegInf, kNegInf};
   int cc[4] = {0, 0, 0, 0};
@@ -735,8 +749,9 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
   const int co0 = sl * 16;
   const int txl = 16 * grp + c16;  // tile within the range = (row txl / (W/2), column)
   const int tyl = txl / (W / 2), tx = txl - tyl * (W / 2);
-  const float* xp = x_s + (2 * tyl * Wl + 2 * tx) * PP + 4 * g;
-  const float* up = U_s + (g * COUT + co0 + c16) * 4;
+  // CIN 16: 4 channels 4g.. of each patch pixel; CIN 4: channel g
+  const float* xp = x_s + (2 * tyl * Wl + 2 * tx) * PP + (CIN == 16 ? 4 * g : g);
+  const float* up = CIN == 16 ? U_s + (g * COUT + co0 + c16) * 4 : U_s + g * COUT + co0 + c16;
   const f4 bv = *reinterpret_cast<const f4*>(a.bias + co0 + 4 * g);
 
   for (;;) {
@@ -758,39 +773,69 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
     if (!knob(a.ablate, 1)) {
-      f4 d[16];
+      if constexpr (CIN == 16) {
+        constexpr int USTR = 16 * COUT;  // floats per xi
+        f4 d[16];
 #pragma unroll
-      for (int dy = 0; dy < 4; ++dy)
+        for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
-        for (int dx = 0; dx < 4; ++dx)
-          d[4 * dy + dx] = *reinterpret_cast<const f4*>(xp + dy * rowstr + dx * PP);
-      f4 s[16];
+          for (int dx = 0; dx < 4; ++dx)
+            d[4 * dy + dx] = *reinterpret_cast<const f4*>(xp + dy * rowstr + dx * PP);
+        f4 s[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        s[q] = d[q] - d[8 + q];
-        s[4 + q] = d[4 + q] + d[8 + q];
-        s[8 + q] = d[8 + q] - d[4 + q];
-        s[12 + q] = d[4 + q] - d[12 + q];
-      }
-      f4 V[16];
+        for (int q = 0; q < 4; ++q) {
+          s[q] = d[q] - d[8 + q];
+          s[4 + q] = d[4 + q] + d[8 + q];
+          s[8 + q] = d[8 + q] - d[4 + q];
+          s[12 + q] = d[4 + q] - d[12 + q];
+        }
+        f4 V[16];
 #pragma unroll
-      for (int ra = 0; ra < 4; ++ra) {
-        V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
-        V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
-        V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
-        V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
-      }
+        for (int ra = 0; ra < 4; ++ra) {
+          V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
+          V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
+          V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
+          V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
+        }
 #pragma unroll
-      for (int xp2 = 0; xp2 < 8; ++xp2) {
-        f4 ua[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          ua[q] = *reinterpret_cast<const f4*>(up + (2 * xp2 + q) * USTR);
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
+        for (int xp2 = 0; xp2 < 8; ++xp2) {
+          f4 ua[2];
 #pragma unroll
           for (int q = 0; q < 2; ++q)
-            acc[2 * xp2 + q] = mfma4(ua[q][v], V[2 * xp2 + q][v], acc[2 * xp2 + q]);
+            ua[q] = *reinterpret_cast<const f4*>(up + (2 * xp2 + q) * USTR);
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              acc[2 * xp2 + q] = mfma4(ua[q][v], V[2 * xp2 + q][v], acc[2 * xp2 + q]);
+        }
+      } else {
+        float d[16];
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 4; ++dx) d[4 * dy + dx] = xp[dy * rowstr + dx * PP];
+        float s[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s[q] = d[q] - d[8 + q];
+          s[4 + q] = d[4 + q] + d[8 + q];
+          s[8 + q] = d[8 + q] - d[4 + q];
+          s[12 + q] = d[4 + q] - d[12 + q];
+        }
+        float V[16];
+#pragma unroll
+        for (int ra = 0; ra < 4; ++ra) {
+          V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
+          V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
+          V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
+          V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
+        }
+        float ua[16];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) ua[xi] = up[xi * 4 * COUT];
+#pragma unroll
+        for (int xi = 0; xi < 16; ++xi) acc[xi] = mfma4(ua[xi], V[xi], acc[xi]);
       }
     }
     __syncthreads();  // every wave's patch reads are done: x_s becomes the image
@@ -842,8 +887,8 @@ __global__ __launch_bounds__(8 * RT, 3) void wino_conv_pool_kernel(WinoPoolArgs 
           *reinterpret_cast<f4*>(pa.pooled + cdst) = best;
           *reinterpret_cast<uint32_t*>(pa.arg + cdst) = pack_codes(code);
         } else {  // the run's first range: the previous workgroup holds rows 4k-2, 4k-1
-          pa.side_v[blockIdx.x * (WP * 8) + pt] = best;
-          pa.side_c[blockIdx.x * (WP * 8) + pt] = pack_codes(code);
+          pa.side_v[blockIdx.x * (WP * CQ) + pt] = best;
+          pa.side_c[blockIdx.x * (WP * CQ) + pt] = pack_codes(code);
         }
       }
       // (b) pooled row 2k: pixel rows 4k .. 4k+2
@@ -894,19 +939,21 @@ __global__ __launch_bounds__(256) void wino_pool_fix_kernel(const f4* __restrict
                                                             const uint32_t* __restrict__ side_c,
                                                             float* __restrict__ pooled,
                                                             uint8_t* __restrict__ arg,
-                                                            int nranges, int KP, int Hp, int WP) {
+                                                            int nranges, int KP, int Hp, int WP,
+                                                            int COUT) {
   const int b = blockIdx.x;
   const int r = static_cast<int>(static_cast<int64_t>(b) * nranges / gridDim.x);
   const int n = r / KP, k = r - n * KP;
-  if (k == 0 || static_cast<int>(threadIdx.x) >= WP * 8) return;
-  const int pj = threadIdx.x >> 3, pq = threadIdx.x & 7;
-  const int64_t o = ((static_cast<int64_t>(n) * Hp + 2 * k - 1) * WP + pj) * 32 + 4 * pq;
+  const int CQ = COUT / 4;
+  if (k == 0 || static_cast<int>(threadIdx.x) >= WP * CQ) return;
+  const int pj = threadIdx.x / CQ, pq = threadIdx.x - pj * CQ;
+  const int64_t o = ((static_cast<int64_t>(n) * Hp + 2 * k - 1) * WP + pj) * COUT + 4 * pq;
   f4 best = *reinterpret_cast<const f4*>(pooled + o);
   const uint32_t c0 = *reinterpret_cast<const uint32_t*>(arg + o);
   int code[4] = {static_cast<int>(c0 & 0xFF), static_cast<int>((c0 >> 8) & 0xFF),
                  static_cast<int>((c0 >> 16) & 0xFF), static_cast<int>(c0 >> 24)};
-  const f4 sv = side_v[b * (WP * 8) + threadIdx.x];
-  const uint32_t sc = side_c[b * (WP * 8) + threadIdx.x];
+  const f4 sv = side_v[b * (WP * CQ) + threadIdx.x];
+  const uint32_t sc = side_c[b * (WP * CQ) + threadIdx.x];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (sv[q] > best[q]) {
@@ -917,14 +964,16 @@ __global__ __launch_bounds__(256) void wino_pool_fix_kernel(const f4* __restrict
   *reinterpret_cast<uint32_t*>(arg + o) = pack_codes(code);
 }
 
-template <int RT>
+template <int CIN, int COUT, int RT>
 bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled, uint8_t* arg,
                    float* side, int64_t side_floats, int N, int H, int W, hipStream_t s) {
-  using P = PoolGeo<RT>;
+  using P = PoolGeo<CIN, COUT, RT>;
   if (W != P::W || H % 4 != 0 || H < 4) return false;
   const int TY = H / 2, TX = W / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
-  if (NT >= (1 << 22) || static_cast<int64_t>(N) * H * W * P::CIN * 4 > kMaxBufBytes) return false;
+  // integer range / tile index math throughout (no fdivi): int32 bounds only
+  if (NT >= (int64_t{1} << 30) || static_cast<int64_t>(N) * H * W * CIN * 4 > kMaxBufBytes)
+    return false;
   WinoArgs a{};
   a.src = x;
   a.w = w;
@@ -934,26 +983,30 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   a.nranges = static_cast<int>(NT / RT);
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
-  a.wcin = P::CIN; a.wcout = P::COUT;
+  a.wcin = CIN; a.wcout = COUT;
   a.maxrows = P::ROWS;
   a.runs = 1;
   static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_WINO_ABLATE", 0) : 0;
   a.ablate = ablate;  // 1 no MFMA tasks, 16 no pool phase, 32 no image writes
-  const int per_cu = std::max(1, std::min(3 * 4 / P::NW, static_cast<int>((160 * 1024) / (P::bytes + 256))));
+  // workgroups per CU: LDS-bound, capped at 3 waves per SIMD unless
+  // SA_WINO_POOL_OCC asks for another count (sweeps)
+  static const int occ = env_int("SA_WINO_POOL_OCC", 0);
+  const int lds_cu = static_cast<int>((160 * 1024) / (P::bytes + 256));
+  const int per_cu = std::max(1, std::min(occ > 0 ? occ : 3 * 4 / P::NW, lds_cu));
   const int G = std::max(1, std::min(a.nranges, 256 * per_cu));
-  const int WP = W / 2;
-  if (static_cast<int64_t>(G) * WP * 8 * 5 > side_floats) return false;
+  const int side_n = (W / 2) * P::CQ;
+  if (static_cast<int64_t>(G) * side_n * 5 > side_floats) return false;
   WinoPoolArgs pa{};
   pa.c = a;
   pa.pooled = pooled;
   pa.arg = arg;
   pa.side_v = reinterpret_cast<f4*>(side);
-  pa.side_c = reinterpret_cast<uint32_t*>(side + static_cast<int64_t>(G) * WP * 8 * 4);
-  auto kern = wino_conv_pool_kernel<RT>;
+  pa.side_c = reinterpret_cast<uint32_t*>(side + static_cast<int64_t>(G) * side_n * 4);
+  auto kern = wino_conv_pool_kernel<CIN, COUT, RT>;
   allow_lds_w(kern, P::bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * P::NW), P::bytes, s, pa);
   hipLaunchKernelGGL(wino_pool_fix_kernel, dim3(G), dim3(256), 0, s, pa.side_v, pa.side_c,
-                     pooled, arg, a.nranges, TY / 2, TY, WP);
+                     pooled, arg, a.nranges, TY / 2, TY, W / 2, COUT);
   return true;
 }
 
@@ -2342,16 +2395,27 @@ bool wino_enabled() {
   return on;
 }
 
-int64_t wino_conv_pool_side_floats(int W) { return int64_t{256} * 3 * (W / 2) * 8 * 5; }
+int64_t wino_conv_pool_side_floats(int W, int Cout) {
+  return int64_t{256} * 8 * (W / 2) * (Cout / 4) * 5;  // up to 8 workgroups per CU
+}
 
 bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float* pooled,
                            uint8_t* arg, float* side, int64_t side_floats, int N, int H, int W,
-                           hipStream_t s) {
-  static const bool on = env_int("SA_F32_WINO_POOL", 1) != 0;
-  if (!on) return false;
-  if (W == 48) return run_wino_pool<48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
-  if (W == 32) return run_wino_pool<32>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
-  if (W == 64) return run_wino_pool<64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+                           int Cin, int Cout, int stages, hipStream_t s) {
+  // bit 0: stage 1, bit 1: stage 0 (stage 0: 412 vs 529 us for the direct
+  // conv+pool, 10.02 -> 9.93 ms per step); stages >= 0 overrides the
+  // environment (tests)
+  static const int env_on = env_int("SA_F32_WINO_POOL", 3);
+  const int on = stages >= 0 ? stages : env_on;
+  if (Cin == 16 && Cout == 32 && (on & 1)) {
+    if (W == 48) return run_wino_pool<16, 32, 48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    if (W == 32) return run_wino_pool<16, 32, 32>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    if (W == 64) return run_wino_pool<16, 32, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+  }
+  if (Cin == 4 && Cout == 16 && (on & 2)) {
+    if (W == 96) return run_wino_pool<4, 16, 96>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    if (W == 64) return run_wino_pool<4, 16, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+  }
   return false;
 }
 

@@ -135,10 +135,12 @@ class _DeepTorsoF32(torch.autograd.Function):
       H, W = x.shape[1], x.shape[2]
       pbh = layers.same_pads(H, 3, 2)[0]
       pbw = layers.same_pads(W, 3, 2)[0]
-      fused = C.cf32_wino_conv_pool_fwd(x, w, b) if s > 0 else []
+      fused = (C.cf32_wino_conv_pool_fwd(x, w, b) if x.dtype == torch.float32
+               else [])
       if fused:
-        # 16 -> 32 head with the pool in the Winograd epilogue (the
-        # pre-pool map only in LDS); other shapes: conv + maxpool_fwd
+        # stage 0 (4-channel image -> 16) and stage 1 (16 -> 32) heads
+        # with the pool in the Winograd epilogue (the pre-pool map only in
+        # LDS); other shapes: the direct conv+pool or conv + maxpool_fwd
         xa, arg = fused
       elif s in FUSED_POOL_STAGES:
         xa, arg = C.cf32_conv_pool_fwd(x, w, b, pbh, pbw)

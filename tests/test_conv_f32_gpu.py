@@ -327,6 +327,43 @@ def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w):
     assert int(arg.max()) == 0
 
 
+@pytest.mark.parametrize('N,H,W,zero_w', [(6, 72, 96, False), (120, 72, 96, False),
+                                           (3, 8, 64, False), (5, 72, 96, True)])
+def test_wino_conv_pool_stage0_matches_float64(cuda, N, H, W, zero_w):
+  """Stage-0 head (4-channel image -> 16) with the pool in the Winograd
+  epilogue against the float64 conv + 3x3/2 max-pool: values to fp32
+  rounding, argmax codes wherever the float64 window has a clear maximum
+  (gap > 1e-5: elsewhere fp32 and float64 may legitimately pick another
+  tap); zero weights: every tap ties and the first must win."""
+  C = _C()
+  g = torch.Generator().manual_seed(13)
+  x = torch.rand(N, H, W, 4, generator=g)
+  x[..., 3] = 0  # the image's pad channel
+  w = (torch.zeros(3, 3, 4, 16) if zero_w else
+       torch.randn(3, 3, 4, 16, generator=g) / 6.0)
+  w[:, :, 3] = 0
+  b = torch.randn(16, generator=g) * 0.1
+  # stage 0 is opt-in (SA_F32_WINO_POOL bit 1): enabled explicitly here
+  out = C.cf32_wino_conv_pool_fwd(x.to(cuda), w.to(cuda), b.to(cuda), stages=3)
+  assert len(out) == 2
+  y, arg = out[0].cpu().double(), out[1].cpu().long()
+  conv = layers.conv2d_same_nhwc(x.double(), w.double(), b.double(), 1)
+  # windows (3x3, stride 2, pad-before 0, -inf beyond the bottom/right edge)
+  cp = torch.nn.functional.pad(conv.permute(0, 3, 1, 2), (0, 1, 0, 1), value=float('-inf'))
+  win = cp.unfold(2, 3, 2).unfold(3, 3, 2)            # [N, C, Hp, Wp, 3, 3]
+  win = win.reshape(*win.shape[:4], 9).permute(0, 2, 3, 1, 4)  # [N, Hp, Wp, C, 9]
+  ref = win.max(-1).values
+  first = (win == ref.unsqueeze(-1)).double().argmax(-1)       # first maximal tap
+  assert rel_err(y, ref) <= 1e-5
+  top2 = win.topk(2, dim=-1).values
+  clear = (top2[..., 0] - top2[..., 1]) > 1e-5 * ref.abs().max()
+  assert torch.equal(arg[clear], first[clear])
+  if zero_w:
+    assert int(arg.max()) == 0
+  else:
+    assert clear.float().mean() > 0.99
+
+
 def test_wino_conv_pool_declines_other_shapes(cuda):
   C = _C()
   x = torch.randn(2, 18, 24, 32, device=cuda)  # stage 2 (32 -> 32): not covered
@@ -335,6 +372,29 @@ def test_wino_conv_pool_declines_other_shapes(cuda):
   x = torch.randn(2, 42, 42, 16, device=cuda)  # Atari stage 1 (H % 4 != 0)
   assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 16, 32, device=cuda),
                                    torch.zeros(32, device=cuda)) == []
+
+
+@pytest.mark.parametrize('shape', [(3232 // 101, 72, 96, 3), (3, 5, 7, 3), (2, 84, 84, 4),
+                                   (3, 5, 7, 1), (2, 6, 5, 2)])
+@pytest.mark.parametrize('misaligned', [False, True])
+def test_frames_f32_is_exact_division(cuda, shape, misaligned):
+  """uint8 frames -> the 4-channel fp32 x / 255 image: bitwise torch's
+  correctly rounded division, zero pad channels, any pixel count (tail) and
+  a frame pointer that is not word aligned."""
+  C = _C()
+  g = torch.Generator().manual_seed(17)
+  n = 1
+  for d in shape:
+    n *= d
+  buf = torch.randint(0, 256, (n + 1,), generator=g, dtype=torch.uint8).to(cuda)
+  fr = (buf[1:] if misaligned else buf[:n]).view(shape)
+  y = C.cf32_frames_f32(fr).cpu()
+  # correctly rounded fp32 quotients (the reference's IEEE division; the
+  # GPU torch scalar division multiplies by a rounded reciprocal instead)
+  table = (torch.arange(256, dtype=torch.float64) / 255.0).float()
+  ref = torch.zeros(shape[:3] + (4,))
+  ref[..., :shape[3]] = table[fr.cpu().long()]
+  assert y.shape == ref.shape and torch.equal(y, ref)
 
 
 def test_oversized_conv_call_fails_loudly(cuda):
