@@ -377,11 +377,12 @@ std::vector<at::Tensor> wino_conv_pool_fwd(at::Tensor x, at::Tensor w, at::Tenso
   TORCH_CHECK(x.scalar_type() == at::kFloat, "x must be float32");
   TORCH_CHECK(b.scalar_type() == at::kFloat && b.is_contiguous() && b.numel() == w.size(3), "bias");
   const int64_t Cin = x.size(3), Cout = w.size(3);
-  if (w.size(0) != 3 || w.size(2) != Cin || !((Cin == 16 && Cout == 32) || (Cin == 4 && Cout == 16)))
+  if (w.size(0) != 3 || w.size(2) != Cin ||
+      !((Cin == 16 && Cout == 32) || (Cin == 4 && Cout == 16) || (Cin == 32 && Cout == 32)))
     return {};
   const c10::DeviceGuard g(x.device());
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
-  if (H % 4 != 0 || W % 2 != 0) return {};
+  if (H % 2 != 0 || W % 2 != 0) return {};
   auto y = at::empty({N, H / 2, W / 2, Cout}, x.options());
   check_size(y, "y");
   auto arg = at::empty(y.sizes(), x.options().dtype(at::kByte));

@@ -1010,6 +1010,251 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   return true;
 }
 
+// Stage-2 head (32 -> 32 at 18x24 -> 9x12): its 9 tile rows per image are
+// odd, so tile-row pairs would straddle images; here a range is one WHOLE
+// image (108 tiles, padded to 7 groups of 16), every pooled window lies
+// inside it, and no carry or fix-up is needed.  The 20 staged input rows
+// (75 KB) and U (64 KB) leave one workgroup per CU; 7 waves take the 14
+// (group, 16-channel slice) tasks two each, hold each task's A^T M A in
+// registers until every wave has read its patches, then write the image.
+template <int CIN, int COUT, int H, int W>
+struct PoolImgGeo {
+  static constexpr int TY = H / 2, TX = W / 2, NTI = TY * TX;
+  static constexpr int RT = (NTI + 15) / 16 * 16;
+  static constexpr int NG = RT / 16, NS = COUT / 16, NTASK = NG * NS;
+  static constexpr int NW = (NTASK + 1) / 2;        // two tasks per wave
+  static constexpr int ROWS = H + 2, Wl = W + 2;
+  static constexpr int PP = CIN + 4, IPP = COUT + 4;
+  static constexpr int XREG = (ROWS * Wl * PP > H * W * IPP) ? ROWS * Wl * PP : H * W * IPP;
+  static constexpr int MAXC = (ROWS * Wl * (CIN / 4) + 64 * NW - 1) / (64 * NW);
+  static constexpr size_t bytes = sizeof(float) * (16 * CIN * COUT + XREG + ROWS);
+};
+
+template <int CIN, int COUT, int H, int W>
+__global__ __launch_bounds__(448, 1) void wino_conv_pool_img_kernel(WinoPoolArgs pa) {
+  using P = PoolImgGeo<CIN, COUT, H, W>;
+  constexpr int TX = P::TX, NTI = P::NTI, NG = P::NG, NTASK = P::NTASK, NW = P::NW;
+  constexpr int NTH = 64 * NW, ROWS = P::ROWS, Wl = P::Wl, PP = P::PP, IPP = P::IPP;
+  constexpr int MAXC = P::MAXC, C4 = CIN / 4, LC4 = C4 == 8 ? 3 : 2, NB = CIN / 16;
+  constexpr int USTR = NB * 4 * COUT * 4, rowstr = Wl * PP;
+  constexpr int Hp = H / 2, Wp = W / 2, CQ = COUT / 4;
+  static_assert(NTH == 448 && CIN % 16 == 0 && H % 2 == 0 && W % 2 == 0 && MAXC <= 32, "shape");
+  const WinoArgs& a = pa.c;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* U_s = smem;                    // [16 xi][NB][4 g][COUT][4]
+  float* x_s = smem + 16 * CIN * COUT;  // staged rows [ROWS][Wl][PP], then the image [H][W][IPP]
+  float* img = x_s;
+  int* tab_s = reinterpret_cast<int*>(x_s + P::XREG);
+
+  for (int e = threadIdx.x; e < CIN * COUT; e += NTH) {
+    const int co = e % COUT, ci = e / COUT;
+    float gk[3][3];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) gk[ky][kx] = a.w[((ky * 3 + kx) * CIN + ci) * COUT + co];
+    float t[4][3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      t[0][kx] = gk[0][kx];
+      t[1][kx] = 0.5f * ((gk[0][kx] + gk[1][kx]) + gk[2][kx]);
+      t[2][kx] = 0.5f * ((gk[0][kx] - gk[1][kx]) + gk[2][kx]);
+      t[3][kx] = gk[2][kx];
+    }
+    const int b = ci >> 4, gq = (ci >> 2) & 3, v = ci & 3;
+#pragma unroll
+    for (int ra = 0; ra < 4; ++ra) {
+      const float u[4] = {t[ra][0], 0.5f * ((t[ra][0] + t[ra][1]) + t[ra][2]),
+                          0.5f * ((t[ra][0] - t[ra][1]) + t[ra][2]), t[ra][2]};
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        U_s[(4 * ra + rb) * USTR + ((b * 4 + gq) * COUT + co) * 4 + v] = u[rb];
+    }
+  }
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const RangeWalk rw = range_walk(a.nranges, 1);  // a range = one image
+  int r = rw.r;
+  if (r >= rw.end) return;
+
+  int sl_L[MAXC], sl_x[MAXC];
+#pragma unroll
+  for (int k = 0; k < MAXC; ++k) {
+    const int e = threadIdx.x + k * NTH;
+    const int ch = e & (C4 - 1), pix = e >> LC4;
+    const int L = pix / Wl, col = pix - L * Wl;
+    sl_L[k] = L < ROWS ? L : -1;
+    sl_x[k] = (col >= 1 && col <= W) ? (col - 1) * CIN + 4 * ch : -1;
+  }
+  auto build_tab = [&](int n) {
+    const int L = threadIdx.x;
+    if (L < ROWS) {
+      const int y = L - 1;
+      tab_s[L] = (y >= 0 && y < H) ? ((n * H + y) * W) * CIN : -1;
+    }
+  };
+  f4 stg[MAXC];
+  const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * H * W * CIN);
+  auto prefetch = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
+      const bool in = rb >= 0 && sl_x[k] >= 0;
+      stg[k] = bload(srcr, in ? static_cast<uint32_t>(rb + sl_x[k]) * 4u : kOOB);
+    }
+  };
+  build_tab(r);
+  __syncthreads();
+  prefetch();
+  constexpr float kNegInf = -__builtin_inff();
+
+  for (;;) {
+    __syncthreads();  // U_s written / the previous image's pool reads are done
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      if (sl_L[k] >= 0) {
+        const int e = threadIdx.x + k * NTH;
+        *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = stg[k];
+      }
+    }
+    const int n = r;
+    ++r;
+    if (r < rw.end) build_tab(r);
+    __syncthreads();
+    if (r < rw.end) prefetch();
+
+    f4 Yt[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int task = wave + NW * i;
+      const int grp = task % NG, sl = task / NG;
+      const int t0 = 16 * grp + c16;
+      const int t = t0 < NTI ? t0 : 0;
+      const int ty = t / TX, tx = t - ty * TX;
+      const int co0 = sl * 16;
+      const float* xp = x_s + (2 * ty * Wl + 2 * tx) * PP + 4 * g;
+      const float* up = U_s + (g * COUT + co0 + c16) * 4;
+      f4 acc[16];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) acc[xi] = f4{0.f, 0.f, 0.f, 0.f};
+      if (task < NTASK) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          f4 d[16];
+#pragma unroll
+          for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 4; ++dx)
+              d[4 * dy + dx] = *reinterpret_cast<const f4*>(xp + dy * rowstr + dx * PP + 16 * b);
+          f4 s[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            s[q] = d[q] - d[8 + q];
+            s[4 + q] = d[4 + q] + d[8 + q];
+            s[8 + q] = d[8 + q] - d[4 + q];
+            s[12 + q] = d[4 + q] - d[12 + q];
+          }
+          f4 V[16];
+#pragma unroll
+          for (int ra = 0; ra < 4; ++ra) {
+            V[4 * ra + 0] = s[4 * ra + 0] - s[4 * ra + 2];
+            V[4 * ra + 1] = s[4 * ra + 1] + s[4 * ra + 2];
+            V[4 * ra + 2] = s[4 * ra + 2] - s[4 * ra + 1];
+            V[4 * ra + 3] = s[4 * ra + 1] - s[4 * ra + 3];
+          }
+          const float* ub = up + b * 4 * COUT * 4;
+#pragma unroll
+          for (int xp2 = 0; xp2 < 8; ++xp2) {
+            f4 ua[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              ua[q] = *reinterpret_cast<const f4*>(ub + (2 * xp2 + q) * USTR);
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                acc[2 * xp2 + q] = mfma4(ua[q][v], V[2 * xp2 + q][v], acc[2 * xp2 + q]);
+          }
+        }
+      }
+      f4 tt[4][2];
+#pragma unroll
+      for (int ra = 0; ra < 4; ++ra) {
+        tt[ra][0] = (acc[4 * ra] + acc[4 * ra + 1]) + acc[4 * ra + 2];
+        tt[ra][1] = (acc[4 * ra + 1] - acc[4 * ra + 2]) - acc[4 * ra + 3];
+      }
+      const f4 bv = *reinterpret_cast<const f4*>(a.bias + (co0 < COUT ? co0 : 0) + 4 * g);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        Yt[i][c] = (tt[0][c] + tt[1][c]) + tt[2][c] + bv;
+        Yt[i][2 + c] = (tt[1][c] - tt[2][c]) - tt[3][c] + bv;
+      }
+    }
+    __syncthreads();  // every wave's patch reads are done: x_s becomes the image
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int task = wave + NW * i;
+      const int grp = task % NG, sl = task / NG;
+      const int t = 16 * grp + c16;
+      if (task < NTASK && t < NTI) {
+        const int ty = t / TX, tx = t - ty * TX;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx)
+            *reinterpret_cast<f4*>(img + ((2 * ty + dy) * W + 2 * tx + dx) * IPP + sl * 16 + 4 * g) =
+                Yt[i][2 * dy + dx];
+      }
+    }
+    __syncthreads();
+    // pool phase: every window of the image (pad-before 0, the bottom /
+    // right tap row beyond the image is padding)
+    for (int e = threadIdx.x; e < Hp * Wp * CQ; e += NTH) {
+      const int pr = e / (Wp * CQ), rem = e - pr * (Wp * CQ);
+      const int pc = rem / CQ, pq = rem - pc * CQ;
+      f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
+      int code[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int y = 2 * pr + dy, x = 2 * pc + dx;
+          if (y < H && x < W)
+            pool_take(best, code,
+                      *reinterpret_cast<const f4*>(img + (y * W + x) * IPP + 4 * pq), 3 * dy + dx);
+        }
+      const int64_t o = ((static_cast<int64_t>(n) * Hp + pr) * Wp + pc) * COUT + 4 * pq;
+      *reinterpret_cast<f4*>(pa.pooled + o) = best;
+      *reinterpret_cast<uint32_t*>(pa.arg + o) = pack_codes(code);
+    }
+    if (r >= rw.end) break;
+  }
+}
+
+template <int CIN, int COUT, int H, int W>
+bool run_wino_pool_img(const float* x, const float* w, const float* b, float* pooled,
+                       uint8_t* arg, int N, int Hr, int Wr, hipStream_t s) {
+  using P = PoolImgGeo<CIN, COUT, H, W>;
+  if (Hr != H || Wr != W || static_cast<int64_t>(N) * H * W * CIN * 4 > kMaxBufBytes) return false;
+  WinoArgs a{};
+  a.src = x;
+  a.w = w;
+  a.bias = b;
+  a.N = N; a.H = H; a.W = W;
+  a.nranges = N;
+  a.runs = 1;
+  const int G = std::max(1, std::min(N, 256));
+  auto kern = wino_conv_pool_img_kernel<CIN, COUT, H, W>;
+  allow_lds_w(kern, P::bytes);
+  WinoPoolArgs pa{};
+  pa.c = a;
+  pa.pooled = pooled;
+  pa.arg = arg;
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * P::NW), P::bytes, s, pa);
+  return true;
+}
+
 
 // ------------------------------------------------------------ weight grad
 // Winograd F(2x2, 3x3) weight gradient.  With Z = A dY A^T (4x4 per 2x2 dY
@@ -2403,8 +2648,8 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
                            uint8_t* arg, float* side, int64_t side_floats, int N, int H, int W,
                            int Cin, int Cout, int stages, hipStream_t s) {
   // bit 0: stage 1, bit 1: stage 0 (stage 0: 412 vs 529 us for the direct
-  // conv+pool, 10.02 -> 9.93 ms per step); stages >= 0 overrides the
-  // environment (tests)
+  // conv+pool, 10.02 -> 9.93 ms per step), bit 2: stage 2 (whole-image
+  // ranges); stages >= 0 overrides the environment (tests)
   static const int env_on = env_int("SA_F32_WINO_POOL", 3);
   const int on = stages >= 0 ? stages : env_on;
   if (Cin == 16 && Cout == 32 && (on & 1)) {
@@ -2412,6 +2657,8 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
     if (W == 32) return run_wino_pool<16, 32, 32>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 64) return run_wino_pool<16, 32, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
   }
+  if (Cin == 32 && Cout == 32 && (on & 4) && H == 18 && W == 24)
+    return run_wino_pool_img<32, 32, 18, 24>(x, w, b, pooled, arg, N, H, W, s);
   if (Cin == 4 && Cout == 16 && (on & 2)) {
     if (W == 96) return run_wino_pool<4, 16, 96>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 64) return run_wino_pool<4, 16, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);

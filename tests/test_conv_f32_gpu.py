@@ -299,23 +299,25 @@ def test_torso_f32_learner_scale_batch(cuda):
   assert rel_err(fa[-2:], ref) <= 1e-4
 
 
-@pytest.mark.parametrize('N,H,W,zero_w', [(256, 36, 48, False), (5, 36, 48, False),
-                                           (3, 16, 32, False), (2, 8, 64, False),
-                                           (7, 36, 48, True)])
-def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w):
+@pytest.mark.parametrize('N,H,W,zero_w,cin', [(256, 36, 48, False, 16), (5, 36, 48, False, 16),
+                                               (3, 16, 32, False, 16), (2, 8, 64, False, 16),
+                                               (7, 36, 48, True, 16), (300, 18, 24, False, 32),
+                                               (3, 18, 24, True, 32)])
+def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w, cin):
   """The 16 -> 32 stage head with the max-pool in the Winograd epilogue
   (wino_conv_pool_kernel): pooled values and argmax codes bitwise those of
   the Winograd conv followed by maxpool_fwd.  N = 256: long contiguous runs
   per workgroup (the register carry between tile-row pairs); N = 5: one
   range per workgroup, so every pooled odd row goes through the run-boundary
-  merge; zero weights: every tap ties, the first one must win everywhere."""
+  merge; zero weights: every tap ties, the first one must win everywhere.
+  cin 32: the stage-2 head (18x24, whole-image ranges, opt-in bit 2)."""
   C = _C()
   g = torch.Generator().manual_seed(11)
-  x = torch.randn(N, H, W, 16, generator=g).to(cuda)
-  w = (torch.zeros(3, 3, 16, 32) if zero_w else
-       torch.randn(3, 3, 16, 32, generator=g) / 12.0).to(cuda)
+  x = torch.randn(N, H, W, cin, generator=g).to(cuda)
+  w = (torch.zeros(3, 3, cin, 32) if zero_w else
+       torch.randn(3, 3, cin, 32, generator=g) / 12.0).to(cuda)
   b = torch.randn(32, generator=g).to(cuda)
-  out = C.cf32_wino_conv_pool_fwd(x, w, b)
+  out = C.cf32_wino_conv_pool_fwd(x, w, b, stages=7)
   assert len(out) == 2
   y, arg = out
   conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
@@ -366,9 +368,9 @@ def test_wino_conv_pool_stage0_matches_float64(cuda, N, H, W, zero_w):
 
 def test_wino_conv_pool_declines_other_shapes(cuda):
   C = _C()
-  x = torch.randn(2, 18, 24, 32, device=cuda)  # stage 2 (32 -> 32): not covered
+  x = torch.randn(2, 20, 24, 32, device=cuda)  # 32 -> 32 off the 18x24 instance
   assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 32, 32, device=cuda),
-                                   torch.zeros(32, device=cuda)) == []
+                                   torch.zeros(32, device=cuda), stages=7) == []
   x = torch.randn(2, 42, 42, 16, device=cuda)  # Atari stage 1 (H % 4 != 0)
   assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 16, 32, device=cuda),
                                    torch.zeros(32, device=cuda)) == []
