@@ -265,8 +265,13 @@ int gemm_f32_splits(int M, int N, int K, int ones_row) {
   const int bm = BM * gemm_rm(M + ones_row);
   const int tiles = ((M + ones_row + bm - 1) / bm) * ((N + BN - 1) / BN);
   int s = 1;
-  // enough workgroups to fill 256 CUs twice over, each K chunk >= 128
-  while (tiles * s < 512 && K / (2 * s) >= 128 && s < 16) s *= 2;
+  // enough workgroups to fill 256 CUs twice over (SA_GEMM_WG_TARGET), each
+  // K chunk >= 128
+  static const int target = [] {
+    const char* e = std::getenv("SA_GEMM_WG_TARGET");
+    return e ? std::max(1, std::atoi(e)) : 512;
+  }();
+  while (tiles * s < target && K / (2 * s) >= 128 && s < 16) s *= 2;
   return s;
 }
 
