@@ -1022,23 +1022,25 @@ struct PoolImgGeo {
   static constexpr int TY = H / 2, TX = W / 2, NTI = TY * TX;
   static constexpr int RT = (NTI + 15) / 16 * 16;
   static constexpr int NG = RT / 16, NS = COUT / 16, NTASK = NG * NS;
-  static constexpr int NW = (NTASK + 1) / 2;        // two tasks per wave
+  static constexpr int NW = 8;                       // tasks: two per wave (0..5), one (6, 7)
   static constexpr int ROWS = H + 2, Wl = W + 2;
   static constexpr int PP = CIN + 4, IPP = COUT + 4;
   static constexpr int XREG = (ROWS * Wl * PP > H * W * IPP) ? ROWS * Wl * PP : H * W * IPP;
-  static constexpr int MAXC = (ROWS * Wl * (CIN / 4) + 64 * NW - 1) / (64 * NW);
+  // only the image interior is staged (the zero border is rewritten per image)
+  static constexpr int MAXC = (H * W * (CIN / 4) + 64 * NW - 1) / (64 * NW);
   static constexpr size_t bytes = sizeof(float) * (16 * CIN * COUT + XREG + ROWS);
 };
 
 template <int CIN, int COUT, int H, int W>
-__global__ __launch_bounds__(448, 1) void wino_conv_pool_img_kernel(WinoPoolArgs pa) {
+__global__ __launch_bounds__(512, 1) void wino_conv_pool_img_kernel(WinoPoolArgs pa) {
   using P = PoolImgGeo<CIN, COUT, H, W>;
   constexpr int TX = P::TX, NTI = P::NTI, NG = P::NG, NTASK = P::NTASK, NW = P::NW;
   constexpr int NTH = 64 * NW, ROWS = P::ROWS, Wl = P::Wl, PP = P::PP, IPP = P::IPP;
   constexpr int MAXC = P::MAXC, C4 = CIN / 4, LC4 = C4 == 8 ? 3 : 2, NB = CIN / 16;
   constexpr int USTR = NB * 4 * COUT * 4, rowstr = Wl * PP;
   constexpr int Hp = H / 2, Wp = W / 2, CQ = COUT / 4;
-  static_assert(NTH == 448 && CIN % 16 == 0 && H % 2 == 0 && W % 2 == 0 && MAXC <= 32, "shape");
+  static_assert(NTH == 512 && NTASK <= 2 * NW && CIN % 16 == 0 && H % 2 == 0 && W % 2 == 0 &&
+                MAXC <= 32, "shape");
   const WinoArgs& a = pa.c;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* U_s = smem;                    // [16 xi][NB][4 g][COUT][4]
@@ -1078,30 +1080,19 @@ __global__ __launch_bounds__(448, 1) void wino_conv_pool_img_kernel(WinoPoolArgs
   int r = rw.r;
   if (r >= rw.end) return;
 
-  int sl_L[MAXC], sl_x[MAXC];
-#pragma unroll
-  for (int k = 0; k < MAXC; ++k) {
-    const int e = threadIdx.x + k * NTH;
-    const int ch = e & (C4 - 1), pix = e >> LC4;
-    const int L = pix / Wl, col = pix - L * Wl;
-    sl_L[k] = L < ROWS ? L : -1;
-    sl_x[k] = (col >= 1 && col <= W) ? (col - 1) * CIN + 4 * ch : -1;
-  }
+  // staging slot k of a thread: image element e = (pixel, channel quad) of
+  // the interior (its LDS place is row y + 1, column x + 1)
   auto build_tab = [&](int n) {
-    const int L = threadIdx.x;
-    if (L < ROWS) {
-      const int y = L - 1;
-      tab_s[L] = (y >= 0 && y < H) ? ((n * H + y) * W) * CIN : -1;
-    }
+    if (threadIdx.x == 0) tab_s[0] = n * H * W * CIN;
   };
   f4 stg[MAXC];
   const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * H * W * CIN);
   auto prefetch = [&]() __attribute__((always_inline)) {
+    const int base = tab_s[0];
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
-      const int rb = sl_L[k] >= 0 ? tab_s[sl_L[k]] : -1;
-      const bool in = rb >= 0 && sl_x[k] >= 0;
-      stg[k] = bload(srcr, in ? static_cast<uint32_t>(rb + sl_x[k]) * 4u : kOOB);
+      const int e = threadIdx.x + k * NTH;
+      stg[k] = bload(srcr, e < H * W * C4 ? static_cast<uint32_t>(base + 4 * e) * 4u : kOOB);
     }
   };
   build_tab(r);
@@ -1113,10 +1104,19 @@ __global__ __launch_bounds__(448, 1) void wino_conv_pool_img_kernel(WinoPoolArgs
     __syncthreads();  // U_s written / the previous image's pool reads are done
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
-      if (sl_L[k] >= 0) {
-        const int e = threadIdx.x + k * NTH;
-        *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = stg[k];
+      const int e = threadIdx.x + k * NTH;
+      if (e < H * W * C4) {
+        const int pix = e >> LC4, q = e & (C4 - 1);
+        const int y = pix / W, x = pix - y * W;
+        *reinterpret_cast<f4*>(x_s + ((y + 1) * Wl + x + 1) * PP + 4 * q) = stg[k];
       }
+    }
+    // the zero border (the previous image's pre-pool map overwrote it)
+    for (int e = threadIdx.x; e < (2 * Wl + 2 * H) * C4; e += NTH) {
+      const int q = e % C4, c = e / C4;
+      const int pix = c < 2 * Wl ? (c < Wl ? c : (ROWS - 1) * Wl + c - Wl)
+                                 : ((c - 2 * Wl) / 2 + 1) * Wl + ((c - 2 * Wl) & 1) * (Wl - 1);
+      *reinterpret_cast<f4*>(x_s + pix * PP + 4 * q) = f4{0.f, 0.f, 0.f, 0.f};
     }
     const int n = r;
     ++r;
