@@ -106,11 +106,12 @@ bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
 // Stage head with the 3x3/2 SAME max-pool fused (conv_wino.hip): x [N,H,W,Cin]
 // -> pooled [N,H/2,W/2,Cout] + argmax codes, the 3x3/1 conv + bias in
 // Winograd form, the pre-pool map only in LDS.  (Cin, Cout) = (16, 32) with
-// W in {32, 48, 64} (stage 1) or (4, 16) with W in {64, 96} (stage 0 on the
-// 4-channel image); H % 4 == 0; `side` holds >= wino_conv_pool_side_floats
-// floats of scratch.  False (nothing launched) when the shape is not
-// covered.  `stages` (or SA_F32_WINO_POOL when < 0): bit 0 stage 1, bit 1
-// stage 0 (default 3).
+// W in {32, 48, 64} and H % 4 == 0 (stage 1), (4, 16) with W in {64, 96} and
+// H % 4 == 0 (stage 0 on the 4-channel image), (32, 32) at 18x24 (stage 2,
+// whole-image ranges); `side` holds >= wino_conv_pool_side_floats floats of
+// scratch.  False (nothing launched) when the shape is not covered.
+// `stages` (or SA_F32_WINO_POOL when < 0): bit 0 stage 1, bit 1 stage 0,
+// bit 2 stage 2 (default 7).
 int64_t wino_conv_pool_side_floats(int W, int Cout);
 bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float* pooled,
                            uint8_t* arg, float* side, int64_t side_floats, int N, int H, int W,

@@ -2649,8 +2649,8 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
                            int Cin, int Cout, int stages, hipStream_t s) {
   // bit 0: stage 1, bit 1: stage 0 (stage 0: 412 vs 529 us for the direct
   // conv+pool, 10.02 -> 9.93 ms per step), bit 2: stage 2 (whole-image
-  // ranges); stages >= 0 overrides the environment (tests)
-  static const int env_on = env_int("SA_F32_WINO_POOL", 3);
+  // ranges: 9.93 -> 9.90 ms); stages >= 0 overrides the environment (tests)
+  static const int env_on = env_int("SA_F32_WINO_POOL", 7);
   const int on = stages >= 0 ? stages : env_on;
   if (Cin == 16 && Cout == 32 && (on & 1)) {
     if (W == 48) return run_wino_pool<16, 32, 48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
