@@ -30,10 +30,14 @@ import os
 # debug hook (tools/debug): when a dict, the deep torso backward records its
 # intermediate gradients in it
 DEBUG_TAPE = None
-# Deep-torso stage heads (conv -> max-pool): stages (0-based) whose forward
-# runs the fused conv+pool kernel (pre-pool map only in LDS), and whether the
-# backward gathers the pre-pool gradient from (dP, argmax) inside the conv
-# kernels' loads instead of materialising it with maxpool_bwd.
+# Deep-torso stage heads (conv -> max-pool).  By default every head whose
+# shape the fused Winograd conv+pool kernel covers (conv_wino.hip
+# wino_conv_pool_kernel: the 72x96 torso's three heads; SA_F32_WINO_POOL
+# selects) runs conv + pool + argmax in one kernel.  Otherwise: stages
+# (0-based) listed here run the direct fused conv+pool kernel (pre-pool map
+# only in LDS), the rest conv + maxpool_fwd; and whether the backward gathers
+# the pre-pool gradient from (dP, argmax) inside the conv kernels' loads
+# instead of materialising it with maxpool_bwd.
 FUSED_POOL_STAGES = tuple(int(c) for c in os.environ.get('SA_F32_FUSED_POOL', '0')
                           if c.isdigit())
 # SA_F32_POOL_GATHER=1: every stage; a digit string (e.g. '0'): those stages
