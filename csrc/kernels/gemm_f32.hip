@@ -222,6 +222,165 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Args a) {
   }
 }
 
+// The same tile program with the operand layout (TA, TB) compile-time and
+// every global load a range-checked buffer load (an out-of-range element -
+// past M / N / the K chunk - gets an offset past the buffer's end and reads
+// zero), so the K-step loads carry no branches: the generic kernel's
+// runtime layout switches and per-load bounds branches (123 exec branches,
+// 78 scalar edge loads in its ISA) made the compiler wait on loads early.
+// Needs M % 4 == 0 when TA (whole m quads) and N % 4 == 0 when !TB.
+constexpr uint32_t kGemmOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gemm_rsrc(const float* p, int64_t floats) {
+  const int64_t bytes = floats * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0,
+                                           static_cast<int>(bytes >= 0xFFFFFF00ll
+                                                                ? 0xFFFFFF00u
+                                                                : static_cast<uint32_t>(bytes)),
+                                           0x00020000);
+}
+__device__ __forceinline__ f4 gemm_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+template <int RM, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f32_bl_kernel(Args a) {
+  constexpr int BMt = BM * RM;
+  __shared__ __attribute__((aligned(16))) float As[2][BMt * PK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * PK];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int m0 = blockIdx.x * BMt, n0 = blockIdx.y * BN;
+  const int Mr = a.M + a.ones_row;
+  const int kbeg = blockIdx.z * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  constexpr int KQ = BK / 16;
+  const auto ar = gemm_rsrc(a.A, TA ? static_cast<int64_t>(a.K) * a.lda
+                                    : static_cast<int64_t>(a.M) * a.lda);
+  const auto br = gemm_rsrc(a.B, TB ? static_cast<int64_t>(a.N) * a.ldb
+                                    : static_cast<int64_t>(a.K) * a.ldb);
+  // per-thread fixed parts of the operand addresses
+  f4 ra[RM][KQ], rb[KQ];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        if constexpr (!TA) {  // A[m][k]: thread = (m, k quad)
+          const int m = m0 + 64 * r + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
+          const bool in = m < a.M && k < kend;
+          f4 v = gemm_bload(ar, in ? static_cast<uint32_t>(m * a.lda + k) * 4u : kGemmOOB);
+          if (a.ones_row && m == a.M && k < kend) v = f4{1.f, 1.f, 1.f, 1.f};
+          ra[r][j] = v;
+        } else {  // A[k][m]: thread = (k, m quad)
+          const int k = k0 + (t >> 4) + 16 * j, m = m0 + 64 * r + 4 * (t & 15);
+          const bool in = k < kend && m < a.M;
+          f4 v = gemm_bload(ar, in ? static_cast<uint32_t>(k * a.lda + m) * 4u : kGemmOOB);
+          if (a.ones_row && m == a.M && k < kend) v[0] = 1.f;
+          ra[r][j] = v;
+        }
+      }
+      if constexpr (!TB) {  // B[k][n]: thread = (k, n quad)
+        const int k = k0 + (t >> 4) + 16 * j, n = n0 + 4 * (t & 15);
+        const bool in = k < kend && n < a.N;
+        rb[j] = gemm_bload(br, in ? static_cast<uint32_t>(k * a.ldb + n) * 4u : kGemmOOB);
+      } else {  // B[n][k]: thread = (n, k quad)
+        const int n = n0 + (t >> 2), k = k0 + 4 * (t & 3) + 16 * j;
+        const bool in = n < a.N && k < kend;
+        rb[j] = gemm_bload(br, in ? static_cast<uint32_t>(n * a.ldb + k) * 4u : kGemmOOB);
+      }
+    }
+  };
+  auto commit = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KQ; ++j) {
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        if constexpr (!TA) {
+          *reinterpret_cast<f4*>(&As[buf][(64 * r + (t >> 2)) * PK + 4 * (t & 3) + 16 * j]) =
+              ra[r][j];
+        } else {
+          const int k = (t >> 4) + 16 * j, m = 64 * r + 4 * (t & 15);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[r][j][q];
+        }
+      }
+      if constexpr (!TB) {
+        const int k = (t >> 4) + 16 * j, n = 4 * (t & 15);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Bs[buf][(n + q) * PK + k] = rb[j][q];
+      } else {
+        *reinterpret_cast<f4*>(&Bs[buf][(t >> 2) * PK + 4 * (t & 3) + 16 * j]) = rb[j];
+      }
+    }
+  };
+
+  f16v acc[RM];
+#pragma unroll
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
+  const int arow = (wm * 32 * RM + l32) * PK + (BK / 2) * h;
+  const int brow = (wn * 32 + l32) * PK + (BK / 2) * h;
+  int buf = 0;
+  if (kbeg < kend) {
+    load(kbeg);
+    commit(0);
+    __syncthreads();
+  }
+  // branch-free loop body: the step after the last loads only zeros (every
+  // element out of the K chunk) into the idle buffer, which nothing reads;
+  // a conditional load / commit made the compiler copy the accumulators
+  // through VGPRs at the loop header, right behind the last MFMA
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    load(k0 + BK);  // in flight under the MFMAs
+#pragma unroll
+    for (int c = 0; c < BK / 8; ++c) {
+      const f4 bv = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4 * c]);
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        const f4 av = *reinterpret_cast<const f4*>(&As[buf][arow + 32 * r * PK + 4 * c]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[r], 0, 0, 0);
+      }
+    }
+    commit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  const int n = n0 + wn * 32 + l32;
+  if (a.splits > 1) {
+    float* p = a.part + static_cast<int64_t>(blockIdx.z) * Mr * a.N;
+#pragma unroll
+    for (int r = 0; r < RM; ++r)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * 32 * RM + 32 * r + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m < Mr && n < a.N) p[static_cast<int64_t>(m) * a.N + n] = acc[r][e];
+      }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = m0 + wm * 32 * RM + 32 * r + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (n >= a.N) continue;
+      if (m < a.M) store_out(a.ep, m, n, acc[r][e]);
+      else if (m == a.M && a.ones_row) a.ep.colsum[n] += acc[r][e];
+    }
+  if (a.ep.aug_c0 > 0 && blockIdx.y == 0) {
+    const int naug = a.ep.ldc - a.ep.aug_c0;
+    for (int e = t; e < BMt * naug; e += 256) {
+      const int m = m0 + e / naug;
+      if (m < a.M) store_aug(a.ep, m, e % naug);
+    }
+  }
+}
+
 // Fixed-order sum of the split partials + the epilogue.
 __global__ __launch_bounds__(256) void gemm_f32_reduce_kernel(Args a) {
   const int Mr = a.M + a.ones_row;
@@ -296,7 +455,20 @@ bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int ld
   const int Mr = M + (ones_row ? 1 : 0);
   const int rm = gemm_rm(Mr);
   dim3 grid((Mr + BM * rm - 1) / (BM * rm), (N + BN - 1) / BN, a.splits);
-  if (rm == 2)
+  // branch-free buffer-load variant (SA_GEMM_BL=0: the generic kernel):
+  // whole quads along every f4 operand axis, byte offsets within 32 bits
+  static const int bl = [] {
+    const char* e = std::getenv("SA_GEMM_BL");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int64_t abytes = (ta ? static_cast<int64_t>(K) * lda : static_cast<int64_t>(M) * lda) * 4;
+  const int64_t bbytes = (tb ? static_cast<int64_t>(N) * ldb : static_cast<int64_t>(K) * ldb) * 4;
+  if (bl && rm == 1 && (!ta || M % 4 == 0) && (tb || N % 4 == 0) && abytes < 0xFFFFFF00ll &&
+      bbytes < 0xFFFFFF00ll) {
+    auto k = ta ? (tb ? gemm_f32_bl_kernel<1, true, true> : gemm_f32_bl_kernel<1, true, false>)
+                : (tb ? gemm_f32_bl_kernel<1, false, true> : gemm_f32_bl_kernel<1, false, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, a);
+  } else if (rm == 2)
     hipLaunchKernelGGL(gemm_f32_kernel<2>, grid, dim3(256), 0, stream, a);
   else
     hipLaunchKernelGGL(gemm_f32_kernel<1>, grid, dim3(256), 0, stream, a);
