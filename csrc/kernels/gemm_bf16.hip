@@ -27,6 +27,7 @@
 #include "gemm_bf16.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sa {
 namespace {
@@ -122,6 +123,25 @@ __device__ __forceinline__ unsigned half(const uint4& v, int q) {
   return w;
 }
 
+// 16-B loads through a buffer descriptor: an element range past the
+// operand's end (offset kOOB) reads zeros, so the K-step loads of the
+// layout-specialised kernel carry no bounds branches (callers guarantee
+// whole 8-element chunks along M / N: R % 8 == 0)
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bf_rsrc(const bf16_t* p, int64_t elems) {
+  const int64_t bytes = elems * 2;
+  return __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(p), 0,
+      static_cast<int>(bytes >= 0xFFFFFF00ll ? 0xFFFFFF00u : static_cast<uint32_t>(bytes)),
+      0x00020000);
+}
+__device__ __forceinline__ uint4 bl16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// TA / TB: the operand layouts as compile-time constants (BL: branch-free
+// buffer loads, whole 8-element chunks along M and N)
+template <bool TA, bool TB, bool BL>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) bf16_t As[2][BM * PK];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BN * PK];
@@ -139,28 +159,51 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(Args a) {
   // M/N-contiguous: thread = (k pair t>>3, column chunk 8 (t&7)), rows
   // k = 2 (t>>3) and 2 (t>>3) + 1.
   uint4 ra[2], rb[2];
+  const auto arr = bf_rsrc(a.A, TA ? static_cast<int64_t>(a.K) * a.lda
+                                   : static_cast<int64_t>(a.M) * a.lda);
+  const auto brr = bf_rsrc(a.B, TB ? static_cast<int64_t>(a.N) * a.ldb
+                                   : static_cast<int64_t>(a.K) * a.ldb);
+  const unsigned o2 = kOne | (static_cast<unsigned>(kOne) << 16);
   auto load = [&](int k0) __attribute__((always_inline)) {
-    if (!a.ta) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        ra[j] = load_row8(a.A, a.lda, m0 + (t >> 3) + 32 * j, a.M, a.ones_row,
-                          k0 + 8 * (t & 7), kend);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        ra[j] = load_col8(a.A, a.lda, k0 + 2 * (t >> 3) + j, kend, m0 + 8 * (t & 7), a.M,
-                          a.ones_row);
-    }
-    if (a.tb) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        rb[j] = load_row8(a.B, a.ldb, n0 + (t >> 3) + 32 * j, a.N, false,
-                          k0 + 8 * (t & 7), kend);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        rb[j] = load_col8(a.B, a.ldb, k0 + 2 * (t >> 3) + j, kend, n0 + 8 * (t & 7), a.N,
-                          false);
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (BL) {
+        if constexpr (!TA) {  // A[m][k]: row m, k chunk
+          const int r = m0 + (t >> 3) + 32 * j, c = k0 + 8 * (t & 7);
+          const bool in = r < a.M && c < kend;
+          uint4 v = bl16(arr, in ? static_cast<uint32_t>(r * a.lda + c) * 2u : kOOB);
+          if (a.ones_row && r == a.M && c < kend) v = make_uint4(o2, o2, o2, o2);
+          ra[j] = v;
+        } else {  // A[k][m]: K-row k, m chunk
+          const int k = k0 + 2 * (t >> 3) + j, c = m0 + 8 * (t & 7);
+          const bool in = k < kend && c < a.M;
+          uint4 v = bl16(arr, in ? static_cast<uint32_t>(k * a.lda + c) * 2u : kOOB);
+          if (a.ones_row && c == a.M && k < kend) v.x = kOne;
+          ra[j] = v;
+        }
+        if constexpr (TB) {  // B[n][k]
+          const int r = n0 + (t >> 3) + 32 * j, c = k0 + 8 * (t & 7);
+          const bool in = r < a.N && c < kend;
+          rb[j] = bl16(brr, in ? static_cast<uint32_t>(r * a.ldb + c) * 2u : kOOB);
+        } else {  // B[k][n]
+          const int k = k0 + 2 * (t >> 3) + j, c = n0 + 8 * (t & 7);
+          const bool in = k < kend && c < a.N;
+          rb[j] = bl16(brr, in ? static_cast<uint32_t>(k * a.ldb + c) * 2u : kOOB);
+        }
+      } else {
+        if constexpr (!TA)
+          ra[j] = load_row8(a.A, a.lda, m0 + (t >> 3) + 32 * j, a.M, a.ones_row,
+                            k0 + 8 * (t & 7), kend);
+        else
+          ra[j] = load_col8(a.A, a.lda, k0 + 2 * (t >> 3) + j, kend, m0 + 8 * (t & 7), a.M,
+                            a.ones_row);
+        if constexpr (TB)
+          rb[j] = load_row8(a.B, a.ldb, n0 + (t >> 3) + 32 * j, a.N, false,
+                            k0 + 8 * (t & 7), kend);
+        else
+          rb[j] = load_col8(a.B, a.ldb, k0 + 2 * (t >> 3) + j, kend, n0 + 8 * (t & 7), a.N,
+                            false);
+      }
     }
   };
   auto commit_op = [&](bf16_t* S, const uint4 (&r)[2], bool kcontig) __attribute__((always_inline)) {
@@ -180,8 +223,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(Args a) {
     }
   };
   auto commit = [&](int buf) __attribute__((always_inline)) {
-    commit_op(As[buf], ra, !a.ta);
-    commit_op(Bs[buf], rb, a.tb);
+    commit_op(As[buf], ra, !TA);
+    commit_op(Bs[buf], rb, TB);
   };
 
   f16v acc;
@@ -196,20 +239,21 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(Args a) {
     commit(0);
     __syncthreads();
   }
+  // branch-free loop body (the step after the last loads zeros - every k is
+  // past the chunk - into the idle buffer, which nothing reads): with a
+  // conditional load / commit the compiler copied the accumulators through
+  // VGPRs at the loop header every step (gemm_f32.hip's finding)
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    if (more) load(k0 + BK);  // in flight under the MFMAs
+    load(k0 + BK);  // in flight under the MFMAs
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const s8v av = *reinterpret_cast<const s8v*>(&As[buf][arow + 16 * kk]);
       const s8v bv = *reinterpret_cast<const s8v*>(&Bs[buf][brow + 16 * kk]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
     }
-    if (more) {
-      commit(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
-    }
+    commit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
   }
 
   // D[i][j]: j = lane & 31, i = (e & 3) + 8 (e >> 2) + 4 h
@@ -293,7 +337,25 @@ bool gemm_bf16_launch(const uint16_t* A, const uint16_t* B, int M, int N, int K,
   a.ep = ep;
   const int Mr = M + (ones_row ? 1 : 0);
   dim3 grid((Mr + BM - 1) / BM, (N + BN - 1) / BN, a.splits);
-  hipLaunchKernelGGL(gemm_bf16_kernel, grid, dim3(256), 0, stream, a);
+  // layout-specialised kernels; the branch-free buffer-load form needs whole
+  // 8-element chunks along the M / N-contiguous operands and 32-bit offsets
+  // (SA_GEMM_BL=0: bounds-checked loads)
+  static const int blenv = [] {
+    const char* e = std::getenv("SA_GEMM_BL");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int64_t abytes = (ta ? static_cast<int64_t>(K) * lda : static_cast<int64_t>(M) * lda) * 2;
+  const int64_t bbytes = (tb ? static_cast<int64_t>(N) * ldb : static_cast<int64_t>(K) * ldb) * 2;
+  const bool bl = blenv && (!ta || M % 8 == 0) && (tb || N % 8 == 0) && abytes < 0xFFFFFF00ll &&
+                  bbytes < 0xFFFFFF00ll;
+  void (*kern)(Args);
+  if (bl)
+    kern = ta ? (tb ? gemm_bf16_kernel<true, true, true> : gemm_bf16_kernel<true, false, true>)
+              : (tb ? gemm_bf16_kernel<false, true, true> : gemm_bf16_kernel<false, false, true>);
+  else
+    kern = ta ? (tb ? gemm_bf16_kernel<true, true, false> : gemm_bf16_kernel<true, false, false>)
+              : (tb ? gemm_bf16_kernel<false, true, false> : gemm_bf16_kernel<false, false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, a);
   if (a.splits > 1) {
     const int64_t total = static_cast<int64_t>(Mr) * N;
     const int64_t aug = ep.aug_c0 > 0 ? static_cast<int64_t>(M) * (ep.ldc - ep.aug_c0) : 0;
