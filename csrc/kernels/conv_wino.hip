@@ -347,9 +347,11 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     }
     const int cur = r;
     r += rw.step;
-    if (r < rw.end) build_tab(r);
+    // unconditional (the last range re-stages itself, unused): a
+    // conditional prefetch leaves a join at the loop back-edge
+    build_tab(r < rw.end ? r : cur);
     __syncthreads();
-    if (r < rw.end) prefetch();  // in flight under the MFMAs below
+    prefetch();  // in flight under the MFMAs below
     const RangeGeom gm = range_geom(a, cur, RT);
 
     for (int task = knob(a.ablate, 1) ? NTASK : wave; task < NTASK; task += NW) {
@@ -765,9 +767,9 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
     }
     const int cur = r;
     ++r;
-    if (r < rw.end) build_tab(r);
+    build_tab(r < rw.end ? r : cur);  // unconditional: see wino_conv_kernel
     __syncthreads();
-    if (r < rw.end) prefetch();  // in flight under the MFMAs below
+    prefetch();  // in flight under the MFMAs below
 
     f4 acc[16];
 #pragma unroll
@@ -1120,9 +1122,9 @@ __global__ __launch_bounds__(512, 1) void wino_conv_pool_img_kernel(WinoPoolArgs
     }
     const int n = r;
     ++r;
-    if (r < rw.end) build_tab(r);
+    build_tab(r < rw.end ? r : n);  // unconditional: see wino_conv_kernel
     __syncthreads();
-    if (r < rw.end) prefetch();
+    prefetch();
 
     f4 Yt[2][4];
 #pragma unroll
@@ -1810,9 +1812,9 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
       }
       tile_s[threadIdx.x] = v;
     }
-    if (r < rw.end) build_tab(r);
+    build_tab(r < rw.end ? r : cur);  // unconditional: see wino_conv_kernel
     __syncthreads();
-    if (r < rw.end) prefetch();
+    prefetch();
 
     // ---- data gradient: waves 0..3, one 16-tile group each
     if (wave < NG && gm.t0 + 16 * wave < gm.t1) {
@@ -2234,9 +2236,9 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
       }
       tile_s[threadIdx.x] = v;
     }
-    if (r < r_end) build_tab(r);
+    build_tab(r < r_end ? r : cur);  // unconditional: see wino_conv_kernel
     __syncthreads();
-    if (r < r_end) prefetch();  // in flight under the MFMAs below
+    prefetch();  // in flight under the MFMAs below
     return gm;
   };
 
