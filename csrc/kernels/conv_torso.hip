@@ -909,8 +909,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if (RESID) rop.load(resid, img0, Rv * W, W);
     const int nt = it.next(tile);
     auto prefetch = [&]() {
-      if (it.valid(nt)) {
-        const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
+      {  // unconditional: see issue() in the backward kernels
+        const int t2 = it.valid(nt) ? nt : tile;
+        const int n2 = t2 / tpi, r2 = (t2 - n2 * tpi) * R, Rv2 = min(R, H - r2);
         sx.issue(x, n2, H, W, r2 - 1, Rv2 + 2);
       }
     };
@@ -995,8 +996,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     EpiOperand<C, FwdChunks<C, C>> rop;  // skip = raw x rows [r0, r0+Rv)
     rop.load(x, img0, Rv * W, W);
     const int nt = it.next(tile);
-    if (it.valid(nt)) {
-      const int n2 = nt / tpi, r2 = (nt - n2 * tpi) * R, Rv2 = min(R, H - r2);
+    {  // unconditional: see issue() in the backward kernels
+      const int t2 = it.valid(nt) ? nt : tile;
+      const int n2 = t2 / tpi, r2 = (t2 - n2 * tpi) * R, Rv2 = min(R, H - r2);
       sx.issue(x, n2, H, W, r2 - 2, Rv2 + 4);
     }
     if (kKeep(xcd, 4))
@@ -1059,7 +1061,9 @@ __global__ __launch_bounds__(kThreads) void conv_pool_fwd_kernel(
     if (kKeep(xcd, 8))
     sx.template commit<false, true>(x_s, W);
     __syncthreads();
-    if (it.valid(it.next(tile))) issue(it.next(tile));
+    // unconditional (no next tile: re-issue this one, unused) - a conditional
+    // issue leaves a join at the loop back-edge
+    issue(it.valid(it.next(tile)) ? it.next(tile) : tile);
     if (kKeep(xcd, 4))
     conv_tile_fwd<CIN, COUT>(x_s, w_s, W, Rc * W, [&](int q, int co0, float v[4], int) {
 #pragma unroll
@@ -1126,7 +1130,9 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_fwd_kernel(
     if (kKeep(xcd, 8))
     commit_x4(sx, x4, W, Rc + 2, 4);
     __syncthreads();
-    if (it.valid(it.next(tile))) issue(it.next(tile));
+    // unconditional (no next tile: re-issue this one, unused) - a conditional
+    // issue leaves a join at the loop back-edge
+    issue(it.valid(it.next(tile)) ? it.next(tile) : tile);
     s4 a[3];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
@@ -1366,7 +1372,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     if (kKeep(xcd, 8))
     sg.commit(g_s);
     __syncthreads();
-    if (it.valid(it.next(tile))) issue(it.next(tile));
+    // unconditional (no next tile: re-issue this one, unused) - a conditional
+    // issue leaves a join at the loop back-edge
+    issue(it.valid(it.next(tile)) ? it.next(tile) : tile);
     if (kKeep(xcd, 1))
     gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
                                   Rv + 2, d_s);
@@ -1446,7 +1454,9 @@ __global__ __launch_bounds__(kThreads) void conv1_pool_bwd_kernel(
     if (kKeep(xcd, 8))
     sg.commit(g_s);
     __syncthreads();
-    if (it.valid(it.next(tile))) issue(it.next(tile));
+    // unconditional (no next tile: re-issue this one, unused) - a conditional
+    // issue leaves a join at the loop back-edge
+    issue(it.valid(it.next(tile)) ? it.next(tile) : tile);
     const int npix = Rv * W;
     if (kKeep(xcd, 1))
     gather_pool_grad_blocks<COUT>(p_s, g_s, lo, hi, W, Wo, pb_h, pb_w, r0 - 1,
