@@ -376,7 +376,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(ConvArgs a, int R
     __syncthreads();
     const int cur = tile;
     tile += gridDim.x;
-    if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
+    // unconditional (the last tile re-stages itself, unused): a conditional
+    // prefetch leaves a join at the loop back-edge
+    prefetch(tile < ntiles ? tile : cur);  // in flight during the MFMAs below
     const int n = cur / tiles_per_img;
     const int oy0 = (cur - n * tiles_per_img) * R;
     const int P = min(R, a.Ho - oy0) * a.Wo;
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_pool_fwd_kernel(
     __syncthreads();
     const int cur = tile;
     tile += gridDim.x;
-    if (tile < ntiles) prefetch(tile);
+    prefetch(tile < ntiles ? tile : cur);  // unconditional: see conv_fwd_kernel
     const int n = cur / tiles_per_img;
     const int pi0 = (cur - n * tiles_per_img) * R;
     const int cr0 = 2 * pi0 - pbh;  // image row of the tile's conv row 0
@@ -730,8 +732,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a, int R
     sx.commit(x_s, XP, xtotal);
     sd.commit(d_s, DP, P * (CG / 4));
     __syncthreads();
+    const int cur_t = tile;
     tile += gridDim.x;
-    if (tile < ntiles) prefetch(tile);  // in flight during the MFMAs below
+    prefetch(tile < ntiles ? tile : cur_t);  // unconditional: see conv_fwd_kernel
     const int nq = (P + 3) >> 2;
     if constexpr (CINP % 16 == 0 && WSM == 1) {
       // 16-channel-multiple inputs, one wave row set (res16 391 vs 438 us,
