@@ -74,16 +74,34 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   const int er = tid >> 2, eu = tid & 3;
   const int egr = r0 + er;
   const int ej = blk * 4 + eu;
-  float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, hp = 0.f, ekeep = 0.f;
-  if (tid < 4 * RW && egr < B) {
-    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+  // Every operand load below is issued up front with a clamped (always valid)
+  // address and consumed only where it is needed: converting a done byte
+  // next to its load (or loading under a per-row branch) made each group of
+  // loads wait for all earlier ones, three serialized memory round trips per
+  // step instead of one.  The done-reset of the A operand is applied to the
+  // reduced product rows instead of to h ((keep h) W == keep (h W) row by
+  // row, keep in {0, 1}, selected rather than multiplied: bitwise the same).
+  // The done defaults are the (non-constant, nonzero) B: with a constant
+  // default the compiler folds the done test into the loading branch, which
+  // then waits for the byte right there.
+  float xi = 0.f, xc = 0.f, xf = 0.f, xo = 0.f, cp = 0.f, hp = 0.f;
+  uint32_t edone = static_cast<uint32_t>(B);
+  if (tid < 4 * RW) {
+    const int egc = egr < B ? egr : B - 1;
+    const int64_t g0 = static_cast<int64_t>(egc) * 4 * H + ej;
     xi = xw_t[g0];
     xc = xw_t[g0 + H];
     xf = xw_t[g0 + 2 * H];
     xo = xw_t[g0 + 3 * H];
-    cp = c_prev[static_cast<int64_t>(egr) * H + ej];
-    if (hpm_t) hp = h_prev[static_cast<int64_t>(egr) * H + ej];
-    ekeep = done_t[egr] ? 0.f : 1.f;
+    cp = c_prev[static_cast<int64_t>(egc) * H + ej];
+    if (hpm_t) hp = h_prev[static_cast<int64_t>(egc) * H + ej];
+    edone = done_t[egc];
+  }
+  // reduce-thread row (tid < 16 RW): its done byte masks the product row
+  uint32_t rdone = static_cast<uint32_t>(B);
+  if (tid < 16 * RW) {
+    const int rg = r0 + (tid >> 4);
+    rdone = done_t[rg < B ? rg : B - 1];
   }
   // B operand: W[k = kw0 + 4s + (l>>4)][n = l&15]
   const int kw0 = wave * KW;
@@ -91,26 +109,22 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
   const float* wsrc = w4 + (static_cast<int64_t>(blk) * H + kw0 + (lane >> 4)) * 16 + (lane & 15);
 #pragma unroll
   for (int s = 0; s < NS; ++s) wb[s] = wsrc[s * 4 * 16];
-  // A operand: h[row = r0 + 16 mt + (l&15)][k = kw0 + 4s + (l>>4)] * keep
+  // A operand: h[row = r0 + 16 mt + (l&15)][k = kw0 + 4s + (l>>4)]
   float ha[NMT][NS];
   if (h_pk_in != nullptr) {
     const float* pk = h_pk_in + static_cast<int64_t>(t32) * 32 * H +
                       wave * 2 * NS * 64 + lane;
 #pragma unroll
-    for (int mt = 0; mt < NMT; ++mt) {
-      const int row = r0 + 16 * mt + (lane & 15);
-      const float kf = (row < B && !done_t[row < B ? row : 0]) ? 1.f : 0.f;
+    for (int mt = 0; mt < NMT; ++mt)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) ha[mt][s] = pk[((mt0 + mt) * NS + s) * 64] * kf;
-    }
+      for (int s = 0; s < NS; ++s) ha[mt][s] = pk[((mt0 + mt) * NS + s) * 64];
   } else {
 #pragma unroll
     for (int mt = 0; mt < NMT; ++mt) {
       const int row = r0 + 16 * mt + (lane & 15);
-      const bool ok = row < B && !done_t[row < B ? row : 0];
-      const float* hr = h_prev + static_cast<int64_t>(ok ? row : 0) * H + kw0 + (lane >> 4);
+      const float* hr = h_prev + static_cast<int64_t>(row < B ? row : B - 1) * H + kw0 + (lane >> 4);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) ha[mt][s] = ok ? hr[4 * s] : 0.f;
+      for (int s = 0; s < NS; ++s) ha[mt][s] = hr[4 * s];
     }
   }
   f4v acc[2] = {f4v{0.f, 0.f, 0.f, 0.f}, f4v{0.f, 0.f, 0.f, 0.f}};
@@ -130,10 +144,11 @@ __global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
     float sum = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) sum += red[w][mt][src_lane][i];
-    g_s[m][n] = sum;
+    g_s[m][n] = rdone ? 0.f : sum;
   }
   __syncthreads();
   if (tid < 4 * RW && egr < B) {
+    const float ekeep = edone ? 0.f : 1.f;
     const float i = sigm(g_s[er][eu * 4 + 0] + xi);
     const float g = tanhf(g_s[er][eu * 4 + 1] + xc);
     const float f = sigm(g_s[er][eu * 4 + 2] + xf + 1.0f);
@@ -192,11 +207,15 @@ __global__ __launch_bounds__(64 * NW) void lstm_bwd_step_kernel(
   const int egr = r0 + er;
   const int ej = u0 + eu;
   const bool eok = tid < 16 * RW && egr < B;
+  // operands issued up front from clamped addresses, done bytes converted
+  // only in the epilogue (see the forward kernel: one memory round trip)
   float dho = 0.f, ai = 0.f, ag = 0.f, af = 0.f, ao = 0.f, cc = 0.f, cpv = 0.f,
-        dci = 0.f, kf = 0.f, knext = 1.f;
-  if (eok) {
-    const int64_t hj = static_cast<int64_t>(egr) * H + ej;
-    const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
+        dci = 0.f;
+  uint32_t kdone = static_cast<uint32_t>(B), ndone = static_cast<uint32_t>(B);
+  if (tid < 16 * RW) {
+    const int egc = egr < B ? egr : B - 1;
+    const int64_t hj = static_cast<int64_t>(egc) * H + ej;
+    const int64_t g0 = static_cast<int64_t>(egc) * 4 * H + ej;
     dho = dh_out_t[hj];
     ai = acts_t[g0];
     ag = acts_t[g0 + H];
@@ -205,8 +224,8 @@ __global__ __launch_bounds__(64 * NW) void lstm_bwd_step_kernel(
     cc = c_t[hj];
     cpv = c_prev[hj];
     if (dcarry_in) dci = dcarry_in[hj];
-    kf = done_t[egr] ? 0.f : 1.f;
-    if (done_next) knext = done_next[egr] ? 0.f : 1.f;
+    kdone = done_t[egc];
+    ndone = done_next ? done_next[egc] : 0u;
   }
   if (dg_next != nullptr) {
     // B[k = n][col = unit]: W_h[u0 + (l&15)][n0 + 4s + (l>>4)] (packed)
@@ -242,6 +261,8 @@ __global__ __launch_bounds__(64 * NW) void lstm_bwd_step_kernel(
     __syncthreads();
   }
   if (eok) {
+    const float kf = kdone ? 0.f : 1.f;
+    const float knext = ndone ? 0.f : 1.f;
     const float rec = dg_next != nullptr ? r_s[er][eu] : 0.f;
     const int64_t hj = static_cast<int64_t>(egr) * H + ej;
     const int64_t g0 = static_cast<int64_t>(egr) * 4 * H + ej;
