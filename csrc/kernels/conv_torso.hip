@@ -1675,8 +1675,8 @@ namespace {
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-// Compiled geometries: the IMPALA frame (72x96) and the Doom frame (72x128)
-// at every torso stage.  f(IC<H>, IC<W>, IC<R>) is called with the matching
+// Compiled geometries: the IMPALA frame (72x96), the Doom frame (72x128) and
+// the Atari frame (84x84: BASELINE config #2) at every torso stage.  f(IC<H>, IC<W>, IC<R>) is called with the matching
 // compile-time geometry, or with zeros (runtime shapes).
 template <int HH, int WW, int RR, typename F>
 bool geo_try(int H, int W, int R, F& f) {
@@ -1696,15 +1696,19 @@ void with_geo(int H, int W, int R, F&& f) {
     if constexpr (STAGE == kConv1) {
       if (geo_try<72, 96, RF::rows(72, 96)>(H, W, R, f)) return;
       if (geo_try<72, 128, RF::rows(72, 128)>(H, W, R, f)) return;
+      if (geo_try<84, 84, RF::rows(84, 84)>(H, W, R, f)) return;
     } else if constexpr (STAGE == kStage1) {
       if (geo_try<36, 48, RF::rows(36, 48)>(H, W, R, f)) return;
       if (geo_try<36, 64, RF::rows(36, 64)>(H, W, R, f)) return;
+      if (geo_try<42, 42, RF::rows(42, 42)>(H, W, R, f)) return;
     } else if constexpr (STAGE == kStage2) {
       if (geo_try<18, 24, RF::rows(18, 24)>(H, W, R, f)) return;
       if (geo_try<18, 32, RF::rows(18, 32)>(H, W, R, f)) return;
+      if (geo_try<21, 21, RF::rows(21, 21)>(H, W, R, f)) return;
     } else {
       if (geo_try<9, 12, RF::rows(9, 12)>(H, W, R, f)) return;
       if (geo_try<9, 16, RF::rows(9, 16)>(H, W, R, f)) return;
+      if (geo_try<11, 11, RF::rows(11, 11)>(H, W, R, f)) return;
     }
   }
   f(IC<0>{}, IC<0>{}, IC<0>{});

@@ -227,49 +227,53 @@ def test_deep_torso_matches_fp32_reference(cuda, shape):
     assert c_hip > min(0.99, c_tbf - 0.01), (n, c_hip, c_tbf)
 
 
-@pytest.mark.parametrize('frame', [(72, 96), (72, 128)])
+@pytest.mark.parametrize('frame', [(72, 96, 3), (72, 128, 3), (84, 84, 4)])
 def test_specialized_geometry_matches_generic(cuda, frame):
-  """Compile-time-geometry kernels (IMPALA 72x96 and Doom 72x128 stages) give
-  the same results as the runtime-geometry kernels."""
+  """Compile-time-geometry kernels (IMPALA 72x96, Doom 72x128 and Atari
+  84x84x4 stages, the last with odd 21 / 11 maps and a pool pad-before of 1)
+  give the same results as the runtime-geometry kernels."""
   C = _C()
   torch.manual_seed(7)
   N = 2
-  H0, W0 = frame
-  frames = torch.randint(0, 256, (N, H0, W0, 3), device=cuda, dtype=torch.uint8)
-  w1 = torch.randn(3, 3, 3, 16, device=cuda) * 0.2
+  H0, W0, CH = frame
+  frames = torch.randint(0, 256, (N, H0, W0, CH), device=cuda, dtype=torch.uint8)
+  w1 = torch.randn(3, 3, CH, 16, device=cuda) * 0.2
   b16 = torch.randn(16, device=cuda) * 0.1
   b32 = torch.randn(32, device=cuda) * 0.1
   w16 = bf(torch.randn(3, 3, 16, 16, device=cuda) * 0.1)
   w1632 = bf(torch.randn(3, 3, 16, 32, device=cuda) * 0.1)
   w32 = bf(torch.randn(3, 3, 32, 32, device=cuda) * 0.1)
-  H1, W1 = H0 // 2, W0 // 2
-  H2, W2 = H1 // 2, W1 // 2
+  half = lambda n: (n + 1) // 2
+  pb = lambda n: max((half(n) - 1) * 2 + 3 - n, 0) // 2  # SAME pool pad-before
+  H1, W1 = half(H0), half(W0)
+  H2, W2 = half(H1), half(W1)
   x16 = torch.randn(N, H1, W1, 16, device=cuda).to(torch.bfloat16)
   x32 = torch.randn(N, H2, W2, 32, device=cuda).to(torch.bfloat16)
-  x9 = torch.randn(N, H2 // 2, W2 // 2, 32, device=cuda).to(torch.bfloat16)
+  x9 = torch.randn(N, half(H2), half(W2), 32, device=cuda).to(torch.bfloat16)
 
   def run():
     out = []
-    p1, a1 = C.conv1_pool_fwd(frames, w1, b16, 0, 0)
+    p1, a1 = C.conv1_pool_fwd(frames, w1, b16, pb(H0), pb(W0))
     out += [p1, a1]
     out.append(C.res_conv_fwd(x16, w16, b16, x16, False))
     out.append(C.res_conv_fwd(x32, w32, b32, None, False))
     out.append(C.res_conv_fwd(x9, w32, b32, x9, True))
     out.append(C.res_conv_fwd(x16, w16, b16, None, True, True))
     out.append(C.res_conv_fwd(x32, w32, b32, x32, False, False))
-    p2, a2 = C.conv_pool_fwd(x16, w1632, b32, 0, 0)
-    p3, a3 = C.conv_pool_fwd(x32, w32, b32, 0, 0)
+    p2, a2 = C.conv_pool_fwd(x16, w1632, b32, pb(H1), pb(W1))
+    p3, a3 = C.conv_pool_fwd(x32, w32, b32, pb(H2), pb(W2))
     out += [p2, a2, p3, a3]
     for x, w, b in ((x16, w16, b16), (x32, w32, b32), (x9, w32, b32)):
       dw, db = torch.zeros_like(w, dtype=torch.float32), torch.zeros_like(b)
       out += [C.res_conv_bwd(x, x, x, w, dw, db), dw, db]
       dw2, db2 = torch.zeros_like(dw), torch.zeros_like(db)
       out += [C.res_conv_bwd(x, x, None, w, dw2, db2, False), dw2, db2]
-    for (pp, aa, x, w, b) in ((p2, a2, x16, w1632, b32), (p3, a3, x32, w32, b32)):
+    for (pp, aa, x, w, b, hh, ww) in ((p2, a2, x16, w1632, b32, H1, W1),
+                                      (p3, a3, x32, w32, b32, H2, W2)):
       dw, db = torch.zeros_like(w, dtype=torch.float32), torch.zeros_like(b)
-      out += [C.pool_conv_bwd(pp, aa, x, w, dw, db, True, 0, 0), dw, db]
+      out += [C.pool_conv_bwd(pp, aa, x, w, dw, db, True, pb(hh), pb(ww)), dw, db]
     dw1, db1 = torch.zeros_like(w1), torch.zeros_like(b16)
-    C.conv1_pool_bwd(p1, a1, frames, dw1, db1, 0, 0)
+    C.conv1_pool_bwd(p1, a1, frames, dw1, db1, pb(H0), pb(W0))
     out += [dw1, db1]
     return out
 
