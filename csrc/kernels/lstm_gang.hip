@@ -165,7 +165,13 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
       h[e] = h0[er * H + ej + e];
     }
   }
-  float xv[2][4] = {}, ekeep = 0.f;
+  // The step's done byte is fetched raw with its xw operands one step ahead
+  // and tested only where it is used: a test next to the load (or a fresh
+  // done load per step) made the wave wait for the load - and, with one
+  // vmcnt for loads and stores, for all of its step's output stores - before
+  // its next sweep could start.  Nonzero default (B): rows >= B read as done.
+  float xv[2][4] = {};
+  uint32_t dnext = static_cast<uint32_t>(B);
   auto fetch = [&](int t) {
     if (live) {
       const int64_t g0 = (static_cast<int64_t>(t) * B + er) * 4 * H + ej;
@@ -175,19 +181,21 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
         xv[0][g] = x2.x;
         xv[1][g] = x2.y;
       }
-      ekeep = done[t * B + er] ? 0.f : 1.f;
+      dnext = done[t * B + er];
     }
   };
   fetch(0);
   const int arow = lane & 15, ak = 8 * (lane >> 4);
   for (int t = 0; t < T; ++t) {
-    // ---- LDS A image: keep_t * h_{t-1}, bf16
+    // ---- LDS A image: keep_t * h_{t-1}, bf16 (the A-image row of this
+    // thread is its epilogue row er: keep_t = live && !done[t][er])
     bool fail = false;
+    const uint32_t dcur = dnext;
     {
       const int sr = tid >> 4, u0 = 16 * (tid & 15);
-      const bool keep = sr < B && !done[t * B + (sr < B ? sr : 0)];
       uint32_t v[8];
       if (t == 0) {
+        const bool keep = live && dcur == 0u;
         const float* hr = h0 + (sr < B ? sr : 0) * H + u0;
 #pragma unroll
         for (int p = 0; p < 8; ++p)
@@ -195,7 +203,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
       } else {
         fail = !sweep<8>(xbuf + ((t - 1) & 1) * kFSlot + 8 * tid,
                          static_cast<unsigned>(t), v, err, nap);
-        if (!keep) {
+        if (!(live && dcur == 0u)) {
 #pragma unroll
           for (int p = 0; p < 8; ++p) v[p] = 0u;
         }
@@ -227,6 +235,7 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_gang_kernel(
       const float4 ga = *reinterpret_cast<const float4*>(&g_s[er][8 * q]);
       const float4 gb = *reinterpret_cast<const float4*>(&g_s[er][8 * q + 4]);
       const float gv[2][4] = {{ga.x, ga.y, ga.z, ga.w}, {gb.x, gb.y, gb.z, gb.w}};
+      const float ekeep = dcur ? 0.f : 1.f;
       float hn[2], gi[2], gg[2], gf[2], go[2], hprev[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -295,8 +304,10 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     live[e] = r0 + e < B;
     if (live[e] && dc_last) carry[e] = dc_last[(r0 + e) * H + ej];
   }
+  // done bytes fetched raw and tested in the epilogue (see the forward)
   float dho[2] = {}, ai[2] = {}, ag[2] = {}, af[2] = {}, ao[2] = {}, cc[2] = {},
-        cpv[2] = {}, kf[2] = {}, knext[2] = {1.f, 1.f};
+        cpv[2] = {};
+  uint32_t kraw[2] = {0u, 0u}, nraw[2] = {0u, 0u};
   auto fetch = [&](int t) {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -311,8 +322,8 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
       ao[e] = acts[g0 + 3 * H];
       cc[e] = cs[hj];
       cpv[e] = t > 0 ? cs[hj - static_cast<int64_t>(B) * H] : c0[r * H + ej];
-      kf[e] = done[t * B + r] ? 0.f : 1.f;
-      knext[e] = t + 1 < T ? (done[(t + 1) * B + r] ? 0.f : 1.f) : 1.f;
+      kraw[e] = done[t * B + r];
+      nraw[e] = t + 1 < T ? done[(t + 1) * B + r] : 0u;
     }
   };
   fetch(T - 1);
@@ -336,12 +347,14 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
     for (int e = 0; e < 2; ++e) {
       float dgv[4] = {0.f, 0.f, 0.f, 0.f};
       if (live[e]) {
-        const float dh = dho[e] + knext[e] * rec[e];
+        const float kf = kraw[e] ? 0.f : 1.f;
+        const float knext = nraw[e] ? 0.f : 1.f;
+        const float dh = dho[e] + knext * rec[e];
         const float tc = tanhf(cc[e]);
         const float dc = carry[e] + dh * ao[e] * (1.f - tc * tc);
         dgv[0] = dc * ag[e] * ai[e] * (1.f - ai[e]);
         dgv[1] = dc * ai[e] * (1.f - ag[e] * ag[e]);
-        dgv[2] = dc * kf[e] * cpv[e] * af[e] * (1.f - af[e]);
+        dgv[2] = dc * kf * cpv[e] * af[e] * (1.f - af[e]);
         dgv[3] = dh * tc * ao[e] * (1.f - ao[e]);
         const int64_t g0 = (static_cast<int64_t>(t) * B + r0 + e) * 4 * H + ej;
 #pragma unroll
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_gang_kernel(
           dg[g0 + g * H] = dgv[g];
           if (dg16) dg16[g0 + g * H] = __float2bfloat16(dgv[g]);
         }
-        carry[e] = dc * af[e] * kf[e];
+        carry[e] = dc * af[e] * kf;
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) d_s[par][r0 + e][g * kU + ul] = f2bf(dgv[g]);
