@@ -1367,6 +1367,53 @@ __global__ __launch_bounds__(256) void frames_f32_kernel(const uint8_t* __restri
   }
 }
 
+// Same conversion, 1024 pixels per workgroup step: the tile's Cs * 1024
+// bytes come in as coalesced dword loads (3 per thread for RGB) through LDS,
+// then thread i writes pixels i + 256 k (k < 4), so each wave stores 1 KB
+// contiguously.  (Per-pixel byte loads were the one-pixel kernel's limit;
+// four pixels per thread straight from registers made the stores 64 B
+// apart across the wave.)  Needs a 4-byte aligned source.
+__global__ __launch_bounds__(256) void frames_f32_tile_kernel(const uint8_t* __restrict__ x,
+                                                              f4* __restrict__ y, int64_t P,
+                                                              int Cs) {
+  __shared__ float lut[256];
+  __shared__ uint32_t raw[1024];  // Cs * 1024 bytes, Cs <= 4
+  lut[threadIdx.x] = static_cast<float>(static_cast<double>(threadIdx.x) / 255.0);
+  const int64_t ntiles = (P + 1023) / 1024;
+  const uint8_t* rb = reinterpret_cast<const uint8_t*>(raw);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t p0 = t * 1024;
+    const int np = static_cast<int>(P - p0 < 1024 ? P - p0 : 1024);
+    const int nbytes = np * Cs;
+    const uint8_t* src = x + p0 * Cs;
+    __syncthreads();  // previous tile's LDS reads (and the table) done
+    for (int d = threadIdx.x; 4 * d < nbytes; d += 256) {
+      uint32_t v;
+      if (4 * d + 4 <= nbytes) {
+        v = reinterpret_cast<const uint32_t*>(src)[d];
+      } else {
+        v = 0;
+        for (int b = 0; 4 * d + b < nbytes; ++b) v |= static_cast<uint32_t>(src[4 * d + b]) << (8 * b);
+      }
+      raw[d] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < np) {
+        const uint8_t* q = rb + i * Cs;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        v[0] = lut[q[0]];
+        if (Cs > 1) v[1] = lut[q[1]];
+        if (Cs > 2) v[2] = lut[q[2]];
+        if (Cs > 3) v[3] = lut[q[3]];
+        y[p0 + i] = v;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void relu_mask_kernel(f4* __restrict__ dy,
                                                         const f4* __restrict__ ref,
                                                         int64_t n4) {
@@ -1721,6 +1768,13 @@ bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, i
 }
 
 void frames_f32_launch(const uint8_t* x, float* y, int64_t P, int Cs, hipStream_t s) {
+  static const bool tiled = env_knob("SA_FRAMES_TILE", 1) != 0;  // 0: one pixel per thread
+  if (tiled && (reinterpret_cast<uintptr_t>(x) & 3) == 0 && Cs >= 1 && Cs <= 4) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((P + 1023) / 1024, 8192));
+    hipLaunchKernelGGL(frames_f32_tile_kernel, dim3(blocks), dim3(256), 0, s, x,
+                       reinterpret_cast<f4*>(y), P, Cs);
+    return;
+  }
   int64_t blocks = std::min<int64_t>((P + 255) / 256, 8192);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(frames_f32_kernel, dim3(blocks), dim3(256), 0, s, x,

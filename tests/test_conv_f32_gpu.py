@@ -377,7 +377,8 @@ def test_wino_conv_pool_declines_other_shapes(cuda):
 
 
 @pytest.mark.parametrize('shape', [(3232 // 101, 72, 96, 3), (3, 5, 7, 3), (2, 84, 84, 4),
-                                   (3, 5, 7, 1), (2, 6, 5, 2)])
+                                   (3, 5, 7, 1), (2, 6, 5, 2),
+                                   (1300, 72, 96, 3)])  # > 8192 tiles: grid stride
 @pytest.mark.parametrize('misaligned', [False, True])
 def test_frames_f32_is_exact_division(cuda, shape, misaligned):
   """uint8 frames -> the 4-channel fp32 x / 255 image: bitwise torch's
