@@ -1536,9 +1536,10 @@ int num_cus() {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+    if (cus <= 0) cus = 256;  // MI355X
   }
   return cus;
 }
@@ -1554,10 +1555,11 @@ int grid_for(int ntiles, size_t smem, int per_cu_cap) {
 
 template <typename K>
 void set_smem(K kernel, size_t bytes) {
-  if (bytes > 64 * 1024)
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                        static_cast<int>(bytes));
+  if (bytes > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(bytes)) != hipSuccess)
+    (void)hipGetLastError();  // the launch itself reports an LDS request it cannot meet
 }
 
 // ----- tile-height rules (constexpr: the same rule picks the compiled
