@@ -316,13 +316,15 @@ void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                        stream, w, w4, wt);
 }
 
-// Default 4 (working blocks on 2 of the 8 XCDs): measured 469 -> 448 us fwd
-// and 739 -> 724 us bwd per T=101 unroll at B=32 (tools/micro/lstm_probe.py,
-// two runs); 8 (one XCD) oversubscribes its 32 CUs in the fwd (533 us).
+// Default 2 (working blocks on 4 of the 8 XCDs).  Round 1 measured 4 best
+// (469 -> 448 us fwd, 739 -> 724 us bwd per T=101 unroll vs 1; 8 = one XCD
+// oversubscribes its 32 CUs); with every operand load issued up front
+// (round 4) the full fp32 step is 9.650 / 9.654 ms at 2 vs 9.782 at 4, 9.664
+// at 1 and 9.650-9.685 at 3 (SA_LSTM_XPACK sweep on one box).
 static int g_xpack = [] {
   const char* e = std::getenv("SA_LSTM_XPACK");
-  const int v = e ? std::atoi(e) : 4;
-  return v >= 1 && v <= 8 ? v : 4;
+  const int v = e ? std::atoi(e) : 2;
+  return v >= 1 && v <= 8 ? v : 2;
 }();
 // 16 batch rows per step workgroup (twice the workgroups, each streaming
 // half the packed h / dG): fp32 learner 13.01/13.05 -> 12.75/12.81 ms per
