@@ -333,6 +333,12 @@ static bool g_rows16 = [] {
   const char* e = std::getenv("SA_LSTM_ROWS");
   return !(e && std::atoi(e) == 32);
 }();
+// backward packing (SA_LSTM_XPACK_BWD; 0 = the forward's)
+static int g_xpack_bwd = [] {
+  const char* e = std::getenv("SA_LSTM_XPACK_BWD");
+  const int v = e ? std::atoi(e) : 0;
+  return v >= 1 && v <= 8 ? v : 0;
+}();
 int lstm_xpack(int v) {
   const int old = g_xpack;
   if (v >= 1 && v <= 8) g_xpack = v;
@@ -371,7 +377,7 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
                           const float* dcarry_in, float* dcarry_out,
                           float* dg_t, float* dg_pk_out, void* dg16_t, int B,
                           int H, hipStream_t stream) {
-  const int xp = g_xpack;
+  const int xp = g_xpack_bwd ? g_xpack_bwd : g_xpack;
   dim3 grid(H / 16 * xp, (B + 31) / 32);
   __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
   static const bool w8 = [] {
