@@ -463,10 +463,15 @@ bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int ld
   }();
   const int64_t abytes = (ta ? static_cast<int64_t>(K) * lda : static_cast<int64_t>(M) * lda) * 4;
   const int64_t bbytes = (tb ? static_cast<int64_t>(N) * ldb : static_cast<int64_t>(K) * ldb) * 4;
-  if (bl && rm == 1 && (!ta || M % 4 == 0) && (tb || N % 4 == 0) && abytes < 0xFFFFFF00ll &&
+  if (bl && (!ta || M % 4 == 0) && (tb || N % 4 == 0) && abytes < 0xFFFFFF00ll &&
       bbytes < 0xFFFFFF00ll) {
-    auto k = ta ? (tb ? gemm_f32_bl_kernel<1, true, true> : gemm_f32_bl_kernel<1, true, false>)
-                : (tb ? gemm_f32_bl_kernel<1, false, true> : gemm_f32_bl_kernel<1, false, false>);
+    auto k = rm == 2
+                 ? (ta ? (tb ? gemm_f32_bl_kernel<2, true, true> : gemm_f32_bl_kernel<2, true, false>)
+                       : (tb ? gemm_f32_bl_kernel<2, false, true>
+                             : gemm_f32_bl_kernel<2, false, false>))
+                 : (ta ? (tb ? gemm_f32_bl_kernel<1, true, true> : gemm_f32_bl_kernel<1, true, false>)
+                       : (tb ? gemm_f32_bl_kernel<1, false, true>
+                             : gemm_f32_bl_kernel<1, false, false>));
     hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, a);
   } else if (rm == 2)
     hipLaunchKernelGGL(gemm_f32_kernel<2>, grid, dim3(256), 0, stream, a);
