@@ -46,15 +46,16 @@ __device__ __forceinline__ f4v mfma_f32(float a, float b, f4v c) {
 // keep_t * h_prev, the A operand of the dW_h = sum_t hpm_t^T dG_t GEMM.
 // RW: batch rows per workgroup (32, or 16 = half a packed row tile: twice
 // the workgroups, each streaming half of h)
-template <int H, int RW = 32>
-__global__ __launch_bounds__(512) void lstm_fwd_step_kernel(
+template <int H, int RW = 32, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void lstm_fwd_step_kernel(
     const float* __restrict__ xw_t, const float* __restrict__ h_pk_in,
     const float* __restrict__ h_prev, const float* __restrict__ c_prev,
     const uint8_t* __restrict__ done_t, const float* __restrict__ w4,
     float* __restrict__ h_t, float* __restrict__ h_pk_out,
     float* __restrict__ c_t, float* __restrict__ acts_t,
     float* __restrict__ hpm_t, int B, int xpack) {
-  constexpr int NW = 8;
+  static_assert(NW == 8 || NW == 4, "waves per workgroup");
+  static_assert(16 * RW <= 64 * NW, "one reduce thread per output");
   constexpr int KW = H / NW;     // k per wave
   constexpr int NS = KW / 4;     // mfma k-steps per wave
   __shared__ f4v red[NW][2][64];  // per wave, per row tile, per lane
@@ -351,6 +352,18 @@ void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           float* h_pk_out, float* c_t, float* acts_t,
                           float* hpm_t, int B, int H, hipStream_t stream) {
   const int xp = g_xpack;
+  // SA_LSTM_FWD_NW=4: four waves per workgroup (K split four ways)
+  static const bool w4w = [] {
+    const char* e = std::getenv("SA_LSTM_FWD_NW");
+    return e && std::atoi(e) == 4;
+  }();
+  if (H == 256 && g_rows16 && w4w) {
+    dim3 grid16(H / 4 * xp, (B + 15) / 16);
+    hipLaunchKernelGGL((lstm_fwd_step_kernel<256, 16, 4>), grid16, dim3(256), 0, stream,
+                       xw_t, h_pk_in, h_prev, c_prev, done_t, w4, h_t, h_pk_out,
+                       c_t, acts_t, hpm_t, B, xp);
+    return;
+  }
   if (H == 256 && g_rows16) {
     dim3 grid16(H / 4 * xp, (B + 15) / 16);
     hipLaunchKernelGGL((lstm_fwd_step_kernel<256, 16>), grid16, dim3(512), 0, stream,
