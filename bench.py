@@ -37,32 +37,69 @@ import sys
 import time
 
 
+def _pdeathsig():
+  """preexec_fn of a rank (runs in the GPU-free child before it starts
+  python): the kernel SIGKILLs the rank if the launcher dies."""
+  import ctypes
+  import signal
+  try:
+    ctypes.CDLL('libc.so.6', use_errno=True).prctl(1, int(signal.SIGKILL))
+  except OSError:  # pragma: no cover - not Linux
+    pass
+
+
+def _gpu_shortfall(n, device, env):
+  """Message when `--gpus n` asks for more GPUs than are visible (sysfs +
+  *_VISIBLE_DEVICES only: this process never touches the GPU), else None.
+  A gloo rehearsal (SA_DIST_BACKEND=gloo) may share cards."""
+  if device == 'cpu' or env.get('SA_DIST_BACKEND') == 'gloo':
+    return None
+  import importlib.util
+  # the module file alone: the package __init__ would import torch
+  spec = importlib.util.spec_from_file_location('_sa_affinity', os.path.join(
+      os.path.dirname(os.path.abspath(__file__)), 'scalable_agent_amd',
+      'parallel', 'affinity.py'))
+  aff = importlib.util.module_from_spec(spec)
+  spec.loader.exec_module(aff)
+  have = aff.visible_gpu_count(env.get('SA_SYSFS_ROOT', '/sys'), env)
+  if have is None or have >= n:
+    return None
+  return ('bench.py: --gpus %d but only %d GPU(s) are visible (KFD topology '
+          'and *_VISIBLE_DEVICES); one rank per GPU over RCCL needs %d '
+          'distinct GPUs (SA_DIST_BACKEND=gloo rehearses ranks sharing a '
+          'card)' % (n, have, n))
+
+
 def _self_launch(argv):
   """`--gpus N` (N>1) with no WORLD_SIZE in the env: run N ranks as child
-  processes of this (GPU-free) launcher.  Returns the exit code."""
+  processes of this (GPU-free) launcher.  Returns the exit code.
+
+  Lifetime: each rank runs in its own process group (so a kill reaches its
+  children too) with PR_SET_PDEATHSIG, so ranks never outlive the launcher;
+  SIGTERM / SIGINT to the launcher kill every rank group first.  The limit
+  (SA_BENCH_TIMEOUT_S, default 540 s) stays under a 600 s driver timeout.
+  Rank 0's stdout goes to a file and its JSON line is relayed only when
+  every rank exits 0."""
   import signal
   import socket
   import subprocess
+  import tempfile
   ap = argparse.ArgumentParser(add_help=False)
   ap.add_argument('--gpus', type=int, default=1)
+  ap.add_argument('--device', default='auto')
   known, _ = ap.parse_known_args(argv)
   n = known.gpus
+  msg = _gpu_shortfall(n, known.device, os.environ)
+  if msg:
+    sys.stderr.write(msg + '\n')
+    return 2
   s = socket.socket()
   s.bind(('127.0.0.1', 0))
   port = s.getsockname()[1]
   s.close()
-  limit = float(os.environ.get('SA_BENCH_TIMEOUT_S', '1500'))
+  limit = float(os.environ.get('SA_BENCH_TIMEOUT_S', '540'))
   procs = []
-  for r in range(n):
-    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-               LOCAL_WORLD_SIZE=str(n), GROUP_RANK='0',
-               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
-    # rank 0 owns stdout (the one JSON line); the others' stdout is dropped
-    procs.append(subprocess.Popen(
-        [sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-        stdout=None if r == 0 else subprocess.DEVNULL,
-        start_new_session=True))
+  out0 = tempfile.TemporaryFile(mode='w+')
 
   def kill_all():
     for p in procs:
@@ -74,31 +111,55 @@ def _self_launch(argv):
     for p in procs:
       p.wait()
 
-  t0 = time.time()
-  last_note = t0
-  while True:
-    codes = [p.poll() for p in procs]
-    bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-    if bad:
-      r, c = bad[0]
-      sys.stderr.write('bench.py launcher: rank %d exited with %d; stopping '
-                       'the other ranks\n' % (r, c))
-      kill_all()
-      return c if c > 0 else 1
-    if all(c == 0 for c in codes):
-      return 0
-    now = time.time()
-    if now - t0 > limit:
-      sys.stderr.write('bench.py launcher: ranks still running after %.0f s; '
-                       'killing them\n' % limit)
-      kill_all()
-      return 124
-    if now - last_note > 60:
-      last_note = now
-      sys.stderr.write('bench.py launcher: %d/%d ranks running (%.0f s)\n' %
-                       (sum(c is None for c in codes), n, now - t0))
-      sys.stderr.flush()
-    time.sleep(0.2)
+  def on_signal(signum, _frame):
+    sys.stderr.write('bench.py launcher: signal %d; killing the ranks\n' %
+                     signum)
+    kill_all()
+    os._exit(128 + signum)
+
+  signal.signal(signal.SIGTERM, on_signal)
+  signal.signal(signal.SIGINT, on_signal)
+  try:
+    for r in range(n):
+      env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r),
+                 WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK='0',
+                 MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+      env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+      # rank 0 owns the one JSON line; the others' stdout is dropped
+      procs.append(subprocess.Popen(
+          [sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+          stdout=out0 if r == 0 else subprocess.DEVNULL,
+          start_new_session=True, preexec_fn=_pdeathsig))
+    t0 = time.time()
+    last_note = t0
+    while True:
+      codes = [p.poll() for p in procs]
+      bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+      if bad:
+        r, c = bad[0]
+        sys.stderr.write('bench.py launcher: rank %d exited with %d; '
+                         'stopping the other ranks\n' % (r, c))
+        kill_all()
+        return c if c > 0 else 1
+      if all(c == 0 for c in codes):
+        out0.seek(0)
+        sys.stdout.write(out0.read())
+        sys.stdout.flush()
+        return 0
+      now = time.time()
+      if now - t0 > limit:
+        sys.stderr.write('bench.py launcher: ranks still running after '
+                         '%.0f s; killing them\n' % limit)
+        kill_all()
+        return 124
+      if now - last_note > 60:
+        last_note = now
+        sys.stderr.write('bench.py launcher: %d/%d ranks running (%.0f s)\n'
+                         % (sum(c is None for c in codes), n, now - t0))
+        sys.stderr.flush()
+      time.sleep(0.2)
+  finally:
+    kill_all()
 
 
 def _wants_self_launch(argv):
@@ -322,6 +383,9 @@ def main():
   ap.add_argument('--pipeline_chunks', type=int, default=1,
                   help='time chunks of the torso || LSTM pipeline (1 = off)')
   args = ap.parse_args()
+  if args.torso == 'shallow' and args.dtype == 'bf16' and args.backend != 'torch':
+    raise SystemExit('bench.py: --dtype bf16 --torso shallow: the shallow '
+                     'torso has exact-fp32 HIP kernels only')
 
   if args.device in ('auto', 'cuda') or args.device.startswith('cuda:'):
     if torch.cuda.device_count() > 0:  # does not initialise the GPU
@@ -329,6 +393,16 @@ def main():
       # node, before any pinned allocation (sysfs only; no-op if unknown)
       parallel.pin_to_gpu_numa(parallel.world_info()[2] %
                                torch.cuda.device_count())
+  world_env = parallel.world_info()[1]
+  if (world_env > 1 and args.device != 'cpu' and
+      os.environ.get('SA_DIST_BACKEND') != 'gloo'):
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world_env)))
+    have = torch.cuda.device_count()  # does not initialise the GPU
+    if have < local_world:
+      raise SystemExit(
+          'bench.py: %d ranks on this node but only %d visible GPU(s); RCCL '
+          'needs one distinct GPU per rank (SA_DIST_BACKEND=gloo rehearses '
+          'ranks sharing a card)' % (local_world, have))
   rank, world, local = parallel.init_distributed()
   if args.gpus != world:
     raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' %
@@ -355,7 +429,8 @@ def main():
 
   main_res = measure(args, args.dtype, device, backend, rank, world)
   extra = None
-  if args.dtype == 'fp32' and args.also_bf16 and backend == 'hip':
+  if (args.dtype == 'fp32' and args.also_bf16 and backend == 'hip' and
+      args.torso == 'deep'):  # the shallow torso has fp32 kernels only
     extra = measure(args, 'bf16', device, backend, rank, world)
 
   def fps(r):
@@ -395,6 +470,8 @@ def main():
                      'loss_finite': extra['loss_finite'],
                      'learner_health': extra['health'],
                      'h2d_slab': extra['h2d_slab']}
+  rec = None
+  if rank == 0:
     rec = {
         'metric': METRIC, 'value': round(value, 1), 'unit': 'env-frames/s',
         'n_gpus': world if device.type == 'cuda' else 0,
@@ -406,6 +483,14 @@ def main():
         'data': 'synthetic (random uint8 frames, random-init weights)',
         'config': cfg,
     }
+  if world > 1:
+    # every rank got here (its measurements finished) before rank 0 reports:
+    # a rank that failed earlier never joins, so no line is printed
+    done = torch.ones(1, device=device if device.type == 'cuda' else 'cpu')
+    torch.distributed.all_reduce(done)
+    if int(done.item()) != world:
+      raise SystemExit('bench.py: not every rank finished')
+  if rank == 0:
     print(json.dumps(rec), flush=True)
   parallel.cleanup()
 

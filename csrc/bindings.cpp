@@ -60,6 +60,18 @@ void rmsprop(at::Tensor w, at::Tensor g, at::Tensor ms, at::Tensor mom,
                      (float)gscale, gp, ep, cur_stream());
 }
 
+void err_poison(at::Tensor slot, at::Tensor err) {
+  SA_CHECK(slot); SA_CHECK_F32(slot); SA_CHECK_CUDA(err);
+  TORCH_CHECK(slot.numel() >= 1, "sentinel slot must hold one element");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 2,
+              "err must be the int32 error words");
+  TORCH_CHECK(slot.device() == err.device(), "slot and err on one device");
+  const c10::DeviceGuard dguard(slot.device());
+  sa::err_poison_launch(slot.data_ptr<float>(),
+                        reinterpret_cast<unsigned*>(err.data_ptr<int>()),
+                        cur_stream());
+}
+
 std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
                                     at::Tensor actions, at::Tensor rewards,
                                     at::Tensor done, at::Tensor values,
@@ -332,6 +344,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("decay"), pybind11::arg("momentum"), pybind11::arg("eps"),
         pybind11::arg("guard") = pybind11::none(),
         pybind11::arg("lstm_err") = pybind11::none(), pybind11::arg("gscale") = 1.0);
+  m.def("err_poison", &err_poison);
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd, pybind11::arg("xw"), pybind11::arg("done"),
         pybind11::arg("c0"), pybind11::arg("h0"), pybind11::arg("w_h"),

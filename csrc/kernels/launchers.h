@@ -17,6 +17,10 @@ void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     float eps, float gscale, int* guard, unsigned* lstm_err,
                     hipStream_t stream);
 
+// NaN into *slot when err[0] | err[1] is set (the DP guard: one rank's
+// fault makes every rank's finite check skip the same step).
+void err_poison_launch(float* slot, unsigned* err, hipStream_t stream);
+
 // ---- vtrace_loss.hip -------------------------------------------------------
 // Fused V-trace (from logits) + IMPALA loss + analytic gradients.
 // behaviour/target logits [T,B,A] f32, actions [T,B] i64, rewards/values

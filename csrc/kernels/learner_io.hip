@@ -123,13 +123,19 @@ __global__ __launch_bounds__(kHeadThreads) void learner_head_fwd_kernel(
   const int lane = tid & 63;
   const int wave = tid >> 6;
   // this column's value head and its PopArt statistics (identity without)
-  const int kt = tk.task != nullptr ? static_cast<int>(tk.task[b]) : 0;
+  // a task id outside [0, K) reads head 0 (no out-of-bounds access) with a
+  // NaN sigma: the column's gradients turn NaN and the RMSProp step guard
+  // drops the update (counted in skipped_updates) instead of training on it
+  const int64_t kt_raw = tk.task != nullptr ? tk.task[b] : 0;
+  const bool kt_bad = kt_raw < 0 || kt_raw >= tk.K;
+  const int kt = kt_bad ? 0 : static_cast<int>(kt_raw);
   float sig = 1.f, mu = 0.f;
   if (tk.mu != nullptr) {
     mu = tk.mu[kt];
     const float var = fmaxf(tk.nu[kt] - mu * mu, kPopArtSigmaMin * kPopArtSigmaMin);
     sig = fminf(fmaxf(sqrtf(var), kPopArtSigmaMin), kPopArtSigmaMax);
   }
+  if (kt_bad) sig = __builtin_nanf("");
   const float rsig = 1.f / sig;
 
   HEAD_TRACE(0);
@@ -435,7 +441,8 @@ __global__ __launch_bounds__(256) void learner_head_bwd_kernel(
       if (c < A) {
         v = dlogits[static_cast<int64_t>(r) * A + c];
       } else {
-        const int kt = task != nullptr ? static_cast<int>(task[r % B]) : 0;
+        const int64_t kt = task != nullptr ? task[r % B] : 0;  // out of
+        // range: no column matches (the forward made this row NaN already)
         v = (c - A == kt) ? dvalues[r] : 0.f;
       }
     }

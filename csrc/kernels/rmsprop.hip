@@ -86,7 +86,28 @@ __global__ __launch_bounds__(256) void rmsprop_kernel(
   }
 }
 
+// Data-parallel step guard: run on every rank before the gradient
+// all-reduce.  When this device's sticky error words are set (a stale
+// recurrence or conv backward), a NaN goes into the flat gradient buffer's
+// reserved sentinel element; the all-reduce spreads it to every rank, whose
+// finite check then skips the SAME step (one rank's fault cannot leave the
+// others applying a sum that holds its stale gradients).  The words are left
+// for the local finite check to count and reset.
+__global__ void err_poison_kernel(float* __restrict__ slot,
+                                  unsigned* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  const unsigned e0 = __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned e1 = __hip_atomic_load((gu32*)(err + 1), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+  if ((e0 | e1) != 0u) slot[0] = __builtin_nanf("");
+}
+
 }  // namespace
+
+void err_poison_launch(float* slot, unsigned* err, hipStream_t stream) {
+  hipLaunchKernelGGL(err_poison_kernel, dim3(1), dim3(64), 0, stream, slot, err);
+}
 
 void rmsprop_launch(float* w, const float* g, float* ms, float* mom,
                     const int64_t* frames, int64_t n, float lr0,

@@ -183,7 +183,20 @@ def parse_flags(argv: Optional[List[str]] = None):
   flags, unknown = parser.parse_known_args(argv)
   if unknown:
     raise SystemExit('Unknown flags: %s' % ' '.join(unknown))
+  check_flags(flags)
   return flags
+
+
+def check_flags(flags):
+  """Rejects combinations the kernels do not implement (instead of quietly
+  running something else): the shallow torso has exact-fp32 HIP kernels
+  only, so `--dtype bf16 --torso shallow` on the HIP backend is refused."""
+  if (getattr(flags, 'dtype', 'fp32') == 'bf16' and
+      getattr(flags, 'torso', 'deep') == 'shallow' and
+      getattr(flags, 'backend', 'auto') != 'torch'):
+    raise SystemExit('--dtype bf16 --torso shallow: the shallow torso has no '
+                     'bf16 HIP kernels (its fp32 kernels would run); use '
+                     '--dtype fp32, the deep torso, or --backend torch')
 
 
 def default_flags(**overrides):

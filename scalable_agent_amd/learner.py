@@ -43,6 +43,7 @@ def compute_loss(agent, data, flags, use_fused=False, popart=None,
   instr = env_outputs.observation[1]
   task_ids = data.level_name if popart is not None else None
   if (use_fused and agent.fused_core_ready(instr) and
+      agent.num_actions <= 31 and
       agent.num_actions + agent.num_value_heads <= 64 and
       (agent.num_value_heads == 1 or task_ids is not None)):
     # HIP learner path: fused core + fused heads/V-trace/loss; same math.
@@ -243,6 +244,13 @@ class Learner:
 
   def _apply(self):
     if self.grad_sync is not None:
+      if self.opt.lstm_err is not None:
+        # a stale LSTM unroll / conv backward on THIS rank poisons the
+        # reduced gradient, so every rank's guard skips the same step and
+        # the replicas stay identical (the error words are counted locally)
+        from . import ops
+        s = self.flat.sentinel
+        ops.poison_on_error(self.flat.grads[s:s + 1], self.opt.lstm_err)
       with trace('allreduce'):
         self.grad_sync.all_reduce()
     with trace('optimizer'):

@@ -8,7 +8,7 @@ callers (models/layers.py, vtrace.py, losses.py, optim.py).
 """
 
 from ._ext import available, load, ext  # noqa: F401
-from .rmsprop import rmsprop_step  # noqa: F401
+from .rmsprop import poison_on_error, rmsprop_step  # noqa: F401
 from .vtrace_loss import vtrace_loss, vtrace_fused_forward  # noqa: F401
 from .lstm import lstm_unroll  # noqa: F401
 from .conv import torso_forward, linear_relu  # noqa: F401

@@ -20,3 +20,11 @@ def rmsprop_step(params, grads, ms, mom, frames, lr0, total_frames, decay,
   ext().rmsprop(params, grads, ms, mom, frames, float(lr0),
                 float(total_frames), float(decay), float(momentum),
                 float(epsilon), guard, lstm_err, float(grad_scale))
+
+
+def poison_on_error(slot, err):
+  """DP step guard (before the gradient all-reduce): NaN into `slot` (the
+  flat gradient buffer's reserved sentinel element) when this device's
+  sticky error words are set, so every rank's finite check skips the step."""
+  check_cuda(slot, err)
+  ext().err_poison(slot, err)

@@ -38,6 +38,10 @@ class FlatParams:
   ALIGN = 64  # elements; keeps every tensor 256-B aligned for vector loads
 
   def __init__(self, module):
+    # the buffer ends with ALIGN reserved elements that belong to no
+    # parameter: `sentinel` (their first) is where the data-parallel step
+    # guard writes a NaN that the gradient all-reduce carries to every rank
+    # (Learner._apply); the update leaves them at zero
     self.module = module
     self.named = [(n, p) for n, p in module.named_parameters()]
     device = self.named[0][1].device
@@ -46,6 +50,8 @@ class FlatParams:
     for _, p in self.named:
       offsets.append(off)
       off += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+    self.sentinel = off
+    off += self.ALIGN
     self.numel = off
     self.offsets = offsets
     self.params = torch.zeros(off, dtype=torch.float32, device=device)
@@ -157,5 +163,8 @@ class RMSProp:
     return {'ms': self.ms.detach().clone(), 'mom': self.mom.detach().clone()}
 
   def load_state_dict(self, sd):
-    self.ms.copy_(sd['ms'].to(self.ms.device))
-    self.mom.copy_(sd['mom'].to(self.mom.device))
+    # checkpoints written before the sentinel tail existed are ALIGN
+    # elements shorter; the tail's slots keep their initial values
+    for dst, key in ((self.ms, 'ms'), (self.mom, 'mom')):
+      src = sd[key].to(dst.device)
+      dst[:src.numel()].copy_(src)

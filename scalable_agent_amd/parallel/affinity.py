@@ -99,26 +99,54 @@ def visible_index(local_rank, env=None):
   return idx
 
 
-def numa_node_count(root='/sys'):
-  """Number of NUMA nodes with CPUs (1 when unknown)."""
+def cpu_numa_nodes(root='/sys'):
+  """Ids of the NUMA nodes that have CPUs (empty when unknown)."""
   base = os.path.join(root, 'devices/system/node')
   try:
     names = [n for n in os.listdir(base)
              if n.startswith('node') and n[4:].isdigit()]
   except OSError:
-    return 1
-  n = sum(1 for name in names
-          if parse_cpulist(_read(os.path.join(base, name, 'cpulist'))))
-  return max(1, n)
+    return set()
+  return {int(name[4:]) for name in names
+          if parse_cpulist(_read(os.path.join(base, name, 'cpulist')))}
 
 
-def auto_pin_wanted(local_world, root='/sys'):
+def numa_node_count(root='/sys'):
+  """Number of NUMA nodes with CPUs (1 when unknown)."""
+  return max(1, len(cpu_numa_nodes(root)))
+
+
+def visible_gpu_count(root='/sys', env=None):
+  """GPUs this process may use, from sysfs and the *_VISIBLE_DEVICES masks
+  only (no HIP call); None when the KFD topology is unreadable."""
+  env = os.environ if env is None else env
+  phys = len(gpu_pci_addresses(root))
+  if phys == 0 and not os.path.isdir(os.path.join(
+      root, 'class/kfd/kfd/topology/nodes')):
+    return None
+  n = phys
+  for var in ('ROCR_VISIBLE_DEVICES',
+              'HIP_VISIBLE_DEVICES' if env.get('HIP_VISIBLE_DEVICES')
+              else 'CUDA_VISIBLE_DEVICES'):
+    spec = env.get(var)
+    if spec is None:
+      continue
+    ids = [int(x) for x in spec.split(',') if x.strip().isdigit()]
+    n = len([i for i in ids if i < n])
+  return n
+
+
+def auto_pin_wanted(local_world, root='/sys', env=None):
   """'auto' NUMA pinning policy: pin a rank (and the actor / env processes
-  it forks, which inherit the mask) to its GPU's node only when the node's
-  ranks together cover every socket.  A single rank on a 2-socket box would
-  otherwise confine every CPU-bound actor to half of the machine."""
-  nodes = numa_node_count(root)
-  return nodes > 1 and local_world >= nodes
+  it forks, which inherit the mask) to its GPU's node only when the GPUs of
+  the node's ranks together sit on every NUMA node that has CPUs.  A single
+  rank on a 2-socket box, or two ranks whose GPUs both hang off socket 0,
+  would otherwise confine every CPU-bound actor to half of the machine."""
+  cpu_nodes = cpu_numa_nodes(root)
+  if len(cpu_nodes) <= 1:
+    return False
+  gpu_nodes = {gpu_numa_node(r, root, env) for r in range(local_world)}
+  return cpu_nodes <= gpu_nodes
 
 
 def gpu_numa_node(local_rank, root='/sys', env=None):

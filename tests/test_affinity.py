@@ -89,3 +89,23 @@ def test_auto_pin_only_when_ranks_cover_every_socket(tmp_path):
   assert affinity.auto_pin_wanted(8, root)
   assert affinity.numa_node_count(str(tmp_path / 'missing')) == 1
   assert not affinity.auto_pin_wanted(8, str(tmp_path / 'missing'))
+
+
+def test_auto_pin_needs_the_gpus_on_every_socket(tmp_path):
+  # two ranks whose GPUs both hang off socket 0: pinning would idle socket 1
+  _fake_sysfs(tmp_path, [(0x05, 0), (0x15, 0), (0x85, 1)])
+  root = str(tmp_path)
+  assert not affinity.auto_pin_wanted(2, root, env={})
+  assert affinity.auto_pin_wanted(3, root, env={})
+  # the visible mask decides which physical GPUs the ranks get
+  assert affinity.auto_pin_wanted(2, root, env={'HIP_VISIBLE_DEVICES': '0,2'})
+
+
+def test_visible_gpu_count(tmp_path):
+  _fake_sysfs(tmp_path, [(0x05, 0), (0x15, 0), (0x85, 1), (0x95, 1)])
+  root = str(tmp_path)
+  assert affinity.visible_gpu_count(root, env={}) == 4
+  assert affinity.visible_gpu_count(root, env={'HIP_VISIBLE_DEVICES': '1,3'}) == 2
+  assert affinity.visible_gpu_count(root, env={'ROCR_VISIBLE_DEVICES': '2'}) == 1
+  assert affinity.visible_gpu_count(root, env={'CUDA_VISIBLE_DEVICES': '0,7'}) == 1
+  assert affinity.visible_gpu_count(str(tmp_path / 'missing'), env={}) is None

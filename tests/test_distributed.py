@@ -119,3 +119,57 @@ def test_default_reduction_is_mean():
   single-learner equivalent of 8 ranks the summed gradient does not learn at
   the reference learning rate, the 1/N-scaled one does)."""
   assert flags_lib.default_flags().grad_reduce == 'mean'
+
+
+def _poison_worker(rank, world, port, result_path):
+  os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                    MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+  from scalable_agent_amd import parallel
+  parallel.init_distributed(backend='gloo')
+  f = flags_lib.default_flags(batch_size=B // world, unroll_length=T,
+                              torso='shallow')
+  learner = Learner(Agent(9, torso='shallow', frame_shape=SHAPE, seed=10), f,
+                    'cpu', world_size=world)
+  parallel.broadcast_params(learner.flat.params)
+  sync = learner.grad_sync
+  real = sync.all_reduce
+  state = {'poison': rank == 1}
+
+  def all_reduce():
+    # what ops.poison_on_error does on a GPU rank whose error words are set
+    if state['poison']:
+      learner.flat.grads[learner.flat.sentinel] = float('nan')
+      state['poison'] = False
+    real()
+
+  sync.all_reduce = all_reduce
+  full = make_synthetic_batch(B, T, SHAPE, 9, seed=7)
+  per = B // world
+  mine = _slice_batch(full, rank * per, (rank + 1) * per)
+  p0 = learner.flat.params.clone()
+  learner.step(mine)
+  skipped_first = torch.equal(learner.flat.params, p0)
+  consistent = parallel.param_checksum_consistent(learner.flat.params)
+  learner.step(mine)
+  torch.save({'skipped_first': skipped_first, 'consistent': consistent,
+              'applied_second': not torch.equal(learner.flat.params, p0),
+              'consistent2': parallel.param_checksum_consistent(
+                  learner.flat.params),
+              'skipped': learner.opt.skipped_steps,
+              'sentinel': float(learner.flat.params[learner.flat.sentinel])},
+             '%s.%d' % (result_path, rank))
+  parallel.cleanup()
+
+
+def test_poisoned_sentinel_skips_the_step_on_every_rank(tmp_path):
+  """The DP step guard's transport: a NaN in one rank's gradient sentinel
+  reaches every rank through the all-reduce, so all skip the same step and
+  the replicas stay identical; the next step applies everywhere."""
+  path = str(tmp_path / 'poison.pt')
+  mp.spawn(_poison_worker, args=(2, _free_port(), path), nprocs=2, join=True)
+  for r in (0, 1):
+    rec = torch.load('%s.%d' % (path, r), weights_only=True)
+    assert rec['skipped_first'] and rec['consistent']
+    assert rec['applied_second'] and rec['consistent2']
+    assert rec['skipped'] == 1
+    assert rec['sentinel'] == 0.0

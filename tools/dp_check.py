@@ -8,6 +8,12 @@ flat-gradient all-reduce (--grad_reduce=sum), and rank 0 writes the
 parameters; with WORLD_SIZE=1 the same script runs the whole batch on one
 learner.  Under the reference's sum losses both must give the same update.
 usage: dp_check.py --out params.pt [--dtype fp32|bf16] [--batch 4]
+
+--fault_rank R (fp32, eager steps): rank R's fused Winograd backward gets the
+injected hand-off timeout on the first step only.  Every rank writes
+`<out>.<rank>` with whether each of two steps applied, the replicas'
+consistency after each, and its health counters: the collective step guard
+must make every rank skip step 1 and apply step 2.
 """
 import argparse
 import os
@@ -31,6 +37,7 @@ def main():
   ap.add_argument('--batch', type=int, default=4)
   ap.add_argument('--unroll', type=int, default=6)
   ap.add_argument('--graph', type=int, default=1)
+  ap.add_argument('--fault_rank', type=int, default=-1)
   args = ap.parse_args()
   rank, world, local = parallel.init_distributed()
   device = torch.device('cuda', local % torch.cuda.device_count())
@@ -51,6 +58,25 @@ def main():
     return t[rank * B:(rank + 1) * B].contiguous()  # [B, ...] (agent state)
 
   mine = _map_tensors(full, lambda t: cols(t).to(device))
+  if args.fault_rank >= 0:
+    from scalable_agent_amd.ops import _ext
+    rec = {'world': world, 'rank': rank}
+    for step in (1, 2):
+      p0 = learner.flat.params.clone()
+      prev = _ext.ext().cf32_wino_fault(
+          1 if (step == 1 and rank == args.fault_rank) else 0)
+      try:
+        learner.step(mine)
+        torch.cuda.synchronize()
+      finally:
+        _ext.ext().cf32_wino_fault(prev)
+      rec['applied%d' % step] = not torch.equal(learner.flat.params, p0)
+      rec['consistent%d' % step] = parallel.param_checksum_consistent(
+          learner.flat.params)
+      rec['health%d' % step] = learner.health()
+    torch.save(rec, '%s.%d' % (args.out, rank))
+    parallel.cleanup()
+    return
   if args.graph:
     learner.capture(mine)
     learner.graph_step()
