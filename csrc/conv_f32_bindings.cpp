@@ -480,6 +480,9 @@ void register_conv_f32_ops(pybind11::module& m) {
   m.def("cf32_relu_mask_", &relu_mask_);
   m.def("cf32_frames_f32", &frames_f32);
   m.def("cf32_wino_fault", [](int v) { return sa::cf32::conv_wino_fault(v); });
+  // 1: compile-time-geometry Winograd instances where the map has one
+  // (default), 0: runtime geometry everywhere; returns the previous setting
+  m.def("cf32_wino_geo", [](int v) { return sa::cf32::conv_wino_geo(v); });
   // deferred weight-gradient reductions: defer(True) ... flush() -> one launch
   m.def("cf32_wgrad_defer", [](bool on) {
     t_defer = on;

@@ -207,12 +207,89 @@ __device__ __forceinline__ RangeGeom range_geom(const WinoArgs& a, int r, int RT
   return g;
 }
 
+// ---- tile-grid geometry: runtime or compile-time
+// GH == 0: the map's H, W and the tile-grid divisors come from the kernel
+// arguments (reciprocal index math, up to kMaxParts images per range, the
+// row capacity `maxrows` an argument).  GH > 0: the map is GH x GW at
+// compile time, so every divisor is a constant, the number of images a
+// range can touch (MP) and the staged-row capacity fold to constants, the
+// output-bounds tests of even maps vanish and offsets are 32-bit.  Both
+// forms walk the same ranges in the same order with the same arithmetic
+// (bitwise the same results, tests/test_conv_f32_gpu.py).
+__host__ __device__ constexpr int wino_parts(int RT, int per_img) {
+  return (RT - 1 + per_img - 1) / per_img + 1;
+}
+__host__ __device__ constexpr int wino_maxrows(int RT, int TX, int TY) {
+  return (RT % TX == 0 && (TY * TX) % RT == 0)
+             ? 2 * (RT / TX) + 2
+             : 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * wino_parts(RT, TY * TX);
+}
+
+template <int GH, int GW, int RT>
+struct TileGeo {
+  static constexpr bool kCt = GH > 0;
+  static constexpr int cTY = (GH + 1) / 2, cTX = (GW + 1) / 2;
+  // images one range may touch
+  static constexpr int MP = kCt ? wino_parts(RT, cTY * cTX) : kMaxParts;
+  static constexpr int cMaxRows = kCt ? wino_maxrows(RT, cTX, cTY) : 0;
+  static_assert(MP <= kMaxParts, "range spans too many images");
+  int H, W, TY, TX, NT, maxrows;
+  float rTX, rTY;
+  __device__ __forceinline__ TileGeo(int H_, int W_, int TY_, int TX_, int NT_, float rTX_,
+                                     float rTY_, int maxrows_)
+      : H(kCt ? GH : H_), W(kCt ? GW : W_), TY(kCt ? cTY : TY_), TX(kCt ? cTX : TX_), NT(NT_),
+        maxrows(kCt ? cMaxRows : maxrows_), rTX(rTX_), rTY(rTY_) {}
+  // (t, R >= 0: unsigned constant division is a multiply-high and a shift)
+  __device__ __forceinline__ int div_tx(int t) const {
+    return kCt ? static_cast<int>(static_cast<unsigned>(t) / cTX) : fdivi(t, rTX);
+  }
+  __device__ __forceinline__ int div_ty(int R) const {
+    return kCt ? static_cast<int>(static_cast<unsigned>(R) / cTY) : fdivi(R, rTY);
+  }
+  // output pixel (oy, ox) of a tile lies inside the map: always for even maps
+  __device__ __forceinline__ bool in_y(int oy) const { return (kCt && GH % 2 == 0) || oy < H; }
+  __device__ __forceinline__ bool in_x(int ox) const { return (kCt && GW % 2 == 0) || ox < W; }
+  // image part of LDS row L / its first row
+  __device__ __forceinline__ int part_of(const RangeGeom& g, int L) const {
+    return (L >= g.off1) + (MP > 2 ? (L >= g.off2) : 0) + (MP > 3 ? (L >= g.off3) : 0);
+  }
+  __device__ __forceinline__ int part_off(const RangeGeom& g, int p) const {
+    return p == 0 ? 0 : (p == 1 || MP <= 2 ? g.off1 : (p == 2 || MP <= 3 ? g.off2 : g.off3));
+  }
+  __device__ __forceinline__ RangeGeom range(int r) const {
+    RangeGeom g;
+    g.t0 = r * RT;
+    g.t1 = min(g.t0 + RT, NT);
+    const int R0 = div_tx(g.t0);
+    const int R1 = div_tx(g.t1 - 1);
+    g.n0 = div_ty(R0);
+    const int n1 = div_ty(R1);
+    g.tya0 = R0 - g.n0 * TY;
+    int off[MP + 1];
+    off[0] = 0;
+#pragma unroll
+    for (int p = 0; p < MP; ++p) {
+      const int n = g.n0 + p;
+      const int tya = p == 0 ? g.tya0 : 0;
+      const int tyb = n == n1 ? R1 - n1 * TY : TY - 1;
+      off[p + 1] = off[p] + (n <= n1 ? 2 * (tyb - tya) + 4 : 0);
+    }
+    g.off1 = off[1];
+    g.off2 = MP > 2 ? off[2] : off[MP];
+    g.off3 = MP > 3 ? off[3] : off[MP];
+    g.rows = off[MP];
+    return g;
+  }
+};
+
 // FL: compile-time epilogue / stager flags (bit 0 ReLU on the input, 1 ReLU
 // on the output, 2 mask, 3 residual add, 4 bias), or -1 = read them from
 // the arguments (a runtime ReLU is a max + select per staged value)
-template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1, int GH = 0,
+          int GW = 0>
 __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
+  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
   constexpr bool kPk = SA_WINO_PK == 1;
   const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
   const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
@@ -274,7 +351,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int Wl = 2 * a.TX + 2;
+  const int Wl = 2 * G.TX + 2;
   const int rowstr = Wl * PP;
 
   const RangeWalk rw = range_walk(a.nranges, a.runs);
@@ -291,7 +368,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   // dummy address and are zeroed at commit, where the ReLU-on-load is
   // applied too): a branch or a use right after a load makes the compiler
   // wait for it, serialising the prefetch.
-  int* tab_s = reinterpret_cast<int*>(x_s + a.maxrows * Wl * PP);  // [maxrows]
+  int* tab_s = reinterpret_cast<int*>(x_s + G.maxrows * Wl * PP);  // [maxrows]
   static_assert(MAXC <= 32, "stager mask");
   int sl_L[MAXC], sl_x[MAXC];
 #pragma unroll
@@ -299,26 +376,26 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4 - 1), pix = e >> LC4;
     const int L = pix / Wl, col = pix - L * Wl;
-    sl_L[k] = L < a.maxrows ? L : -1;
+    sl_L[k] = L < G.maxrows ? L : -1;
     // -1: column in the zero padding
-    sl_x[k] = (col >= 1 && col <= a.W) ? (col - 1) * CIN + 4 * ch : -1;
+    sl_x[k] = (col >= 1 && col <= G.W) ? (col - 1) * CIN + 4 * ch : -1;
   }
   auto build_tab = [&](int rr) {
-    const RangeGeom gm = range_geom(a, rr, RT);
+    const RangeGeom gm = G.range(rr);
     const int L = threadIdx.x;
-    if (L < a.maxrows) {
+    if (L < G.maxrows) {
       int v = -1;
       if (L < gm.rows) {
-        const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
-        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int p = G.part_of(gm, L);
+        const int offp = G.part_off(gm, p);
         const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
-        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W * CIN;
+        if (y >= 0 && y < G.H) v = ((gm.n0 + p) * G.H + y) * G.W * CIN;
       }
       tab_s[L] = v;
     }
   };
   f4 stg[MAXC];
-  const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * a.H * a.W * CIN);
+  const auto srcr = buf_rsrc(a.src, static_cast<int64_t>(a.N) * G.H * G.W * CIN);
   auto prefetch = [&]() __attribute__((always_inline)) {  // reads tab_s
 #pragma unroll
     for (int k = 0; k < MAXC; ++k) {
@@ -352,7 +429,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
     build_tab(r < rw.end ? r : cur);
     __syncthreads();
     prefetch();  // in flight under the MFMAs below
-    const RangeGeom gm = range_geom(a, cur, RT);
+    const RangeGeom gm = G.range(cur);
 
     for (int task = knob(a.ablate, 1) ? NTASK : wave; task < NTASK; task += NW) {
       const int grp = task % NG, sl = task / NG;
@@ -361,10 +438,10 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
       int t = gm.t0 + 16 * grp + c16;
       const bool valid = t < gm.t1;
       if (!valid) t = gm.t0;
-      const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
-      const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+      const int R = G.div_tx(t), tx = t - R * G.TX;
+      const int n = G.div_ty(R), ty = R - n * G.TY;
       const int p = n - gm.n0;
-      const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+      const int offp = G.part_off(gm, p);
       const int base = offp + 2 * (ty - (p == 0 ? gm.tya0 : 0));
       const float* xp = x_s + (base * Wl + 2 * tx) * PP + 4 * g;
       const float* up = U_s + (g * COUT + co0 + c16) * 4;
@@ -380,8 +457,8 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-            const bool in = valid && oy < a.H && ox < a.W;
-            const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT +
+            const bool in = valid && G.in_y(oy) && G.in_x(ox);
+            const int64_t o = in ? ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * COUT +
                                        co0 + 16 * h + 4 * g
                                  : 0;
             pm[h][q] = (f_mask && in) ? *reinterpret_cast<const f4*>(a.mask + o)
@@ -470,8 +547,8 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
           for (int dx = 0; dx < 2; ++dx) {
             const int oy = 2 * ty + dy, ox = 2 * tx + dx;
-            if (!valid || oy >= a.H || ox >= a.W || knob(a.ablate, 8)) continue;
-            const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * COUT + co;
+            if (!valid || !G.in_y(oy) || !G.in_x(ox) || knob(a.ablate, 8)) continue;
+            const int64_t o = ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * COUT + co;
             f4 v = Y[2 * dy + dx] + bv;
             const f4 m = pm[h][2 * dy + dx];
 #pragma unroll
@@ -506,9 +583,11 @@ int env_int(const char* name, int def) {
 
 int g_wino_fault = 0;  // conv_wino_fault(): tests of the fail-loud hand-off
 
-template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
-bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1, int GH = 0,
+          int GW = 0>
+bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   const int H = c.Ho, W = c.Wo;
+  if (GH > 0 && (H != GH || W != GW)) return false;
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(c.N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
@@ -554,10 +633,50 @@ bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
   static const int occ_env = env_int("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
   const int G = std::max(1, std::min(a.nranges, 256 * occ));
-  auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS, FL>;
+  auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS, FL, GH, GW>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), bytes, s, a);
   return true;
+}
+
+// Compile-time-geometry switch of the fp32 Winograd kernels (TileGeo):
+// SA_WINO_GEO=0 keeps every map on the runtime-geometry instances.
+int g_wino_geo = -1;  // -1: not read yet; conv_wino_geo() sets it (tests)
+bool wino_geo_enabled() {
+  if (g_wino_geo < 0) g_wino_geo = env_int("SA_WINO_GEO", 1) != 0 ? 1 : 0;
+  return g_wino_geo != 0;
+}
+
+// The deep torso's maps get compile-time instances (only where that layer
+// runs): the IMPALA / DMLab 72x96 ladder (36x48, 18x24, 9x12) and the Atari
+// 84x84 ladder (42x42, 21x21, 11x11); any other map runs the runtime-
+// geometry kernel.  Per channel configuration: 16 -> 16 (res16) and 16 -> 32
+// (stage-1 head) at 36x48 / 42x42, 32 -> 32 (res32, stage-2 head) at 18x24,
+// 9x12, 21x21, 11x11.
+#define SA_GEO(h, w) \
+  if (HH == (h) && WW == (w) && SA_CALL(h, w)) return true;
+#define SA_WINO_GEO_DISPATCH(CI, CO)                             \
+  if (wino_geo_enabled()) {                                      \
+    if constexpr ((CI) == 16) { SA_GEO(36, 48) SA_GEO(42, 42) }  \
+    if constexpr ((CI) == 32 && (CO) == 32) {                    \
+      SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) \
+    }                                                            \
+  }
+
+// runtime geometry only (the opt-in experiment variants)
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL = -1>
+bool run_wino(const ConvArgs& c, bool flip, hipStream_t s) {
+  return run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, FL>(c, flip, s);
+}
+
+// compile-time geometry where the map has an instance, else runtime
+template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
+bool run_wino_ct(const ConvArgs& c, bool flip, hipStream_t s) {
+  const int HH = c.Ho, WW = c.Wo;
+#define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, -1, h, w>(c, flip, s)
+  SA_WINO_GEO_DISPATCH(CIN, COUT)
+#undef SA_CALL
+  return run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
 
 // The deep torso's forward flag sets get compile-time instances: residual
@@ -578,7 +697,7 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
     if (fl == 26) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 26>(c, flip, s);
     if (fl == 16) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 16>(c, flip, s);
   }
-  return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
+  return run_wino_ct<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
 
 // ------------------------------------------------------- fused stage heads
@@ -1676,9 +1795,11 @@ struct WinoBwdArgs {
 // RT / 4 k-steps evenly.  NW = 12 over 96-tile ranges (three waves per SIMD)
 // does not fit: capped at 168 VGPRs the kernel spills 121 (it needs ~256 at
 // two waves per SIMD), so only NW = 8 is instantiated.
-template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false, int NW = 8>
+template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false, int NW = 8,
+          int GH = 0, int GW = 0>
 __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   constexpr int NTH = 64 * NW;
+  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
   constexpr int PP = C + 4;
   constexpr int C4 = C / 4;
   constexpr int LC4 = C4 == 4 ? 2 : 3;
@@ -1691,13 +1812,13 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
   static_assert(WWG ? (RT % 16 == 0) : (RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0),
                 "work split");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Wl = 2 * a.TX + 2;
+  const int Wl = 2 * G.TX + 2;
   const int rowstr = Wl * PP;
   float* U_s = smem;                         // [16 xi][4 g][C][4]
   float* d_s = U_s + 16 * C * C;             // dY rows [maxrows][Wl][PP]
-  float* x_s = d_s + a.maxrows * rowstr;     // x rows, same geometry
-  int* tab_s = reinterpret_cast<int*>(x_s + a.maxrows * rowstr);  // [maxrows]
-  int* tile_s = tab_s + a.maxrows;                                // [RT]
+  float* x_s = d_s + G.maxrows * rowstr;     // x rows, same geometry
+  int* tab_s = reinterpret_cast<int*>(x_s + G.maxrows * rowstr);  // [maxrows]
+  int* tile_s = tab_s + G.maxrows;                                // [RT]
 
   // U = G g' G^T of the flipped / transposed weights (the dgrad conv)
   for (int e = threadIdx.x; e < C * C; e += NTH) {
@@ -1727,8 +1848,6 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
 
-  WinoArgs ga{};
-  ga.NT = a.NT; ga.TX = a.TX; ga.TY = a.TY; ga.rTX = a.rTX; ga.rTY = a.rTY;
   const RangeWalk rw = range_walk(a.nranges, a.runs);
   int r = rw.r;
   if (r >= rw.end) return;
@@ -1744,25 +1863,25 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4 - 1), pix = e >> LC4;
     const int L = pix / Wl, col = pix - L * Wl;
-    sl_L[k] = L < a.maxrows ? L : -1;
-    sl_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * C + 4 * ch : -1;
+    sl_L[k] = L < G.maxrows ? L : -1;
+    sl_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * C + 4 * ch : -1;
   }
   auto build_tab = [&](int rr) {
-    const RangeGeom gm = range_geom(ga, rr, RT);
+    const RangeGeom gm = G.range(rr);
     const int L = threadIdx.x;
-    if (L < a.maxrows) {
+    if (L < G.maxrows) {
       int v = -1;
       if (L < gm.rows) {
-        const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
-        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int p = G.part_of(gm, L);
+        const int offp = G.part_off(gm, p);
         const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
-        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W * C;
+        if (y >= 0 && y < G.H) v = ((gm.n0 + p) * G.H + y) * G.W * C;
       }
       tab_s[L] = v;
     }
   };
   f4 sd[MAXC], sx[MAXC];
-  const int64_t nfl = static_cast<int64_t>(a.N) * a.H * a.W * C;
+  const int64_t nfl = static_cast<int64_t>(a.N) * G.H * G.W * C;
   const auto dyr = buf_rsrc(a.dy, nfl), xr = buf_rsrc(a.x, nfl);
   auto prefetch = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -1798,16 +1917,16 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
     }
     const int cur = r;
     r += rw.step;
-    const RangeGeom gm = range_geom(ga, cur, RT);
+    const RangeGeom gm = G.range(cur);
     // tile table of this range: LDS offset of each tile's patch origin
     if (threadIdx.x < RT) {
       const int t = gm.t0 + threadIdx.x;
       int v = -1;
       if (t < gm.t1) {
-        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
-        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int R = G.div_tx(t), tx = t - R * G.TX;
+        const int n = G.div_ty(R), ty = R - n * G.TY;
         const int p = n - gm.n0;
-        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int offp = G.part_off(gm, p);
         v = ((offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx) * PP;
       }
       tile_s[threadIdx.x] = v;
@@ -1821,8 +1940,8 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
       int t = gm.t0 + 16 * wave + c16;
       const bool valid = t < gm.t1;
       if (!valid) t = gm.t0;
-      const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
-      const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+      const int R = G.div_tx(t), tx = t - R * G.TX;
+      const int n = G.div_ty(R), ty = R - n * G.TY;
       const int base = tile_s[valid ? 16 * wave + c16 : 0];
       const float* dp = d_s + base + 4 * g;
       // the skip operand of the 4 outputs: global loads issued before the
@@ -1831,8 +1950,8 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-        const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
-        const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + 4 * g : 0;
+        const bool in = a.add != nullptr && valid && G.in_y(oy) && G.in_x(ox);
+        const int64_t o = in ? ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * C + 4 * g : 0;
         addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
       }
       f4 acc[16];
@@ -1889,8 +2008,8 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
           const int oy = 2 * ty + dy, ox = 2 * tx + dx;
-          if (!valid || oy >= a.H || ox >= a.W) continue;
-          const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * C + 4 * g;
+          if (!valid || !G.in_y(oy) || !G.in_x(ox)) continue;
+          const int64_t o = ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * C + 4 * g;
           const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rowstr + (dx + 1) * PP);
           f4 v = Y[2 * dy + dx];
 #pragma unroll
@@ -2075,9 +2194,11 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
 // mask.  Each workgroup walks a CONTIGUOUS run of ranges, so the halo rows
 // a range shares with the previous one come from this CU's L2 instead of
 // being refetched by another XCD.
-template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK>
+template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK, int GH = 0,
+          int GW = 0>
 __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a) {
   constexpr int NW = 8, NTH = 512;
+  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
   constexpr int PPX = CX + 4, PPY = CY + 4;  // odd 16-B units per pixel
   constexpr int C4X = CX / 4, C4Y = CY / 4;
   constexpr int LC4X = C4X == 4 ? 2 : 3, LC4Y = C4Y == 4 ? 2 : 3;
@@ -2092,15 +2213,15 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   static_assert(C4Y == 4 || C4Y == 8, "CY");
   static_assert(MAXCX <= 32 && MAXCY <= 32, "stager masks");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Wl = 2 * a.TX + 2;
+  const int Wl = 2 * G.TX + 2;
   const int rsx = Wl * PPX, rsy = Wl * PPY;
   float* U_s = smem;                         // [16 xi][NBY][4 g][CX][4]
   float* d_s = U_s + 16 * CX * CY;           // dY rows [maxrows][Wl][PPY]
-  float* x_s = d_s + a.maxrows * rsy;        // x rows [maxrows][Wl][PPX]
-  f4* ybuf = reinterpret_cast<f4*>(x_s + a.maxrows * rsx);  // [2 pairs][4][64] (DSPLIT 2)
+  float* x_s = d_s + G.maxrows * rsy;        // x rows [maxrows][Wl][PPX]
+  f4* ybuf = reinterpret_cast<f4*>(x_s + G.maxrows * rsx);  // [2 pairs][4][64] (DSPLIT 2)
   int* flag_s = reinterpret_cast<int*>(ybuf + (DSPLIT == 2 ? 2 * 4 * 64 : 0));  // [2]
   int* tab_s = flag_s + 2;                   // [maxrows]
-  int* tile_s = tab_s + a.maxrows;           // [RT] patch-origin pixel (row * Wl + col)
+  int* tile_s = tab_s + G.maxrows;           // [RT] patch-origin pixel (row * Wl + col)
 
   // U = G g' G^T of the flipped / transposed weights (the dgrad conv);
   // forward weights HWIO [3][3][CX][CY]
@@ -2133,8 +2254,6 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
 
-  WinoArgs ga{};
-  ga.NT = a.NT; ga.TX = a.TX; ga.TY = a.TY; ga.rTX = a.rTX; ga.rTY = a.rTY;
   // this workgroup's contiguous run of ranges (G <= nranges: never empty)
   const int r_end = static_cast<int>((static_cast<int64_t>(blockIdx.x) + 1) * a.nranges / gridDim.x);
   int r = static_cast<int>(static_cast<int64_t>(blockIdx.x) * a.nranges / gridDim.x);
@@ -2151,34 +2270,34 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4Y - 1), pix = e >> LC4Y;
     const int L = pix / Wl, col = pix - L * Wl;
-    sy_L[k] = L < a.maxrows ? L : -1;
-    sy_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * CY + 4 * ch : -1;
+    sy_L[k] = L < G.maxrows ? L : -1;
+    sy_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * CY + 4 * ch : -1;
   }
 #pragma unroll
   for (int k = 0; k < MAXCX; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4X - 1), pix = e >> LC4X;
     const int L = pix / Wl, col = pix - L * Wl;
-    sx_L[k] = L < a.maxrows ? L : -1;
-    sx_o[k] = (col >= 1 && col <= a.W) ? (col - 1) * CX + 4 * ch : -1;
+    sx_L[k] = L < G.maxrows ? L : -1;
+    sx_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * CX + 4 * ch : -1;
   }
   // row table: global PIXEL index (n H + y) W of LDS row L, or -1
   auto build_tab = [&](int rr) __attribute__((always_inline)) {
-    const RangeGeom gm = range_geom(ga, rr, RT);
+    const RangeGeom gm = G.range(rr);
     const int L = threadIdx.x;
-    if (L < a.maxrows) {
+    if (L < G.maxrows) {
       int v = -1;
       if (L < gm.rows) {
-        const int p = (L >= gm.off1) + (L >= gm.off2) + (L >= gm.off3);
-        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int p = G.part_of(gm, L);
+        const int offp = G.part_off(gm, p);
         const int y = 2 * (p == 0 ? gm.tya0 : 0) - 1 + (L - offp);
-        if (y >= 0 && y < a.H) v = ((gm.n0 + p) * a.H + y) * a.W;
+        if (y >= 0 && y < G.H) v = ((gm.n0 + p) * G.H + y) * G.W;
       }
       tab_s[L] = v;
     }
   };
   f4 sy[MAXCY], sx[MAXCX];
-  const int64_t npx = static_cast<int64_t>(a.N) * a.H * a.W;
+  const int64_t npx = static_cast<int64_t>(a.N) * G.H * G.W;
   const auto dyr = buf_rsrc(a.dy, npx * CY), xr = buf_rsrc(a.x, npx * CX);
   auto prefetch = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -2223,15 +2342,15 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
     }
     const int cur = r;
     ++r;
-    const RangeGeom gm = range_geom(ga, cur, RT);
+    const RangeGeom gm = G.range(cur);
     if (threadIdx.x < RT) {
       const int t = gm.t0 + threadIdx.x;
       int v = -1;
       if (t < gm.t1) {
-        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
-        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int R = G.div_tx(t), tx = t - R * G.TX;
+        const int n = G.div_ty(R), ty = R - n * G.TY;
         const int p = n - gm.n0;
-        const int offp = p == 0 ? 0 : (p == 1 ? gm.off1 : (p == 2 ? gm.off2 : gm.off3));
+        const int offp = G.part_off(gm, p);
         v = (offp + 2 * (ty - (p == 0 ? gm.tya0 : 0))) * Wl + 2 * tx;
       }
       tile_s[threadIdx.x] = v;
@@ -2257,8 +2376,8 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
         int t = gm.t0 + 16 * grp + c16;
         const bool valid = t < gm.t1;
         if (!valid) t = gm.t0;
-        const int R = fdivi(t, a.rTX), tx = t - R * a.TX;
-        const int n = fdivi(R, a.rTY), ty = R - n * a.TY;
+        const int R = G.div_tx(t), tx = t - R * G.TX;
+        const int n = G.div_ty(R), ty = R - n * G.TY;
         const int bpx = tile_s[valid ? 16 * grp + c16 : 0];
         const int co = 16 * cb + 4 * g;  // this lane's 4 dX channels
         f4 addv[4];
@@ -2266,8 +2385,8 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int oy = 2 * ty + (q >> 1), ox = 2 * tx + (q & 1);
-            const bool in = a.add != nullptr && valid && oy < a.H && ox < a.W;
-            const int64_t o = in ? ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * CX + co : 0;
+            const bool in = a.add != nullptr && valid && G.in_y(oy) && G.in_x(ox);
+            const int64_t o = in ? ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * CX + co : 0;
             addv[q] = in ? *reinterpret_cast<const f4*>(a.add + o) : f4{0.f, 0.f, 0.f, 0.f};
           }
         }
@@ -2365,8 +2484,8 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
 #pragma unroll
             for (int dx = 0; dx < 2; ++dx) {
               const int oy = 2 * ty + dy, ox = 2 * tx + dx;
-              if (!valid || oy >= a.H || ox >= a.W) continue;
-              const int64_t o = ((static_cast<int64_t>(n) * a.H + oy) * a.W + ox) * CX + co;
+              if (!valid || !G.in_y(oy) || !G.in_x(ox)) continue;
+              const int64_t o = ((static_cast<int64_t>(n) * G.H + oy) * G.W + ox) * CX + co;
               f4 v = Y[2 * dy + dx];
               if constexpr (MASK) {
                 const f4 m = *reinterpret_cast<const f4*>(xm + (dy + 1) * rsx + (dx + 1) * PPX);
@@ -2519,10 +2638,12 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   for (int co = threadIdx.x; co < CY; co += NTH) slot[9 * CX * CY + co] = dB[co];
 }
 
-template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK>
-bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const float* add,
-                    float* out, int relu_x, int mask_x, int N, int H, int W, float* ws,
-                    int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK, int GH = 0,
+          int GW = 0>
+bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const float* add,
+                      float* out, int relu_x, int mask_x, int N, int H, int W, float* ws,
+                      int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+  if (GH > 0 && (H != GH || W != GW)) return false;
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
@@ -2560,11 +2681,30 @@ bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const flo
   a.fault = g_wino_fault;
   static const int fprio = env_int("SA_FUSED_PRIO", 0);
   a.prio = fprio;
-  auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>;
+  auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK, GH, GW>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(512), bytes, s, a);
   wgrad_reduce_slots(ws, G, rows16, CY, CX, dw, db, s);
   return true;
+}
+
+template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK>
+bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const float* add,
+                      float* out, int relu_x, int mask_x, int N, int H, int W, float* ws,
+                      int64_t ws_floats, float* dw, float* db, hipStream_t s) {
+  // the residual convs (MASK, with or without the ReLU'd operand) and the
+  // stage heads (neither); the relu-without-mask form is never called
+  if constexpr (MASK || !RELU) {
+    const int HH = H, WW = W;
+#define SA_CALL(h, w_)                                                                     \
+  run_wino_bwd32_g<CX, CY, RT, MAXCX, MAXCY, RELU, MASK, h, w_>(dy, w, x, add, out, relu_x, \
+                                                                mask_x, N, H, W, ws,        \
+                                                                ws_floats, dw, db, s)
+    if constexpr (CX == 32 || !MASK) { SA_WINO_GEO_DISPATCH(CX, CY) }
+#undef SA_CALL
+  }
+  return run_wino_bwd32_g<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>(
+      dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
 }
 
 // relu_x / mask_x are compile-time in the kernel (the wgrad waves' ReLU on
@@ -2587,10 +2727,11 @@ bool run_wino_bwd32(const float* dy, const float* w, const float* x, const float
       dy, w, x, add, out, relu_x, mask_x, N, H, W, ws, ws_floats, dw, db, s);
 }
 
-template <int C, int RT, int MAXC, int KD, bool WWG = false, int NW = 8>
-bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
-                  float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
-                  float* dw, float* db, hipStream_t s) {
+template <int C, int RT, int MAXC, int KD, bool WWG = false, int NW = 8, int GH = 0, int GW = 0>
+bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float* add,
+                    float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
+                    float* dw, float* db, hipStream_t s) {
+  if (GH > 0 && (H != GH || W != GW)) return false;
   const int TY = (H + 1) / 2, TX = (W + 1) / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   if (NT >= (1 << 22) || TX > 1024 || TY > 1024) return false;
@@ -2621,12 +2762,30 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
   a.runs = runs;
   static const int fprio = env_int("SA_FUSED_PRIO", 0);
   a.prio = fprio;
-  auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true, NW>
-                     : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false, NW>;
+  auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true, NW, GH, GW>
+                     : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false, NW, GH, GW>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), bytes, s, a);
   wgrad_reduce_slots(ws, G, rows16, C, C, dw, db, s);
   return true;
+}
+
+// runtime geometry (the opt-in variants) / compile-time where the map has an
+// instance (the default WWG kernel)
+template <int C, int RT, int MAXC, int KD, bool WWG = false, int NW = 8>
+bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* add,
+                  float* out, int relu_x, int N, int H, int W, float* ws, int64_t ws_floats,
+                  float* dw, float* db, hipStream_t s) {
+  if constexpr (WWG) {
+    const int HH = H, WW = W;
+#define SA_CALL(h, w_)                                                                  \
+  run_wino_bwd_g<C, RT, MAXC, KD, WWG, NW, h, w_>(dy, w, x, add, out, relu_x, N, H, W, ws, \
+                                                  ws_floats, dw, db, s)
+    SA_WINO_GEO_DISPATCH(C, C)
+#undef SA_CALL
+  }
+  return run_wino_bwd_g<C, RT, MAXC, KD, WWG, NW>(dy, w, x, add, out, relu_x, N, H, W, ws,
+                                                  ws_floats, dw, db, s);
 }
 
 }  // namespace
@@ -2634,6 +2793,12 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
 int conv_wino_fault(int v) {
   const int old = g_wino_fault;
   if (v == 0 || v == 1) g_wino_fault = v;
+  return old;
+}
+
+int conv_wino_geo(int v) {
+  const int old = wino_geo_enabled() ? 1 : 0;
+  if (v == 0 || v == 1) g_wino_geo = v;
   return old;
 }
 

@@ -187,7 +187,10 @@ class _DeepTorsoF32(torch.autograd.Function):
       # the incoming gradient is masked in place below: copy unless it is
       # the fused core's own scratch dfeats buffer (never a caller's tensor)
       dy = dy.to(torch.float32).clone(memory_format=torch.contiguous_format)
-    C.cf32_relu_mask_(dy, out)  # final ReLU of the torso
+    if not getattr(grad_out, '_sa_relu_masked', False):
+      # final ReLU of the torso (the fused fp32 core masks dfeats in its
+      # GEMM epilogue already; masking twice would be harmless)
+      C.cf32_relu_mask_(dy, out)
     # the ~15 fixed-order weight-gradient slot sums of this backward are
     # queued and launched as ONE kernel at the end (cf32_wgrad_flush)
     C.cf32_wgrad_defer(True)

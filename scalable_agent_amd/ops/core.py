@@ -160,7 +160,7 @@ class _CoreLSTMF32(torch.autograd.Function):
     xw    = h_aug W_x[:K] + b_lstm                                  GEMM
   Backward:
     dh     = (dG W_x[:256]^T) * (h > 0)                             GEMM + mask
-    dfeats = dh W_fc^T                                              GEMM
+    dfeats = (dh W_fc^T) * (feats > 0)                              GEMM + mask
     dW_h  += hpm^T dG                                               GEMM (split-K)
     dW_x  += h_aug^T dG ; db_lstm += 1^T dG                         ONE GEMM (ones row)
     dW_fc += feats^T dh ; db_fc   += 1^T dh                         ONE GEMM (ones row)
@@ -221,8 +221,12 @@ class _CoreLSTMF32(torch.autograd.Function):
     dh = torch.empty(N, CORE, dtype=torch.float32, device=dev)
     C.gemm_f32(dg2, kernel[:CORE], False, True, dh, mask=h_aug[:, :CORE])
     dfeats = torch.empty_like(feats)
-    C.gemm_f32(dh, w_fc, False, True, dfeats)
+    # feats is the ReLU'd torso output (core_lstm's contract): its ReLU
+    # gradient mask (feats > 0) is applied in this GEMM's epilogue, so the
+    # torso backward skips its own relu_mask pass over dfeats
+    C.gemm_f32(dh, w_fc, False, True, dfeats, mask=feats)
     dfeats._sa_scratch = True  # the torso backward may mask it in place
+    dfeats._sa_relu_masked = True
     C.gemm_f32(hpm.view(N, CORE), dg2, True, False, gk[f_in:],
                accumulate=True)                                     # W_h
     C.gemm_f32(h_aug[:, :K], dg2, True, False, gk[:K], accumulate=True,

@@ -610,3 +610,72 @@ def test_residual_block_forward_flags(cuda, H, W, C, block_conv):
     y = Cmod.cf32_conv_fwd(x.to(cuda), w.to(cuda), b.to(cuda), 1, 1, 1, H, W,
                            add=add.to(cuda))
   assert rel_err(y, ref) <= TOL
+
+
+GEO_FWD = [(36, 48, 16, 16), (42, 42, 16, 16), (36, 48, 16, 32), (42, 42, 16, 32),
+           (18, 24, 32, 32), (9, 12, 32, 32), (21, 21, 32, 32), (11, 11, 32, 32)]
+
+
+@pytest.mark.parametrize('H,W,Cin,Cout', GEO_FWD)
+@pytest.mark.parametrize('flags', ['plain', 'resblock1', 'resblock2'])
+def test_wino_geometry_instances_match_runtime_fwd(cuda, H, W, Cin, Cout, flags):
+  """Compile-time-geometry Winograd forward instances (conv_wino.hip
+  TileGeo, every map of the IMPALA and Atari ladders) are bitwise the
+  runtime-geometry kernel: same ranges, same arithmetic.  N = 37 frames:
+  ranges cross images, the batch's last range is partial."""
+  C = _C()
+  N = 37
+  g = torch.Generator().manual_seed(H * W + Cin + Cout)
+  x = torch.randn(N, H, W, Cin, generator=g).to(cuda)
+  w = (torch.randn(3, 3, Cin, Cout, generator=g) / (9 * Cin) ** 0.5).to(cuda)
+  b = (torch.randn(Cout, generator=g) * 0.1).to(cuda)
+  add = torch.randn(N, H, W, Cout, generator=g).to(cuda)
+  kw = {'plain': {}, 'resblock1': dict(relu_in=True, relu_out=True),
+        'resblock2': dict(add=add)}[flags]
+  if flags == 'resblock2' and Cin != Cout:
+    pytest.skip('the skip add needs Cin == Cout')
+  outs = []
+  prev = C.cf32_wino_geo(1)
+  try:
+    for geo in (1, 0):
+      C.cf32_wino_geo(geo)
+      outs.append(C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W, **kw))
+  finally:
+    C.cf32_wino_geo(prev)
+  assert torch.equal(outs[0], outs[1])
+
+
+GEO_BWD = [(36, 48, 16, 16, True), (42, 42, 16, 16, True), (36, 48, 16, 32, False),
+           (42, 42, 16, 32, False), (18, 24, 32, 32, True), (18, 24, 32, 32, False),
+           (9, 12, 32, 32, True), (21, 21, 32, 32, True), (21, 21, 32, 32, False),
+           (11, 11, 32, 32, True)]
+
+
+@pytest.mark.parametrize('H,W,Cx,Cy,mask', GEO_BWD)
+@pytest.mark.parametrize('relu_x', [False, True])
+def test_wino_geometry_instances_match_runtime_bwd(cuda, H, W, Cx, Cy, mask, relu_x):
+  """Compile-time-geometry fused backward instances (wino_bwd_fused_kernel,
+  wino_bwd_fused32_kernel) are bitwise the runtime-geometry kernels: dX, dW
+  and db, N = 37 frames."""
+  if relu_x and not mask:
+    pytest.skip('stage heads: no ReLU on the operand')
+  C = _C()
+  N = 37
+  g = torch.Generator().manual_seed(H * W + Cx + 3 * Cy)
+  x = torch.randn(N, H, W, Cx, generator=g).to(cuda)
+  w = (torch.randn(3, 3, Cx, Cy, generator=g) / (9 * Cx) ** 0.5).to(cuda)
+  dy = torch.randn(N, H, W, Cy, generator=g).to(cuda)
+  add = torch.randn(N, H, W, Cx, generator=g).to(cuda) if mask else None
+  res = []
+  prev = C.cf32_wino_geo(1)
+  try:
+    for geo in (1, 0):
+      C.cf32_wino_geo(geo)
+      dw = torch.zeros(3, 3, Cx, Cy, device=cuda)
+      db = torch.zeros(Cy, device=cuda)
+      dx = C.cf32_conv_bwd_fused(dy, w, x, relu_x, dw, db, add=add, mask=mask)
+      res.append((dx, dw, db))
+  finally:
+    C.cf32_wino_geo(prev)
+  for a, b_ in zip(*res):
+    assert torch.equal(a, b_)
