@@ -483,6 +483,8 @@ void register_conv_f32_ops(pybind11::module& m) {
   // 1: compile-time-geometry Winograd instances where the map has one
   // (default), 0: runtime geometry everywhere; returns the previous setting
   m.def("cf32_wino_geo", [](int v) { return sa::cf32::conv_wino_geo(v); });
+  // R CUs per XCD left out of every persistent conv grid (-1 reads)
+  m.def("cf32_cu_reserve", [](int r) { return sa::cf32::conv_cu_reserve(r); });
   // deferred weight-gradient reductions: defer(True) ... flush() -> one launch
   m.def("cf32_wgrad_defer", [](bool on) {
     t_defer = on;

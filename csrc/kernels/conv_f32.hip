@@ -34,6 +34,24 @@
 
 namespace sa {
 namespace cf32 {
+
+namespace {
+int g_cu_reserve = -1;  // -1: not read yet (SA_CU_RESERVE)
+}  // namespace
+
+int conv_cu_reserve(int r) {
+  if (g_cu_reserve < 0) {
+    const char* e = std::getenv("SA_CU_RESERVE");
+    const int v = (e && *e) ? std::atoi(e) : 0;
+    g_cu_reserve = v < 0 ? 0 : (v > 16 ? 16 : v);
+  }
+  const int old = g_cu_reserve;
+  if (r >= 0 && r <= 16) g_cu_reserve = r;
+  return old;
+}
+
+int conv_cus() { return 256 - 8 * conv_cu_reserve(-1); }
+
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1478,7 +1496,7 @@ bool run_conv(const ConvArgs& a, hipStream_t s) {
   static const int occ_env = env_knob("SA_F32_FWD_OCC", 0);
   const int occ_cap = occ_env ? occ_env : (CINP <= 16 && COUT_T <= 16 ? 3 : 2);
   const int per_cu = occupancy(bytes(R), occ_cap);
-  const int G = std::max(1, std::min(ntiles, 256 * per_cu / gy));
+  const int G = std::max(1, std::min(ntiles, conv_cus() * per_cu / gy));
   auto kern = conv_fwd_kernel<CINP, COUT_T, K, S, SRC, FLIP>;
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G, gy), dim3(kThreads), bytes(R), s, a, R, nt, ntiles);
@@ -1510,7 +1528,7 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
   const int ntiles = a.N * nt;
   static const int occ_cap = env_knob("SA_F32_POOL_OCC", 3);
   const int per_cu = occupancy(bytes(R), occ_cap);
-  const int G = std::max(1, std::min(ntiles, 256 * per_cu));
+  const int G = std::max(1, std::min(ntiles, conv_cus() * per_cu));
   auto kern = conv_pool_fwd_kernel<CINP, COUT, SRC>;
   allow_lds(kern, bytes(R));
   hipLaunchKernelGGL(kern, dim3(G), dim3(kThreads), bytes(R), s, a, R, nt, ntiles, pbh, pbw,

@@ -632,7 +632,7 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   const int per_cu = std::max(1, std::min(WPS * 4 / NW, static_cast<int>((160 * 1024) / (bytes + 256))));
   static const int occ_env = env_int("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
-  const int G = std::max(1, std::min(a.nranges, 256 * occ));
+  const int G = std::max(1, std::min(a.nranges, conv_cus() * occ));
   auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS, FL, GH, GW>;
   allow_lds_w(kern, bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * NW), bytes, s, a);
@@ -690,7 +690,21 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   // SA_WINO_FL: 1 = every instance (measured 10.85 vs 10.77 ms/step with
   // none: the 32-channel instances spilled), 2 = the 16-channel-input
   // instances only (no spill risk at 112 VGPRs), 0 = none
-  static const int on = env_int("SA_WINO_FL", 0);
+  // 3 (default): the compile-time-geometry 16 -> 16 instances with the two
+  // residual flag sets compile-time too (conv 1 = 19, conv 2 = 24): full
+  // fp32 step 9.546 / 9.547 -> 9.502 / 9.460 ms (geometry alone; one box)
+  static const int on = env_int("SA_WINO_FL", 3);
+  if constexpr (CIN == 16 && COUT == 16) {
+    if (on == 3 && !flip && wino_geo_enabled()) {
+      const int HH = c.Ho, WW = c.Wo;
+#define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
+      if (fl == 19) { SA_GEO(36, 48) SA_GEO(42, 42) }
+#undef SA_CALL
+#define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
+      if (fl == 24) { SA_GEO(36, 48) SA_GEO(42, 42) }
+#undef SA_CALL
+    }
+  }
   if ((on == 1 || (on == 2 && CIN == 16)) && !flip) {
     if (fl == 19) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 19>(c, flip, s);
     if (fl == 24) return run_wino<CIN, COUT, NH, NW, RT, MAXC, WPS, 24>(c, flip, s);
@@ -1114,7 +1128,7 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   static const int occ = env_int("SA_WINO_POOL_OCC", 0);
   const int lds_cu = static_cast<int>((160 * 1024) / (P::bytes + 256));
   const int per_cu = std::max(1, std::min(occ > 0 ? occ : 3 * 4 / P::NW, lds_cu));
-  const int G = std::max(1, std::min(a.nranges, 256 * per_cu));
+  const int G = std::max(1, std::min(a.nranges, conv_cus() * per_cu));
   const int side_n = (W / 2) * P::CQ;
   if (static_cast<int64_t>(G) * side_n * 5 > side_floats) return false;
   WinoPoolArgs pa{};
@@ -1365,7 +1379,7 @@ bool run_wino_pool_img(const float* x, const float* w, const float* b, float* po
   a.N = N; a.H = H; a.W = W;
   a.nranges = N;
   a.runs = 1;
-  const int G = std::max(1, std::min(N, 256));
+  const int G = std::max(1, std::min(N, conv_cus()));
   auto kern = wino_conv_pool_img_kernel<CIN, COUT, H, W>;
   allow_lds_w(kern, P::bytes);
   WinoPoolArgs pa{};
@@ -1731,7 +1745,7 @@ bool run_wino_wgrad(const WgradArgs& c, float* ws, hipStream_t s) {
   const int nranges = static_cast<int>((NT + RT - 1) / RT);
   // slots: one per resident workgroup (<= the direct kernel's workspace)
   const int64_t cap = wgrad_workspace_floats(3, CIN, COUT) / (static_cast<int64_t>(rows16) * COUT);
-  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  const int G = static_cast<int>(std::min<int64_t>({nranges, conv_cus(), cap}));
   WinoWgArgs a{};
   a.x = static_cast<const float*>(c.src);
   a.dy = c.dy;
@@ -2664,7 +2678,7 @@ bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const flo
   const int rows16 = ((9 * CX + 16) / 16) * 16;
   const int nranges = static_cast<int>((NT + RT - 1) / RT);
   const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * CY);
-  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  const int G = static_cast<int>(std::min<int64_t>({nranges, conv_cus(), cap}));
   if (G < 1) return false;
   WinoBwdArgs a{};
   a.dy = dy; a.w = w; a.x = x; a.add = add; a.out = out; a.part = ws;
@@ -2748,7 +2762,7 @@ bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float
   const int rows16 = ((9 * C + 16) / 16) * 16;
   const int nranges = static_cast<int>((NT + RT - 1) / RT);
   const int64_t cap = ws_floats / (static_cast<int64_t>(rows16) * C);
-  const int G = static_cast<int>(std::min<int64_t>({nranges, 256, cap}));
+  const int G = static_cast<int>(std::min<int64_t>({nranges, conv_cus(), cap}));
   if (G < 1) return false;
   WinoBwdArgs a{};
   a.dy = dy; a.w = w; a.x = x; a.add = add; a.out = out; a.part = ws;

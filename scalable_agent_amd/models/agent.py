@@ -22,6 +22,8 @@ Parameters are fp32 master weights in TF layouts (see models/layers.py).
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -94,6 +96,23 @@ def torso_spec(torso, frame_shape):
   else:
     raise ValueError('unknown torso %r' % torso)
   return specs, h * w * c, (h, w, c)
+
+
+def _chunk_bounds(T, chunks, split=None):
+  """Time-chunk boundaries [0, ..., T]: `chunks` equal chunks, or chunk
+  lengths in the proportions of `split` ("9,9,2"), every chunk >= 1 step."""
+  if split:
+    w = [float(x) for x in split.split(',') if x.strip()]
+    w = [max(x, 0.0) for x in w][:T] or [1.0]
+    tot = sum(w) or 1.0
+    b = [0]
+    acc = 0.0
+    for x in w[:-1]:
+      acc += x
+      b.append(min(T - (len(w) - len(b)), max(b[-1] + 1, int(round(T * acc / tot)))))
+    b.append(T)
+    return b
+  return [(T * k) // chunks for k in range(chunks + 1)]
 
 
 class Agent(nn.Module):
@@ -338,40 +357,60 @@ class Agent(nn.Module):
                       chunks):
     """Time-chunked torso || LSTM pipeline (HIP backend, GPU only).
 
-    The torso, FC and core-input assembly of time chunk k run on the current
-    (main) stream; the x W_x projection and the recurrence of chunk k run on
-    a side stream as soon as chunk k's inputs exist, overlapping the torso of
-    chunk k+1.  Autograd runs every backward node on its forward stream, so
-    the backward overlaps the same way in reverse: once the recurrence of the
-    last chunk has produced its input gradient, that chunk's torso backward
-    runs while the recurrence backward continues on earlier chunks.  Both
-    directions are fork/join DAGs that a captured hipGraph replays
-    concurrently (tools/micro/graph_fork.hip).  Same math as core_unroll.
+    The conv torso of time chunk k runs on the current (main) stream; the
+    core of chunk k (fused torso-FC / core-input / x-projection GEMMs and
+    the recurrence, ops.core_lstm - the same kernels as the unchunked path,
+    with the LSTM state carried from chunk to chunk) runs on a side stream as
+    soon as chunk k's features exist, overlapping the torso of chunk k+1.
+    Autograd runs every backward node on its forward stream, so the backward
+    overlaps the same way in reverse: once the recurrence of the last chunk
+    has produced its input gradient, that chunk's torso backward runs while
+    the recurrence backward continues on earlier chunks.  Both directions
+    are fork/join DAGs that a captured hipGraph replays concurrently
+    (tools/micro/graph_fork.hip).  The persistent conv grids leave
+    cf32_cu_reserve() CUs per XCD to the side stream (set before capture).
+
+    Chunk lengths: equal, or in the proportions of SA_PIPELINE_SPLIT (e.g.
+    "9,9,2": a short last chunk keeps the exposed recurrence short at the
+    end of the forward and the start of the backward).  Same math as
+    unroll_core (the recurrence is sequential either way).
     """
     from .. import ops
     T, B = done.shape
     dev = frames.device
     main = torch.cuda.current_stream(dev)
     side = self._core_stream(dev)
+    bounds = _chunk_bounds(T, chunks, os.environ.get('SA_PIPELINE_SPLIT'))
+    fused = self.fused_core_ready(instr)
     F_in = self.core_input_size
-    w_x = self.lstm_kernel[:F_in]
-    w_h = self.lstm_kernel[F_in:]
-    bounds = [(T * k) // chunks for k in range(chunks + 1)]
     outs = []
-    for k in range(chunks):
+    for k in range(len(bounds) - 1):
       t0, t1 = bounds[k], bounds[k + 1]
       n0, n1 = t0 * B, t1 * B
       ins = None
       if instr is not None:
         ins = (instr[0][n0:n1], instr[1][n0:n1])
-      x = self.core_inputs(frames[n0:n1], reward[n0:n1], actions[n0:n1], ins)
-      x = x.view(t1 - t0, B, -1)
+      if fused:
+        feats = self.conv_features(frames[n0:n1])
+        instr_enc = (None if ins is None else
+                     self.instruction_encoding(ins, n1 - n0, dev))
+      else:
+        x = self.core_inputs(frames[n0:n1], reward[n0:n1], actions[n0:n1],
+                             ins).view(t1 - t0, B, -1)
       side.wait_stream(main)
-      x.record_stream(side)
       with torch.cuda.stream(side):
-        hs, state = ops.lstm_unroll(x, done[t0:t1], state, self.lstm_kernel,
-                                    self.lstm_bias, w_x=w_x, w_h=w_h,
-                                    exact=self.compute_dtype == torch.float32)
+        if fused:
+          feats.record_stream(side)
+          hs, state = ops.core_lstm(
+              feats, self.linear_w, self.linear_b, self.lstm_kernel,
+              self.lstm_bias, reward[n0:n1], actions[n0:n1], done[t0:t1],
+              state, self.num_actions, instr_enc=instr_enc, allow_gang=False)
+        else:
+          x.record_stream(side)
+          hs, state = ops.lstm_unroll(
+              x, done[t0:t1], state, self.lstm_kernel, self.lstm_bias,
+              w_x=self.lstm_kernel[:F_in], w_h=self.lstm_kernel[F_in:],
+              exact=self.compute_dtype == torch.float32)
       outs.append(hs)
     main.wait_stream(side)
     for h in outs:

@@ -53,7 +53,7 @@ class _CoreLSTM(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc):
+              done_u8, num_actions, instr_enc, allow_gang=True):
     C = ext()
     T, B = done_u8.shape
     N = T * B
@@ -81,7 +81,10 @@ class _CoreLSTM(torch.autograd.Function):
     wx16 = kernel[:K].to(bf)
     xw = torch.empty(N, 4 * CORE, dtype=torch.float32, device=feats.device)
     C.gemm_bf16(h_aug, wx16, False, False, xw, bias=bias)
-    mode = C.lstm_mode(CORE, B, T, False)  # bf16 path: the gang may run
+    # bf16 path: the gang may run - unless the caller runs the conv torso
+    # concurrently (the time-chunked pipeline): the gang's 8 workgroups must
+    # co-reside, which persistent conv grids next to it cannot guarantee
+    mode = C.lstm_mode(CORE, B, T, not allow_gang)
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
                                        kernel[f_in:], mode)
     ctx.mode = mode
@@ -135,8 +138,11 @@ class _CoreLSTM(torch.autograd.Function):
                   colsum=gbfc)                                      # W_fc, b_fc
     dh0 = None
     if ctx.needs_input_grad[8]:
+      # (a chunk boundary of the pipelined unroll): exact-fp32 MFMA GEMM
       keep0 = (done_u8[0] == 0).to(torch.float32).unsqueeze(-1)
-      dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
+      dh0 = torch.empty(B, CORE, dtype=torch.float32, device=dg.device)
+      C.gemm_f32(dg[0], kernel[f_in:], False, True, dh0)
+      dh0.mul_(keep0)
     if not ctx.needs_input_grad[7]:
       dc0 = None
     d_instr = None
@@ -146,7 +152,7 @@ class _CoreLSTM(torch.autograd.Function):
       C.gemm_bf16(dg16_2, wx16[ctx.c_instr:f_in], False, True, d_instr)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
     return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
-            d_instr)
+            d_instr, None)
 
 
 class _CoreLSTMF32(torch.autograd.Function):
@@ -170,7 +176,7 @@ class _CoreLSTMF32(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc):
+              done_u8, num_actions, instr_enc, allow_gang=True):
     C = ext()
     T, B = done_u8.shape
     N = T * B
@@ -235,8 +241,11 @@ class _CoreLSTMF32(torch.autograd.Function):
                colsum=gbfc)                                         # W_fc, b_fc
     dh0 = None
     if ctx.needs_input_grad[8]:
+      # (a chunk boundary of the pipelined unroll): exact-fp32 MFMA GEMM
       keep0 = (done_u8[0] == 0).to(torch.float32).unsqueeze(-1)
-      dh0 = (dg[0] @ kernel[f_in:].t()) * keep0
+      dh0 = torch.empty(B, CORE, dtype=torch.float32, device=dg.device)
+      C.gemm_f32(dg[0], kernel[f_in:], False, True, dh0)
+      dh0.mul_(keep0)
     if not ctx.needs_input_grad[7]:
       dc0 = None
     d_instr = None
@@ -245,7 +254,7 @@ class _CoreLSTMF32(torch.autograd.Function):
       C.gemm_f32(dg2, kernel[ctx.c_instr:f_in], False, True, d_instr)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
     return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
-            d_instr)
+            d_instr, None)
 
 
 def _as_u8(done):
@@ -258,7 +267,7 @@ def _as_u8(done):
 
 
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
-              num_actions, instr_enc=None):
+              num_actions, instr_enc=None, allow_gang=True):
   """feats [T*B, F] (ReLU'd torso output: bf16 -> the bf16-operand path,
   fp32 -> the exact-fp32 path), rewards [T*B] f32, actions [T*B] (last
   actions), done [T,B] bool, state (c, h) [B,256], instr_enc None or the
@@ -272,5 +281,6 @@ def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
       actions.reshape(-1).to(torch.int64).contiguous(),
       c0.float().contiguous(), h0.float().contiguous(),
       _as_u8(done), int(num_actions),
-      None if instr_enc is None else instr_enc.float().contiguous())
+      None if instr_enc is None else instr_enc.float().contiguous(),
+      bool(allow_gang))
   return hs, (c_last, hs[-1])
