@@ -646,6 +646,12 @@ bool wino_geo_enabled() {
   if (g_wino_geo < 0) g_wino_geo = env_int("SA_WINO_GEO", 1) != 0 ? 1 : 0;
   return g_wino_geo != 0;
 }
+// per kernel family (SA_WINO_GEO_MASK, sweeps): bit 0 the forward, bit 1 the
+// 16-channel fused backward, bit 2 the fused32 backward
+bool wino_geo_family(int bit) {
+  static const int mask = env_int("SA_WINO_GEO_MASK", 7);
+  return wino_geo_enabled() && (mask & bit) != 0;
+}
 
 // The deep torso's maps get compile-time instances (only where that layer
 // runs): the IMPALA / DMLab 72x96 ladder (36x48, 18x24, 9x12) and the Atari
@@ -655,8 +661,8 @@ bool wino_geo_enabled() {
 // 9x12, 21x21, 11x11.
 #define SA_GEO(h, w) \
   if (HH == (h) && WW == (w) && SA_CALL(h, w)) return true;
-#define SA_WINO_GEO_DISPATCH(CI, CO)                             \
-  if (wino_geo_enabled()) {                                      \
+#define SA_WINO_GEO_DISPATCH(CI, CO, FAM)                        \
+  if (wino_geo_family(FAM)) {                                    \
     if constexpr ((CI) == 16) { SA_GEO(36, 48) SA_GEO(42, 42) }  \
     if constexpr ((CI) == 32 && (CO) == 32) {                    \
       SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) \
@@ -674,7 +680,7 @@ template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS>
 bool run_wino_ct(const ConvArgs& c, bool flip, hipStream_t s) {
   const int HH = c.Ho, WW = c.Wo;
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, -1, h, w>(c, flip, s)
-  SA_WINO_GEO_DISPATCH(CIN, COUT)
+  SA_WINO_GEO_DISPATCH(CIN, COUT, 1)
 #undef SA_CALL
   return run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS>(c, flip, s);
 }
@@ -2714,7 +2720,7 @@ bool run_wino_bwd32_t(const float* dy, const float* w, const float* x, const flo
   run_wino_bwd32_g<CX, CY, RT, MAXCX, MAXCY, RELU, MASK, h, w_>(dy, w, x, add, out, relu_x, \
                                                                 mask_x, N, H, W, ws,        \
                                                                 ws_floats, dw, db, s)
-    if constexpr (CX == 32 || !MASK) { SA_WINO_GEO_DISPATCH(CX, CY) }
+    if constexpr (CX == 32 || !MASK) { SA_WINO_GEO_DISPATCH(CX, CY, 4) }
 #undef SA_CALL
   }
   return run_wino_bwd32_g<CX, CY, RT, MAXCX, MAXCY, RELU, MASK>(
@@ -2795,7 +2801,7 @@ bool run_wino_bwd(const float* dy, const float* w, const float* x, const float* 
 #define SA_CALL(h, w_)                                                                  \
   run_wino_bwd_g<C, RT, MAXC, KD, WWG, NW, h, w_>(dy, w, x, add, out, relu_x, N, H, W, ws, \
                                                   ws_floats, dw, db, s)
-    SA_WINO_GEO_DISPATCH(C, C)
+    SA_WINO_GEO_DISPATCH(C, C, 2)
 #undef SA_CALL
   }
   return run_wino_bwd_g<C, RT, MAXC, KD, WWG, NW>(dy, w, x, add, out, relu_x, N, H, W, ws,

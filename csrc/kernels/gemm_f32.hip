@@ -292,6 +292,13 @@ __global__ __launch_bounds__(256) void gemm_f32_bl_kernel(Args a) {
       }
     }
   };
+  // LDS images: an operand whose global rows run along K (A[m][k], B[n][k])
+  // is stored [m or n][k] (pitch PK: conflict-free 16-B k-quad reads); one
+  // whose rows run along M / N (A[k][m] when TA, B[k][n] when !TB) is
+  // stored as it comes, [k][m or n] with 16-B stores, and read one k at a
+  // time (consecutive lanes, consecutive m / n: conflict-free 4-B reads).
+  // Transposing those on the commit (four 4-B stores per quad, rows 4 PK
+  // apart) cost 9-14 bank-conflict cycles per LDS instruction (PMC).
   auto commit = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < KQ; ++j) {
@@ -302,14 +309,12 @@ __global__ __launch_bounds__(256) void gemm_f32_bl_kernel(Args a) {
               ra[r][j];
         } else {
           const int k = (t >> 4) + 16 * j, m = 64 * r + 4 * (t & 15);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) As[buf][(m + q) * PK + k] = ra[r][j][q];
+          *reinterpret_cast<f4*>(&As[buf][k * BMt + m]) = ra[r][j];
         }
       }
       if constexpr (!TB) {
         const int k = (t >> 4) + 16 * j, n = 4 * (t & 15);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Bs[buf][(n + q) * PK + k] = rb[j][q];
+        *reinterpret_cast<f4*>(&Bs[buf][k * BN + n]) = rb[j];
       } else {
         *reinterpret_cast<f4*>(&Bs[buf][(t >> 2) * PK + 4 * (t & 3) + 16 * j]) = rb[j];
       }
@@ -323,6 +328,7 @@ __global__ __launch_bounds__(256) void gemm_f32_bl_kernel(Args a) {
     for (int e = 0; e < 16; ++e) acc[r][e] = 0.f;
   const int arow = (wm * 32 * RM + l32) * PK + (BK / 2) * h;
   const int brow = (wn * 32 + l32) * PK + (BK / 2) * h;
+  const int kh = (BK / 2) * h;
   int buf = 0;
   if (kbeg < kend) {
     load(kbeg);
@@ -337,10 +343,24 @@ __global__ __launch_bounds__(256) void gemm_f32_bl_kernel(Args a) {
     load(k0 + BK);  // in flight under the MFMAs
 #pragma unroll
     for (int c = 0; c < BK / 8; ++c) {
-      const f4 bv = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4 * c]);
+      // k = BK/2 h + 4 c + s for MFMA s of lane half h (both operands)
+      f4 bv;
+      if constexpr (TB) {
+        bv = *reinterpret_cast<const f4*>(&Bs[buf][brow + 4 * c]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[s] = Bs[buf][(kh + 4 * c + s) * BN + wn * 32 + l32];
+      }
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
-        const f4 av = *reinterpret_cast<const f4*>(&As[buf][arow + 32 * r * PK + 4 * c]);
+        f4 av;
+        if constexpr (!TA) {
+          av = *reinterpret_cast<const f4*>(&As[buf][arow + 32 * r * PK + 4 * c]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            av[s] = As[buf][(kh + 4 * c + s) * BMt + wm * 32 * RM + 32 * r + l32];
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s)
           acc[r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], bv[s], acc[r], 0, 0, 0);
