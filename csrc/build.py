@@ -172,11 +172,20 @@ def main():
   ap.add_argument('--force', action='store_true')
   ap.add_argument('--only', choices=['C', 'native'], default=None)
   ap.add_argument('--sanitize', choices=['thread', 'address'], default=None)
+  ap.add_argument('--define', action='append', default=[],
+                  help='experiment builds: -D NAME=VAL for the HIP extension '
+                       '(objects in their own build dir); use with --out')
+  ap.add_argument('--out', default=None,
+                  help='HIP extension output path (experiment builds, loaded '
+                       'with SA_EXT_PATH)')
   args = ap.parse_args()
-  if args.only in (None, 'native'):
+  if args.define and not args.out:
+    ap.error('--define needs --out (the in-tree _C.so stays the default build)')
+  if args.only in (None, 'native') and not args.define:
     build_native(args.j, args.force, args.sanitize)
   if args.only in (None, 'C') and not args.sanitize:
-    build_hip(args.j, args.force)
+    build_hip(args.j, args.force, extra_flags=['-D' + d for d in args.define],
+              out=args.out)
 
 
 if __name__ == '__main__':
