@@ -1009,6 +1009,13 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
   extern __shared__ __attribute__((aligned(16))) f4 xs[];  // [2*kPwRows+3][W+2]
   const int co = threadIdx.x & 15, ps = threadIdx.x >> 4;
   const int Wl = pw_pitch(W);
+  if constexpr (U8) {
+    // exact x / 255 (the fp32 quotient the frame conversion produces)
+    float* lut = reinterpret_cast<float*>(
+        reinterpret_cast<uint32_t*>(xs + (2 * kPwRows + 3) * Wl) + (2 * kPwRows + 3) * 64 * 4);
+    for (int i = threadIdx.x; i < 256; i += kThreads)
+      lut[i] = static_cast<float>(static_cast<double>(i) / 255.0);
+  }
   float acc[9][4];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -1038,23 +1045,45 @@ __global__ __launch_bounds__(kThreads) void pool_wgrad_kernel(
       }
     }
     __syncthreads();  // the previous tile's LDS reads are done
-    for (int e = threadIdx.x; e < rows * Wl; e += kThreads) {
-      const int r = e / Wl, c = e - r * Wl;
-      const int yy = ybase + r, xx = c - 1;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const int64_t pix = (static_cast<int64_t>(n) * H + yy) * W + xx;
-        if constexpr (U8) {
-          const uint8_t* p = xu + pix * u8_cs;
-          v[0] = static_cast<float>(p[0]) / 255.f;
-          if (u8_cs > 1) v[1] = static_cast<float>(p[1]) / 255.f;
-          if (u8_cs > 2) v[2] = static_cast<float>(p[2]) / 255.f;
-          if (u8_cs > 3) v[3] = static_cast<float>(p[3]) / 255.f;
-        } else {
-          v = x[pix];
-        }
+    if constexpr (U8) {
+      // the tile's frame rows as raw bytes (coalesced dword loads: a row is
+      // W * u8_cs bytes, a multiple of 4 - the launcher checks), then each
+      // LDS pixel expanded from them through the exact x / 255 table
+      uint32_t* raw = reinterpret_cast<uint32_t*>(xs + (2 * kPwRows + 3) * Wl);
+      const float* lut = reinterpret_cast<const float*>(raw + (2 * kPwRows + 3) * 64 * 4);
+      const int rowd = W * u8_cs / 4;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(xu);
+      for (int d = threadIdx.x; d < rows * rowd; d += kThreads) {
+        const int r = d / rowd, k = d - r * rowd;
+        const int yy = ybase + r;
+        uint32_t v = 0u;
+        if (yy >= 0 && yy < H) v = src[(static_cast<int64_t>(n) * H + yy) * rowd + k];
+        raw[r * rowd + k] = v;
       }
-      xs[e] = v;
+      __syncthreads();
+      const uint8_t* rb = reinterpret_cast<const uint8_t*>(raw);
+      for (int e = threadIdx.x; e < rows * Wl; e += kThreads) {
+        const int r = e / Wl, c = e - r * Wl;
+        const int xx = c - 1;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (xx >= 0 && xx < W) {
+          const uint8_t* q = rb + (r * W + xx) * u8_cs;
+          v[0] = lut[q[0]];
+          if (u8_cs > 1) v[1] = lut[q[1]];
+          if (u8_cs > 2) v[2] = lut[q[2]];
+          if (u8_cs > 3) v[3] = lut[q[3]];
+        }
+        xs[e] = v;
+      }
+    } else {
+      for (int e = threadIdx.x; e < rows * Wl; e += kThreads) {
+        const int r = e / Wl, c = e - r * Wl;
+        const int yy = ybase + r, xx = c - 1;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          v = x[(static_cast<int64_t>(n) * H + yy) * W + xx];
+        xs[e] = v;
+      }
     }
     __syncthreads();
     int pyl = 0, px = ps;  // (row, col) of pooled pixel p = ps + 16 k
@@ -1691,9 +1720,15 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, int u8_cs, hipStream_t
   const int ntiles = a.N * tpi;
   static const int slots = std::max(1, std::min(kPwSlots, env_knob("SA_F32_PW_SLOTS", kPwSlots)));
   const int G = std::min(ntiles, slots);
-  const size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
-                                      sizeof(float) * 4 * 37 * 16);
+  size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
+                                sizeof(float) * 4 * 37 * 16);
   if (u8_cs > 0) {
+    // raw byte rows (W * u8_cs <= 256 dwords per row) + the 256-entry table
+    // after the f4 image; rows must be whole dwords
+    if ((a.W * u8_cs) % 4 != 0 || a.W * u8_cs > 1024) return false;
+    lds = std::max<size_t>(lds, sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W) +
+                                    sizeof(uint32_t) * (2 * kPwRows + 3) * 256 +
+                                    sizeof(float) * 256);
     allow_lds(pool_wgrad_kernel<true>, lds);
     hipLaunchKernelGGL(pool_wgrad_kernel<true>, dim3(G), dim3(kThreads), lds, s, a.src,
                        u8_cs, a.dy, pg.arg, a.H, a.W, pg.Hp, pg.Wp, pg.pbh, pg.pbw, tpi,

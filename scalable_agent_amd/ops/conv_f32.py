@@ -54,6 +54,12 @@ POOL_SCATTER = os.environ.get('SA_F32_POOL_SCATTER', '1') != '0'
 # measured slower on bytes (conv+pool 639 vs 529 + 120 us, scatter wgrad
 # 463 vs 229 us: per-pixel byte loads) and the shallow learner step too
 # (5.15 vs 5.01 ms), so both default to the fp32 image; kept switchable
+# Stage-0 scatter wgrad reading the uint8 frames (coalesced dword rows, exact
+# x / 255 table in LDS) instead of the 4-channel fp32 image the forward conv
+# reads (the image is then dropped after the forward): opt-in
+# (SA_F32_PW_U8=1) - measured slower, 9.47-9.52 vs 9.37 ms per fp32 step
+# (the byte expansion in LDS costs more than the image reads it saves)
+PW_U8 = os.environ.get('SA_F32_PW_U8', '0') == '1'
 U8_DIRECT = {
     'deep': os.environ.get('SA_F32_U8_DEEP', '0') == '1',
     'shallow': os.environ.get('SA_F32_U8_SHALLOW', '0') == '1'}
@@ -153,7 +159,13 @@ class _DeepTorsoF32(torch.autograd.Function):
         xa, arg = C.cf32_maxpool_fwd(conv, pbh, pbw)
         del conv
       h, w_ = xa.shape[1], xa.shape[2]
-      saved += [x, arg]
+      # stage 0 on the scatter wgrad path: its backward reads the uint8
+      # frames, so the fp32 image is not kept alive for it
+      keep = (frames if (s == 0 and PW_U8 and POOL_SCATTER and
+                         x.dtype == torch.float32 and frames.dtype == torch.uint8 and
+                         frames.shape[3] <= 4 and xa.shape[3] == 16)
+              else x)
+      saved += [keep, arg]
       for blk in range(2):
         w1, b1, w2, b2 = params[p:p + 4]
         p += 4
