@@ -699,15 +699,30 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   // 3 (default): the compile-time-geometry 16 -> 16 instances with the two
   // residual flag sets compile-time too (conv 1 = 19, conv 2 = 24): full
   // fp32 step 9.546 / 9.547 -> 9.502 / 9.460 ms (geometry alone; one box)
-  static const int on = env_int("SA_WINO_FL", 3);
+  // 4 (default) adds the 32 -> 32 residual convs at 18x24: 9.474 / 9.449 /
+  // 9.446 (3) -> 9.466 / 9.434 / 9.429 ms
+  static const int on = env_int("SA_WINO_FL", 4);
   if constexpr (CIN == 16 && COUT == 16) {
-    if (on == 3 && !flip && wino_geo_enabled()) {
+    if (on >= 3 && !flip && wino_geo_enabled()) {
       const int HH = c.Ho, WW = c.Wo;
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
       if (fl == 19) { SA_GEO(36, 48) SA_GEO(42, 42) }
 #undef SA_CALL
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
       if (fl == 24) { SA_GEO(36, 48) SA_GEO(42, 42) }
+#undef SA_CALL
+    }
+  }
+  // 4: also the 32 -> 32 residual convs at 18x24 (188 / 210 VGPRs, no
+  // spills in the geometry instances)
+  if constexpr (CIN == 32 && COUT == 32) {
+    if (on >= 4 && !flip && wino_geo_enabled()) {
+      const int HH = c.Ho, WW = c.Wo;
+#define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
+      if (fl == 19) { SA_GEO(18, 24) }
+#undef SA_CALL
+#define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
+      if (fl == 24) { SA_GEO(18, 24) }
 #undef SA_CALL
     }
   }
