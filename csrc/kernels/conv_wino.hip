@@ -719,10 +719,11 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
     if (on >= 4 && !flip && wino_geo_enabled()) {
       const int HH = c.Ho, WW = c.Wo;
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
+      // (the 19 instances of the odd maps spill 4-6 VGPRs: runtime flags there)
       if (fl == 19) { SA_GEO(18, 24) }
 #undef SA_CALL
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
-      if (fl == 24) { SA_GEO(18, 24) }
+      if (fl == 24) { SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) }
 #undef SA_CALL
     }
   }
