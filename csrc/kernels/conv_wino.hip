@@ -806,6 +806,13 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   constexpr int C4 = CIN / 4, LC4 = C4 == 4 ? 2 : 0;
   constexpr int NG = RT / 16;
   constexpr int Wl = W + 2, rowstr = Wl * PP;
+  // CIN == 4 (stage 0): the staged rows are channel planes [4][ROWS][Wl] with
+  // an odd plane stride, so a lane's scalar patch reads (16 tiles x 2 pixels
+  // apart, channel g) hit 32 distinct banks; the interleaved [pixel][4]
+  // layout put the 16 tiles of a half-wave on 4 banks (PMC: 5.0 bank-
+  // conflict cycles per LDS instruction)
+  constexpr int PS = (P::ROWS * Wl) | 1;
+  static_assert(CIN != 4 || 4 * PS <= P::XREG, "planes fit the staging region");
   static_assert(CIN == 4 || CIN == 16, "CIN");
   static_assert(NW * 64 == 2 * WP * CQ, "two pooled rows x WP columns x CQ quads = the workgroup");
   static_assert(RT % 16 == 0 && MAXC <= 32, "shape");
@@ -907,7 +914,8 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   const int txl = 16 * grp + c16;  // tile within the range = (row txl / (W/2), column)
   const int tyl = txl / (W / 2), tx = txl - tyl * (W / 2);
   // CIN 16: 4 channels 4g.. of each patch pixel; CIN 4: channel g
-  const float* xp = x_s + (2 * tyl * Wl + 2 * tx) * PP + (CIN == 16 ? 4 * g : g);
+  const float* xp = CIN == 16 ? x_s + (2 * tyl * Wl + 2 * tx) * PP + 4 * g
+                              : x_s + g * PS + 2 * tyl * Wl + 2 * tx;
   const float* up = CIN == 16 ? U_s + (g * COUT + co0 + c16) * 4 : U_s + g * COUT + co0 + c16;
   const f4 bv = *reinterpret_cast<const f4*>(a.bias + co0 + 4 * g);
 
@@ -917,7 +925,12 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
     for (int k = 0; k < MAXC; ++k) {
       if (sl_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
-        *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = stg[k];
+        if constexpr (CIN == 16) {
+          *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = stg[k];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x_s[q * PS + e] = stg[k][q];
+        }
       }
     }
     const int cur = r;
@@ -971,7 +984,7 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
 #pragma unroll
         for (int dy = 0; dy < 4; ++dy)
 #pragma unroll
-          for (int dx = 0; dx < 4; ++dx) d[4 * dy + dx] = xp[dy * rowstr + dx * PP];
+          for (int dx = 0; dx < 4; ++dx) d[4 * dy + dx] = xp[dy * Wl + dx];
         float s[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
