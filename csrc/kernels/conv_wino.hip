@@ -797,6 +797,54 @@ __device__ __forceinline__ uint32_t pack_codes(const int (&code)[4]) {
          (static_cast<uint32_t>(code[2]) << 16) | (static_cast<uint32_t>(code[3]) << 24);
 }
 
+// Pool-phase lane -> (pooled column, channel quad) map of one wave (64 / CQ
+// columns x CQ quads): every 16-lane group of a ds_read_b128 (gfx950 lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
+// {36-43,48-51,60-63}) reads 16 distinct 16-B bank segments of the pre-pool
+// image (pixel pitch IPP floats, pooled column pj -> pixel 2 pj): each
+// segment s = (pj IPP / 2 + pq) mod 16 is taken by exactly one (pj, pq) per
+// group.  The natural map (pq = lane % CQ) put 2-4 lanes of a group on one
+// segment.
+__host__ __device__ constexpr int b128_group(int l) {
+  const int h = l & 31;
+  const int g = (h < 4 || (h >= 12 && h < 16) || (h >= 20 && h < 28)) ? 0 : 1;
+  return g + 2 * (l >> 5);
+}
+template <int CQ, int IPP>
+struct PoolLaneMap {
+  unsigned char pj[64] = {}, pq[64] = {};
+  constexpr PoolLaneMap() {
+    constexpr int NP = 64 / CQ;
+    bool used[64] = {};
+    for (int g = 0; g < 4; ++g) {
+      int next = 0;  // next lane of group g to assign
+      for (int seg = 0; seg < 16; ++seg) {
+        int pick = -1;
+        for (int c = 0; c < NP && pick < 0; ++c)
+          for (int q = 0; q < CQ && pick < 0; ++q)
+            if (!used[c * CQ + q] && (c * (IPP / 2) + q) % 16 == seg) pick = c * CQ + q;
+        while (b128_group(next) != g) ++next;
+        used[pick] = true;
+        pj[next] = static_cast<unsigned char>(pick / CQ);
+        pq[next] = static_cast<unsigned char>(pick % CQ);
+        ++next;
+      }
+    }
+  }
+};
+template <int CQ, int IPP>
+constexpr bool pool_lane_map_ok() {
+  constexpr PoolLaneMap<CQ, IPP> m{};
+  bool seen[64] = {};
+  for (int l = 0; l < 64; ++l) {
+    const int id = m.pj[l] * CQ + m.pq[l];
+    if (m.pj[l] >= 64 / CQ || seen[id]) return false;
+    seen[id] = true;
+  }
+  return true;
+}
+static_assert(pool_lane_map_ok<8, 36>() && pool_lane_map_ok<4, 20>(), "pool lane map");
+
 template <int CIN, int COUT, int RT>
 __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
     WinoPoolArgs pa) {
@@ -900,7 +948,9 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   // threads own pooled row 2k (9 taps), the rest the odd row 2k+1 (its
   // carried part + 3 taps of the next range, then 6 taps): balanced
   const int pt = threadIdx.x % (WP * CQ);
-  const int pj = pt / CQ, pq = pt % CQ;
+  static_assert((WP * CQ) % 64 == 0, "whole waves per pooled row");
+  constexpr PoolLaneMap<CQ, IPP> kMap{};
+  const int pj = (pt >> 6) * (64 / CQ) + kMap.pj[pt & 63], pq = kMap.pq[pt & 63];
   const bool even_row = threadIdx.x < WP * CQ;
   constexpr float kNegInf = -__builtin_inff();
   f4 cv = {kNegInf, kNegInf, kNegInf, kNegInf};
@@ -1057,8 +1107,9 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
           *reinterpret_cast<f4*>(pa.pooled + cdst) = best;
           *reinterpret_cast<uint32_t*>(pa.arg + cdst) = pack_codes(code);
         } else {  // the run's first range: the previous workgroup holds rows 4k-2, 4k-1
-          pa.side_v[blockIdx.x * (WP * CQ) + pt] = best;
-          pa.side_c[blockIdx.x * (WP * CQ) + pt] = pack_codes(code);
+          // (indexed by (pj, pq): wino_pool_fix_kernel's thread numbering)
+          pa.side_v[blockIdx.x * (WP * CQ) + pj * CQ + pq] = best;
+          pa.side_c[blockIdx.x * (WP * CQ) + pj * CQ + pq] = pack_codes(code);
         }
       }
       // (b) pooled row 2k: pixel rows 4k .. 4k+2
