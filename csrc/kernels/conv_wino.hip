@@ -1431,7 +1431,14 @@ __global__ __launch_bounds__(512, 1) void wino_conv_pool_img_kernel(WinoPoolArgs
     __syncthreads();
     // pool phase: every window of the image (pad-before 0, the bottom /
     // right tap row beyond the image is padding)
-    for (int e = threadIdx.x; e < Hp * Wp * CQ; e += NTH) {
+    // lanes permuted inside each 64-element chunk (8 pooled pixels x 8
+    // quads) by the conflict-free pool lane map (wino_conv_pool_kernel)
+    static_assert(CQ == 8, "lane map for 8 channel quads");
+    constexpr PoolLaneMap<CQ, IPP> kMap{};
+    const int lmap = kMap.pj[threadIdx.x & 63] * CQ + kMap.pq[threadIdx.x & 63];
+    for (int e0 = threadIdx.x & ~63; e0 < Hp * Wp * CQ; e0 += NTH) {
+      const int e = e0 + lmap;
+      if (e >= Hp * Wp * CQ) continue;
       const int pr = e / (Wp * CQ), rem = e - pr * (Wp * CQ);
       const int pc = rem / CQ, pq = rem - pc * CQ;
       f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
