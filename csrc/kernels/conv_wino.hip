@@ -225,20 +225,66 @@ __host__ __device__ constexpr int wino_maxrows(int RT, int TX, int TY) {
              : 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * wino_parts(RT, TY * TX);
 }
 
-template <int GH, int GW, int RT>
+// Staged-row pitch padding (compile-time geometry only).  A 16-tile patch
+// read whose tiles wrap to the next tile row jumps by 2 Wl - 2 TX pixels
+// instead of 0; at 5 (20-float pitch) or 9 (36-float pitch) 16-B units per
+// pixel that jump lands the wrapped lanes on the 16-B bank groups of the
+// unwrapped ones unless Wl - TX = 0 mod 8.  Padding each LDS row to that
+// makes the wrap free: modelled b128 cycles per patch read 1.33 -> 1.00 at
+// 36x48, 1.71 -> 1.03 at 42x42, 1.89 -> 1.11 at 18x24, 2.36 -> 1.12 at
+// 21x21 (9x12 and 11x11 need no pad).  The stagers keep the unpadded
+// element numbering; only the LDS address of a staged row moves.
+// SA_WINO_LPAD bit 0: the forward kernel, 1: the fused 16-channel backward,
+// 2: the fused32 backward (where its LDS budget allows).  Measured (in-step
+// PMC, profiles/experiments.md round 5): the conflicts drop as modelled but
+// the step time does not move, and the fused32 instances spill more with
+// it, so only the forward (no spills either way) pads by default.
+#ifndef SA_WINO_LPAD
+#define SA_WINO_LPAD 1
+#endif
+constexpr bool wino_lpad_on(int bit) { return (SA_WINO_LPAD >> bit) & 1; }
+__host__ __device__ constexpr int wino_lpad(int TX) {
+  return (8 - (TX + 2) % 8) % 8;
+}
+// L * padc for a stager commit.  SA_WINO_LPAD_OPQ=1 recomputes it at every
+// commit from an opaque copy of L (keeps the products out of the range
+// loop's invariants; measured: more spills, not fewer)
+#ifndef SA_WINO_LPAD_OPQ
+#define SA_WINO_LPAD_OPQ 0
+#endif
+template <int PADC>
+__device__ __forceinline__ int pad_pix(int L) {
+  if constexpr (PADC == 0) {
+    return 0;
+  } else {
+    if constexpr (SA_WINO_LPAD_OPQ) asm volatile("" : "+v"(L));
+    return L * PADC;
+  }
+}
+// LDS row pitch (pixels) of a kernel instance at tile-grid width TX
+template <int GH, bool LP = true>
+constexpr int wino_wl(int TX) {
+  return 2 * TX + 2 + (GH > 0 && LP ? wino_lpad(TX) : 0);
+}
+
+template <int GH, int GW, int RT, bool LP = true>
 struct TileGeo {
   static constexpr bool kCt = GH > 0;
   static constexpr int cTY = (GH + 1) / 2, cTX = (GW + 1) / 2;
   // images one range may touch
   static constexpr int MP = kCt ? wino_parts(RT, cTY * cTX) : kMaxParts;
   static constexpr int cMaxRows = kCt ? wino_maxrows(RT, cTX, cTY) : 0;
+  // row padding (pixels): staged row L sits at LDS pixel L * WL, its
+  // element e (unpadded numbering over WL0-pixel rows) at e + L * PADC
+  static constexpr int PADC = kCt && LP ? wino_lpad(cTX) : 0;
   static_assert(MP <= kMaxParts, "range spans too many images");
-  int H, W, TY, TX, NT, maxrows;
+  int H, W, TY, TX, NT, maxrows, WL0, WL;
   float rTX, rTY;
   __device__ __forceinline__ TileGeo(int H_, int W_, int TY_, int TX_, int NT_, float rTX_,
                                      float rTY_, int maxrows_)
       : H(kCt ? GH : H_), W(kCt ? GW : W_), TY(kCt ? cTY : TY_), TX(kCt ? cTX : TX_), NT(NT_),
-        maxrows(kCt ? cMaxRows : maxrows_), rTX(rTX_), rTY(rTY_) {}
+        maxrows(kCt ? cMaxRows : maxrows_), WL0(2 * TX + 2), WL(2 * TX + 2 + PADC), rTX(rTX_),
+        rTY(rTY_) {}
   // (t, R >= 0: unsigned constant division is a multiply-high and a shift)
   __device__ __forceinline__ int div_tx(int t) const {
     return kCt ? static_cast<int>(static_cast<unsigned>(t) / cTX) : fdivi(t, rTX);
@@ -289,7 +335,8 @@ template <int CIN, int COUT, int NH, int NW, int RT, int MAXC, int WPS, int FL =
           int GW = 0>
 __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
-  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
+  const TileGeo<GH, GW, RT, wino_lpad_on(0)> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY,
+                                                a.maxrows);
   constexpr bool kPk = SA_WINO_PK == 1;
   const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
   const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
@@ -351,7 +398,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int Wl = 2 * G.TX + 2;
+  const int Wl = G.WL;
   const int rowstr = Wl * PP;
 
   const RangeWalk rw = range_walk(a.nranges, a.runs);
@@ -375,7 +422,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   for (int k = 0; k < MAXC; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4 - 1), pix = e >> LC4;
-    const int L = pix / Wl, col = pix - L * Wl;
+    const int L = pix / G.WL0, col = pix - L * G.WL0;
     sl_L[k] = L < G.maxrows ? L : -1;
     // -1: column in the zero padding
     sl_x[k] = (col >= 1 && col <= G.W) ? (col - 1) * CIN + 4 * ch : -1;
@@ -419,7 +466,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) v[q] = relu0(v[q]);
         }
-        *reinterpret_cast<f4*>(x_s + (e >> LC4) * PP + 4 * (e & (C4 - 1))) = v;
+        *reinterpret_cast<f4*>(x_s + ((e >> LC4) + pad_pix<decltype(G)::PADC>(sl_L[k])) * PP + 4 * (e & (C4 - 1))) = v;
       }
     }
     const int cur = r;
@@ -594,7 +641,7 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   const int per_img = TY * TX;
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
-  const int Wl = 2 * TX + 2;
+  const int Wl = 2 * TX + 2, WlP = wino_wl<GH, wino_lpad_on(0)>(TX);
   // staged rows <= 2 (tile rows spanned) + 2 (images touched); exactly
   // 2 RT / TX + 2 when every range is whole tile rows of one image
   int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
@@ -602,7 +649,7 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   if (static_cast<int64_t>(maxrows) * Wl * (CIN / 4) > static_cast<int64_t>(MAXC) * 64 * NW)
     return false;
   const size_t bytes = sizeof(float) * (16 * CIN * COUT +
-                                        static_cast<size_t>(maxrows) * Wl * (CIN + 4) +
+                                        static_cast<size_t>(maxrows) * WlP * (CIN + 4) +
                                         maxrows);
   if (static_cast<int64_t>(c.N) * H * W * CIN * 4 > kMaxBufBytes || maxrows > 64 * NW)
     return false;
@@ -1906,7 +1953,8 @@ template <int C, int RT, int MAXC, int KD, bool WWG = false, bool RELU = false, 
           int GH = 0, int GW = 0>
 __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(WinoBwdArgs a) {
   constexpr int NTH = 64 * NW;
-  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
+  const TileGeo<GH, GW, RT, wino_lpad_on(1)> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY,
+                                                a.maxrows);
   constexpr int PP = C + 4;
   constexpr int C4 = C / 4;
   constexpr int LC4 = C4 == 4 ? 2 : 3;
@@ -1919,7 +1967,7 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
   static_assert(WWG ? (RT % 16 == 0) : (RT - 4 * KD >= 0 && (RT - 4 * KD) % 4 == 0),
                 "work split");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Wl = 2 * G.TX + 2;
+  const int Wl = G.WL;
   const int rowstr = Wl * PP;
   float* U_s = smem;                         // [16 xi][4 g][C][4]
   float* d_s = U_s + 16 * C * C;             // dY rows [maxrows][Wl][PP]
@@ -1969,7 +2017,7 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
   for (int k = 0; k < MAXC; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4 - 1), pix = e >> LC4;
-    const int L = pix / Wl, col = pix - L * Wl;
+    const int L = pix / G.WL0, col = pix - L * G.WL0;
     sl_L[k] = L < G.maxrows ? L : -1;
     sl_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * C + 4 * ch : -1;
   }
@@ -2017,7 +2065,7 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
       if (sl_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
         const f4 vd = sd[k], vx = sx[k];  // zero where out of the image
-        const int o = (e >> LC4) * PP + 4 * (e & (C4 - 1));
+        const int o = ((e >> LC4) + pad_pix<decltype(G)::PADC>(sl_L[k])) * PP + 4 * (e & (C4 - 1));
         *reinterpret_cast<f4*>(d_s + o) = vd;
         *reinterpret_cast<f4*>(x_s + o) = vx;
       }
@@ -2301,11 +2349,31 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
 // mask.  Each workgroup walks a CONTIGUOUS run of ranges, so the halo rows
 // a range shares with the previous one come from this CU's L2 instead of
 // being refetched by another XCD.
+// LDS bytes of the fused32 kernel at a staged-row pitch of Wl pixels, and
+// whether a compile-time-geometry instance can afford the padded pitch
+// (the 16 -> 32 head at 36x48 cannot: 166 KB)
+constexpr size_t fused32_lds(int CX, int CY, int RT, int maxrows, int Wl) {
+  return sizeof(float) * (16 * CX * CY + static_cast<size_t>(maxrows) * Wl * (CX + CY + 8)) +
+         ((RT / 16) * (CX / 16) == 2 ? sizeof(float) * 2 * 4 * 64 * 4 : 0) +
+         sizeof(int) * (2 + maxrows + RT);
+}
+template <int CX, int CY, int RT, int GH, int GW>
+constexpr bool fused32_pad() {
+  if constexpr (GH == 0 || !wino_lpad_on(2)) {
+    return false;
+  } else {
+    constexpr int TY = (GH + 1) / 2, TX = (GW + 1) / 2;
+    constexpr int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * wino_parts(RT, TY * TX);
+    return fused32_lds(CX, CY, RT, maxrows, wino_wl<GH>(TX)) <= 160 * 1024;
+  }
+}
+
 template <int CX, int CY, int RT, int MAXCX, int MAXCY, bool RELU, bool MASK, int GH = 0,
           int GW = 0>
 __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a) {
   constexpr int NW = 8, NTH = 512;
-  const TileGeo<GH, GW, RT> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY, a.maxrows);
+  const TileGeo<GH, GW, RT, fused32_pad<CX, CY, RT, GH, GW>()> G(a.H, a.W, a.TY, a.TX, a.NT,
+                                                                 a.rTX, a.rTY, a.maxrows);
   constexpr int PPX = CX + 4, PPY = CY + 4;  // odd 16-B units per pixel
   constexpr int C4X = CX / 4, C4Y = CY / 4;
   constexpr int LC4X = C4X == 4 ? 2 : 3, LC4Y = C4Y == 4 ? 2 : 3;
@@ -2320,7 +2388,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   static_assert(C4Y == 4 || C4Y == 8, "CY");
   static_assert(MAXCX <= 32 && MAXCY <= 32, "stager masks");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Wl = 2 * G.TX + 2;
+  const int Wl = G.WL;
   const int rsx = Wl * PPX, rsy = Wl * PPY;
   float* U_s = smem;                         // [16 xi][NBY][4 g][CX][4]
   float* d_s = U_s + 16 * CX * CY;           // dY rows [maxrows][Wl][PPY]
@@ -2376,7 +2444,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   for (int k = 0; k < MAXCY; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4Y - 1), pix = e >> LC4Y;
-    const int L = pix / Wl, col = pix - L * Wl;
+    const int L = pix / G.WL0, col = pix - L * G.WL0;
     sy_L[k] = L < G.maxrows ? L : -1;
     sy_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * CY + 4 * ch : -1;
   }
@@ -2384,7 +2452,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
   for (int k = 0; k < MAXCX; ++k) {
     const int e = threadIdx.x + k * NTH;
     const int ch = e & (C4X - 1), pix = e >> LC4X;
-    const int L = pix / Wl, col = pix - L * Wl;
+    const int L = pix / G.WL0, col = pix - L * G.WL0;
     sx_L[k] = L < G.maxrows ? L : -1;
     sx_o[k] = (col >= 1 && col <= G.W) ? (col - 1) * CX + 4 * ch : -1;
   }
@@ -2436,7 +2504,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
       if (sy_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
         const f4 v = sy[k];  // zero where out of the image
-        *reinterpret_cast<f4*>(d_s + (e >> LC4Y) * PPY + 4 * (e & (C4Y - 1))) = v;
+        *reinterpret_cast<f4*>(d_s + ((e >> LC4Y) + pad_pix<decltype(G)::PADC>(sy_L[k])) * PPY + 4 * (e & (C4Y - 1))) = v;
       }
     }
 #pragma unroll
@@ -2444,7 +2512,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
       if (sx_L[k] >= 0) {
         const int e = threadIdx.x + k * NTH;
         const f4 v = sx[k];  // zero where out of the image
-        *reinterpret_cast<f4*>(x_s + (e >> LC4X) * PPX + 4 * (e & (C4X - 1))) = v;
+        *reinterpret_cast<f4*>(x_s + ((e >> LC4X) + pad_pix<decltype(G)::PADC>(sx_L[k])) * PPX + 4 * (e & (C4X - 1))) = v;
       }
     }
     const int cur = r;
@@ -2759,14 +2827,12 @@ bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const flo
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
+  const int WlP = wino_wl<GH, fused32_pad<CX, CY, RT, GH, GW>()>(TX);
   const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
   if (maxrows * Wl * (CY / 4) > MAXCY * 512 || maxrows * Wl * (CX / 4) > MAXCX * 512 ||
       maxrows > 512)
     return false;
-  constexpr int NTASK = (RT / 16) * (CX / 16);
-  const size_t ybytes = NTASK == 2 ? sizeof(float) * 2 * 4 * 64 * 4 : 0;
-  const size_t bytes = sizeof(float) * (16 * CX * CY + static_cast<size_t>(maxrows) * Wl * (CX + CY + 8)) +
-                       ybytes + sizeof(int) * (2 + maxrows + RT);
+  const size_t bytes = fused32_lds(CX, CY, RT, maxrows, WlP);
   if (bytes > 160 * 1024) return false;
   const int rows16 = ((9 * CX + 16) / 16) * 16;
   const int nranges = static_cast<int>((NT + RT - 1) / RT);
@@ -2846,10 +2912,10 @@ bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float
   const int per_img = TY * TX;
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
-  const int Wl = 2 * TX + 2;
+  const int Wl = 2 * TX + 2, WlP = wino_wl<GH, wino_lpad_on(1)>(TX);
   const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
   if (maxrows * Wl * (C / 4) > MAXC * 64 * NW || maxrows > 64 * NW) return false;
-  const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * Wl * (C + 4)) +
+  const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * WlP * (C + 4)) +
                        sizeof(int) * (maxrows + RT);
   if (bytes > 160 * 1024) return false;
   const int rows16 = ((9 * C + 16) / 16) * 16;
