@@ -152,6 +152,16 @@ def test_flags_defaults_and_parsing():
     flags_lib.parse_flags(['--no_such_flag=1'])
 
 
+def test_flags_reject_bf16_shallow_on_hip():
+  # the shallow torso has exact-fp32 HIP kernels only: refused, not run fp32
+  with pytest.raises(SystemExit, match='shallow torso has no bf16'):
+    flags_lib.parse_flags(['--dtype=bf16', '--torso=shallow'])
+  f = flags_lib.parse_flags(['--dtype=bf16', '--torso=shallow', '--backend=torch'])
+  assert f.dtype == 'bf16' and f.torso == 'shallow'
+  f = flags_lib.parse_flags(['--dtype=bf16', '--torso=deep'])
+  assert f.dtype == 'bf16'
+
+
 def test_timing_and_decay_utils():
   from scalable_agent_amd.utils.decay import LinearDecay
   from scalable_agent_amd.utils.timing import Timing, StepTimer
