@@ -14,7 +14,14 @@ first-person view:
     player counts and per-player frags for multiplayer);
   * rewards: living_reward per tic, the scenario's kill reward, death
     penalty; episodes end on death (single player) or `episode_timeout`;
-  * `screen_buffer` is [3, H, W] uint8 (CRCGCB) at the set resolution.
+  * `screen_buffer` is [3, H, W] uint8 (CRCGCB) at the set resolution;
+  * the map comes from the cfg's `doom_scenario_path` / `doom_map` when that
+    WAD holds a UDMF map (the self-authored scenario WADs of
+    scenario_maps.py, or any TEXTMAP WAD): the arena is its bounding box, the
+    player spawns at its player / deathmatch starts, its monsters and health
+    pickups are the ones the episode starts with, and a damaging floor
+    (sector `damageamount`) hurts every 32 tics; without a readable map a
+    1024 x 1024 arena with random monsters and medikits is used.
 
 It is selected with `SA_DOOM_BACKEND=sim` (or `doom_gym.doom_backend('sim')`);
 real ViZDoom is used whenever it is importable and not overridden.  It is a
@@ -22,10 +29,12 @@ test double for the framework plumbing, not a Doom reimplementation.
 """
 
 import math
+import os
 import re
 
 import numpy as np
 
+from . import wad as wadlib
 from .scenarios import parse_cfg
 
 RESOLUTIONS = ['160x120', '200x125', '200x150', '256x144', '256x160',
@@ -148,6 +157,7 @@ class SimDoomGame(object):
     self._living = float(self._cfg.get('living_reward', 0))
     self._death_penalty = float(self._cfg.get('death_penalty', 0))
     self._kill_reward = 1.0
+    self._load_map()
     self._initialized = True
     self._deaths = 0
     self.new_episode()
@@ -156,14 +166,70 @@ class SimDoomGame(object):
   def close(self):
     self._initialized = False
 
+  def _load_map(self):
+    """Arena, starts, monsters, pickups and floor damage of the cfg's map
+    (see the module docstring); None fields = the default arena."""
+    self._lo = np.zeros(2)
+    self._hi = np.full(2, ARENA)
+    self._starts = []
+    self._map_monsters = None
+    self._map_medkits = None
+    self._poison = np.zeros((0, 2))
+    self._floor_damage = 0.0
+    self.map_loaded = False
+    path = self._cfg.get('doom_scenario_path')
+    if not path:
+      return
+    try:
+      lumps = wadlib.read_wad(path)
+      ml = wadlib.map_lumps(lumps, self._cfg.get('doom_map', 'map01'))
+      m = wadlib.parse_udmf(ml['TEXTMAP'].decode('latin1'))
+    except (OSError, ValueError, KeyError):
+      return  # binary-format or missing map: the default arena
+    vx = np.array([[v['x'], v['y']] for v in m['vertices']], np.float64)
+    if len(vx) < 3:
+      return
+    self._lo, self._hi = vx.min(0), vx.max(0)
+    things = m['things']
+
+    def pos(types):
+      return np.array([[t['x'], t['y']] for t in things if t.get('type') in types],
+                      np.float64).reshape(-1, 2)
+    multi = self._max_players > 1 or self._bots > 0
+    starts = pos({wadlib.DEATHMATCH_START} if multi else {wadlib.PLAYER1_START})
+    if not len(starts):
+      starts = pos({wadlib.PLAYER1_START, wadlib.DEATHMATCH_START})
+    self._starts = [(p, next((t.get('angle', 0) for t in things
+                              if (t['x'], t['y']) == tuple(p)), 0)) for p in starts]
+    mons = pos(set(wadlib.MONSTERS))
+    self._map_monsters = mons if len(mons) else None
+    # two-colour scenarios: stimpacks are the poison pickups
+    poison = 'two_colors' in os.path.basename(path)
+    heal = set(wadlib.HEALTH_ITEMS) - ({2011} if poison else set())
+    meds = pos(heal)
+    self._map_medkits = meds if len(meds) else None
+    if poison:
+      self._poison = pos({2011})
+    self._floor_damage = float(max((sec.get('damageamount', 0)
+                                    for sec in m['sectors']), default=0))
+    self.map_loaded = True
+
+  def _uniform(self, rng, n, margin=50.0):
+    return rng.uniform(self._lo + margin, self._hi - margin, size=(n, 2))
+
   # -- episode ---------------------------------------------------------------
   def new_episode(self, recording_path=''):
     del recording_path
     rng = self._rng
     self._tic = 0
     self._finished = False
-    self._pos = rng.uniform(200, ARENA - 200, size=2)
-    self._angle = rng.uniform(0, 360)
+    if self._starts:
+      p, a = self._starts[rng.randint(len(self._starts))]
+      self._pos = np.array(p, np.float64)
+      self._angle = float(a)
+    else:
+      self._pos = self._uniform(rng, 1, 200.0)[0]
+      self._angle = rng.uniform(0, 360)
     self._health = 100.0
     self._armor = 0.0
     self._weapons = np.zeros(10)
@@ -176,9 +242,11 @@ class SimDoomGame(object):
     self._damage = 0.0
     self._cooldown = 0
     self._dead = False
-    n = 8
-    self._monsters = rng.uniform(50, ARENA - 50, size=(n, 2))
-    self._medkits = rng.uniform(50, ARENA - 50, size=(6, 2))
+    self._monsters = (self._map_monsters.copy() if self._map_monsters is not None
+                      else self._uniform(rng, 8))
+    self._medkits = (self._map_medkits.copy() if self._map_medkits is not None
+                     else self._uniform(rng, 6))
+    self._poison_items = self._poison.copy()
     self._bot_frags = np.zeros(9)
 
   def is_episode_finished(self):
@@ -248,7 +316,7 @@ class SimDoomGame(object):
     left = np.array([-math.sin(th), math.cos(th)])
     self._pos = np.clip(self._pos + 8.0 * speed * (move[0] * fwd +
                                                    move[1] * left),
-                        16, ARENA - 16)
+                        self._lo + 16, self._hi - 16)
     reward = self._living
     # monsters drift towards the player and bite when close
     d = self._pos[None] - self._monsters
@@ -262,7 +330,14 @@ class SimDoomGame(object):
     dm = np.linalg.norm(self._medkits - self._pos[None], axis=1)
     for i in np.nonzero(dm < 40)[0]:
       self._health = min(100.0, self._health + 25.0)
-      self._medkits[i] = rng.uniform(50, ARENA - 50, size=2)
+      self._medkits[i] = self._uniform(rng, 1)[0]
+    if len(self._poison_items):
+      dp = np.linalg.norm(self._poison_items - self._pos[None], axis=1)
+      for i in np.nonzero(dp < 40)[0]:
+        self._health -= 25.0
+        self._poison_items[i] = self._uniform(rng, 1)[0]
+    if self._floor_damage and self._tic % 32 == 31:
+      self._health -= self._floor_damage
     self._cooldown = max(0, self._cooldown - 1)
     if attack and self._cooldown == 0 and self._ammo[self._selected] > 0:
       self._cooldown = 4
@@ -278,7 +353,7 @@ class SimDoomGame(object):
         self._damage += 20
         self._kills += 1
         reward += self._kill_reward
-        self._monsters[j] = rng.uniform(50, ARENA - 50, size=2)
+        self._monsters[j] = self._uniform(rng, 1)[0]
         if rng.rand() < 0.5:
           self._ammo[self._selected] += 5
     if self._bots and rng.rand() < 0.002 * self._bots:
@@ -349,7 +424,8 @@ class SimDoomGame(object):
     cols = np.arange(w)
     ray = self._angle + np.degrees(FOV) * (0.5 - (cols + 0.5) / w)
     for objs, color in ((self._monsters, (200, 40, 40)),
-                        (self._medkits, (40, 200, 60))):
+                        (self._medkits, (40, 200, 60)),
+                        (self._poison_items, (200, 60, 200))):
       rel = objs - self._pos[None]
       dist = np.linalg.norm(rel, axis=1) + 1e-3
       ang = np.degrees(np.arctan2(rel[:, 1], rel[:, 0]))
