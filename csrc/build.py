@@ -175,16 +175,22 @@ def main():
   ap.add_argument('--define', action='append', default=[],
                   help='experiment builds: -D NAME=VAL for the HIP extension '
                        '(objects in their own build dir); use with --out')
+  ap.add_argument('--flag', action='append', default=[],
+                  help='experiment builds: an extra compiler flag for the HIP '
+                       'extension (e.g. --flag=-mllvm --flag=-amdgpu-...); use '
+                       'with --out')
   ap.add_argument('--out', default=None,
                   help='HIP extension output path (experiment builds, loaded '
                        'with SA_EXT_PATH)')
   args = ap.parse_args()
-  if args.define and not args.out:
-    ap.error('--define needs --out (the in-tree _C.so stays the default build)')
-  if args.only in (None, 'native') and not args.define:
+  if (args.define or args.flag) and not args.out:
+    ap.error('--define / --flag need --out (the in-tree _C.so stays the '
+             'default build)')
+  if args.only in (None, 'native') and not (args.define or args.flag):
     build_native(args.j, args.force, args.sanitize)
   if args.only in (None, 'C') and not args.sanitize:
-    build_hip(args.j, args.force, extra_flags=['-D' + d for d in args.define],
+    build_hip(args.j, args.force,
+              extra_flags=['-D' + d for d in args.define] + list(args.flag),
               out=args.out)
 
 
