@@ -1565,6 +1565,25 @@ void set_smem(K kernel, size_t bytes) {
 // ----- tile-height rules (constexpr: the same rule picks the compiled
 // geometry at build time and the runtime tile height at launch) -----------
 
+// SA_ROWS_BALANCE=1: when a rule's tallest fitting tile R leaves a last tile
+// of under R / 4 rows, the image's ceil(H / R) tiles are made equally tall
+// (ceil(H / n) rows): the same number of tiles and staged halo rows without
+// the sliver (Atari 21 rows: 7+7+7 instead of 10+10+1; 42 rows of the
+// 16->32 head backward: 9+9+9+9+6 instead of 10+10+10+10+2).  Measured
+// (bf16 learner, one box, 3 runs per arm): Atari 84x84x4 4.767-4.779 ->
+// 4.714-4.731 ms with every tile balanced; balancing the IMPALA 18x24 maps
+// too (8+8+2 -> 6+6+6) cost the 72x96 learner 0.02-0.04 ms, hence the R / 4
+// threshold, which leaves every 72x96 tile unchanged.
+#ifndef SA_ROWS_BALANCE
+#define SA_ROWS_BALANCE 1
+#endif
+constexpr int balance_rows(int H, int R) {
+  if (!SA_ROWS_BALANCE || R >= H || R < 1) return R;
+  const int n = (H + R - 1) / R;
+  const int last = H - (n - 1) * R;
+  return 4 * last < R ? (H + n - 1) / n : R;
+}
+
 // rows per tile such that the staged halo fits NREG*256 16-B chunks per
 // stream and the tile holds ~target pixels
 constexpr int rows_for(int H, int W, int C, int target) {
@@ -1573,7 +1592,7 @@ constexpr int rows_for(int H, int W, int C, int target) {
   while (R > 1 && ((R + 2) * W * C / 8 > NREG * kThreads ||
                    tile_groups(C, R, W) > kMaxTilePx(C) / 16))
     --R;
-  return R < H ? R : H;
+  return balance_rows(H, R < H ? R : H);
 }
 // fused residual block: x staged with 2 halo rows each side, t computed
 // for R + 2 rows
@@ -1592,14 +1611,20 @@ constexpr int rows_pool_fwd(int H, int W, int CIN, int px) {
   while (Rp > 1 && ((2 * Rp + 3) * W * CIN / 8 > NREG * kThreads ||
                     tile_groups(CIN, 2 * Rp + 1, W) > kMaxTilePx(CIN) / 16))
     --Rp;
-  return Rp > Hp ? Hp : Rp;
+  return balance_rows(Hp, Rp > Hp ? Hp : Rp);
+}
+// LDS bytes of conv1_pool_fwd_kernel at Rp pooled rows (its launcher's smem)
+constexpr int conv1_fwd_lds(int Rp, int W) {
+  return (3 * 16 * 16 + (2 * Rp + 1) * (W + 2) * 16 + ((2 * Rp + 3) * (W + 2) + 4) * 4) * 2;
 }
 constexpr int rows_conv1_fwd(int H, int W, int px) {
   const int Hp = (H + 1) / 2;
   int Rp = (px / W - 1) / 2;
   if (Rp < 1) Rp = 1;
   while (Rp > 1 && ((2 * Rp + 3) * W + 3) / 4 > kU8Groups * kThreads) --Rp;
-  return Rp > Hp ? Hp : Rp;
+  // four forward workgroups per CU (ConvTune::cap_fwd) must fit in its LDS
+  while (Rp > 1 && conv1_fwd_lds(Rp, W) * 4 > 160 * 1024) --Rp;
+  return balance_rows(Hp, Rp > Hp ? Hp : Rp);
 }
 constexpr int rows_pool_bwd(int H, int W, int CIN, int COUT, int px) {
   const int Wo = (W + 1) / 2;
@@ -1607,7 +1632,7 @@ constexpr int rows_pool_bwd(int H, int W, int CIN, int COUT, int px) {
   while (R > 1 && (((R + 2) / 2 + 2) * Wo * COUT * 2 > NREG * kThreads * 16 ||
                    tile_groups(COUT, R, W) > kMaxTilePx(CIN < COUT ? CIN : COUT) / 16))
     --R;
-  return R;
+  return balance_rows(H, R);
 }
 constexpr int rows_conv1_bwd(int H, int W, int px) {
   const int Wo = (W + 1) / 2;
@@ -1616,7 +1641,7 @@ constexpr int rows_conv1_bwd(int H, int W, int px) {
   while (R > 1 && (((R + 2) / 2 + 2) * Wo * 16 * 2 > NREG * kThreads * 16 ||
                    ((R + 2) * W + 3) / 4 > kU8Groups * kThreads))
     --R;
-  return R > H ? H : R;
+  return balance_rows(H, R > H ? H : R);
 }
 
 // Host-side guard: the tile-height rules stop at one row, so a frame too wide
