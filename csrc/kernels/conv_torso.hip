@@ -1667,9 +1667,12 @@ struct ConvTune {
   int px_res_fwd = 384;   // target pixels per tile
   int px_res_bwd = 384;
   int px_pool_fwd = 400;  // conv pixels per tile (pre-pool)
-  int px_conv1_fwd = 960;
+  // stage 0: 4 pooled rows at W = 96 and 84 (84x84: 5 rows measured 4 %
+  // slower), 12 conv rows at 96 and 14 (6 equal tiles) at 84 (13 rows: 7 %
+  // slower, tools/micro/conv1_probe.py SWEEP=1)
+  int px_conv1_fwd = 900;
   int px_pool_bwd = 512;
-  int px_conv1_bwd = 1152;
+  int px_conv1_bwd = 1176;
   int specialize = 1;     // use compile-time-geometry kernels when they match
   int ablate = 0;         // timing-only, -DSA_CONV_ABLATE builds: skip phases
   int deterministic = 0;  // wgrad: per-workgroup slots + fixed-order reduce
