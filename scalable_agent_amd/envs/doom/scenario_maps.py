@@ -47,48 +47,39 @@ def _basic():
   b.room(W.rect(0, 0, 512, 448), wall='BRICK9', floor='FLOOR0_1',
          ceiling='FLAT4', ceiling_h=104, light=210)
   b.thing(64, 224, W.PLAYER1_START, angle=0, tid=100)
-  acs = _ACS_HEAD + """int target_tid = 10;
+  acs = _ACS_HEAD + """// basic: shoot the monster that appears on the far wall.
+// Rules (the scenario's published reward): +106 when it dies (the episode
+// ends), -5 per shot fired, -1 per tic from the .cfg's living_reward.
 
-// a stationary, one-hit target somewhere along the far wall
-function void SpawnTarget(void)
-{
-    int y = Random(32.0, 416.0);
-    Spawn("Cacodemon", 448.0, y, 0.0, target_tid, 128);
-    SetActorProperty(target_tid, APROP_Speed, 0);
-    SetActorProperty(target_tid, APROP_Health, 1);
-    SetThingSpecial(target_tid, ACS_ExecuteAlways, 4);
-}
+#define MONSTER 10
 
-script 1 OPEN
+script "basic_setup" OPEN
 {
     reward = 0;
-    SpawnTarget();
+    // one motionless, one-hit Cacodemon at a random height on the east wall
+    Spawn("Cacodemon", 448.0, Random(32.0, 416.0), 0.0, MONSTER, 128);
+    SetActorProperty(MONSTER, APROP_Speed, 0);
+    SetActorProperty(MONSTER, APROP_Health, 1);
+    SetThingSpecial(MONSTER, ACS_NamedExecuteAlways, "basic_kill");
 }
 
-script 2 ENTER
+script "basic_player" ENTER
 {
     TakeInventory("Fist", 1);
-    ACS_Execute(3, 0, 0, 0, 0);
-}
-
-// every shot fired costs 5
-script 3 (void)
-{
-    int ammo = CheckInventory("Clip");
-    while (true)
+    int clips = CheckInventory("Clip");
+    for (;;)
     {
+        // every clip spent since the last tic is a shot
         int now = CheckInventory("Clip");
-        if (now < ammo)
-            reward = reward - 5.0;
-        ammo = now;
-        delay(1);
+        reward -= 5.0 * (clips - now);
+        clips = now;
+        Delay(1);
     }
 }
 
-// the target died: pay and end the episode
-script 4 (void)
+script "basic_kill" (void)
 {
-    reward = reward + 106.0;
+    reward += 106.0;
     Exit_Normal(0);
 }
 """
@@ -116,14 +107,14 @@ def _deadly_corridor():
   b.thing(L - 48, 64, 2018, tid=30)
   acs = _ACS_HEAD + """int goal_x = 1488.0;
 
-script 1 OPEN
+script "dc_setup" OPEN
 {
     reward = 0;
     shaping_reward = 0;
 }
 
 // reward = progress towards the armor (x distance travelled this tic)
-script 2 ENTER
+script "dc_player" ENTER
 {
     int last_x = GetActorX(0);
     while (true)
@@ -162,35 +153,39 @@ def _pickup_room(size, n_good, n_bad, damage, seed, wall, floor):
 def _health_gathering():
   size = 1216
   b = _pickup_room(size, 16, 0, 5, 1, 'GSTONE1', 'NUKAGE1')
-  acs = _ACS_HEAD + """int room = 1216.0;
-int medikit_tid = 111;
+  acs = _ACS_HEAD + """// health_gathering: the floor hurts; medikits (tid 111) are the only
+// healing.  The map starts with 16 of them; one more appears every 30 tics.
+// shaping_reward (USER1) counts +100 per medikit picked up.
 
-function void SpawnMedikit(void)
+#define MEDIKIT 111
+
+function void drop_medikit(void)
 {
-    while (Spawn("Medikit", Random(32.0, room - 32.0),
-                 Random(32.0, room - 32.0), 20.0, medikit_tid) == 0);
-    SetThingSpecial(medikit_tid, ACS_ExecuteAlways, 3);
+    // retry until the spot is free
+    int ok = 0;
+    while (!ok)
+        ok = Spawn("Medikit", Random(32.0, 1184.0), Random(32.0, 1184.0), 20.0, MEDIKIT);
+    SetThingSpecial(MEDIKIT, ACS_NamedExecuteAlways, "hg_pickup");
 }
 
-// a new medikit every 30 tics for as long as the player lives
-script 1 OPEN
+script "hg_setup" OPEN
 {
     reward = 0;
     shaping_reward = 0;
-    SetThingSpecial(medikit_tid, ACS_ExecuteAlways, 3);
-    while (true)
+    SetThingSpecial(MEDIKIT, ACS_NamedExecuteAlways, "hg_pickup");
+    for (;;)
     {
-        SpawnMedikit();
-        delay(30);
+        Delay(30);
+        drop_medikit();
     }
 }
 
-script 2 ENTER
+script "hg_player" ENTER
 {
     ClearInventory();
 }
 
-script 3 (void)
+script "hg_pickup" (void)
 {
     shaping_reward += 100.0;
 }
@@ -206,24 +201,24 @@ def _two_colors(hard):
 int bad_tid = 112;
 
 // medikits heal; stimpacks are poison in this scenario
-script 1 OPEN
+script "tc_setup" OPEN
 {
     reward = 0;
-    SetThingSpecial(good_tid, ACS_ExecuteAlways, 3);
-    SetThingSpecial(bad_tid, ACS_ExecuteAlways, 4);
+    SetThingSpecial(good_tid, ACS_NamedExecuteAlways, "tc_good");
+    SetThingSpecial(bad_tid, ACS_NamedExecuteAlways, "tc_bad");
 }
 
-script 2 ENTER
+script "tc_player" ENTER
 {
     ClearInventory();
 }
 
-script 3 (void)
+script "tc_good" (void)
 {
     shaping_reward += 100.0;
 }
 
-script 4 (void)
+script "tc_bad" (void)
 {
     DamageThing(%d);
     shaping_reward -= 100.0;
@@ -274,21 +269,21 @@ _BATTLE_ACS = _ACS_HEAD + """global int 2:kills;  // ViZDoom's USER2
 int monster_tid = 50;
 
 // kills count into USER2; a dead monster comes back after a while
-script 1 OPEN
+script "battle_setup" OPEN
 {
     reward = 0;
     kills = 0;
-    SetThingSpecial(monster_tid, ACS_ExecuteAlways, 3);
+    SetThingSpecial(monster_tid, ACS_NamedExecuteAlways, "battle_kill");
 }
 
-script 2 ENTER
+script "battle_player" ENTER
 {
     ClearInventory();
     GiveInventory("Pistol", 1);
     GiveInventory("Clip", 50);
 }
 
-script 3 (void)
+script "battle_kill" (void)
 {
     reward = reward + 1.0;
     kills = kills + 1;
@@ -314,7 +309,7 @@ _DM_ITEMS = ([2001, 82, 2002, 2003, 2004] + [2007, 2008, 2048, 2049, 2010, 2047]
              [2018, 2019] + [2012] * 4 + [2011] * 4)
 
 _DM_ACS = _ACS_HEAD + """// deathmatch: the frag counters of the engine are the score
-script 1 OPEN
+script "dm_setup" OPEN
 {
     reward = 0;
 }
