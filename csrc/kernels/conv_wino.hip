@@ -819,13 +819,20 @@ template <int CIN_, int COUT_, int RT>
 struct PoolGeo {
   static constexpr int CIN = CIN_, COUT = COUT_;
   static constexpr int W = RT;                      // one tile-row pair = RT tiles
-  static constexpr int NW = (RT / 16) * (COUT / 16);  // one task per wave
+  // 16-tile groups: the last one partly past the range when RT % 16 != 0
+  // (the 84-wide Atari frame: 84 tiles in 6 groups, 12 lanes idle)
+  static constexpr int NG = (RT + 15) / 16;
+  static constexpr int NW = NG * (COUT / 16);       // one task per wave
   static constexpr int PP = CIN == 4 ? 4 : CIN + 4;  // staged pixel pitch (floats)
   static constexpr int IPP = COUT + 4;               // pre-pool image pixel pitch
   static constexpr int ROWS = 6;                     // staged input rows per range
   static constexpr int XREG = (ROWS * (W + 2) * PP > 4 * W * IPP) ? ROWS * (W + 2) * PP
                                                                    : 4 * W * IPP;
   static constexpr int MAXC = (ROWS * (W + 2) * (CIN / 4) + 64 * NW - 1) / (64 * NW);
+  // pool-phase threads (two pooled rows x WP columns x CQ quads) and whether
+  // each pooled row is whole waves (the conflict-free lane map needs it)
+  static constexpr int PTH = (W / 2) * (COUT / 4);
+  static constexpr bool kWaveRows = PTH % 64 == 0;
   static constexpr int WP = W / 2;                   // pooled width
   static constexpr int CQ = COUT / 4;                // channel quads
   static constexpr size_t bytes = sizeof(float) * (16 * CIN * COUT + XREG + ROWS);
@@ -893,13 +900,13 @@ constexpr bool pool_lane_map_ok() {
 static_assert(pool_lane_map_ok<8, 36>() && pool_lane_map_ok<4, 20>(), "pool lane map");
 
 template <int CIN, int COUT, int RT>
-__global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
+__global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_conv_pool_kernel(
     WinoPoolArgs pa) {
   using P = PoolGeo<CIN, COUT, RT>;
   constexpr int W = P::W, NW = P::NW, NTH = 64 * NW;
   constexpr int PP = P::PP, IPP = P::IPP, MAXC = P::MAXC, WP = P::WP, CQ = P::CQ;
   constexpr int C4 = CIN / 4, LC4 = C4 == 4 ? 2 : 0;
-  constexpr int NG = RT / 16;
+  constexpr int NG = P::NG;
   constexpr int Wl = W + 2, rowstr = Wl * PP;
   // CIN == 4 (stage 0): the staged rows are channel planes [4][ROWS][Wl] with
   // an odd plane stride, so a lane's scalar patch reads (16 tiles x 2 pixels
@@ -909,8 +916,8 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   constexpr int PS = (P::ROWS * Wl) | 1;
   static_assert(CIN != 4 || 4 * PS <= P::XREG, "planes fit the staging region");
   static_assert(CIN == 4 || CIN == 16, "CIN");
-  static_assert(NW * 64 == 2 * WP * CQ, "two pooled rows x WP columns x CQ quads = the workgroup");
-  static_assert(RT % 16 == 0 && MAXC <= 32, "shape");
+  static_assert(NW * 64 >= 2 * WP * CQ, "two pooled rows x WP columns x CQ quads fit the workgroup");
+  static_assert(RT % 2 == 0 && MAXC <= 32, "shape");
   const WinoArgs& a = pa.c;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // U: CIN 16 [16 xi][4 g][COUT][4 v] (f4 A fragments), CIN 4 [16 xi][4 ci][COUT]
@@ -994,11 +1001,14 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   // pool-phase thread: pooled column pj, channel quad pq; the first WP * CQ
   // threads own pooled row 2k (9 taps), the rest the odd row 2k+1 (its
   // carried part + 3 taps of the next range, then 6 taps): balanced
+  // (rows of whole waves take the conflict-free lane map, other widths the
+  // natural quad-fastest numbering; threads past the two rows idle)
   const int pt = threadIdx.x % (WP * CQ);
-  static_assert((WP * CQ) % 64 == 0, "whole waves per pooled row");
   constexpr PoolLaneMap<CQ, IPP> kMap{};
-  const int pj = (pt >> 6) * (64 / CQ) + kMap.pj[pt & 63], pq = kMap.pq[pt & 63];
+  const int pj = P::kWaveRows ? (pt >> 6) * (64 / CQ) + kMap.pj[pt & 63] : pt / CQ;
+  const int pq = P::kWaveRows ? kMap.pq[pt & 63] : pt % CQ;
   const bool even_row = threadIdx.x < WP * CQ;
+  const bool pool_thread = NW * 64 == 2 * WP * CQ || threadIdx.x < 2 * WP * CQ;
   constexpr float kNegInf = -__builtin_inff();
   f4 cv = {kNegInf, kNegInf, kNegInf, kNegInf};
   int cc[4] = {0, 0, 0, 0};
@@ -1008,7 +1018,10 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
   // this wave's task: 16-tile group grp, 16-channel slice sl
   const int grp = wave % NG, sl = wave / NG;
   const int co0 = sl * 16;
-  const int txl = 16 * grp + c16;  // tile within the range = (row txl / (W/2), column)
+  // tile within the range = (row txl / (W/2), column); lanes past the range
+  // (RT % 16 != 0) compute tile 0 again and store nothing
+  const bool tvalid = RT % 16 == 0 || 16 * grp + c16 < RT;
+  const int txl = tvalid ? 16 * grp + c16 : 0;
   const int tyl = txl / (W / 2), tx = txl - tyl * (W / 2);
   // CIN 16: 4 channels 4g.. of each patch pixel; CIN 4: channel g
   const float* xp = CIN == 16 ? x_s + (2 * tyl * Wl + 2 * tx) * PP + 4 * g
@@ -1125,14 +1138,14 @@ __global__ __launch_bounds__(RT * COUT / 4, 3) void wino_conv_pool_kernel(
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx)
-          if (!knob(a.ablate, 32))
+          if (tvalid && !knob(a.ablate, 32))
             *reinterpret_cast<f4*>(img + ((2 * tyl + dy) * W + 2 * tx + dx) * IPP + co0 + 4 * g) =
                 Y[2 * dy + dx] + bv;
     }
     __syncthreads();
 
     // pool phase
-    if (!knob(a.ablate, 16)) {
+    if (pool_thread && !knob(a.ablate, 16)) {
       const int n = cur / KP, k = cur - n * KP;
       auto tap = [&](int row, int dx) -> f4 {
         return *reinterpret_cast<const f4*>(img + (row * W + 2 * pj + dx) * IPP + 4 * pq);
@@ -3002,6 +3015,8 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
   if (Cin == 4 && Cout == 16 && (on & 2)) {
     if (W == 96) return run_wino_pool<4, 16, 96>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 64) return run_wino_pool<4, 16, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    // the Atari frame (BASELINE config #2): 84 tiles per range in 6 groups
+    if (W == 84) return run_wino_pool<4, 16, 84>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
   }
   return false;
 }

@@ -330,7 +330,8 @@ def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w, cin):
 
 
 @pytest.mark.parametrize('N,H,W,zero_w', [(6, 72, 96, False), (120, 72, 96, False),
-                                           (3, 8, 64, False), (5, 72, 96, True)])
+                                           (3, 8, 64, False), (5, 72, 96, True),
+                                           (7, 84, 84, False), (3, 84, 84, True)])
 def test_wino_conv_pool_stage0_matches_float64(cuda, N, H, W, zero_w):
   """Stage-0 head (4-channel image -> 16) with the pool in the Winograd
   epilogue against the float64 conv + 3x3/2 max-pool: values to fp32
@@ -340,10 +341,11 @@ def test_wino_conv_pool_stage0_matches_float64(cuda, N, H, W, zero_w):
   C = _C()
   g = torch.Generator().manual_seed(13)
   x = torch.rand(N, H, W, 4, generator=g)
-  x[..., 3] = 0  # the image's pad channel
   w = (torch.zeros(3, 3, 4, 16) if zero_w else
        torch.randn(3, 3, 4, 16, generator=g) / 6.0)
-  w[:, :, 3] = 0
+  if W != 84:  # RGB: the image's pad channel; 84x84 Atari stacks: 4 frames
+    x[..., 3] = 0
+    w[:, :, 3] = 0
   b = torch.randn(16, generator=g) * 0.1
   # stage 0 is opt-in (SA_F32_WINO_POOL bit 1): enabled explicitly here
   out = C.cf32_wino_conv_pool_fwd(x.to(cuda), w.to(cuda), b.to(cuda), stages=3)
