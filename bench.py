@@ -425,7 +425,8 @@ def main():
     backend = 'torch'
     if device.type == 'cuda':
       from scalable_agent_amd import ops
-      backend = 'hip' if ops.available() else 'torch'
+      ops.load()  # a GPU run without the kernels fails loudly (no silent torch)
+      backend = 'hip'
 
   main_res = measure(args, args.dtype, device, backend, rank, world)
   extra = None

@@ -110,6 +110,7 @@ def build_hip(workers=8, force=False, extra_flags=(), out=None):
       max(os.path.getmtime(o) for o in objs) > os.path.getmtime(out)):
     # link to a temporary name and rename: a concurrent reader (a gpurun
     # snapshot, an importing process) never sees a half-written library
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     tmp_out = out + '.tmp'
     cmd = [HIPCC, '-shared', '-fPIC', '-o', tmp_out] + objs + [
         '--offload-arch=' + ARCH, '-L' + lib, '-Wl,-rpath,' + lib,

@@ -899,7 +899,9 @@ constexpr bool pool_lane_map_ok() {
 }
 static_assert(pool_lane_map_ok<8, 36>() && pool_lane_map_ok<4, 20>(), "pool lane map");
 
-template <int CIN, int COUT, int RT>
+// OT: the map may have an odd number of tile rows (H % 4 == 2: the image's
+// last range is one tile row); compiled only where such a map runs
+template <int CIN, int COUT, int RT, bool OT = false>
 __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_conv_pool_kernel(
     WinoPoolArgs pa) {
   using P = PoolGeo<CIN, COUT, RT>;
@@ -963,7 +965,9 @@ __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_con
   int r = rw.r;
   if (r >= rw.end) return;  // uniform
   const int rfirst = r;
-  const int KP = a.TY / 2;  // ranges (tile-row pairs) per image
+  // ranges (tile-row pairs) per image; an odd tile-row count (H % 4 == 2,
+  // the 42-row Atari stage-1 map) leaves a last range of one tile row
+  const int KP = OT ? (a.TY + 1) / 2 : a.TY / 2;
   const int Hp = a.H / 2;
 
   // staging: the generic kernel's register prefetch (row table in LDS)
@@ -1019,7 +1023,8 @@ __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_con
   const int grp = wave % NG, sl = wave / NG;
   const int co0 = sl * 16;
   // tile within the range = (row txl / (W/2), column); lanes past the range
-  // (RT % 16 != 0) compute tile 0 again and store nothing
+  // (RT % 16 != 0) compute tile 0 again and store nothing; tiles of a
+  // missing second tile row (odd TY) store -inf (pool padding)
   const bool tvalid = RT % 16 == 0 || 16 * grp + c16 < RT;
   const int txl = tvalid ? 16 * grp + c16 : 0;
   const int tyl = txl / (W / 2), tx = txl - tyl * (W / 2);
@@ -1122,6 +1127,8 @@ __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_con
 
     // output transform Y = A^T M A + b into the pre-pool image
     {
+      const int kk = cur - (cur / KP) * KP;  // this range's tile-row pair
+      const bool row_ok = !OT || 2 * kk + tyl < a.TY;
       f4 tt[4][2];
 #pragma unroll
       for (int ra = 0; ra < 4; ++ra) {
@@ -1140,7 +1147,7 @@ __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_con
         for (int dx = 0; dx < 2; ++dx)
           if (tvalid && !knob(a.ablate, 32))
             *reinterpret_cast<f4*>(img + ((2 * tyl + dy) * W + 2 * tx + dx) * IPP + co0 + 4 * g) =
-                Y[2 * dy + dx] + bv;
+                row_ok ? Y[2 * dy + dx] + bv : f4{kNegInf, kNegInf, kNegInf, kNegInf};
     }
     __syncthreads();
 
@@ -1186,7 +1193,8 @@ __global__ __launch_bounds__((64 * PoolGeo<CIN, COUT, RT>::NW), 3) void wino_con
         *reinterpret_cast<uint32_t*>(pa.arg + o) = pack_codes(code);
       }
       // (c) pooled row 2k+1: pixel rows 4k+2, 4k+3 here, 4k+4 in the next range
-      if (!even_row) {
+      // (none in an odd-TY image's last range)
+      if (!even_row && (!OT || 2 * k + 1 < Hp)) {
         f4 best = {kNegInf, kNegInf, kNegInf, kNegInf};
         int code[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1249,7 +1257,7 @@ template <int CIN, int COUT, int RT>
 bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled, uint8_t* arg,
                    float* side, int64_t side_floats, int N, int H, int W, hipStream_t s) {
   using P = PoolGeo<CIN, COUT, RT>;
-  if (W != P::W || H % 4 != 0 || H < 4) return false;
+  if (W != P::W || H % 2 != 0 || H < 4) return false;
   const int TY = H / 2, TX = W / 2;
   const int64_t NT = static_cast<int64_t>(N) * TY * TX;
   // integer range / tile index math throughout (no fdivi): int32 bounds only
@@ -1261,7 +1269,7 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   a.bias = b;
   a.N = N; a.H = H; a.W = W;
   a.TY = TY; a.TX = TX; a.NT = static_cast<int>(NT);
-  a.nranges = static_cast<int>(NT / RT);
+  a.nranges = N * ((TY + 1) / 2);  // tile-row pairs; odd TY: a last single row
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
   a.wcin = CIN; a.wcout = COUT;
@@ -1283,11 +1291,15 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   pa.arg = arg;
   pa.side_v = reinterpret_cast<f4*>(side);
   pa.side_c = reinterpret_cast<uint32_t*>(side + static_cast<int64_t>(G) * side_n * 4);
-  auto kern = wino_conv_pool_kernel<CIN, COUT, RT>;
+  // odd tile-row maps: the OT instance, compiled for the widths that have one
+  constexpr bool kHasOT = RT == 42 || RT == 48;
+  if (TY % 2 != 0 && !kHasOT) return false;
+  auto kern = TY % 2 != 0 ? wino_conv_pool_kernel<CIN, COUT, RT, kHasOT>
+                          : wino_conv_pool_kernel<CIN, COUT, RT>;
   allow_lds_w(kern, P::bytes);
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * P::NW), P::bytes, s, pa);
   hipLaunchKernelGGL(wino_pool_fix_kernel, dim3(G), dim3(256), 0, s, pa.side_v, pa.side_c,
-                     pooled, arg, a.nranges, TY / 2, TY, W / 2, COUT);
+                     pooled, arg, a.nranges, (TY + 1) / 2, TY, W / 2, COUT);
   return true;
 }
 
@@ -3002,13 +3014,19 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
                            int Cin, int Cout, int stages, hipStream_t s) {
   // bit 0: stage 1, bit 1: stage 0 (stage 0: 412 vs 529 us for the direct
   // conv+pool, 10.02 -> 9.93 ms per step), bit 2: stage 2 (whole-image
-  // ranges: 9.93 -> 9.90 ms); stages >= 0 overrides the environment (tests)
+  // ranges: 9.93 -> 9.90 ms), bit 3: the 42-wide stage-1 head (opt-in);
+  // stages >= 0 overrides the environment (tests)
   static const int env_on = env_int("SA_F32_WINO_POOL", 7);
   const int on = stages >= 0 ? stages : env_on;
   if (Cin == 16 && Cout == 32 && (on & 1)) {
     if (W == 48) return run_wino_pool<16, 32, 48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 32) return run_wino_pool<16, 32, 32>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 64) return run_wino_pool<16, 32, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    // the Atari stage-1 map (42x42: 21 tile rows, a one-row last range) -
+    // opt-in (bit 3): fp32 Atari step 10.04-10.07 (conv + maxpool_fwd) vs
+    // 10.07-10.09 ms fused (42 tiles fill 3 groups of 16, 2 workgroups per CU)
+    if (W == 42 && (on & 8))
+      return run_wino_pool<16, 32, 42>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
   }
   if (Cin == 32 && Cout == 32 && (on & 4) && H == 18 && W == 24)
     return run_wino_pool_img<32, 32, 18, 24>(x, w, b, pooled, arg, N, H, W, s);

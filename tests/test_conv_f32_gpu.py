@@ -302,7 +302,11 @@ def test_torso_f32_learner_scale_batch(cuda):
 @pytest.mark.parametrize('N,H,W,zero_w,cin', [(256, 36, 48, False, 16), (5, 36, 48, False, 16),
                                                (3, 16, 32, False, 16), (2, 8, 64, False, 16),
                                                (7, 36, 48, True, 16), (300, 18, 24, False, 32),
-                                               (3, 18, 24, True, 32)])
+                                               (3, 18, 24, True, 32),
+                                               # odd tile-row counts (H % 4 == 2):
+                                               # the Atari 42x42 head, and 10 rows at 48
+                                               (64, 42, 42, False, 16), (5, 42, 42, False, 16),
+                                               (3, 42, 42, True, 16), (4, 10, 48, False, 16)])
 def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w, cin):
   """The 16 -> 32 stage head with the max-pool in the Winograd epilogue
   (wino_conv_pool_kernel): pooled values and argmax codes bitwise those of
@@ -317,7 +321,7 @@ def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w, cin):
   w = (torch.zeros(3, 3, cin, 32) if zero_w else
        torch.randn(3, 3, cin, 32, generator=g) / 12.0).to(cuda)
   b = torch.randn(32, generator=g).to(cuda)
-  out = C.cf32_wino_conv_pool_fwd(x, w, b, stages=7)
+  out = C.cf32_wino_conv_pool_fwd(x, w, b, stages=15)  # 15: the 42-wide head too
   assert len(out) == 2
   y, arg = out
   conv = C.cf32_conv_fwd(x, w, b, 1, 1, 1, H, W)
@@ -373,7 +377,7 @@ def test_wino_conv_pool_declines_other_shapes(cuda):
   x = torch.randn(2, 20, 24, 32, device=cuda)  # 32 -> 32 off the 18x24 instance
   assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 32, 32, device=cuda),
                                    torch.zeros(32, device=cuda), stages=7) == []
-  x = torch.randn(2, 42, 42, 16, device=cuda)  # Atari stage 1 (H % 4 != 0)
+  x = torch.randn(2, 42, 44, 16, device=cuda)  # a width with no instance
   assert C.cf32_wino_conv_pool_fwd(x, torch.zeros(3, 3, 16, 32, device=cuda),
                                    torch.zeros(32, device=cuda)) == []
 
