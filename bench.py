@@ -274,6 +274,16 @@ def measure(args, dtype, device, backend, rank, world):
   # diagnostic only (never the reported benchmark): SA_BENCH_SKIP_H2D=1 drops
   # the per-step host->device prefetch of the next batch
   skip_h2d = os.environ.get('SA_BENCH_SKIP_H2D') == '1'
+  # who orders the prefetch against the steps.  'host' (default): the host
+  # waits for slot j's previous step before enqueuing the copy into it and for
+  # the copy before launching the step that reads it, so neither stream holds
+  # a device-side wait on the other.  'device': stream-waits on the two
+  # events.  Measured with tools/micro/step_jitter.py: the device-side waits
+  # cost 0.15-0.2 ms per step plus 1-4 ms outlier steps (fp32 9.50 ms mean vs
+  # 9.13 with no copy at all); host-side 9.15 (bf16: 4.63 / 4.41 / 4.44).
+  # The host stays a step ahead: it is released ~1.2 ms into step k (copy
+  # done) and enqueues step k+1 in 2-4 ms
+  host_sync = os.environ.get('SA_BENCH_PREFETCH_SYNC', 'host') != 'device'
 
   def run_step(k):
     i = k % 2
@@ -281,7 +291,10 @@ def measure(args, dtype, device, backend, rank, world):
       return learner.step(host_batches[i])
     # prefetch batch k+1 into the other slot while computing on slot i
     j = (k + 1) % 2
-    comp.wait_event(slot_ready[i])
+    if host_sync:
+      slot_ready[i].synchronize()
+    else:
+      comp.wait_event(slot_ready[i])
     if use_graph:
       (learner._graph, learner._static_in, learner._static_loss,
        learner._graph_keep) = graphs[i]
@@ -290,7 +303,10 @@ def measure(args, dtype, device, backend, rank, world):
       loss = learner.step(slots[i])
     slot_free[i].record(comp)
     with torch.cuda.stream(copy_stream):
-      copy_stream.wait_event(slot_free[j])
+      if host_sync:
+        slot_free[j].synchronize()  # step k-1, slot j's reader, is done
+      else:
+        copy_stream.wait_event(slot_free[j])
       if not skip_h2d:
         dev_flat[j].copy_from(host_flat[(k + 1) % len(host_flat)])
       slot_ready[j].record(copy_stream)
@@ -344,6 +360,7 @@ def measure(args, dtype, device, backend, rank, world):
       'enqueue_s': t_enq, 'frames_per_step': learner.frames_per_step,
       'health': learner.health(), 'torso': torso_precision(agent),
       'hip_graph': use_graph, 'h2d_prefetch': not skip_h2d,
+      'h2d_prefetch_sync': 'host' if host_sync else 'device',
       'h2d_slab': ({'mbytes': round(h2d_mb, 1), 'ms': round(h2d_ms, 3),
                     'gbps': round(h2d_mb / max(h2d_ms, 1e-6), 1)} if cuda else None),
       'dist_extra': dist_extra,
@@ -456,6 +473,7 @@ def main():
            'host_enqueue_ms_per_step': round(
                1000 * main_res['enqueue_s'] / args.steps, 3),
            'h2d_prefetch': main_res['h2d_prefetch'],
+           'h2d_prefetch_sync': main_res['h2d_prefetch_sync'],
            'h2d_slab': main_res['h2d_slab'],
            'dist': dict(dist_info, **main_res['dist_extra']),
            'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '

@@ -239,6 +239,7 @@ class _TrajFeeder(object):
     self.graphs = [None] * n
     self.pending = collections.deque()
     self.k = 0
+    self.host_sync = os.environ.get('SA_H2D_SYNC', 'host') != 'device'
     if self.cuda:
       self.copy_stream = _h2d_stream(device)
       self.free = [torch.cuda.Event() for _ in range(n)]
@@ -307,13 +308,24 @@ class _TrajFeeder(object):
       self.last_host_s = time.time() - t1
       return loss, info, wait
     j = self.k % 2
+    # host-side ordering (as bench.py): device-side waits between the copy
+    # and compute streams cost 0.15-0.2 ms per learner step plus outliers;
+    # the host instead waits for slot j's last graph before the copy and for
+    # the copy before the launch (the previous step keeps the GPU busy)
+    host_sync = self.host_sync
     with torch.cuda.stream(self.copy_stream):
-      self.copy_stream.wait_event(self.free[j])  # slot j's last graph is done
+      if host_sync:
+        self.free[j].synchronize()
+      else:
+        self.copy_stream.wait_event(self.free[j])  # slot j's last graph is done
       self.slots[j].copy_(self.tq.host_tensor(slab), non_blocking=True)
       copied = torch.cuda.Event()
       copied.record(self.copy_stream)
     comp = torch.cuda.current_stream(self.device)
-    comp.wait_event(copied)
+    if host_sync:
+      copied.synchronize()
+    else:
+      comp.wait_event(copied)
     self.pending.append((slab, copied))
     if self.use_graph:
       if self.graphs[j] is None:
