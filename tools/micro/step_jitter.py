@@ -5,6 +5,8 @@ the slowest steps.  usage: python tools/micro/step_jitter.py [fp32|bf16] [K] [on
 import os
 import sys
 
+import time
+
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
@@ -99,6 +101,7 @@ slot_ready[0].record(copy_stream)
 comp = torch.cuda.current_stream()
 
 
+host_t = []  # host seconds per graph_step() call
 cev = []  # (start, end) of each prefetch copy
 wev = []  # compute-stream events around the wait for the slot
 
@@ -121,7 +124,9 @@ def step(k):
     wev.append(w)
   (learner._graph, learner._static_in, learner._static_loss,
    learner._graph_keep) = graphs[i]
+  t = time.perf_counter()
   learner.graph_step()
+  host_t.append(time.perf_counter() - t)
   if (mode.startswith('h2d') or mode in ('d2d', 'ev')) and mode != 'h2d_mid':
     slot_free[i].record(comp)
     prefetch(slot_free[j])
@@ -161,5 +166,8 @@ if cev:
 mean = sum(ts) / K
 print('%s/%s: %d steps, mean %.3f ms, p50 %.3f, p90 %.3f, p99 %.3f, max %.3f' % (
     dtype, mode, K, mean, ts[K // 2], ts[int(K * .9)], ts[int(K * .99)], ts[-1]))
+ht = sorted(host_t[-K:])
+print('host graph_step ms: p50 %.3f p90 %.3f max %.3f' % (
+    1e3 * ht[K // 2], 1e3 * ht[int(K * .9)], 1e3 * ht[-1]))
 print('slowest:', ['%.3f' % t for t in ts[-8:]])
 print('mean without the 2 %% slowest: %.3f ms' % (sum(ts[:int(K * .98)]) / int(K * .98)))
