@@ -18,9 +18,14 @@
 //   fwd saves: acts [L][N][256] (i, c~, f, o after their nonlinearities),
 //              cs [L][N][64], xh [L][N][84] = [x_t, h_{t-1}] (the A operand of
 //              the kernel-gradient GEMM)
-//   bwd:       dgates [L][N][256] and dx [L][N][20] (the caller turns them
-//              into dK = xh^T dgates, db = 1^T dgates with gemm_f32 and the
-//              embedding gradient with a scatter-add)
+//   bwd:       dgates [L][N][256] (the caller turns them into
+//              dK = xh^T dgates, db = 1^T dgates with gemm_f32) and the
+//              embedding gradient: with egrad, each valid word's dx row is
+//              atomically added to its embedding row here; else dx [L][N][20]
+//              is written for a deterministic one-hot product by the caller.
+//              A scatter-add of all L*N rows of dx (torch index_add_) cost
+//              0.43 ms per learner step: every word past an instruction's
+//              length has dx = 0 and id 0, so half the adds hit row 0.
 #include "launchers.h"
 
 namespace sa {
@@ -138,9 +143,11 @@ __global__ __launch_bounds__(256) void lang_lstm_bwd_kernel(
     const int64_t* __restrict__ lengths, const float* __restrict__ kernel,
     const float* __restrict__ dout, const float* __restrict__ acts,
     const float* __restrict__ cs, int N, int L, float* __restrict__ dgates,
-    float* __restrict__ dx) {
+    float* __restrict__ dx, const int64_t* __restrict__ ids, int V,
+    float* __restrict__ egrad) {
   __shared__ float dg_s[kRows][kG + 4];
   __shared__ float dr_s[kRows][96 + 4];  // [row][k]: dx (k < 20) | dh_rec
+  __shared__ int len_s[kRows];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   const int r0 = blockIdx.x * kRows;
@@ -168,6 +175,7 @@ __global__ __launch_bounds__(256) void lang_lstm_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) dout_v[q] = dout[static_cast<int64_t>(erow) * kH + 4 * eq + q];
   for (int e = tid; e < kRows * 100; e += 256) (&dr_s[0][0])[e] = 0.f;
+  if (eq == 0) len_s[er] = elen;
   __syncthreads();
   for (int t = L - 1; t >= 0; --t) {
     if (eok) {
@@ -222,10 +230,22 @@ __global__ __launch_bounds__(256) void lang_lstm_bwd_kernel(
       for (int r = 0; r < 4; ++r) dr_s[c16][16 * kt + 4 * g + r] = acc[r];
     }
     __syncthreads();
-    // dx_t (the embedding gradient's input)
+    // dx_t: into the embedding row of the word (valid words only; an
+    // out-of-range id read row 0 in the forward, so its gradient goes there)
+    // or out for the caller
     for (int e = tid; e < kRows * kE; e += 256) {
       const int rr = e / kE, k = e - (e / kE) * kE;
-      if (r0 + rr < N) dx[(static_cast<int64_t>(t) * N + r0 + rr) * kE + k] = dr_s[rr][k];
+      const int row = r0 + rr;
+      if (row >= N) continue;
+      if (egrad != nullptr) {
+        if (t < len_s[rr]) {
+          const int64_t id = ids[static_cast<int64_t>(row) * L + t];
+          const int vid = (id >= 0 && id < V) ? static_cast<int>(id) : 0;
+          atomicAdd(egrad + vid * kE + k, dr_s[rr][k]);
+        }
+      } else {
+        dx[(static_cast<int64_t>(t) * N + row) * kE + k] = dr_s[rr][k];
+      }
     }
   }
 }
@@ -242,9 +262,11 @@ void lang_lstm_fwd_launch(const int64_t* ids, const int64_t* lengths, const floa
 
 void lang_lstm_bwd_launch(const int64_t* lengths, const float* kernel, const float* dout,
                           const float* acts, const float* cs, int N, int L, float* dgates,
-                          float* dx, hipStream_t stream) {
+                          float* dx, const int64_t* ids, int V, float* egrad,
+                          hipStream_t stream) {
   hipLaunchKernelGGL(lang_lstm_bwd_kernel, dim3((N + kRows - 1) / kRows), dim3(256), 0,
-                     stream, lengths, kernel, dout, acts, cs, N, L, dgates, dx);
+                     stream, lengths, kernel, dout, acts, cs, N, L, dgates, dx, ids, V,
+                     egrad);
 }
 
 }  // namespace sa

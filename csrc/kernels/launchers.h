@@ -67,14 +67,16 @@ int lstm_xpack(int v);
 // W_h [H,4H] -> fwd-packed w4 and bwd-packed wt (one launch per unroll).
 // Instruction encoder (lang_lstm.hip): embedding + LSTM(64) over L words,
 // output at the last valid word; fwd saves acts [L][N][256], cs [L][N][64],
-// xh [L][N][84]; bwd -> dgates [L][N][256], dx [L][N][20].
+// xh [L][N][84]; bwd -> dgates [L][N][256] and either dx [L][N][20] or,
+// with egrad, dx added straight into the embedding rows of the valid words.
 void lang_lstm_fwd_launch(const int64_t* ids, const int64_t* lengths, const float* embed,
                           const float* kernel, const float* bias, int N, int L, int V,
                           float* out, float* acts, float* cs, float* xh,
                           hipStream_t stream);
 void lang_lstm_bwd_launch(const int64_t* lengths, const float* kernel, const float* dout,
                           const float* acts, const float* cs, int N, int L, float* dgates,
-                          float* dx, hipStream_t stream);
+                          float* dx, const int64_t* ids, int V, float* egrad,
+                          hipStream_t stream);
 
 void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
                               hipStream_t stream);

@@ -402,21 +402,38 @@ std::vector<at::Tensor> lang_lstm_fwd(at::Tensor ids, at::Tensor lengths, at::Te
   return {out, acts, cs, xh};
 }
 
-// -> {dgates [L, N, 256], dx [L, N, 20]}
+// -> {dgates [L, N, 256], dx [L, N, 20]}; with ids [N, L] and egrad [V, 20]
+// the valid words' dx rows are added into egrad instead (dx comes back empty)
 std::vector<at::Tensor> lang_lstm_bwd(at::Tensor lengths, at::Tensor kernel, at::Tensor dout,
-                                      at::Tensor acts, at::Tensor cs) {
+                                      at::Tensor acts, at::Tensor cs,
+                                      c10::optional<at::Tensor> ids,
+                                      c10::optional<at::Tensor> egrad) {
   LB_CHECK(lengths); LB_CHECK(kernel); LB_CHECK(dout); LB_CHECK(acts); LB_CHECK(cs);
   LB_F32(dout); LB_F32(acts); LB_F32(cs); LB_F32(kernel);
   const int L = acts.size(0), N = acts.size(1);
   TORCH_CHECK(dout.numel() == static_cast<int64_t>(N) * 64, "dout [N, 64]");
+  TORCH_CHECK(lengths.scalar_type() == at::kLong && lengths.numel() == N, "lengths [N] int64");
+  const bool fused = egrad.has_value() && egrad->defined();
+  int V = 0;
+  if (fused) {
+    TORCH_CHECK(ids.has_value() && ids->defined(), "egrad needs ids");
+    LB_CHECK(*ids); LB_CHECK(*egrad); LB_F32(*egrad);
+    TORCH_CHECK(ids->scalar_type() == at::kLong && ids->dim() == 2 && ids->size(0) == N &&
+                    ids->size(1) == L, "ids [N, L] int64");
+    TORCH_CHECK(egrad->dim() == 2 && egrad->size(1) == 20 && egrad->size(0) > 0,
+                "egrad [V, 20]");
+    V = egrad->size(0);
+  }
   const c10::DeviceGuard guard(acts.device());
   auto dg = at::empty({L, N, 256}, acts.options());
-  auto dx = at::empty({L, N, 20}, acts.options());
+  auto dx = fused ? at::empty({0}, acts.options()) : at::empty({L, N, 20}, acts.options());
   if (N > 0 && L > 0)
     sa::lang_lstm_bwd_launch(lengths.data_ptr<int64_t>(), kernel.data_ptr<float>(),
                              dout.data_ptr<float>(), acts.data_ptr<float>(),
                              cs.data_ptr<float>(), N, L, dg.data_ptr<float>(),
-                             dx.data_ptr<float>(), stream());
+                             fused ? nullptr : dx.data_ptr<float>(),
+                             fused ? ids->data_ptr<int64_t>() : nullptr, V,
+                             fused ? egrad->data_ptr<float>() : nullptr, stream());
   return {dg, dx};
 }
 
@@ -437,7 +454,9 @@ void register_learner_ops(pybind11::module& m) {
         pybind11::arg("gbb"), pybind11::arg("task") = pybind11::none());
   m.def("core_aug_fwd", &core_aug_fwd);
   m.def("lang_lstm_fwd", &lang_lstm_fwd);
-  m.def("lang_lstm_bwd", &lang_lstm_bwd);
+  m.def("lang_lstm_bwd", &lang_lstm_bwd, pybind11::arg("lengths"), pybind11::arg("kernel"),
+        pybind11::arg("dout"), pybind11::arg("acts"), pybind11::arg("cs"),
+        pybind11::arg("ids") = pybind11::none(), pybind11::arg("egrad") = pybind11::none());
   m.def("gemm_f32", &gemm_f32, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("ta"),
         pybind11::arg("tb"), pybind11::arg("C"), pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("mask") = pybind11::none(), pybind11::arg("relu") = false,

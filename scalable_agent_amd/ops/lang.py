@@ -7,7 +7,8 @@ bias +1.  csrc/kernels/lang_lstm.hip runs the whole word loop of 16 frames
 per workgroup (embedding gather, the [x_t, h_{t-1}] x K product on fp32
 MFMA, the cell update) forward and backward; the parameter gradients are
 dK = xh^T dgates and db = 1^T dgates (one exact-fp32 GEMM with the ones-row
-bias gradient, gemm_f32) and the embedding rows' scatter-add of dx.
+bias gradient, gemm_f32); the backward kernel adds the valid words' dx rows
+into the embedding gradient itself.
 """
 
 import torch
@@ -28,24 +29,27 @@ class _LanguageLSTM(torch.autograd.Function):
   def backward(ctx, dout):
     ids, lengths, embed, kernel, bias, acts, cs, xh = ctx.saved_tensors
     C = ext()
-    dg, dx = C.lang_lstm_bwd(lengths, kernel, dout.float().contiguous(), acts, cs)
-    L, N, G = dg.shape
     (gemb, gk, gb), direct = grad_sink.sinks([embed, kernel, bias])
+    det = torch.are_deterministic_algorithms_enabled()
+    # embedding rows: the backward kernel adds each valid word's dx into its
+    # row (atomics, like a scatter-add); deterministic mode takes dx back and
+    # sums it with a one-hot product in a fixed order
+    dg, dx = C.lang_lstm_bwd(lengths, kernel, dout.float().contiguous(), acts, cs,
+                             ids=None if det else ids,
+                             egrad=None if det else gemb)
+    L, N, G = dg.shape
     xh2, dg2 = xh.view(L * N, xh.shape[2]), dg.view(L * N, G)
     # the A^T B form takes any K (= L * N)
     C.gemm_f32(xh2, dg2, True, False, gk, accumulate=True, colsum=gb)
-    # embedding rows: scatter-add of dx over the word ids (steps past an
-    # instruction's length carry dx = 0); out-of-range ids read row 0 in the
-    # forward kernel, so their gradient goes to row 0 too
-    flat = ids.t().reshape(-1)  # [L*N] in the kernel's (t, n) order
-    flat = torch.where((flat >= 0) & (flat < embed.shape[0]), flat,
-                       torch.zeros_like(flat))
-    dx2 = dx.view(L * N, dx.shape[2])
-    if torch.are_deterministic_algorithms_enabled():
+    if det:
+      # steps past an instruction's length carry dx = 0; out-of-range ids
+      # read row 0 in the forward kernel, so their gradient goes to row 0
+      flat = ids.t().reshape(-1)  # [L*N] in the kernel's (t, n) order
+      flat = torch.where((flat >= 0) & (flat < embed.shape[0]), flat,
+                         torch.zeros_like(flat))
+      dx2 = dx.view(L * N, dx.shape[2])
       onehot = torch.nn.functional.one_hot(flat, embed.shape[0]).to(dx2.dtype)
       gemb.add_(onehot.t() @ dx2)
-    else:
-      gemb.index_add_(0, flat, dx2)
     return (None, None) + grad_sink.returned((gemb, gk, gb), direct)
 
 

@@ -17,8 +17,11 @@ def _rel(a, b):
   return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize('N,L', [(37, 5), (3232, 16)])
-def test_language_lstm_matches_torch(cuda, N, L):
+@pytest.mark.parametrize('N,L,det', [(37, 5, False), (3232, 16, False),
+                                     (3232, 16, True)])
+def test_language_lstm_matches_torch(cuda, N, L, det):
+  # det: deterministic mode sums dx with a one-hot product instead of the
+  # backward kernel's embedding-row atomics
   from scalable_agent_amd import ops
   g = torch.Generator().manual_seed(N + L)
   ids = torch.randint(1, 1000, (N, L), generator=g)
@@ -35,7 +38,12 @@ def test_language_lstm_matches_torch(cuda, N, L):
   assert out.shape == (N, 64) and out.dtype == torch.float32
   assert _rel(out, out_ref) <= 1e-5
   assert torch.all(out[lengths.to(cuda) == 0] == 0)
-  (out * w.float().to(cuda)).sum().backward()
+  prev = torch.are_deterministic_algorithms_enabled()
+  torch.use_deterministic_algorithms(det, warn_only=True)
+  try:
+    (out * w.float().to(cuda)).sum().backward()
+  finally:
+    torch.use_deterministic_algorithms(prev)
   for name in ('embed', 'language_lstm_kernel', 'language_lstm_bias'):
     gr = getattr(ref_agent, name).grad
     gh = getattr(agent, name).grad
