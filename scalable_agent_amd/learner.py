@@ -161,6 +161,8 @@ class Learner:
                             flags.num_action_repeats * world_size)
     self.last_loss = None
     self._graph = None
+    self._early_ev = None  # graph_step's host-side early all-reduce hand-off
+    self._early_stream = None
     self._static_in = None
     self._static_loss = None
     self.grad_sync = None
@@ -333,8 +335,24 @@ class Learner:
       self._popart_tasks = self._static_in.level_name
     if isinstance(self._graph, tuple):
       self._graph[0].replay()
-      self.grad_sync.begin_early()
-      self._graph[1].replay()
+      if os.environ.get('SA_EARLY_SYNC', 'host') == 'host':
+        # the early bucket's all-reduce is enqueued once the host has seen
+        # the first graph end, from an idle stream, so the RCCL stream never
+        # sits in a device-side wait on the compute stream: a queue blocked
+        # on a compute-stream event slows the compute stream's own dispatch
+        # (~0.15 ms per learner step on one GPU, tools/micro/step_jitter.py
+        # dpA vs dpB).  The torso backward is already enqueued meanwhile
+        if self._early_ev is None:
+          self._early_ev = torch.cuda.Event()
+          self._early_stream = torch.cuda.Stream(self.device)
+        self._early_ev.record()
+        self._graph[1].replay()
+        self._early_ev.synchronize()
+        with torch.cuda.stream(self._early_stream):
+          self.grad_sync.begin_early()
+      else:
+        self.grad_sync.begin_early()
+        self._graph[1].replay()
     else:
       self._graph.replay()
     self._apply()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-step time distribution of the graph-replayed learner step (no H2D
 prefetch, no profiler): K steps each bracketed by events, percentiles and
-the slowest steps.  usage: python tools/micro/step_jitter.py [fp32|bf16] [K] [one|two|h2d|h2d_thp|h2d_mid|h2d_chunk|d2d|ev|w_done|rec|hw_ready|hw_both]"""
+the slowest steps.  usage: python tools/micro/step_jitter.py [fp32|bf16] [K] [one|two|h2d|h2d_thp|h2d_mid|h2d_chunk|d2d|ev|w_done|rec|hw_ready|hw_both|side|w_pending|x_wait|x_wait_k|dp0|dpA|dpB|dpC]"""
 import os
 import sys
 
@@ -52,6 +52,7 @@ if mode == 'h2d_thp':
   host_flat.flat = torch.from_numpy(arr)
   print('pinned:', host_flat.flat.is_pinned())
 mid_ev = torch.cuda.Event()
+side_buf = torch.zeros(1024, device=dev)
 src_dev = host_flat.flat[:host_flat.nbytes].to(dev) if mode == 'd2d' else None
 nxt = [0]
 
@@ -84,9 +85,15 @@ def mid_hook():
   prefetch(mid_ev)
 
 
-if mode == 'h2d_mid':  # bench.py's default: the copy under the torso backward
-  learner.split_backward(mid_hook)
-for _ in range(1 if mode in ('one', 'w_done', 'rec') else 2):
+if mode.startswith('dp'):
+  # data-parallel stream pattern on one GPU: split graphs (forward + late
+  # backward, then the conv-torso backward), a stand-in for each all-reduce
+  # bucket on a side stream (10 passes over the bucket, ~ a collective's time)
+  learner._split = True
+  split = learner._torso_offset()
+  side = torch.cuda.Stream()
+  ev0, ev1 = torch.cuda.Event(), torch.cuda.Event()
+for _ in range(1 if mode in ('one', 'w_done', 'rec', 'side', 'w_pending', 'x_wait', 'x_wait_k') else 2):
   dev_flat.append(FlatStaging(hb, dev).load(hb))
   learner.capture(dev_flat[-1].views, clone=False)
   graphs.append((learner._graph, learner._static_in, learner._static_loss,
@@ -106,10 +113,66 @@ cev = []  # (start, end) of each prefetch copy
 wev = []  # compute-stream events around the wait for the slot
 
 
+def dp_bucket(lo, hi):
+  g = learner.flat.grads[lo:hi]
+  for _ in range(10):
+    g.mul_(1.0)
+
+
+dp_t = [0.0, 0.0, 0.0, 0]  # host seconds in g0 / g1 replay / _apply, steps
+
+
+def dp_step(m):
+  g0, g1 = learner._graph
+  n = learner.flat.grads.numel()
+  t0 = time.perf_counter()
+  g0.replay()
+  dp_t[0] += time.perf_counter() - t0
+  dp_t[3] += 1
+  if m == 'dpA':  # device-side waits (torch.distributed's pattern)
+    side.wait_stream(comp)
+    with torch.cuda.stream(side):
+      dp_bucket(0, split)
+    g1.replay()
+  elif m in ('dpB', 'dpC'):  # early bucket enqueued once the host saw g0 end
+    ev0.record(comp)
+    g1.replay()
+    ev0.synchronize()
+    with torch.cuda.stream(side):
+      dp_bucket(0, split)
+  else:
+    t0 = time.perf_counter()
+    g1.replay()
+    dp_t[1] += time.perf_counter() - t0
+  if m in ('dpA', 'dpB'):
+    side.wait_stream(comp)
+  elif m == 'dpC':
+    ev1.record(comp)
+    ev1.synchronize()
+  if m != 'dp0':
+    with torch.cuda.stream(side):
+      dp_bucket(split, n)
+    comp.wait_stream(side)
+  t0 = time.perf_counter()
+  learner._apply()
+  dp_t[2] += time.perf_counter() - t0
+
+
 def step(k):
   # 'h2d': bench.py's loop (prefetch of the next batch on a copy stream)
   i, j = k % len(graphs), (k + 1) % len(graphs)
   nxt[0] = k
+  if mode == 'side':  # the DP all-reduce's stream pattern, a tiny kernel
+    comp.wait_event(slot_ready[0])
+  if mode == 'w_pending':  # wait on a copy-stream record enqueued just now
+    slot_ready[0].record(copy_stream)
+    comp.wait_event(slot_ready[0])
+  if mode == 'x_wait_k':  # the same after one tiny kernel behind the graph
+    side_buf.add_(1.0)
+  if mode in ('x_wait', 'x_wait_k'):  # another stream waits on the compute stream
+    slot_free[0].record(comp)
+    copy_stream.wait_event(slot_free[0])
+    slot_ready[0].record(copy_stream)
   if mode == 'w_done':  # wait on a copy-stream event completed long ago
     comp.wait_event(slot_ready[0])
   if mode == 'rec':  # record a (non-timing) event on the compute stream only
@@ -125,11 +188,20 @@ def step(k):
   (learner._graph, learner._static_in, learner._static_loss,
    learner._graph_keep) = graphs[i]
   t = time.perf_counter()
-  learner.graph_step()
+  if mode.startswith('dp'):
+    dp_step(mode)
+  else:
+    learner.graph_step()
   host_t.append(time.perf_counter() - t)
   if (mode.startswith('h2d') or mode in ('d2d', 'ev')) and mode != 'h2d_mid':
     slot_free[i].record(comp)
     prefetch(slot_free[j])
+  if mode == 'side':
+    slot_free[0].record(comp)
+    with torch.cuda.stream(copy_stream):
+      copy_stream.wait_event(slot_free[0])
+      side_buf.add_(1.0)
+      slot_ready[0].record(copy_stream)
   if mode == 'hw_ready':  # device-side wait for the copy's start only
     slot_free[i].record(comp)
     with torch.cuda.stream(copy_stream):
@@ -169,5 +241,8 @@ print('%s/%s: %d steps, mean %.3f ms, p50 %.3f, p90 %.3f, p99 %.3f, max %.3f' % 
 ht = sorted(host_t[-K:])
 print('host graph_step ms: p50 %.3f p90 %.3f max %.3f' % (
     1e3 * ht[K // 2], 1e3 * ht[int(K * .9)], 1e3 * ht[-1]))
+if dp_t[3]:
+  print('dp host ms per step: g0 %.3f g1 %.3f apply %.3f' % tuple(
+      1e3 * x / dp_t[3] for x in dp_t[:3]))
 print('slowest:', ['%.3f' % t for t in ts[-8:]])
 print('mean without the 2 %% slowest: %.3f ms' % (sum(ts[:int(K * .98)]) / int(K * .98)))
