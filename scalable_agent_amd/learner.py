@@ -168,6 +168,7 @@ class Learner:
     self.grad_sync = None
     self.popart = None
     self._aux = {}
+    self._seed_one = None  # backward seed (see _fwd_late)
     # weight-gradient GEMMs on a side stream next to the torso backward
     # (opt-in: measured within run-to-run noise, profiles/experiments.md)
     self._overlap = os.environ.get('SA_OVERLAP_WGRAD', '0') == '1'
@@ -223,7 +224,13 @@ class Learner:
     with trace('backward'):
       a, b = self._grad_ctx()
       with a, b:
-        loss.backward()
+        # a persistent ones seed: loss.backward() would fill a fresh one
+        # (a kernel launch in the serial chain of every step)
+        one = self._seed_one
+        if one is None or one.shape != loss.shape or one.dtype != loss.dtype \
+            or one.device != loss.device:
+          one = self._seed_one = torch.ones_like(loss)
+        loss.backward(one)
     self._split_pairs = pairs
     return loss
 

@@ -54,6 +54,9 @@ class _CoreLSTM(torch.autograd.Function):
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
               done_u8, num_actions, instr_enc, allow_gang=True):
+    # the final cell state is rarely used: its gradient arrives as None
+    # instead of a zero-filled tensor (the backward handles both)
+    ctx.set_materialize_grads(False)
     C = ext()
     T, B = done_u8.shape
     N = T * B
@@ -177,6 +180,9 @@ class _CoreLSTMF32(torch.autograd.Function):
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
               done_u8, num_actions, instr_enc, allow_gang=True):
+    # the final cell state is rarely used: its gradient arrives as None
+    # instead of a zero-filled tensor (the backward handles both)
+    ctx.set_materialize_grads(False)
     C = ext()
     T, B = done_u8.shape
     N = T * B
