@@ -194,6 +194,13 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
       check_launch("cf32_conv_dgrad(stacked)");
       return dx;
     }
+    // every phase's sub-kernel at once: w zero-padded to Kq * S taps per
+    // axis, tap k = S j + r -> wall[r_y][r_x][j_y][j_x] (missing taps zero);
+    // a pad and one copy instead of a fill and a copy per phase
+    auto wall = at::constant_pad_nd(w, {0, 0, 0, 0, 0, Kq * S - K, 0, Kq * S - K})
+                    .view({Kq, S, Kq, S, Cin, w.size(3)})
+                    .permute({1, 3, 0, 2, 4, 5})
+                    .contiguous();
     for (int64_t ry = 0; ry < S; ++ry) {
       // q range with 0 <= S q + ry - pt < H
       const int64_t qy0 = (pt - ry + S - 1) >= 0 ? (pt - ry + S - 1) / S : 0;
@@ -203,10 +210,7 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
         const int64_t qx0 = (pl - rx + S - 1) >= 0 ? (pl - rx + S - 1) / S : 0;
         const int64_t qx1 = (W - 1 + pl - rx) / S;
         if (qx1 < qx0) continue;
-        auto wsub = at::zeros({Kq, Kq, Cin, w.size(3)}, w.options());
-        const int64_t ny = (K - ry + S - 1) / S, nx = (K - rx + S - 1) / S;
-        wsub.narrow(0, 0, ny).narrow(1, 0, nx).copy_(
-            w.slice(0, ry, K, S).slice(1, rx, K, S));
+        auto wsub = wall.select(0, ry).select(0, rx);  // [Kq, Kq, Cin, Cout]
         sa::cf32::ConvArgs a{};
         a.src = dy.data_ptr();
         a.w = wsub.data_ptr<float>();
