@@ -264,11 +264,22 @@ def _deep_backward(C, ctx, saved, params, gv, dy):
     C.cf32_conv_wgrad(stage_in, dconv, 1, 1, 1, False, gw, gv[pb + 1])
 
 
+_ZPAD = {}
+
+
 def _pad_cin(w, c):
-  """HWIO weights zero-padded on the input-channel axis to c channels."""
-  out = w.new_zeros(w.shape[:2] + (c,) + w.shape[3:])
-  out[:, :, :w.shape[2]] = w
-  return out
+  """HWIO weights zero-padded on the input-channel axis to c channels: one
+  concatenation with a cached zero block (a fill + a copy per call before)."""
+  shape = w.shape[:2] + (c - w.shape[2],) + w.shape[3:]
+  key = (tuple(shape), w.dtype, w.device)
+  z = _ZPAD.get(key)
+  if z is None:
+    z = torch.zeros(shape, dtype=w.dtype, device=w.device)
+    # a block first made inside a graph capture holds zeros only once that
+    # graph has replayed: cache eagerly made blocks only
+    if not (w.is_cuda and torch.cuda.is_current_stream_capturing()):
+      _ZPAD[key] = z
+  return torch.cat([w, z], dim=2)
 
 
 def shallow_param_list(agent):
