@@ -45,6 +45,20 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int kMaxParts = 4;  // images one range may touch
 
+// LDS rows one range of RT tiles can need: 2 pixel rows per tile row it
+// touches in each image part plus 2 halo rows per part.  Ranges start on
+// tile-row boundaries when RT % TX == 0 (then they touch exactly RT / TX tile
+// rows in total) and never straddle images when per_img % RT == 0 (one part);
+// otherwise the general bound (a range may start mid-row and touch
+// ceil((RT - 1) / TX) + 1 tile rows over up to maxparts images).  The tight
+// cases let the fused backward kernels stage the 36x64 / 18x32 maps (72x128
+// Doom frames) in their register slots.
+inline int range_maxrows(int RT, int TX, int per_img, int maxparts) {
+  const int parts = per_img % RT == 0 ? 1 : maxparts;
+  const int trows = RT % TX == 0 ? RT / TX : (RT - 1 + TX - 1) / TX + 1;
+  return 2 * trows + 2 * parts;
+}
+
 // Measurement knobs (SA_WINO_ABLATE / SA_FUSED_ABLATE: drop parts of a
 // kernel's work to time the rest) exist only in builds with
 // -DSA_MEASURE_KNOBS=1; in production builds every knob test folds to false,
@@ -2853,7 +2867,7 @@ bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const flo
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
   const int WlP = wino_wl<GH, fused32_pad<CX, CY, RT, GH, GW>()>(TX);
-  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  const int maxrows = range_maxrows(RT, TX, per_img, maxparts);
   if (maxrows * Wl * (CY / 4) > MAXCY * 512 || maxrows * Wl * (CX / 4) > MAXCX * 512 ||
       maxrows > 512)
     return false;
@@ -2938,7 +2952,7 @@ bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2, WlP = wino_wl<GH, wino_lpad_on(1)>(TX);
-  const int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
+  const int maxrows = range_maxrows(RT, TX, per_img, maxparts);
   if (maxrows * Wl * (C / 4) > MAXC * 64 * NW || maxrows > 64 * NW) return false;
   const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * WlP * (C + 4)) +
                        sizeof(int) * (maxrows + RT);
@@ -3033,6 +3047,8 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
   if (Cin == 4 && Cout == 16 && (on & 2)) {
     if (W == 96) return run_wino_pool<4, 16, 96>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     if (W == 64) return run_wino_pool<4, 16, 64>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
+    // the 72x128 Doom frame (Sample Factory's doom_benchmark resolution)
+    if (W == 128) return run_wino_pool<4, 16, 128>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
     // the Atari frame (BASELINE config #2): 84 tiles per range in 6 groups
     if (W == 84) return run_wino_pool<4, 16, 84>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
   }

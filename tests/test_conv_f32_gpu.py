@@ -335,7 +335,8 @@ def test_wino_conv_pool_matches_conv_then_pool(cuda, N, H, W, zero_w, cin):
 
 @pytest.mark.parametrize('N,H,W,zero_w', [(6, 72, 96, False), (120, 72, 96, False),
                                            (3, 8, 64, False), (5, 72, 96, True),
-                                           (7, 84, 84, False), (3, 84, 84, True)])
+                                           (7, 84, 84, False), (3, 84, 84, True),
+                                           (5, 72, 128, False), (3, 72, 128, True)])
 def test_wino_conv_pool_stage0_matches_float64(cuda, N, H, W, zero_w):
   """Stage-0 head (4-channel image -> 16) with the pool in the Winograd
   epilogue against the float64 conv + 3x3/2 max-pool: values to fp32
@@ -553,7 +554,10 @@ def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
     (5, 11, 11, 16, 16, True), (5, 11, 11, 32, 32, True),
     (256, 36, 48, 16, 32, False), (256, 18, 24, 32, 32, False), (5, 11, 11, 16, 32, False),
     (256, 36, 48, 16, 16, False),
-    (7, 42, 42, 16, 32, False), (3, 36, 64, 16, 32, False)])
+    (7, 42, 42, 16, 32, False), (3, 36, 64, 16, 32, False),
+    # the 72x128 Doom ladder: ranges on tile-row boundaries (tight row bound)
+    (40, 36, 64, 16, 16, True), (40, 36, 64, 16, 32, False),
+    (40, 18, 32, 32, 32, True), (40, 18, 32, 32, 32, False), (40, 9, 16, 32, 32, True)])
 @pytest.mark.parametrize('relu_x,use_add', [(False, False), (True, True)])
 def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
   """A 3x3/1 conv's backward in one pass (conv_wino.hip
@@ -564,8 +568,8 @@ def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
   dW += relu?(x)^T dY, db += sum dY, against float64.  At N = 256 every
   persistent workgroup walks many ranges (contiguous range runs, cross-range
   prefetch, image boundaries inside a range); 11x11 / 42x42 exercise odd
-  tile counts and partial 2x2 tiles; 36x64 (Doom) falls back to the
-  separate kernels."""
+  tile counts and partial 2x2 tiles; 36x64 / 18x32 / 9x16 are the 72x128
+  Doom frame's maps, whose ranges start on tile-row boundaries."""
   C = _C()
   g = torch.Generator().manual_seed(N * H + Cx + Cy)
   x = torch.randn(N, H, W, Cx, generator=g)
