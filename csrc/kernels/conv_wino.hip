@@ -45,20 +45,6 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int kMaxParts = 4;  // images one range may touch
 
-// LDS rows one range of RT tiles can need: 2 pixel rows per tile row it
-// touches in each image part plus 2 halo rows per part.  Ranges start on
-// tile-row boundaries when RT % TX == 0 (then they touch exactly RT / TX tile
-// rows in total) and never straddle images when per_img % RT == 0 (one part);
-// otherwise the general bound (a range may start mid-row and touch
-// ceil((RT - 1) / TX) + 1 tile rows over up to maxparts images).  The tight
-// cases let the fused backward kernels stage the 36x64 / 18x32 maps (72x128
-// Doom frames) in their register slots.
-inline int range_maxrows(int RT, int TX, int per_img, int maxparts) {
-  const int parts = per_img % RT == 0 ? 1 : maxparts;
-  const int trows = RT % TX == 0 ? RT / TX : (RT - 1 + TX - 1) / TX + 1;
-  return 2 * trows + 2 * parts;
-}
-
 // Measurement knobs (SA_WINO_ABLATE / SA_FUSED_ABLATE: drop parts of a
 // kernel's work to time the rest) exist only in builds with
 // -DSA_MEASURE_KNOBS=1; in production builds every knob test folds to false,
@@ -233,10 +219,18 @@ __device__ __forceinline__ RangeGeom range_geom(const WinoArgs& a, int r, int RT
 __host__ __device__ constexpr int wino_parts(int RT, int per_img) {
   return (RT - 1 + per_img - 1) / per_img + 1;
 }
+// LDS rows one range of RT tiles can need: 2 pixel rows per tile row it
+// touches in each image part plus 2 halo rows per part.  Ranges start on
+// tile-row boundaries when RT % TX == 0 (then they touch exactly RT / TX tile
+// rows in total) and never straddle images when TY TX % RT == 0 (one part);
+// otherwise a range may start mid-row (ceil((RT - 1) / TX) + 1 tile rows)
+// and touch wino_parts images.  The host launchers and the compile-time
+// geometry (TileGeo) both use this bound; the tight cases let the fused
+// backward kernels stage the 72x128 frame's 36x64 / 18x32 maps in their
+// register slots.
 __host__ __device__ constexpr int wino_maxrows(int RT, int TX, int TY) {
-  return (RT % TX == 0 && (TY * TX) % RT == 0)
-             ? 2 * (RT / TX) + 2
-             : 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * wino_parts(RT, TY * TX);
+  return 2 * (RT % TX == 0 ? RT / TX : (RT - 1 + TX - 1) / TX + 1) +
+         2 * ((TY * TX) % RT == 0 ? 1 : wino_parts(RT, TY * TX));
 }
 
 // Staged-row pitch padding (compile-time geometry only).  A 16-tile patch
@@ -658,8 +652,7 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   const int Wl = 2 * TX + 2, WlP = wino_wl<GH, wino_lpad_on(0)>(TX);
   // staged rows <= 2 (tile rows spanned) + 2 (images touched); exactly
   // 2 RT / TX + 2 when every range is whole tile rows of one image
-  int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * maxparts;
-  if (RT % TX == 0 && per_img % RT == 0) maxrows = 2 * (RT / TX) + 2;
+  const int maxrows = wino_maxrows(RT, TX, TY);
   if (static_cast<int64_t>(maxrows) * Wl * (CIN / 4) > static_cast<int64_t>(MAXC) * 64 * NW)
     return false;
   const size_t bytes = sizeof(float) * (16 * CIN * COUT +
@@ -715,19 +708,21 @@ bool wino_geo_family(int bit) {
 }
 
 // The deep torso's maps get compile-time instances (only where that layer
-// runs): the IMPALA / DMLab 72x96 ladder (36x48, 18x24, 9x12) and the Atari
-// 84x84 ladder (42x42, 21x21, 11x11); any other map runs the runtime-
-// geometry kernel.  Per channel configuration: 16 -> 16 (res16) and 16 -> 32
-// (stage-1 head) at 36x48 / 42x42, 32 -> 32 (res32, stage-2 head) at 18x24,
-// 9x12, 21x21, 11x11.
+// runs): the IMPALA / DMLab 72x96 ladder (36x48, 18x24, 9x12), the Atari
+// 84x84 ladder (42x42, 21x21, 11x11) and the 72x128 Doom ladder (36x64,
+// 18x32, 9x16); any other map runs the runtime-geometry kernel.  Per channel
+// configuration: 16 -> 16 (res16) and 16 -> 32 (stage-1 head) at 36x48 /
+// 42x42 / 36x64, 32 -> 32 (res32, stage-2 head) at 18x24, 9x12, 21x21,
+// 11x11, 18x32, 9x16.
 #define SA_GEO(h, w) \
   if (HH == (h) && WW == (w) && SA_CALL(h, w)) return true;
-#define SA_WINO_GEO_DISPATCH(CI, CO, FAM)                        \
-  if (wino_geo_family(FAM)) {                                    \
-    if constexpr ((CI) == 16) { SA_GEO(36, 48) SA_GEO(42, 42) }  \
-    if constexpr ((CI) == 32 && (CO) == 32) {                    \
-      SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) \
-    }                                                            \
+#define SA_WINO_GEO_DISPATCH(CI, CO, FAM)                                      \
+  if (wino_geo_family(FAM)) {                                                  \
+    if constexpr ((CI) == 16) { SA_GEO(36, 48) SA_GEO(42, 42) SA_GEO(36, 64) } \
+    if constexpr ((CI) == 32 && (CO) == 32) {                                  \
+      SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11)               \
+      SA_GEO(18, 32) SA_GEO(9, 16)                                             \
+    }                                                                          \
   }
 
 // runtime geometry only (the opt-in experiment variants)
@@ -767,10 +762,10 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
     if (on >= 3 && !flip && wino_geo_enabled()) {
       const int HH = c.Ho, WW = c.Wo;
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
-      if (fl == 19) { SA_GEO(36, 48) SA_GEO(42, 42) }
+      if (fl == 19) { SA_GEO(36, 48) SA_GEO(42, 42) SA_GEO(36, 64) }
 #undef SA_CALL
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
-      if (fl == 24) { SA_GEO(36, 48) SA_GEO(42, 42) }
+      if (fl == 24) { SA_GEO(36, 48) SA_GEO(42, 42) SA_GEO(36, 64) }
 #undef SA_CALL
     }
   }
@@ -781,10 +776,12 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
       const int HH = c.Ho, WW = c.Wo;
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 19, h, w>(c, flip, s)
       // (the 19 instances of the odd maps spill 4-6 VGPRs: runtime flags there)
-      if (fl == 19) { SA_GEO(18, 24) }
+      if (fl == 19) { SA_GEO(18, 24) SA_GEO(18, 32) }
 #undef SA_CALL
 #define SA_CALL(h, w) run_wino_g<CIN, COUT, NH, NW, RT, MAXC, WPS, 24, h, w>(c, flip, s)
-      if (fl == 24) { SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) }
+      if (fl == 24) {
+        SA_GEO(18, 24) SA_GEO(9, 12) SA_GEO(21, 21) SA_GEO(11, 11) SA_GEO(18, 32) SA_GEO(9, 16)
+      }
 #undef SA_CALL
     }
   }
@@ -2402,7 +2399,7 @@ constexpr bool fused32_pad() {
     return false;
   } else {
     constexpr int TY = (GH + 1) / 2, TX = (GW + 1) / 2;
-    constexpr int maxrows = 2 * ((RT - 1 + TX - 1) / TX + 1) + 2 * wino_parts(RT, TY * TX);
+    constexpr int maxrows = wino_maxrows(RT, TX, TY);
     return fused32_lds(CX, CY, RT, maxrows, wino_wl<GH>(TX)) <= 160 * 1024;
   }
 }
@@ -2867,7 +2864,7 @@ bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const flo
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2;
   const int WlP = wino_wl<GH, fused32_pad<CX, CY, RT, GH, GW>()>(TX);
-  const int maxrows = range_maxrows(RT, TX, per_img, maxparts);
+  const int maxrows = wino_maxrows(RT, TX, TY);
   if (maxrows * Wl * (CY / 4) > MAXCY * 512 || maxrows * Wl * (CX / 4) > MAXCX * 512 ||
       maxrows > 512)
     return false;
@@ -2952,7 +2949,7 @@ bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float
   const int maxparts = (RT - 1 + per_img - 1) / per_img + 1;
   if (maxparts > kMaxParts) return false;
   const int Wl = 2 * TX + 2, WlP = wino_wl<GH, wino_lpad_on(1)>(TX);
-  const int maxrows = range_maxrows(RT, TX, per_img, maxparts);
+  const int maxrows = wino_maxrows(RT, TX, TY);
   if (maxrows * Wl * (C / 4) > MAXC * 64 * NW || maxrows > 64 * NW) return false;
   const size_t bytes = sizeof(float) * (16 * C * C + 2 * static_cast<size_t>(maxrows) * WlP * (C + 4)) +
                        sizeof(int) * (maxrows + RT);

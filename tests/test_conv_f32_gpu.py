@@ -623,7 +623,8 @@ def test_residual_block_forward_flags(cuda, H, W, C, block_conv):
 
 
 GEO_FWD = [(36, 48, 16, 16), (42, 42, 16, 16), (36, 48, 16, 32), (42, 42, 16, 32),
-           (18, 24, 32, 32), (9, 12, 32, 32), (21, 21, 32, 32), (11, 11, 32, 32)]
+           (18, 24, 32, 32), (9, 12, 32, 32), (21, 21, 32, 32), (11, 11, 32, 32),
+           (36, 64, 16, 16), (36, 64, 16, 32), (18, 32, 32, 32), (9, 16, 32, 32)]
 
 
 @pytest.mark.parametrize('H,W,Cin,Cout', GEO_FWD)
@@ -658,7 +659,8 @@ def test_wino_geometry_instances_match_runtime_fwd(cuda, H, W, Cin, Cout, flags)
 GEO_BWD = [(36, 48, 16, 16, True), (42, 42, 16, 16, True), (36, 48, 16, 32, False),
            (42, 42, 16, 32, False), (18, 24, 32, 32, True), (18, 24, 32, 32, False),
            (9, 12, 32, 32, True), (21, 21, 32, 32, True), (21, 21, 32, 32, False),
-           (11, 11, 32, 32, True)]
+           (11, 11, 32, 32, True), (36, 64, 16, 16, True), (36, 64, 16, 32, False),
+           (18, 32, 32, 32, True), (18, 32, 32, 32, False), (9, 16, 32, 32, True)]
 
 
 @pytest.mark.parametrize('H,W,Cx,Cy,mask', GEO_BWD)

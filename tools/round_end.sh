@@ -22,6 +22,7 @@ run atari_fp32 --height 84 --width 84 --channels 4 --also_bf16 0
 run popart --popart 30 --also_bf16 0
 run instr --instructions 1 --also_bf16 0
 run shallow --torso shallow --also_bf16 0
+run doom --height 72 --width 128
 SA_DIST_BACKEND=gloo run dp2_gloo --gpus 2 --also_bf16 0 --steps 10
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/pf32 -o run -- python3 bench.py --also_bf16 0 --steps 20 --warmup 3 > $O/pf32.log 2>&1
