@@ -276,8 +276,12 @@ def _pad_cin(w, c):
   if z is None:
     z = torch.zeros(shape, dtype=w.dtype, device=w.device)
     # a block first made inside a graph capture holds zeros only once that
-    # graph has replayed: cache eagerly made blocks only
-    if not (w.is_cuda and torch.cuda.is_current_stream_capturing()):
+    # graph has replayed: cache eagerly made blocks only, and only once their
+    # fill has run (other threads may read the cache from other streams)
+    if not w.is_cuda:
+      _ZPAD[key] = z
+    elif not torch.cuda.is_current_stream_capturing():
+      torch.cuda.current_stream(w.device).synchronize()
       _ZPAD[key] = z
   return torch.cat([w, z], dim=2)
 
