@@ -161,7 +161,10 @@ class Learner:
                             flags.num_action_repeats * world_size)
     self.last_loss = None
     self._graph = None
-    self._early_ev = None  # graph_step's host-side early all-reduce hand-off
+    # graph_step's early all-reduce hand-off: host-side (default) or
+    # device-side stream order (SA_EARLY_SYNC=device)
+    self._early_host = os.environ.get('SA_EARLY_SYNC', 'host') != 'device'
+    self._early_ev = None
     self._early_stream = None
     self._static_in = None
     self._static_loss = None
@@ -342,7 +345,7 @@ class Learner:
       self._popart_tasks = self._static_in.level_name
     if isinstance(self._graph, tuple):
       self._graph[0].replay()
-      if os.environ.get('SA_EARLY_SYNC', 'host') == 'host':
+      if self._early_host:
         # the early bucket's all-reduce is enqueued once the host has seen
         # the first graph end, from an idle stream, so the RCCL stream never
         # sits in a device-side wait on the compute stream: a queue blocked
