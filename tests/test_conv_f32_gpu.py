@@ -557,7 +557,9 @@ def test_conv_f32_many_tiles(cuda, H, W, Cin, Cout):
     (7, 42, 42, 16, 32, False), (3, 36, 64, 16, 32, False),
     # the 72x128 Doom ladder: ranges on tile-row boundaries (tight row bound)
     (40, 36, 64, 16, 16, True), (40, 36, 64, 16, 32, False),
-    (40, 18, 32, 32, 32, True), (40, 18, 32, 32, 32, False), (40, 9, 16, 32, 32, True)])
+    (40, 18, 32, 32, 32, True), (40, 18, 32, 32, 32, False), (40, 9, 16, 32, 32, True),
+    # ranges that never straddle images but start mid-row (per_img % RT == 0)
+    (40, 16, 48, 16, 16, True), (40, 16, 48, 32, 32, True)])
 @pytest.mark.parametrize('relu_x,use_add', [(False, False), (True, True)])
 def test_conv_bwd_fused(cuda, N, H, W, Cx, Cy, mask, relu_x, use_add):
   """A 3x3/1 conv's backward in one pass (conv_wino.hip
