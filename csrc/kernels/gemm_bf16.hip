@@ -312,8 +312,17 @@ int64_t gemm_bf16_part_floats(int M, int N, int K, int ones_row, int splits) {
 int gemm_bf16_splits(int M, int N, int K, int ones_row) {
   const int tiles = ((M + ones_row + BM - 1) / BM) * ((N + BN - 1) / BN);
   int s = 1;
-  // enough workgroups to fill 256 CUs twice over, each K chunk >= 256
-  while (tiles * s < 512 && K / (2 * s) >= 256 && s < 16) s *= 2;
+  // enough workgroups to fill 256 CUs twice over (SA_GEMM16_WG_TARGET), each
+  // K chunk >= 256 (SA_GEMM16_MIN_K)
+  static const int target = [] {
+    const char* e = std::getenv("SA_GEMM16_WG_TARGET");
+    return e ? std::max(1, std::atoi(e)) : 512;
+  }();
+  static const int min_k = [] {
+    const char* e = std::getenv("SA_GEMM16_MIN_K");
+    return e ? std::max(32, std::atoi(e)) : 256;
+  }();
+  while (tiles * s < target && K / (2 * s) >= min_k && s < 16) s *= 2;
   return s;
 }
 
