@@ -185,11 +185,11 @@ from scalable_agent_amd.learner import FlatStaging, Learner  # noqa
 from scalable_agent_amd.models import Agent  # noqa: E402
 from scalable_agent_amd.models.agent import torso_precision  # noqa: E402
 from scalable_agent_amd import parallel  # noqa: E402
+from scalable_agent_amd.utils.knobs import measure_env, set_knobs  # noqa: E402
 
 METRIC = ('learner env-frames/sec, IMPALA deep-ResNet+LSTM, batch=32 '
           'unroll=100, 1/2/4/8 GPU')
 BASELINE_FPS = 250000.0  # BASELINE.md §B best published single-learner figure
-_COPY_STREAMS = {}  # device -> the process's H2D prefetch stream
 
 
 def measure(args, dtype, device, backend, rank, world):
@@ -236,9 +236,7 @@ def measure(args, dtype, device, backend, rank, world):
     # GPU_MAX_HW_QUEUES = 4), and the 67 MB prefetch then serialises with
     # the step (the bf16 field measured 5.8 ms = 4.6 ms of kernels + the
     # 1.2 ms copy, against 4.6 ms when it ran first)
-    copy_stream = _COPY_STREAMS.get(device)
-    if copy_stream is None:
-      copy_stream = _COPY_STREAMS[device] = torch.cuda.Stream(device)
+    copy_stream = parallel.stream_plan(device).copy
     # one flat pinned host buffer per batch and one flat device buffer per
     # staging slot: the per-step prefetch is ONE H2D copy
     host_flat = [FlatStaging(hb, 'cpu', pin=True).load(hb)
@@ -273,7 +271,7 @@ def measure(args, dtype, device, backend, rank, world):
     h2d_mb = dev_flat[1].nbytes / 1e6
   # diagnostic only (never the reported benchmark): SA_BENCH_SKIP_H2D=1 drops
   # the per-step host->device prefetch of the next batch
-  skip_h2d = os.environ.get('SA_BENCH_SKIP_H2D') == '1'
+  skip_h2d = measure_env('SA_BENCH_SKIP_H2D') == '1'
   # who orders the prefetch against the steps.  'host' (default): the host
   # waits for slot j's previous step before enqueuing the copy into it and for
   # the copy before launching the step that reads it, so neither stream holds
@@ -283,7 +281,7 @@ def measure(args, dtype, device, backend, rank, world):
   # 9.13 with no copy at all); host-side 9.15 (bf16: 4.63 / 4.41 / 4.44).
   # The host stays a step ahead: it is released ~1.2 ms into step k (copy
   # done) and enqueues step k+1 in 2-4 ms
-  host_sync = os.environ.get('SA_BENCH_PREFETCH_SYNC', 'host') != 'device'
+  host_sync = measure_env('SA_BENCH_PREFETCH_SYNC', 'host') != 'device'
 
   def run_step(k):
     i = k % 2
@@ -434,8 +432,12 @@ def main():
     device = torch.device(args.device)
   if device.type == 'cuda':
     torch.cuda.set_device(device)
-    # the H2D prefetch stream is the process's first stream (see measure)
-    _COPY_STREAMS.setdefault(device, torch.cuda.Stream(device))
+    # the process's streams in their fixed order (parallel/streams.py: the
+    # H2D prefetch stream first, then the capture and early-all-reduce
+    # streams), then one collective so the communicator is up and working
+    # before the first measured step
+    parallel.stream_plan(device)
+    parallel.warmup_collective(device)
 
   backend = args.backend
   if backend == 'auto':
@@ -476,6 +478,10 @@ def main():
            'h2d_prefetch_sync': main_res['h2d_prefetch_sync'],
            'h2d_slab': main_res['h2d_slab'],
            'dist': dict(dist_info, **main_res['dist_extra']),
+           # every SA_* variable this run was started with (experiment
+           # switches only act in SA_MEASURE_KNOBS runs / builds:
+           # csrc/kernels/knobs.h, utils/knobs.py)
+           'knobs': set_knobs(),
            'baseline_ref': 'IMPALA paper best 1-GPU learner 250K '
                            'frames/s (BASELINE.md B), fp32 P100',
            # the ratio sets this learner-only synthetic number against the

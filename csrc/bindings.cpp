@@ -9,8 +9,10 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "kernels/launchers.h"
+#include "kernels/knobs.h"
 #include "kernels/conv_launchers.h"
 
 namespace {
@@ -121,10 +123,7 @@ std::vector<at::Tensor> vtrace_loss(at::Tensor behaviour, at::Tensor target,
 // B=32) the granule all-gather of h / dG costs 9 / 27.6 us per step against
 // 4.4 / 6.9 us for the graph-replayed per-step kernels, whose operand loads
 // ride the normal L2/MALL path.
-bool g_lstm_persistent = [] {
-  const char* e = std::getenv("SA_LSTM_PERSISTENT");
-  return e && e[0] == '1';
-}();
+bool g_lstm_persistent = sa::measure_knob("SA_LSTM_PERSISTENT", 0) == 1;
 
 bool use_persistent(int H, int B) { return g_lstm_persistent && H == 256 && B <= 32; }
 
@@ -133,10 +132,7 @@ bool use_persistent(int H, int B) { return g_lstm_persistent && H == 256 && B <=
 // selects the exact-fp32 per-step kernels); they take precedence over the
 // fp32 persistent kernels.  Measured at T=101, B=32 (tools/micro/
 // lstm_probe.py): fwd 446 vs 446-460 us, bwd 448 vs 724 us per unroll.
-bool g_lstm_gang = [] {
-  const char* e = std::getenv("SA_LSTM_GANG");
-  return !(e && e[0] == '0');
-}();
+bool g_lstm_gang = sa::env_knob("SA_LSTM_GANG", 1) != 0;
 
 // T == 1 (actor inference steps) stays on the per-step kernels: one step
 // gains nothing from the gang and the inference graphs keep their layout.
@@ -316,6 +312,30 @@ void lstm_set_gang(bool on) { g_lstm_gang = on; }
 bool lstm_get_gang() { return g_lstm_gang; }
 at::Tensor lstm_error(at::Tensor like) { return lstm_err_word(like.device()); }
 
+// A HIP stream on a hardware queue of its own (parallel/streams.py).  HIP
+// hands a plain new stream the least-used of its GPU_MAX_HW_QUEUES (4)
+// queues, so it can share the compute stream's queue and be serialised
+// behind it (profiles/r6_dp_queues.txt: the early all-reduce stream did);
+// a stream with a CU mask always gets a new queue.  The mask enables every
+// CU of the device.  Returns the hipStream_t as an integer for
+// torch.cuda.ExternalStream; the stream lives as long as the process.
+int64_t own_queue_stream(int64_t device) {
+  int prev = 0;
+  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice");
+  TORCH_CHECK(hipSetDevice(static_cast<int>(device)) == hipSuccess, "hipSetDevice");
+  hipDeviceProp_t prop;
+  TORCH_CHECK(hipGetDeviceProperties(&prop, static_cast<int>(device)) == hipSuccess,
+              "hipGetDeviceProperties");
+  const int words = (prop.multiProcessorCount + 31) / 32;
+  std::vector<uint32_t> mask(static_cast<size_t>(words), 0xFFFFFFFFu);
+  if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), mask.data());
+  (void)hipSetDevice(prev);
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(s);
+}
+
 void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
   sa::noop_launch(blocks, threads, counter.data_ptr<int>(), cur_stream());
 }
@@ -364,6 +384,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_error_word", &lstm_error);
   m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);
+  m.def("own_queue_stream", &own_queue_stream);
   register_conv_ops(m);
   register_learner_ops(m);
   register_conv_f32_ops(m);

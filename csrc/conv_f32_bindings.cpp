@@ -11,6 +11,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include "kernels/conv_f32.h"
+#include "kernels/knobs.h"
 
 namespace {
 
@@ -126,10 +127,7 @@ sa::cf32::PoolGeom pool_geom(const c10::optional<at::Tensor>& arg, const at::Ten
 // launches (measured equal: shallow2 391 vs 361-381 us, shallow3 611 vs
 // 584-618 us - the per-tile work stays one tiny image either way)
 bool phase_stacked() {
-  static const bool on = [] {
-    const char* e = std::getenv("SA_F32_DGRAD_STACK");
-    return e && e[0] == '1';
-  }();
+  static const bool on = sa::env_knob("SA_F32_DGRAD_STACK", 0) == 1;
   return on;
 }
 
@@ -145,10 +143,7 @@ at::Tensor conv_dgrad(at::Tensor dy, at::Tensor w, int64_t stride, int64_t pt, i
   const c10::DeviceGuard g(dy.device());
   auto dx = at::empty({dy.size(0), H, W, Cin}, dy.options());
   check_size(dx, "dx");
-  static const bool phase = [] {
-    const char* e = std::getenv("SA_F32_DGRAD_PHASE");
-    return !(e && e[0] == '0');
-  }();
+  static const bool phase = sa::env_knob("SA_F32_DGRAD_PHASE", 1) != 0;
   if (stride > 1 && !(pool_arg.has_value() && pool_arg->defined()) && phase) {
     // Phase decomposition: dX rows i = S q + r - pt get the taps k = r + S j
     // only, so each of the S x S output phases is a stride-1 correlation of

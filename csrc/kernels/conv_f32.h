@@ -102,6 +102,8 @@ int wgrad_flush(hipStream_t s);  // -> number of reductions launched
 // Fault injection (tests): 1 = every bounded intra-workgroup hand-off wait of
 // the fused Winograd backward reports a timeout.  Returns the old setting.
 int conv_wino_fault(int v);
+// Compile-time-geometry Winograd instances on (1) / off (0); returns the old
+// setting (tests compare both forms bitwise).
 int conv_wino_geo(int v);
 // CUs the persistent conv grids are sized for: 256 - 8 R, where R CUs per
 // XCD are left to a concurrently running stream (the time-chunked LSTM
@@ -109,7 +111,8 @@ int conv_wino_geo(int v);
 // previous value; the default comes from SA_CU_RESERVE (0).  Launch-time
 // state: a captured graph keeps the grids it was captured with.
 int conv_cu_reserve(int r);
-int conv_cus();  // compile-time-geometry instances on (1) / off (0); returns old
+// CUs the persistent grids are sized for now: 256 - 8 * conv_cu_reserve(-1).
+int conv_cus();
 bool wino_conv_launch(const ConvArgs& a, bool flip, hipStream_t s);
 // Stage head with the 3x3/2 SAME max-pool fused (conv_wino.hip): x [N,H,W,Cin]
 // -> pooled [N,H/2,W/2,Cout] + argmax codes, the 3x3/1 conv + bias in

@@ -23,6 +23,7 @@
 // its partial sums, and one reduce kernel sums the partials in slot order:
 // bitwise reproducible run to run (no float atomics).
 #include "conv_f32.h"
+#include "knobs.h"
 
 #include <vector>
 
@@ -41,8 +42,7 @@ int g_cu_reserve = -1;  // -1: not read yet (SA_CU_RESERVE)
 
 int conv_cu_reserve(int r) {
   if (g_cu_reserve < 0) {
-    const char* e = std::getenv("SA_CU_RESERVE");
-    const int v = (e && *e) ? std::atoi(e) : 0;
+    const int v = sa::measure_knob("SA_CU_RESERVE", 0);
     g_cu_reserve = v < 0 ? 0 : (v > 16 ? 16 : v);
   }
   const int old = g_cu_reserve;
@@ -61,14 +61,10 @@ constexpr int kThreads = 256;
 constexpr size_t kLdsSoft = 80 * 1024;   // two workgroups per CU
 constexpr size_t kLdsHard = 156 * 1024;  // one workgroup per CU
 
-// Launch-shape knobs read once from the environment (measurement sweeps;
-// the defaults are the tuned values): resident workgroups per CU targeted by
-// the persistent forward / stage-head grids (capped by LDS), and the maximum
+// Launch-shape knobs (knobs.h measure_knob: measurement builds only; the
+// defaults are the tuned values): resident workgroups per CU targeted by the
+// persistent forward / stage-head grids (capped by LDS), and the maximum
 // number of weight-gradient slots.
-int env_knob(const char* name, int def) {
-  const char* e = std::getenv(name);
-  return (e && *e) ? std::atoi(e) : def;
-}
 int occupancy(size_t lds_bytes, int cap) {
   const int fit = static_cast<int>((160 * 1024) / (lds_bytes + 512));
   return std::max(1, std::min(cap, fit));
@@ -1522,7 +1518,7 @@ bool run_conv(const ConvArgs& a, hipStream_t s) {
   const int gy = a.Cout / COUT_T;
   // 16-in/16-out layers gain from a third resident workgroup per CU (res16
   // fwd/dgrad 313 -> 284-292 us); 16->32 loses (518 -> 659 us)
-  static const int occ_env = env_knob("SA_F32_FWD_OCC", 0);
+  static const int occ_env = sa::measure_knob("SA_F32_FWD_OCC", 0);
   const int occ_cap = occ_env ? occ_env : (CINP <= 16 && COUT_T <= 16 ? 3 : 2);
   const int per_cu = occupancy(bytes(R), occ_cap);
   const int G = std::max(1, std::min(ntiles, conv_cus() * per_cu / gy));
@@ -1545,7 +1541,7 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
   const size_t budget = bytes(2) <= kLdsSoft ? kLdsSoft : kLdsHard;
   // pooled rows per tile cap: 2 for the 4-channel stage head (51.7 KB of LDS,
   // three workgroups per CU: 16.57 -> 16.46 ms/step against 3 rows, two)
-  static const int rcap = env_knob("SA_F32_POOL_R", CINP == 4 ? 2 : 1 << 20);
+  static const int rcap = sa::measure_knob("SA_F32_POOL_R", CINP == 4 ? 2 : 1 << 20);
   int R = 0;
   for (int r = 1; r <= std::min(Hp, rcap); ++r) {
     if (bytes(r) > budget || (2 * r + 3) * Wl * (CINP / 4) > kMaxC * kThreads) break;
@@ -1555,7 +1551,7 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
   const int nt = (Hp + R - 1) / R;
   R = (Hp + nt - 1) / nt;
   const int ntiles = a.N * nt;
-  static const int occ_cap = env_knob("SA_F32_POOL_OCC", 3);
+  static const int occ_cap = sa::measure_knob("SA_F32_POOL_OCC", 3);
   const int per_cu = occupancy(bytes(R), occ_cap);
   const int G = std::max(1, std::min(ntiles, conv_cus() * per_cu));
   auto kern = conv_pool_fwd_kernel<CINP, COUT, SRC>;
@@ -1567,7 +1563,7 @@ bool run_conv_pool(const ConvArgs& a, int pbh, int pbw, float* pooled, uint8_t* 
 
 // output-channel tile: 32 when the weight slice stays small, else 16
 int cout_tile(int cinp, int cout, int K) {
-  static const int force = env_knob("SA_F32_COUT_T", 0);  // sweeps: 16 forces 16
+  static const int force = sa::measure_knob("SA_F32_COUT_T", 0);  // sweeps: 16 forces 16
   if (force == 16) return 16;
   if (cout % 32 == 0 && 4ll * K * K * 32 * cinp <= 48 * 1024) return 32;
   return 16;
@@ -1640,7 +1636,7 @@ int wgrad_flush(hipStream_t s) {
 }
 
 static bool pool_scatter_on() {
-  static const bool on = env_knob("SA_F32_POOL_SCATTER", 1) != 0;
+  static const bool on = sa::env_knob("SA_F32_POOL_SCATTER", 1) != 0;
   return on;
 }
 static bool pool_scatter_shape(int K, int S, int cinp, int cout) {
@@ -1654,7 +1650,7 @@ constexpr int kPwSlots = 1280;
 // Workgroup slots of a wgrad launch: the partials stay <= 8M floats, with at
 // least 128 slots (before the tile-count cap) so the reduction fills the GPU.
 int64_t wgrad_slots(int K, int cinp, int cout) {
-  static const int cap = env_knob("SA_F32_WG_SLOTS", 512);
+  static const int cap = sa::measure_knob("SA_F32_WG_SLOTS", 512);
   const int64_t rows = ((K * K * cinp + 16) / 16) * 16;
   return std::max<int64_t>(128, std::min<int64_t>(cap, (8ll << 20) / (rows * cout)));
 }
@@ -1718,7 +1714,7 @@ static bool run_pool_wgrad(const WgradArgs& a, float* ws, int u8_cs, hipStream_t
     return false;
   const int tpi = (pg.Hp + kPwRows - 1) / kPwRows;
   const int ntiles = a.N * tpi;
-  static const int slots = std::max(1, std::min(kPwSlots, env_knob("SA_F32_PW_SLOTS", kPwSlots)));
+  static const int slots = std::max(1, std::min(kPwSlots, sa::measure_knob("SA_F32_PW_SLOTS", kPwSlots)));
   const int G = std::min(ntiles, slots);
   size_t lds = std::max<size_t>(sizeof(float) * 4 * (2 * kPwRows + 3) * pw_pitch(a.W),
                                 sizeof(float) * 4 * 37 * 16);
@@ -1805,7 +1801,7 @@ bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, i
                         int C, int Hp, int Wp, int pb_h, int pb_w, hipStream_t s) {
   const int sh = c4_shift_of(C);
   if (sh < 0) return false;
-  static const bool blk = env_knob("SA_F32_POOL_BWD_BLK", 1) != 0;
+  static const bool blk = sa::env_knob("SA_F32_POOL_BWD_BLK", 1) != 0;
   if (blk && pb_h == 0 && pb_w == 0 && H == 2 * Hp && W == 2 * Wp) {
     const int64_t total = static_cast<int64_t>(N) * Hp * (static_cast<int64_t>(Wp) << sh);
     if (total < (int64_t{1} << 31)) {
@@ -1821,7 +1817,7 @@ bool maxpool_bwd_launch(const float* dy, const uint8_t* arg, float* dx, int N, i
 }
 
 void frames_f32_launch(const uint8_t* x, float* y, int64_t P, int Cs, hipStream_t s) {
-  static const bool tiled = env_knob("SA_FRAMES_TILE", 1) != 0;  // 0: one pixel per thread
+  static const bool tiled = sa::env_knob("SA_FRAMES_TILE", 1) != 0;  // 0: one pixel per thread
   if (tiled && (reinterpret_cast<uintptr_t>(x) & 3) == 0 && Cs >= 1 && Cs <= 4) {
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((P + 1023) / 1024, 8192));
     hipLaunchKernelGGL(frames_f32_tile_kernel, dim3(blocks), dim3(256), 0, s, x,

@@ -32,6 +32,7 @@
 // group, output-channel slice) tasks.  Every range but the batch's last is
 // full, so the waves stay balanced for any image size.
 #include "conv_f32.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -76,41 +77,13 @@ __device__ __forceinline__ f4 bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
 }
 constexpr int64_t kMaxBufBytes = 0xFFFFFF00ll;
 
-// Packed-fp32 transform arithmetic (experiment builds, SA_WINO_PK=1): the
-// Winograd input / output transforms as v_pk_add_f32 pairs (2 lanes of a
-// float4 per instruction) instead of 4 scalar v_add/v_sub_f32.  The backend
-// does not select v_pk_add_f32 for <2 x float> arithmetic here (it stays
-// scalar), so the packed form needs inline asm - and the compiler inserts no
-// wait states inside asm: the output transform then reads MFMA accumulators
-// before the MFMAs have written them (the 32-channel forward computed wrong
-// outputs, profiles/experiments.md round 4).  Default 0: scalar everywhere.
-#ifndef SA_WINO_PK
-#define SA_WINO_PK 0
-#endif
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 lo2(f4 a) { return __builtin_shufflevector(a, a, 0, 1); }
-__device__ __forceinline__ f2 hi2(f4 a) { return __builtin_shufflevector(a, a, 2, 3); }
-__device__ __forceinline__ f4 cat2(f2 a, f2 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3); }
-__device__ __forceinline__ f2 pk_add2(f2 a, f2 b) {
-  f2 r;
-  asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ f2 pk_sub2(f2 a, f2 b) {
-  f2 r;
-  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-template <bool PK = SA_WINO_PK == 1>
-__device__ __forceinline__ f4 tadd(f4 a, f4 b) {
-  if constexpr (PK) return cat2(pk_add2(lo2(a), lo2(b)), pk_add2(hi2(a), hi2(b)));
-  else return a + b;
-}
-template <bool PK = SA_WINO_PK == 1>
-__device__ __forceinline__ f4 tsub(f4 a, f4 b) {
-  if constexpr (PK) return cat2(pk_sub2(lo2(a), lo2(b)), pk_sub2(hi2(a), hi2(b)));
-  else return a - b;
-}
+// Winograd transform add / subtract on float4 channel quads.  (A packed
+// v_pk_add_f32 form was measured in round 4 and removed: the backend keeps
+// <2 x float> arithmetic scalar, an inline-asm form read MFMA accumulators
+// without the required wait states, and packed f32 beside MFMAs is an
+// anti-lever on gfx950.)
+__device__ __forceinline__ f4 tadd(f4 a, f4 b) { return a + b; }
+__device__ __forceinline__ f4 tsub(f4 a, f4 b) { return a - b; }
 
 // ReLU as one integer max on the bit pattern (negative floats, -0 and
 // negative NaNs have the sign bit set: signed-int max with 0 gives +0);
@@ -345,7 +318,6 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   constexpr int NTH = 64 * NW;
   const TileGeo<GH, GW, RT, wino_lpad_on(0)> G(a.H, a.W, a.TY, a.TX, a.NT, a.rTX, a.rTY,
                                                 a.maxrows);
-  constexpr bool kPk = SA_WINO_PK == 1;
   const bool f_relu_in = FL < 0 ? a.relu_in != 0 : (FL & 1) != 0;
   const bool f_relu_out = FL < 0 ? a.relu_out != 0 : (FL & 2) != 0;
   const bool f_mask = FL < 0 ? a.mask != nullptr : (FL & 4) != 0;
@@ -543,18 +515,18 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 s[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          s[q] = tsub<kPk>(d[q], d[8 + q]);
-          s[4 + q] = tadd<kPk>(d[4 + q], d[8 + q]);
-          s[8 + q] = tsub<kPk>(d[8 + q], d[4 + q]);
-          s[12 + q] = tsub<kPk>(d[4 + q], d[12 + q]);
+          s[q] = tsub(d[q], d[8 + q]);
+          s[4 + q] = tadd(d[4 + q], d[8 + q]);
+          s[8 + q] = tsub(d[8 + q], d[4 + q]);
+          s[12 + q] = tsub(d[4 + q], d[12 + q]);
         }
         f4 V[16];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          V[4 * ra + 0] = tsub<kPk>(s[4 * ra + 0], s[4 * ra + 2]);
-          V[4 * ra + 1] = tadd<kPk>(s[4 * ra + 1], s[4 * ra + 2]);
-          V[4 * ra + 2] = tsub<kPk>(s[4 * ra + 2], s[4 * ra + 1]);
-          V[4 * ra + 3] = tsub<kPk>(s[4 * ra + 1], s[4 * ra + 3]);
+          V[4 * ra + 0] = tsub(s[4 * ra + 0], s[4 * ra + 2]);
+          V[4 * ra + 1] = tadd(s[4 * ra + 1], s[4 * ra + 2]);
+          V[4 * ra + 2] = tsub(s[4 * ra + 2], s[4 * ra + 1]);
+          V[4 * ra + 3] = tsub(s[4 * ra + 1], s[4 * ra + 3]);
         }
         // 16 xi x 4 k-steps x NH slices; two xi chains interleaved (the
         // 16x16x4 f32 MFMA's dependent latency is 40 cycles, issue 32)
@@ -588,14 +560,14 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
         f4 tt[4][2];
 #pragma unroll
         for (int ra = 0; ra < 4; ++ra) {
-          tt[ra][0] = tadd<kPk>(tadd<kPk>(acc[h][4 * ra], acc[h][4 * ra + 1]), acc[h][4 * ra + 2]);
-          tt[ra][1] = tsub<kPk>(tsub<kPk>(acc[h][4 * ra + 1], acc[h][4 * ra + 2]), acc[h][4 * ra + 3]);
+          tt[ra][0] = tadd(tadd(acc[h][4 * ra], acc[h][4 * ra + 1]), acc[h][4 * ra + 2]);
+          tt[ra][1] = tsub(tsub(acc[h][4 * ra + 1], acc[h][4 * ra + 2]), acc[h][4 * ra + 3]);
         }
         f4 Y[4];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          Y[c] = tadd<kPk>(tadd<kPk>(tt[0][c], tt[1][c]), tt[2][c]);
-          Y[2 + c] = tsub<kPk>(tsub<kPk>(tt[1][c], tt[2][c]), tt[3][c]);
+          Y[c] = tadd(tadd(tt[0][c], tt[1][c]), tt[2][c]);
+          Y[2 + c] = tsub(tsub(tt[1][c], tt[2][c]), tt[3][c]);
         }
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy)
@@ -631,10 +603,6 @@ void allow_lds_w(Kern k, size_t bytes) {
   }
 }
 
-int env_int(const char* name, int def) {
-  const char* e = std::getenv(name);
-  return (e && *e) ? std::atoi(e) : def;
-}
 
 int g_wino_fault = 0;  // conv_wino_fault(): tests of the fail-loud hand-off
 
@@ -677,14 +645,14 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
   a.wcin = c.wcin; a.wcout = c.wcout; a.flip = flip ? 1 : 0;
   a.relu_in = c.relu_in; a.relu_out = c.relu_out;
   a.maxrows = maxrows;
-  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_WINO_ABLATE", 0) : 0;
+  static const int ablate = measure_knob("SA_WINO_ABLATE", 0);
   a.ablate = ablate;
-  static const int runs = env_int("SA_WINO_RUNS", 1);
+  static const int runs = measure_knob("SA_WINO_RUNS", 1);
   a.runs = runs;
-  static const int prio = env_int("SA_WINO_PRIO", 0);
+  static const int prio = measure_knob("SA_WINO_PRIO", 0);
   a.prio = prio;
   const int per_cu = std::max(1, std::min(WPS * 4 / NW, static_cast<int>((160 * 1024) / (bytes + 256))));
-  static const int occ_env = env_int("SA_WINO_OCC", 0);
+  static const int occ_env = measure_knob("SA_WINO_OCC", 0);
   const int occ = occ_env > 0 ? std::min(occ_env, per_cu) : per_cu;
   const int G = std::max(1, std::min(a.nranges, conv_cus() * occ));
   auto kern = wino_conv_kernel<CIN, COUT, NH, NW, RT, MAXC, WPS, FL, GH, GW>;
@@ -697,13 +665,13 @@ bool run_wino_g(const ConvArgs& c, bool flip, hipStream_t s) {
 // SA_WINO_GEO=0 keeps every map on the runtime-geometry instances.
 int g_wino_geo = -1;  // -1: not read yet; conv_wino_geo() sets it (tests)
 bool wino_geo_enabled() {
-  if (g_wino_geo < 0) g_wino_geo = env_int("SA_WINO_GEO", 1) != 0 ? 1 : 0;
+  if (g_wino_geo < 0) g_wino_geo = env_knob("SA_WINO_GEO", 1) != 0 ? 1 : 0;
   return g_wino_geo != 0;
 }
 // per kernel family (SA_WINO_GEO_MASK, sweeps): bit 0 the forward, bit 1 the
 // 16-channel fused backward, bit 2 the fused32 backward
 bool wino_geo_family(int bit) {
-  static const int mask = env_int("SA_WINO_GEO_MASK", 7);
+  static const int mask = measure_knob("SA_WINO_GEO_MASK", 7);
   return wino_geo_enabled() && (mask & bit) != 0;
 }
 
@@ -757,7 +725,7 @@ bool run_wino_fl(const ConvArgs& c, bool flip, hipStream_t s) {
   // fp32 step 9.546 / 9.547 -> 9.502 / 9.460 ms (geometry alone; one box)
   // 4 (default) adds the 32 -> 32 residual convs at 18x24: 9.474 / 9.449 /
   // 9.446 (3) -> 9.466 / 9.434 / 9.429 ms
-  static const int on = env_int("SA_WINO_FL", 4);
+  static const int on = measure_knob("SA_WINO_FL", 4);
   if constexpr (CIN == 16 && COUT == 16) {
     if (on >= 3 && !flip && wino_geo_enabled()) {
       const int HH = c.Ho, WW = c.Wo;
@@ -1286,11 +1254,11 @@ bool run_wino_pool(const float* x, const float* w, const float* b, float* pooled
   a.wcin = CIN; a.wcout = COUT;
   a.maxrows = P::ROWS;
   a.runs = 1;
-  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_WINO_ABLATE", 0) : 0;
+  static const int ablate = measure_knob("SA_WINO_ABLATE", 0);
   a.ablate = ablate;  // 1 no MFMA tasks, 16 no pool phase, 32 no image writes
   // workgroups per CU: LDS-bound, capped at 3 waves per SIMD unless
   // SA_WINO_POOL_OCC asks for another count (sweeps)
-  static const int occ = env_int("SA_WINO_POOL_OCC", 0);
+  static const int occ = measure_knob("SA_WINO_POOL_OCC", 0);
   const int lds_cu = static_cast<int>((160 * 1024) / (P::bytes + 256));
   const int per_cu = std::max(1, std::min(occ > 0 ? occ : 3 * 4 / P::NW, lds_cu));
   const int G = std::max(1, std::min(a.nranges, conv_cus() * per_cu));
@@ -2884,11 +2852,11 @@ bool run_wino_bwd32_g(const float* dy, const float* w, const float* x, const flo
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
   a.mask_x = mask_x;
-  static const int ablate = SA_MEASURE_KNOBS ? env_int("SA_FUSED_ABLATE", 0) : 0;
+  static const int ablate = measure_knob("SA_FUSED_ABLATE", 0);
   a.ablate = ablate;
   a.err = device_error_words() + 1;
   a.fault = g_wino_fault;
-  static const int fprio = env_int("SA_FUSED_PRIO", 0);
+  static const int fprio = measure_knob("SA_FUSED_PRIO", 0);
   a.prio = fprio;
   auto kern = wino_bwd_fused32_kernel<CX, CY, RT, MAXCX, MAXCY, RELU, MASK, GH, GW>;
   allow_lds_w(kern, bytes);
@@ -2967,9 +2935,9 @@ bool run_wino_bwd_g(const float* dy, const float* w, const float* x, const float
   a.rTX = 1.f / static_cast<float>(TX);
   a.rTY = 1.f / static_cast<float>(TY);
   a.relu_x = relu_x;
-  static const int runs = env_int("SA_WINO_RUNS", 1);
+  static const int runs = measure_knob("SA_WINO_RUNS", 1);
   a.runs = runs;
-  static const int fprio = env_int("SA_FUSED_PRIO", 0);
+  static const int fprio = measure_knob("SA_FUSED_PRIO", 0);
   a.prio = fprio;
   auto kern = relu_x ? wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, true, NW, GH, GW>
                      : wino_bwd_fused_kernel<C, RT, MAXC, KD, WWG, false, NW, GH, GW>;
@@ -3012,7 +2980,7 @@ int conv_wino_geo(int v) {
 }
 
 bool wino_enabled() {
-  static const bool on = env_int("SA_F32_WINO", 1) != 0;
+  static const bool on = env_knob("SA_F32_WINO", 1) != 0;
   return on;
 }
 
@@ -3027,7 +2995,7 @@ bool wino_conv_pool_launch(const float* x, const float* w, const float* b, float
   // conv+pool, 10.02 -> 9.93 ms per step), bit 2: stage 2 (whole-image
   // ranges: 9.93 -> 9.90 ms), bit 3: the 42-wide stage-1 head (opt-in);
   // stages >= 0 overrides the environment (tests)
-  static const int env_on = env_int("SA_F32_WINO_POOL", 7);
+  static const int env_on = env_knob("SA_F32_WINO_POOL", 7);
   const int on = stages >= 0 ? stages : env_on;
   if (Cin == 16 && Cout == 32 && (on & 1)) {
     if (W == 48) return run_wino_pool<16, 32, 48>(x, w, b, pooled, arg, side, side_floats, N, H, W, s);
@@ -3060,14 +3028,14 @@ bool wino_conv_launch(const ConvArgs& c, bool flip, hipStream_t s) {
     return false;
   const int cin = c.Cs, cout = c.Cout;
   // SA_WINO_CFG: alternative instances for measurement sweeps
-  static const int cfg = env_int("SA_WINO_CFG", 0);
+  static const int cfg = measure_knob("SA_WINO_CFG", 0);
   if (cin == 16 && cout == 16) {
     // 3-wave workgroups over 48-tile ranges: at 36x48 every range is two
     // whole tile rows of one image (6 staged rows, 40 KB of LDS), so four
     // workgroups (three waves per SIMD) fit on a CU
     // SA_WINO_CFG=3: 8 waves over 128-tile ranges (one workgroup per CU)
     if (cfg == 3 && run_wino<16, 16, 1, 8, 128, 7, 2>(c, flip, s)) return true;
-    static const int w3 = env_int("SA_WINO16_3W", 0);
+    static const int w3 = measure_knob("SA_WINO16_3W", 0);
     if (w3 && !flip) {
       const int fl = (c.relu_in ? 1 : 0) | (c.relu_out ? 2 : 0) | (c.mask ? 4 : 0) |
                      (c.add ? 8 : 0) | (c.bias ? 16 : 0);
@@ -3098,7 +3066,7 @@ namespace sa {
 namespace cf32 {
 
 bool wino_wgrad_enabled() {
-  static const bool on = env_int("SA_F32_WINO_WG", 1) != 0;
+  static const bool on = measure_knob("SA_F32_WINO_WG", 1) != 0;
   return on;
 }
 
@@ -3109,7 +3077,7 @@ bool wino_wgrad_launch(const WgradArgs& c, float* ws, hipStream_t s) {
   // 16-channel inputs measured slower than the direct MFMA wgrad (res16
   // 449 vs 369-387 us, the stage-1 head 720 vs 623-631 us: one workgroup of
   // four waves per CU, VALU-heavy per MFMA); opt-in for sweeps
-  static const int all = env_int("SA_WINO_WG_ALL", 0);
+  static const int all = measure_knob("SA_WINO_WG_ALL", 0);
   if (all && cin == 16 && cout == 16) return run_wino_wgrad<16, 16, 4, 64, 10, 9>(c, ws, s);
   if (all && cin == 16 && cout == 32) return run_wino_wgrad<16, 32, 2, 64, 10, 19>(c, ws, s);
   if (cin == 32 && cout == 32) return run_wino_wgrad<32, 32, 1, 64, 15, 14>(c, ws, s);
@@ -3123,7 +3091,7 @@ namespace sa {
 namespace cf32 {
 
 bool wino_bwd_fused_enabled() {
-  static const bool on = env_int("SA_F32_FUSED_BWD", 1) != 0;
+  static const bool on = env_knob("SA_F32_FUSED_BWD", 1) != 0;
   return on;
 }
 
@@ -3131,9 +3099,9 @@ bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, cons
                            float* out, int relu_x, int mask_x, int N, int H, int W, int C,
                            int Cy, float* ws, int64_t ws_floats, float* dw, float* db,
                            hipStream_t s) {
-  static const int kd = env_int("SA_FUSED_BWD_KD", 4);
-  static const int wwg = env_int("SA_FUSED_BWD_WWG", 1);
-  static const int v2 = env_int("SA_FUSED16_V2", 0);
+  static const int kd = measure_knob("SA_FUSED_BWD_KD", 4);
+  static const int wwg = measure_knob("SA_FUSED_BWD_WWG", 1);
+  static const int v2 = measure_knob("SA_FUSED16_V2", 0);
   if (C == 16 && Cy == 16 && (v2 || !mask_x))
     return run_wino_bwd32<16, 16, 64, 5, 5>(dy, w, x, add, out, relu_x, mask_x, N, H, W, ws,
                                             ws_floats, dw, db, s);
@@ -3144,7 +3112,7 @@ bool wino_bwd_fused_launch(const float* dy, const float* w, const float* x, cons
     if (kd == 8) return run_wino_bwd<16, 64, 5, 8>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
     return run_wino_bwd<16, 64, 5, 4>(dy, w, x, add, out, relu_x, N, H, W, ws, ws_floats, dw, db, s);
   }
-  static const int f32c = env_int("SA_FUSED_BWD32", 1);
+  static const int f32c = measure_knob("SA_FUSED_BWD32", 1);
   if (!f32c) return false;
   if (C == 32 && Cy == 32)
     return run_wino_bwd32<32, 32, 32, 5, 5>(dy, w, x, add, out, relu_x, mask_x, N, H, W, ws,

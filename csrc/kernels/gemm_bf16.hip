@@ -25,6 +25,7 @@
 // over grid.z into fp32 partial slabs that one kernel sums in split order:
 // deterministic, no float atomics.
 #include "gemm_bf16.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -314,14 +315,8 @@ int gemm_bf16_splits(int M, int N, int K, int ones_row) {
   int s = 1;
   // enough workgroups to fill 256 CUs twice over (SA_GEMM16_WG_TARGET), each
   // K chunk >= 256 (SA_GEMM16_MIN_K)
-  static const int target = [] {
-    const char* e = std::getenv("SA_GEMM16_WG_TARGET");
-    return e ? std::max(1, std::atoi(e)) : 512;
-  }();
-  static const int min_k = [] {
-    const char* e = std::getenv("SA_GEMM16_MIN_K");
-    return e ? std::max(32, std::atoi(e)) : 256;
-  }();
+  static const int target = std::max(1, sa::measure_knob("SA_GEMM16_WG_TARGET", 512));
+  static const int min_k = std::max(32, sa::measure_knob("SA_GEMM16_MIN_K", 256));
   while (tiles * s < target && K / (2 * s) >= min_k && s < 16) s *= 2;
   return s;
 }
@@ -349,10 +344,7 @@ bool gemm_bf16_launch(const uint16_t* A, const uint16_t* B, int M, int N, int K,
   // layout-specialised kernels; the branch-free buffer-load form needs whole
   // 8-element chunks along the M / N-contiguous operands and 32-bit offsets
   // (SA_GEMM_BL=0: bounds-checked loads)
-  static const int blenv = [] {
-    const char* e = std::getenv("SA_GEMM_BL");
-    return e ? std::atoi(e) : 1;
-  }();
+  static const int blenv = sa::env_knob("SA_GEMM_BL", 1);
   const int64_t abytes = (ta ? static_cast<int64_t>(K) * lda : static_cast<int64_t>(M) * lda) * 2;
   const int64_t bbytes = (tb ? static_cast<int64_t>(N) * ldb : static_cast<int64_t>(K) * ldb) * 2;
   const bool bl = blenv && (!ta || M % 8 == 0) && (tb || N % 8 == 0) && abytes < 0xFFFFFF00ll &&

@@ -28,6 +28,7 @@
 // split K over grid.z into per-split partial slabs that one reduction
 // kernel sums in split order: deterministic, no float atomics.
 #include "gemm_f32.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -433,10 +434,7 @@ int64_t gemm_f32_part_floats(int M, int N, int K, int ones_row, int splits) {
 // 10.63 ms with them against 10.51 ms with 64-row tiles (fewer workgroups
 // per GEMM on 256 CUs, 55 KB of LDS each)
 static int gemm_rm(int Mr) {
-  static const int force = [] {
-    const char* e = std::getenv("SA_GEMM_RM");
-    return e ? std::atoi(e) : 1;
-  }();
+  static const int force = sa::measure_knob("SA_GEMM_RM", 1);
   return force == 2 && Mr >= 1024 ? 2 : 1;
 }
 
@@ -446,10 +444,7 @@ int gemm_f32_splits(int M, int N, int K, int ones_row) {
   int s = 1;
   // enough workgroups to fill 256 CUs twice over (SA_GEMM_WG_TARGET), each
   // K chunk >= 128
-  static const int target = [] {
-    const char* e = std::getenv("SA_GEMM_WG_TARGET");
-    return e ? std::max(1, std::atoi(e)) : 512;
-  }();
+  static const int target = std::max(1, sa::measure_knob("SA_GEMM_WG_TARGET", 512));
   while (tiles * s < target && K / (2 * s) >= 128 && s < 16) s *= 2;
   return s;
 }
@@ -477,10 +472,7 @@ bool gemm_f32_launch(const float* A, const float* B, int M, int N, int K, int ld
   dim3 grid((Mr + BM * rm - 1) / (BM * rm), (N + BN - 1) / BN, a.splits);
   // branch-free buffer-load variant (SA_GEMM_BL=0: the generic kernel):
   // whole quads along every f4 operand axis, byte offsets within 32 bits
-  static const int bl = [] {
-    const char* e = std::getenv("SA_GEMM_BL");
-    return e ? std::atoi(e) : 1;
-  }();
+  static const int bl = sa::env_knob("SA_GEMM_BL", 1);
   const int64_t abytes = (ta ? static_cast<int64_t>(K) * lda : static_cast<int64_t>(M) * lda) * 4;
   const int64_t bbytes = (tb ? static_cast<int64_t>(N) * ldb : static_cast<int64_t>(K) * ldb) * 4;
   if (bl && (!ta || M % 4 == 0) && (tb || N % 4 == 0) && abytes < 0xFFFFFF00ll &&

@@ -20,6 +20,7 @@
 // registers (no LDS staging, no bank conflicts); the K dimension is split
 // across the waves of the workgroup and reduced once through LDS.
 #include "launchers.h"
+#include "knobs.h"
 
 #include <hip/hip_bf16.h>
 
@@ -323,21 +324,16 @@ void lstm_pack_weights_launch(const float* w, float* w4, float* wt, int H,
 // (round 4) the full fp32 step is 9.650 / 9.654 ms at 2 vs 9.782 at 4, 9.664
 // at 1 and 9.650-9.685 at 3 (SA_LSTM_XPACK sweep on one box).
 static int g_xpack = [] {
-  const char* e = std::getenv("SA_LSTM_XPACK");
-  const int v = e ? std::atoi(e) : 2;
+  const int v = sa::measure_knob("SA_LSTM_XPACK", 2);
   return v >= 1 && v <= 8 ? v : 2;
 }();
 // 16 batch rows per step workgroup (twice the workgroups, each streaming
 // half the packed h / dG): fp32 learner 13.01/13.05 -> 12.75/12.81 ms per
 // step at B = 32 (A/B/A/B on one box); SA_LSTM_ROWS=32 restores 32 rows
-static bool g_rows16 = [] {
-  const char* e = std::getenv("SA_LSTM_ROWS");
-  return !(e && std::atoi(e) == 32);
-}();
+static bool g_rows16 = sa::measure_knob("SA_LSTM_ROWS", 16) != 32;
 // backward packing (SA_LSTM_XPACK_BWD; 0 = the forward's)
 static int g_xpack_bwd = [] {
-  const char* e = std::getenv("SA_LSTM_XPACK_BWD");
-  const int v = e ? std::atoi(e) : 0;
+  const int v = sa::measure_knob("SA_LSTM_XPACK_BWD", 0);
   return v >= 1 && v <= 8 ? v : 0;
 }();
 int lstm_xpack(int v) {
@@ -353,10 +349,7 @@ void lstm_fwd_step_launch(const float* xw_t, const float* h_pk_in,
                           float* hpm_t, int B, int H, hipStream_t stream) {
   const int xp = g_xpack;
   // SA_LSTM_FWD_NW=4: four waves per workgroup (K split four ways)
-  static const bool w4w = [] {
-    const char* e = std::getenv("SA_LSTM_FWD_NW");
-    return e && std::atoi(e) == 4;
-  }();
+  static const bool w4w = sa::measure_knob("SA_LSTM_FWD_NW", 8) == 4;
   if (H == 256 && g_rows16 && w4w) {
     dim3 grid16(H / 4 * xp, (B + 15) / 16);
     hipLaunchKernelGGL((lstm_fwd_step_kernel<256, 16, 4>), grid16, dim3(256), 0, stream,
@@ -393,10 +386,7 @@ void lstm_bwd_step_launch(const float* dh_out_t, const float* dg_pk_in,
   const int xp = g_xpack_bwd ? g_xpack_bwd : g_xpack;
   dim3 grid(H / 16 * xp, (B + 31) / 32);
   __hip_bfloat16* d16 = static_cast<__hip_bfloat16*>(dg16_t);
-  static const bool w8 = [] {
-    const char* e = std::getenv("SA_LSTM_BWD_W8");
-    return e && std::atoi(e) == 1;
-  }();
+  static const bool w8 = sa::measure_knob("SA_LSTM_BWD_W8", 0) == 1;
   if (H == 256 && g_rows16 && w8) {
     // 8 waves of 128 gate columns each (the packed W_h^T layout is the same:
     // each wave's slice is contiguous); the packed dG layout is private to

@@ -26,6 +26,7 @@
 // the cell state, gates, carries and every output stay fp32.  Requires B <= 32 (rows >= B are computed as zeros and
 // never stored).
 #include "launchers.h"
+#include "knobs.h"
 
 #include <hip/hip_bf16.h>
 
@@ -706,14 +707,10 @@ void lstm_gang_pack_launch(const float* w, void* wf, void* wbk, hipStream_t stre
 // Uniform-role kernels by default; SA_LSTM_GANG_WS=1 selects the wave-
 // specialised ones, measured slower (T=101, B=32: fwd 676-678 vs 446-448 us,
 // bwd 823-839 vs 448-449 us; tools/micro/lstm_probe.py).
-static int g_gang_ws = [] {
-  const char* e = std::getenv("SA_LSTM_GANG_WS");
-  return (e && e[0] == '1') ? 1 : 0;
-}();
+static int g_gang_ws = sa::measure_knob("SA_LSTM_GANG_WS", 0) == 1 ? 1 : 0;
 // s_sleep(1) count between sweep passes (SA_LSTM_GANG_NAP, default 1).
 static int g_gang_nap = [] {
-  const char* e = std::getenv("SA_LSTM_GANG_NAP");
-  const int v = e ? std::atoi(e) : 1;
+  const int v = sa::measure_knob("SA_LSTM_GANG_NAP", 1);
   return v >= 0 && v <= 64 ? v : 1;
 }();
 int lstm_gang_nap(int v) {

@@ -35,6 +35,7 @@ from . import dmlab30
 from . import environments
 from . import flags as flags_lib
 from . import py_process
+from .utils.knobs import measure_env
 
 log = logging.getLogger('scalable_agent_amd')
 
@@ -195,9 +196,6 @@ class EpisodeLogger(object):
 
 
 # --------------------------------------------------------------- feeder
-_H2D_STREAMS = {}
-
-
 def _h2d_stream(device):
   """The process's ONE host->device prefetch stream, created before any
   other stream (train() calls this first): HIP deals streams round-robin over
@@ -205,11 +203,8 @@ def _h2d_stream(device):
   learner's / inference's streams can share the compute stream's queue, which
   serialises the ~1.2 ms slab copy with the learner step (measured in
   bench.py: the bf16 step 4.6 -> 5.8 ms)."""
-  import torch
-  s = _H2D_STREAMS.get(device)
-  if s is None:
-    s = _H2D_STREAMS[device] = torch.cuda.Stream(device)
-  return s
+  from .parallel.streams import stream_plan
+  return stream_plan(device).copy
 
 
 class _TrajFeeder(object):
@@ -239,7 +234,7 @@ class _TrajFeeder(object):
     self.graphs = [None] * n
     self.pending = collections.deque()
     self.k = 0
-    self.host_sync = os.environ.get('SA_H2D_SYNC', 'host') != 'device'
+    self.host_sync = measure_env('SA_H2D_SYNC', 'host') != 'device'
     if self.cuda:
       self.copy_stream = _h2d_stream(device)
       self.free = [torch.cuda.Event() for _ in range(n)]
@@ -503,7 +498,11 @@ def train(flags):
   _install_sigterm_handler()
   if device.type == 'cuda':
     torch.cuda.set_device(device)
-    _h2d_stream(device)  # the first stream of the process (see _h2d_stream)
+    # the process's streams in their fixed order (parallel/streams.py: the
+    # H2D feeder stream first), then one collective: the communicator is up
+    # before the first learner step
+    _h2d_stream(device)
+    parallel.warmup_collective(device)
   torch.manual_seed(flags.seed + rank)
   logdir = flags.logdir if rank == 0 else os.path.join(flags.logdir,
                                                        'rank%d' % rank)

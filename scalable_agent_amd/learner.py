@@ -28,6 +28,7 @@ from . import vtrace as vtrace_lib
 from .optim import FlatParams, RMSProp
 from .structs import ActorOutput, AgentOutput, StepOutput, StepOutputInfo
 from .utils.tracing import trace
+from .utils.knobs import measure_env
 
 
 def compute_loss(agent, data, flags, use_fused=False, popart=None,
@@ -163,7 +164,7 @@ class Learner:
     self._graph = None
     # graph_step's early all-reduce hand-off: host-side (default) or
     # device-side stream order (SA_EARLY_SYNC=device)
-    self._early_host = os.environ.get('SA_EARLY_SYNC', 'host') != 'device'
+    self._early_host = measure_env('SA_EARLY_SYNC', 'host') != 'device'
     self._early_ev = None
     self._early_stream = None
     self._static_in = None
@@ -174,7 +175,7 @@ class Learner:
     self._seed_one = None  # backward seed (see _fwd_late)
     # weight-gradient GEMMs on a side stream next to the torso backward
     # (opt-in: measured within run-to-run noise, profiles/experiments.md)
-    self._overlap = os.environ.get('SA_OVERLAP_WGRAD', '0') == '1'
+    self._overlap = measure_env('SA_OVERLAP_WGRAD', '0') == '1'
     if getattr(flags, 'popart', False):
       from .popart import PopArt
       self.popart = PopArt(self.agent.num_value_heads, flags.popart_beta,
@@ -194,6 +195,11 @@ class Learner:
       if getattr(flags, 'grad_overlap', True) and off is not None:
         self.grad_sync.set_split(off)
         self._split = self.grad_sync.split is not None
+      if self.device.type == 'cuda':
+        # the early all-reduce's issuing stream, from the fixed stream plan
+        # (created here, before any capture, not lazily after it)
+        from .parallel.streams import stream_plan
+        self._early_stream = stream_plan(self.device).early
 
   def _torso_offset(self):
     """Flat offset where the conv-torso parameters start, if they are
@@ -278,12 +284,24 @@ class Learner:
                          self.agent.baseline_b.data)
     self.frames.add_(self.frames_per_step)
 
+  def _begin_early_device_ordered(self):
+    """The early bucket's all-reduce, issued from the early stream (its own
+    hardware queue) behind a device-side wait on the work enqueued so far on
+    the current stream."""
+    early = self._early_stream
+    if early is None:
+      self.grad_sync.begin_early()
+      return
+    early.wait_stream(torch.cuda.current_stream(self.device))
+    with torch.cuda.stream(early):
+      self.grad_sync.begin_early()
+
   def step(self, data):
     """One learner update from a device-resident time-major batch."""
     self._popart_tasks = data.level_name if self.popart is not None else None
     loss = self._fwd_late(data)
     if self._split:
-      self.grad_sync.begin_early()  # under the torso backward
+      self._begin_early_device_ordered()  # under the torso backward
     self._bwd_torso()
     self._split_pairs = None
     self.flat.rebind_grads()
@@ -301,7 +319,10 @@ class Learner:
     self._static_in = batch_to_device(example, self.device)
     if clone:  # the static slot owns its memory
       self._static_in = _map_tensors(self._static_in, lambda t: t.clone())
-    s = torch.cuda.Stream(self.device)
+    # the process's one capture stream (parallel/streams.py: a new stream per
+    # capture would shift which hardware queue every later stream gets)
+    from .parallel.streams import stream_plan
+    s = stream_plan(self.device).capture
     s.wait_stream(torch.cuda.current_stream(self.device))
     saved_p = self.flat.params.clone()
     with torch.cuda.stream(s):
@@ -312,7 +333,7 @@ class Learner:
     g = torch.cuda.CUDAGraph()
     # thread_local: actor-inference threads keep using the GPU (and the
     # caching allocator) while the learner captures
-    mode = os.environ.get('SA_CAPTURE_MODE', 'thread_local')
+    mode = measure_env('SA_CAPTURE_MODE', 'thread_local')
     if self._split:
       # two graphs on one pool, replayed in capture order: forward + late
       # backward, then the torso backward (the early all-reduce is launched
@@ -354,14 +375,16 @@ class Learner:
         # dpA vs dpB).  The torso backward is already enqueued meanwhile
         if self._early_ev is None:
           self._early_ev = torch.cuda.Event()
-          self._early_stream = torch.cuda.Stream(self.device)
+        if self._early_stream is None:
+          from .parallel.streams import stream_plan
+          self._early_stream = stream_plan(self.device).early
         self._early_ev.record()
         self._graph[1].replay()
         self._early_ev.synchronize()
         with torch.cuda.stream(self._early_stream):
           self.grad_sync.begin_early()
       else:
-        self.grad_sync.begin_early()
+        self._begin_early_device_ordered()
         self._graph[1].replay()
     else:
       self._graph.replay()

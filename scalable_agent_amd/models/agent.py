@@ -30,6 +30,7 @@ import torch.nn.functional as F
 
 from ..structs import AgentOutput
 from . import layers
+from ..utils.knobs import measure_env
 
 CORE_SIZE = 256
 INSTR_BUCKETS = 1000
@@ -112,6 +113,7 @@ def _chunk_bounds(T, chunks, split=None):
       b.append(min(T - (len(w) - len(b)), max(b[-1] + 1, int(round(T * acc / tot)))))
     b.append(T)
     return b
+  chunks = max(1, min(int(chunks), T))  # no empty chunk when T < chunks
   return [(T * k) // chunks for k in range(chunks + 1)]
 
 
@@ -380,7 +382,7 @@ class Agent(nn.Module):
     dev = frames.device
     main = torch.cuda.current_stream(dev)
     side = self._core_stream(dev)
-    bounds = _chunk_bounds(T, chunks, os.environ.get('SA_PIPELINE_SPLIT'))
+    bounds = _chunk_bounds(T, chunks, measure_env('SA_PIPELINE_SPLIT'))
     fused = self.fused_core_ready(instr)
     F_in = self.core_input_size
     outs = []
@@ -400,7 +402,12 @@ class Agent(nn.Module):
       side.wait_stream(main)
       with torch.cuda.stream(side):
         if fused:
+          # both side-stream inputs were produced on the main stream: their
+          # blocks must not go back to the main stream's pool before the
+          # side stream has read them
           feats.record_stream(side)
+          if instr_enc is not None:
+            instr_enc.record_stream(side)
           hs, state = ops.core_lstm(
               feats, self.linear_w, self.linear_b, self.lstm_kernel,
               self.lstm_bias, reward[n0:n1], actions[n0:n1], done[t0:t1],

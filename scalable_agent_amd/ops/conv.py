@@ -18,13 +18,14 @@ import torch
 from . import grad_sink
 from ._ext import ext
 from ..models import layers
+from ..utils.knobs import measure_env
 
 TORSO_READY = True
 # whole-residual-block forward kernel (res_block_fwd) instead of two
 # res_conv_fwd launches: opt-in (SA_FUSED_BLOCK=1) - bitwise identical but
 # measured slower (206 vs 169 us at 36x48x16, 143 vs 102 at 18x24x32): the
 # convs are latency/issue bound, not HBM bound (profiles/experiments.md)
-FUSED_BLOCK = os.environ.get('SA_FUSED_BLOCK', '0') == '1'
+FUSED_BLOCK = measure_env('SA_FUSED_BLOCK', '0') == '1'
 
 
 def supports(agent):

@@ -26,6 +26,7 @@ from ._ext import ext
 from ..models import layers
 
 import os
+from ..utils.knobs import measure_env
 
 # debug hook (tools/debug): when a dict, the deep torso backward records its
 # intermediate gradients in it
@@ -38,10 +39,10 @@ DEBUG_TAPE = None
 # only in LDS), the rest conv + maxpool_fwd; and whether the backward gathers
 # the pre-pool gradient from (dP, argmax) inside the conv kernels' loads
 # instead of materialising it with maxpool_bwd.
-FUSED_POOL_STAGES = tuple(int(c) for c in os.environ.get('SA_F32_FUSED_POOL', '0')
+FUSED_POOL_STAGES = tuple(int(c) for c in measure_env('SA_F32_FUSED_POOL', '0')
                           if c.isdigit())
 # SA_F32_POOL_GATHER=1: every stage; a digit string (e.g. '0'): those stages
-_pg = os.environ.get('SA_F32_POOL_GATHER', '')
+_pg = measure_env('SA_F32_POOL_GATHER', '')
 POOL_GATHER_STAGES = (0, 1, 2) if _pg == '1' else tuple(
     int(c) for c in _pg if c.isdigit())
 POOL_GATHER = bool(POOL_GATHER_STAGES)
@@ -59,10 +60,10 @@ POOL_SCATTER = os.environ.get('SA_F32_POOL_SCATTER', '1') != '0'
 # reads (the image is then dropped after the forward): opt-in
 # (SA_F32_PW_U8=1) - measured slower, 9.47-9.52 vs 9.37 ms per fp32 step
 # (the byte expansion in LDS costs more than the image reads it saves)
-PW_U8 = os.environ.get('SA_F32_PW_U8', '0') == '1'
+PW_U8 = measure_env('SA_F32_PW_U8', '0') == '1'
 U8_DIRECT = {
-    'deep': os.environ.get('SA_F32_U8_DEEP', '0') == '1',
-    'shallow': os.environ.get('SA_F32_U8_SHALLOW', '0') == '1'}
+    'deep': measure_env('SA_F32_U8_DEEP', '0') == '1',
+    'shallow': measure_env('SA_F32_U8_SHALLOW', '0') == '1'}
 
 
 def supports(agent):

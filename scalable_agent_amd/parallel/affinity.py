@@ -131,7 +131,12 @@ def visible_gpu_count(root='/sys', env=None):
     spec = env.get(var)
     if spec is None:
       continue
-    ids = [int(x) for x in spec.split(',') if x.strip().isdigit()]
+    toks = [x.strip() for x in spec.split(',') if x.strip()]
+    if not all(x.isdigit() for x in toks):
+      # a UUID mask (GPU-<uuid>) or anything else that is not plain
+      # ordinals: unknown here, the caller defers to the HIP device count
+      return None
+    ids = [int(x) for x in toks]
     n = len([i for i in ids if i < n])
   return n
 

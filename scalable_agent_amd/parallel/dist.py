@@ -101,10 +101,13 @@ class GradientSynchronizer:
   """Flat-bucket gradient all-reduce for FlatParams-based learners."""
 
   def __init__(self, flat, group=None, reduce='sum', bucket_bytes=4 << 20,
-               overlap=False):
+               overlap=False, op=None):
     self.flat = flat
     self.group = group
     self.reduce = reduce
+    # the reduction op (SUM; tools/micro/dp_queues.py uses AVG, which makes a
+    # one-rank RCCL group launch a kernel the trace can place on its queue)
+    self.op = dist.ReduceOp.SUM if op is None else op
     self.world = dist.get_world_size(group) if dist.is_initialized() else 1
     n = flat.numel
     per = max(1, bucket_bytes // 4)
@@ -128,6 +131,11 @@ class GradientSynchronizer:
     by begin_early() while the conv-torso backward still runs; all_reduce()
     then reduces [offset, n) and waits for both."""
     self.split = int(offset) if 0 < offset < self.flat.numel else None
+    # the step guard's NaN sentinel (Learner._apply writes it AFTER the early
+    # bucket went out) must travel with the late bucket
+    sentinel = getattr(self.flat, 'sentinel', None)
+    if self.split is not None and sentinel is not None:
+      assert sentinel >= self.split, (sentinel, self.split)
 
   def _mark_start(self):
     g = self.flat.grads
@@ -141,16 +149,35 @@ class GradientSynchronizer:
       self.last_time_s = self._events[0].elapsed_time(self._events[1]) / 1e3
     self._events[0].record()
 
+  def _stream_ordered(self):
+    """RCCL collectives on GPU tensors are issued stream-ordered
+    (async_op=False): ProcessGroupNCCL runs them on the CURRENT stream, so
+    the caller's stream - the stream plan's early stream with its own
+    hardware queue, or the compute stream - decides where they run
+    (parallel/streams.py).  gloo keeps async work handles."""
+    g = self.flat.grads
+    return g.is_cuda and dist.get_backend(self.group) == 'nccl'
+
   def begin_early(self):
-    """Launches the all-reduce of the early bucket (async; RCCL runs it on
-    its own stream, ordered after the work already enqueued)."""
+    """Launches the all-reduce of the early bucket, ordered after the work
+    already enqueued on the current stream (Learner: the stream plan's early
+    stream, so it runs beside the conv-torso backward)."""
     if self.world <= 1 or self.split is None or self._works:
       return
     self._mark_start()
-    self._works = [dist.all_reduce(self.flat.grads[:self.split],
-                                   group=self.group, async_op=True)]
+    g = self.flat.grads[:self.split]
+    if self._stream_ordered():
+      dist.all_reduce(g, op=self.op, group=self.group)
+      done = torch.cuda.Event()
+      done.record()
+      self._works = [done]
+    else:
+      self._works = [dist.all_reduce(g, op=self.op, group=self.group,
+                                     async_op=True)]
 
   def all_reduce(self):
+    """Reduces what begin_early did not and leaves the current stream
+    ordered after every reduction."""
     if self.world <= 1:
       return
     g = self.flat.grads
@@ -158,11 +185,20 @@ class GradientSynchronizer:
     if self.split is not None:
       if not self._works:  # no early phase this step: reduce both now
         self.begin_early()
-      works = self._works + [dist.all_reduce(g[self.split:], group=self.group,
-                                             async_op=True)]
+      works = self._works
       self._works = []
       for w in works:
-        w.wait()
+        if isinstance(w, torch.cuda.Event):
+          torch.cuda.current_stream(g.device).wait_event(w)
+      late = g[self.split:]
+      if self._stream_ordered():
+        dist.all_reduce(late, op=self.op, group=self.group)
+      else:
+        works = works + [dist.all_reduce(late, op=self.op, group=self.group,
+                                         async_op=True)]
+      for w in works:
+        if not isinstance(w, torch.cuda.Event):
+          w.wait()
       if self.reduce == 'mean':
         g.div_(self.world)
       if timed:
@@ -170,10 +206,12 @@ class GradientSynchronizer:
       return
     if timed:
       self._mark_start()
-    if len(self.buckets) == 1:
-      dist.all_reduce(g, group=self.group)
+    if len(self.buckets) == 1 or self._stream_ordered():
+      for lo, hi in (self.buckets if len(self.buckets) > 1 else [(0, None)]):
+        dist.all_reduce(g[lo:hi], op=self.op, group=self.group)
     else:
-      works = [dist.all_reduce(g[lo:hi], group=self.group, async_op=True)
+      works = [dist.all_reduce(g[lo:hi], op=self.op, group=self.group,
+                               async_op=True)
                for lo, hi in self.buckets]
       for w in works:
         w.wait()

@@ -109,3 +109,8 @@ def test_visible_gpu_count(tmp_path):
   assert affinity.visible_gpu_count(root, env={'ROCR_VISIBLE_DEVICES': '2'}) == 1
   assert affinity.visible_gpu_count(root, env={'CUDA_VISIBLE_DEVICES': '0,7'}) == 1
   assert affinity.visible_gpu_count(str(tmp_path / 'missing'), env={}) is None
+  # a UUID mask is not counted here (unknown): the caller defers to HIP
+  assert affinity.visible_gpu_count(
+      root, env={'ROCR_VISIBLE_DEVICES': 'GPU-1f2e3d4c5b6a7988'}) is None
+  assert affinity.visible_gpu_count(
+      root, env={'HIP_VISIBLE_DEVICES': '0,GPU-1f2e3d4c5b6a7988'}) is None

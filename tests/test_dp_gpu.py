@@ -54,28 +54,37 @@ def test_two_ranks_match_one_rank_with_the_whole_batch(cuda, tmp_path, dtype, to
   assert torch.allclose(a['params'], b['params'], rtol=0, atol=atol)
 
 
-def test_one_rank_conv_fault_skips_the_step_on_every_rank(cuda, tmp_path):
-  """DP step guard: rank 1's fused Winograd backward times out (injected) on
-  step 1 only.  Its error words poison the reduced gradient, so BOTH ranks
-  skip step 1 (replicas stay identical, skipped_updates == 1 on each, the
-  conv timeout counted on rank 1 only) and both apply step 2."""
+@pytest.mark.parametrize('kind,dtype,graph', [('conv', 'fp32', 0),
+                                              ('conv', 'fp32', 1),
+                                              ('lstm', 'bf16', 1)])
+def test_one_rank_fault_skips_the_step_on_every_rank(cuda, tmp_path, kind,
+                                                     dtype, graph):
+  """DP step guard: rank 1's fused Winograd backward (conv) or gang LSTM
+  (lstm) times out (injected) on step 1 only.  Its error words poison the
+  reduced gradient, so BOTH ranks skip step 1 (replicas stay identical,
+  skipped_updates == 1 on each, the timeout counted on rank 1 only) and
+  both apply step 2 - eager, and through the captured split-backward graphs
+  with the host-ordered early all-reduce (Learner.graph_step)."""
   script = os.path.join(ROOT, 'tools', 'dp_check.py')
   out = str(tmp_path / 'fault.pt')
   _run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
         '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
-        '--master-port', str(_port()), script, '--out', out, '--dtype', 'fp32',
-        '--graph', '0', '--fault_rank', '1', '--unroll', '8'],
+        '--master-port', str(_port()), script, '--out', out, '--dtype', dtype,
+        '--graph', str(graph), '--fault_rank', '1', '--fault_kind', kind,
+        '--unroll', '8'],
        {'SA_DIST_BACKEND': 'gloo', 'OMP_NUM_THREADS': '2'})
   recs = [torch.load('%s.%d' % (out, r), weights_only=True) for r in (0, 1)]
   for r, rec in enumerate(recs):
     assert rec['world'] == 2 and rec['rank'] == r
+    assert rec['split'] is True  # the two-phase (split) backward ran
     assert rec['applied1'] is False, 'rank %d applied the poisoned step' % r
     assert rec['consistent1'] and rec['consistent2']
     assert rec['applied2'] is True
     assert rec['health1']['skipped_updates'] == 1
     assert rec['health2']['skipped_updates'] == 1
-    assert rec['health2']['conv_timeouts'] == (1 if r == 1 else 0)
-    assert rec['health2']['lstm_timeouts'] == 0
+    mine = 1 if r == 1 else 0
+    assert rec['health2']['conv_timeouts'] == (mine if kind == 'conv' else 0)
+    assert rec['health2']['lstm_timeouts'] == (mine if kind == 'lstm' else 0)
 
 
 @pytest.mark.gpu

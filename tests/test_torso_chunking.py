@@ -67,3 +67,25 @@ def test_uneven_batch():
 
 def test_default_limit_keeps_the_headline_batch_whole():
   assert conv_f32.MAX_FRAMES >= 32 * 101
+
+
+def _check_bounds(b, T):
+  assert b[0] == 0 and b[-1] == T
+  assert all(b1 - b0 >= 1 for b0, b1 in zip(b, b[1:])), b
+
+
+def test_pipeline_chunk_bounds():
+  """Time-chunk boundaries of the torso || LSTM pipeline (agent.py
+  _chunk_bounds): equal chunks, SA_PIPELINE_SPLIT proportions, more weights
+  than steps, zero weights - every chunk at least one step."""
+  from scalable_agent_amd.models.agent import _chunk_bounds
+  assert _chunk_bounds(20, 1) == [0, 20]
+  assert _chunk_bounds(101, 2) == [0, 50, 101]
+  assert _chunk_bounds(20, 3, '9,9,2') == [0, 9, 18, 20]
+  for T, chunks, split in [(2, 4, None), (3, 8, None), (2, 1, '1,1,1,1'),
+                           (10, 1, '0,0,5'), (10, 1, '5,0,0'),
+                           (5, 1, '0,0,0'), (101, 1, '4,1'),
+                           (1, 3, '9,9,2'), (7, 1, '1e9,1,1')]:
+    b = _chunk_bounds(T, chunks, split)
+    _check_bounds(b, T)
+  assert len(_chunk_bounds(2, 4)) == 3  # capped at T chunks

@@ -9,11 +9,15 @@ parameters; with WORLD_SIZE=1 the same script runs the whole batch on one
 learner.  Under the reference's sum losses both must give the same update.
 usage: dp_check.py --out params.pt [--dtype fp32|bf16] [--batch 4]
 
---fault_rank R (fp32, eager steps): rank R's fused Winograd backward gets the
-injected hand-off timeout on the first step only.  Every rank writes
-`<out>.<rank>` with whether each of two steps applied, the replicas'
-consistency after each, and its health counters: the collective step guard
-must make every rank skip step 1 and apply step 2.
+--fault_rank R: rank R gets an injected hand-off timeout on the first step
+only: --fault_kind conv (fp32: the fused Winograd backward) or lstm (bf16:
+the gang LSTM).  Every rank writes `<out>.<rank>` with whether each of two
+steps applied, the replicas' consistency after each, and its health
+counters: the collective step guard must make every rank skip step 1 and
+apply step 2.  With --graph 1 each step is captured (the injected fault is
+part of the captured launches) and replayed through Learner.graph_step: the
+split backward graphs, the early all-reduce after the host has seen the
+first graph end, the sentinel poison before the late bucket.
 """
 import argparse
 import os
@@ -38,6 +42,7 @@ def main():
   ap.add_argument('--unroll', type=int, default=6)
   ap.add_argument('--graph', type=int, default=1)
   ap.add_argument('--fault_rank', type=int, default=-1)
+  ap.add_argument('--fault_kind', default='conv', choices=('conv', 'lstm'))
   args = ap.parse_args()
   rank, world, local = parallel.init_distributed()
   device = torch.device('cuda', local % torch.cuda.device_count())
@@ -60,16 +65,21 @@ def main():
   mine = _map_tensors(full, lambda t: cols(t).to(device))
   if args.fault_rank >= 0:
     from scalable_agent_amd.ops import _ext
-    rec = {'world': world, 'rank': rank}
+    C = _ext.ext()
+    fault = C.cf32_wino_fault if args.fault_kind == 'conv' else C.lstm_gang_fault
+    rec = {'world': world, 'rank': rank, 'split': learner._split}
     for step in (1, 2):
       p0 = learner.flat.params.clone()
-      prev = _ext.ext().cf32_wino_fault(
-          1 if (step == 1 and rank == args.fault_rank) else 0)
+      prev = fault(1 if (step == 1 and rank == args.fault_rank) else 0)
       try:
-        learner.step(mine)
+        if args.graph:
+          learner.capture(mine)
+          learner.graph_step()
+        else:
+          learner.step(mine)
         torch.cuda.synchronize()
       finally:
-        _ext.ext().cf32_wino_fault(prev)
+        fault(prev)
       rec['applied%d' % step] = not torch.equal(learner.flat.params, p0)
       rec['consistent%d' % step] = parallel.param_checksum_consistent(
           learner.flat.params)
