@@ -171,6 +171,12 @@ def _wants_self_launch(argv):
   return known.gpus > 1
 
 
+# Hardware queues per process before the first HIP call (inherited by
+# self-launched ranks): enough that the compute, H2D copy, early all-reduce
+# and RCCL's own streams each get a queue instead of sharing
+# (scalable_agent_amd/parallel/streams.py, profiles/r6_dp_queues.txt)
+os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+
 if __name__ == '__main__' and _wants_self_launch(sys.argv[1:]):
   sys.exit(_self_launch(sys.argv[1:]))
 
@@ -418,10 +424,7 @@ def main():
           'bench.py: %d ranks on this node but only %d visible GPU(s); RCCL '
           'needs one distinct GPU per rank (SA_DIST_BACKEND=gloo rehearses '
           'ranks sharing a card)' % (local_world, have))
-  rank, world, local = parallel.init_distributed()
-  if args.gpus != world:
-    raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' %
-                     (args.gpus, world))
+  local = parallel.world_info()[2]
   if args.device == 'auto':
     # one-card rehearsal (SA_DIST_BACKEND): ranks share the visible GPUs
     if torch.cuda.is_available():
@@ -432,11 +435,16 @@ def main():
     device = torch.device(args.device)
   if device.type == 'cuda':
     torch.cuda.set_device(device)
-    # the process's streams in their fixed order (parallel/streams.py: the
-    # H2D prefetch stream first, then the capture and early-all-reduce
-    # streams), then one collective so the communicator is up and working
-    # before the first measured step
+    # the process's streams, created and first used in their fixed order
+    # BEFORE RCCL's init (a stream takes its hardware queue at its first
+    # use: parallel/streams.py)
     parallel.stream_plan(device)
+  rank, world, local = parallel.init_distributed()
+  if args.gpus != world:
+    raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%d' %
+                     (args.gpus, world))
+  if device.type == 'cuda':
+    # one collective: the communicator is up before the first measured step
     parallel.warmup_collective(device)
 
   backend = args.backend

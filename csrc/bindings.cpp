@@ -312,30 +312,6 @@ void lstm_set_gang(bool on) { g_lstm_gang = on; }
 bool lstm_get_gang() { return g_lstm_gang; }
 at::Tensor lstm_error(at::Tensor like) { return lstm_err_word(like.device()); }
 
-// A HIP stream on a hardware queue of its own (parallel/streams.py).  HIP
-// hands a plain new stream the least-used of its GPU_MAX_HW_QUEUES (4)
-// queues, so it can share the compute stream's queue and be serialised
-// behind it (profiles/r6_dp_queues.txt: the early all-reduce stream did);
-// a stream with a CU mask always gets a new queue.  The mask enables every
-// CU of the device.  Returns the hipStream_t as an integer for
-// torch.cuda.ExternalStream; the stream lives as long as the process.
-int64_t own_queue_stream(int64_t device) {
-  int prev = 0;
-  TORCH_CHECK(hipGetDevice(&prev) == hipSuccess, "hipGetDevice");
-  TORCH_CHECK(hipSetDevice(static_cast<int>(device)) == hipSuccess, "hipSetDevice");
-  hipDeviceProp_t prop;
-  TORCH_CHECK(hipGetDeviceProperties(&prop, static_cast<int>(device)) == hipSuccess,
-              "hipGetDeviceProperties");
-  const int words = (prop.multiProcessorCount + 31) / 32;
-  std::vector<uint32_t> mask(static_cast<size_t>(words), 0xFFFFFFFFu);
-  if (prop.multiProcessorCount % 32) mask.back() = (1u << (prop.multiProcessorCount % 32)) - 1u;
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), mask.data());
-  (void)hipSetDevice(prev);
-  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
-  return reinterpret_cast<int64_t>(s);
-}
-
 void noop(int64_t blocks, int64_t threads, at::Tensor counter) {
   sa::noop_launch(blocks, threads, counter.data_ptr<int>(), cur_stream());
 }
@@ -384,7 +360,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_error_word", &lstm_error);
   m.def("lstm_xpack", &sa::lstm_xpack);
   m.def("noop", &noop);
-  m.def("own_queue_stream", &own_queue_stream);
   register_conv_ops(m);
   register_learner_ops(m);
   register_conv_f32_ops(m);

@@ -61,6 +61,23 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Pricing builds only (-DSA_WINO_XMFMA=bits, never a production build): the
+// MFMA at an odd (compile-time, unrolled) index becomes ONE VALU FMA on the
+// same operands - half the matrix work, wrong results, everything else
+// unchanged - to measure how much of a kernel the matrix pipe sets.  Bit 0:
+// forward / data-gradient MFMAs, bit 1: weight-gradient MFMAs.
+#ifndef SA_WINO_XMFMA
+#define SA_WINO_XMFMA 0
+#endif
+template <int BIT>
+__device__ __forceinline__ f4 mfma4x(float a, float b, f4 c, int idx) {
+  if ((SA_WINO_XMFMA & BIT) && (idx & 1)) {
+    c[0] = fmaf(a, b, c[0]);
+    return c;
+  }
+  return mfma4(a, b, c);
+}
+
 // 16-B loads through a buffer descriptor: an offset at or past the buffer's
 // end returns zeros (the hardware range check), so a stager's padding and
 // out-of-image elements need no select when they are committed to LDS, and
@@ -546,7 +563,7 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
 #pragma unroll
               for (int h = 0; h < NH; ++h)
                 acc[h][2 * xp2 + q] =
-                    mfma4(ua[h][q][v], V[2 * xp2 + q][v], acc[h][2 * xp2 + q]);
+                    mfma4x<1>(ua[h][q][v], V[2 * xp2 + q][v], acc[h][2 * xp2 + q], v);
         }
       }
 
@@ -2145,8 +2162,8 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
         const f4 u1 = *reinterpret_cast<const f4*>(up + (2 * xp2 + 1) * USTR);
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          acc[2 * xp2] = mfma4(u0[v], V[2 * xp2][v], acc[2 * xp2]);
-          acc[2 * xp2 + 1] = mfma4(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1]);
+          acc[2 * xp2] = mfma4x<1>(u0[v], V[2 * xp2][v], acc[2 * xp2], v);
+          acc[2 * xp2 + 1] = mfma4x<1>(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1], v);
         }
       }
       f4 tt[4][2];
@@ -2224,7 +2241,8 @@ __global__ __launch_bounds__(64 * NW, WWG ? 1 : 2) void wino_bwd_fused_kernel(Wi
             // zeroing V (the patch it reads is staged, finite data)
             const float V[4] = {sq[0] - sq[2], sq[1] + sq[2], sq[2] - sq[1], sq[1] - sq[3]};
 #pragma unroll
-            for (int bc = 0; bc < 4; ++bc) wacc[4 * i + bc] = mfma4(V[bc], zf[i][bc], wacc[4 * i + bc]);
+            for (int bc = 0; bc < 4; ++bc)
+              wacc[4 * i + bc] = mfma4x<2>(V[bc], zf[i][bc], wacc[4 * i + bc], bc);
           }
         }
       }
@@ -2605,8 +2623,8 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
             const f4 u1 = *reinterpret_cast<const f4*>(up + (2 * xp2 + 1) * USTR);
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-              acc[2 * xp2] = mfma4(u0[v], V[2 * xp2][v], acc[2 * xp2]);
-              acc[2 * xp2 + 1] = mfma4(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1]);
+              acc[2 * xp2] = mfma4x<1>(u0[v], V[2 * xp2][v], acc[2 * xp2], v);
+              acc[2 * xp2 + 1] = mfma4x<1>(u1[v], V[2 * xp2 + 1][v], acc[2 * xp2 + 1], v);
             }
           }
         }
@@ -2747,7 +2765,7 @@ __global__ __launch_bounds__(512, 2) void wino_bwd_fused32_kernel(WinoBwdArgs a)
             for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
               for (int b2 = 0; b2 < NBY; ++b2)
-                wacc[bc][b][b2] = mfma4(V[bc], zf[b2][bc], wacc[bc][b][b2]);
+                wacc[bc][b][b2] = mfma4x<2>(V[bc], zf[b2][bc], wacc[bc][b][b2], bc);
           }
         }
     };

@@ -487,6 +487,13 @@ def train(flags):
       envs.append(create_environment(flags, level, seed))
     py_process.start_all(envs)
 
+  device = _device(flags, parallel.world_info()[2])
+  if device.type == 'cuda':
+    torch.cuda.set_device(device)
+    # the process's streams, created and first used in their fixed order
+    # BEFORE RCCL's init (parallel/streams.py: a stream takes its hardware
+    # queue at its first use; the H2D feeder stream is the plan's first)
+    _h2d_stream(device)
   rank, world, local_rank = parallel.init_distributed(
       timeout_s=flags.collective_timeout_secs)
   if flags.num_learners and flags.num_learners != world:
@@ -494,14 +501,9 @@ def train(flags):
         '--num_learners=%d but WORLD_SIZE=%d: launch one process per learner '
         '(python -m torch.distributed.run --nproc-per-node %d ...)' %
         (flags.num_learners, world, flags.num_learners))
-  device = _device(flags, local_rank)
   _install_sigterm_handler()
   if device.type == 'cuda':
-    torch.cuda.set_device(device)
-    # the process's streams in their fixed order (parallel/streams.py: the
-    # H2D feeder stream first), then one collective: the communicator is up
-    # before the first learner step
-    _h2d_stream(device)
+    # one collective: the communicator is up before the first learner step
     parallel.warmup_collective(device)
   torch.manual_seed(flags.seed + rank)
   logdir = flags.logdir if rank == 0 else os.path.join(flags.logdir,
@@ -901,6 +903,10 @@ def test(flags):
 
 
 def main(argv=None):
+  # before the first HIP call (and inherited by the env / actor processes
+  # forked below): see parallel/streams.py reserve_hw_queues
+  from .parallel.streams import reserve_hw_queues
+  reserve_hw_queues()
   logging.basicConfig(level=logging.INFO,
                       format='[%(asctime)s %(levelname)s] %(message)s')
   flags = flags_lib.parse_flags(argv if argv is not None else sys.argv[1:])

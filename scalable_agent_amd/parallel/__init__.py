@@ -15,6 +15,6 @@ from .dist import (init_distributed, GradientSynchronizer, broadcast_params,
                    param_checksum_consistent, world_info, cleanup,
                    backend_info)
 from .streams import (stream_plan, warmup_collective, reset_stream_plans,
-                      StreamPlan)
+                      reserve_hw_queues, StreamPlan)
 from .affinity import (auto_pin_wanted, gpu_numa_node, pin_to_gpu_numa,
                        visible_gpu_count)

@@ -28,8 +28,10 @@ def test_plan_order_and_reuse():
   _Fake.made = []
   try:
     p = parallel.stream_plan('cpu', factory=_Fake)
-    assert streams.ORDER == ('copy', 'capture', 'early')
-    assert [p.copy, p.capture, p.early] == _Fake.made  # creation order
+    # copy and early first: the two pool streams that measured on queues of
+    # their own (parallel/streams.py, profiles/r6_dp_queues.txt)
+    assert streams.ORDER == ('copy', 'early', 'capture')
+    assert [p.copy, p.early, p.capture] == _Fake.made  # creation order
     # a second request (another capture, another measurement) makes nothing
     q = parallel.stream_plan(torch.device('cpu'), factory=_Fake)
     assert q is p and len(_Fake.made) == 3

@@ -1,15 +1,17 @@
 """Which hardware queue each stream of the data-parallel learner path runs on
 (parallel/streams.py).
 
-Run under rocprofv3 on ONE GPU with a world-size-1 RCCL group:
+Run under rocprofv3 on ONE GPU with a world-size-1 RCCL group (with
+GPU_MAX_HW_QUEUES=4, HIP's default, to check the first-use order alone; with
+8, as bench.py sets it - on the rocprofv3 command line either way):
 
-  rocprofv3 --kernel-trace --memory-copy-trace -d OUT -o run -- \
+  GPU_MAX_HW_QUEUES=4 rocprofv3 --kernel-trace --memory-copy-trace -d OUT -o run -- \
       python3 tools/micro/dp_queues.py
   python3 tools/micro/dp_queues.py --parse OUT/<host>/<pid>/run_results.db
 
-The probe brings the process up exactly as bench.py does (RCCL group with
-device_id -> the communicator and its stream at init; then the stream plan;
-then the warm-up collective), captures a small HIP learner step (warm-up
+The probe brings the process up exactly as bench.py does (the stream plan,
+created and first used; the RCCL group with device_id; the warm-up
+collective), captures a small HIP learner step (warm-up
 on the plan's capture stream) and replays it on the default stream, and
 issues the early all-reduce from the plan's early stream after a host wait
 (Learner.graph_step itself, with the synchronizer told world 2).  Each stream also runs one marker kernel: a
@@ -45,10 +47,12 @@ def probe():
   os.environ.setdefault('MASTER_PORT', '29533')
   dev = torch.device('cuda', 0)
   torch.cuda.set_device(dev)
-  # as parallel.init_distributed (device_id: eager communicator + stream)
+  # as bench.py: the stream plan (created and first used) before RCCL's
+  # init, then the group as parallel.init_distributed makes it (device_id:
+  # eager communicator), then the warm-up collective
+  plan = parallel.stream_plan(dev)
   dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev,
                           timeout=datetime.timedelta(seconds=120))
-  plan = parallel.stream_plan(dev)
   parallel.warmup_collective(dev)
   ops.load()
 
@@ -56,7 +60,10 @@ def probe():
     with torch.cuda.stream(stream):
       torch.empty(1 << 16, dtype=dtype, device=dev).fill_(1)
 
-  f = flags_lib.default_flags(batch_size=4, unroll_length=8, torso='deep')
+  # the headline learner shape: the early bucket's all-reduce is issued while
+  # the ~5 ms torso-backward graph runs, so the trace shows whether they overlap
+  B, T = 32, 100
+  f = flags_lib.default_flags(batch_size=B, unroll_length=T, torso='deep')
   agent = Agent(9, torso='deep', frame_shape=(72, 96, 3), seed=1,
                 backend='hip', compute_dtype=torch.float32)
   # the data-parallel learner (split backward graphs, early all-reduce from
@@ -67,7 +74,7 @@ def probe():
   lrn.grad_sync.world = 2
   lrn.grad_sync.op = dist.ReduceOp.AVG
   assert lrn._split
-  batch = batch_to_device(make_synthetic_batch(4, 8, (72, 96, 3), 9), dev)
+  batch = batch_to_device(make_synthetic_batch(B, T, (72, 96, 3), 9), dev)
   lrn.capture(batch)
   host = torch.empty(8 << 20, dtype=torch.uint8).pin_memory()
   slab = torch.empty(8 << 20, dtype=torch.uint8, device=dev)
