@@ -35,6 +35,31 @@ int64_t NowMs() {
 
 }  // namespace
 
+EnvDoorbell::EnvDoorbell() {
+  bytes_ = 4096;
+  void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::runtime_error("EnvDoorbell: mmap failed");
+  std::memset(p, 0, bytes_);
+  word_ = reinterpret_cast<std::atomic<uint32_t>*>(p);
+}
+
+EnvDoorbell::~EnvDoorbell() {
+  if (word_) munmap(word_, bytes_);
+}
+
+uint32_t EnvDoorbell::value() const { return word_->load(std::memory_order_acquire); }
+
+uint32_t EnvDoorbell::Wait(uint32_t seen, int64_t timeout_ms) {
+  const int64_t deadline = NowMs() + std::max<int64_t>(0, timeout_ms);
+  while (true) {
+    const uint32_t v = word_->load(std::memory_order_acquire);
+    if (v != seen) return v;
+    const int64_t left = deadline - NowMs();
+    if (left <= 0) return v;
+    FutexWait(word_, seen, std::min<int64_t>(left, 50));
+  }
+}
+
 EnvChannel::EnvChannel() {
   bytes_ = (sizeof(Slot) + 4095) / 4096 * 4096;
   void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
@@ -59,6 +84,11 @@ uint32_t EnvChannel::Request(int32_t method, int32_t kind, const std::vector<dou
   const uint32_t seq = slot_->req_seq.load(std::memory_order_relaxed) + 1;
   slot_->req_seq.store(seq, std::memory_order_release);
   FutexWake(&slot_->req_seq);
+  if (bell_) {
+    // after req_seq: a worker woken by the bell finds the request posted
+    bell_->fetch_add(1, std::memory_order_acq_rel);
+    FutexWake(bell_);
+  }
   return seq;
 }
 

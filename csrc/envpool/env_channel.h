@@ -22,6 +22,29 @@
 
 namespace sa {
 
+// One wake-up word shared by the channels of the envs ONE worker process
+// hosts (py_process.start_group: k envs per worker).  Every request on an
+// attached channel also bumps the word and wakes it, so the worker sleeps
+// on one futex for all its envs and serves every pending request per wake
+// (one wake per batch of steps instead of one per env).
+class EnvDoorbell {
+ public:
+  EnvDoorbell();  // anonymous shared mapping: create BEFORE forking the worker
+  ~EnvDoorbell();
+  EnvDoorbell(const EnvDoorbell&) = delete;
+  EnvDoorbell& operator=(const EnvDoorbell&) = delete;
+
+  uint32_t value() const;
+  // worker side: sleeps until the word differs from `seen` or timeout_ms
+  // passes; returns the current value
+  uint32_t Wait(uint32_t seen, int64_t timeout_ms);
+  std::atomic<uint32_t>* word() { return word_; }
+
+ private:
+  std::atomic<uint32_t>* word_ = nullptr;
+  size_t bytes_ = 0;
+};
+
 class EnvChannel {
  public:
   static constexpr int kMaxAction = 16;
@@ -34,8 +57,12 @@ class EnvChannel {
   EnvChannel& operator=(const EnvChannel&) = delete;
 
   // ---- caller side
-  // Posts a request; returns its sequence number.
+  // Posts a request (and rings the attached doorbell); returns its sequence
+  // number.
   uint32_t Request(int32_t method, int32_t kind, const std::vector<double>& action);
+  // Rings `bell` after every request from now on (the bell must outlive the
+  // channel; attach before forking the worker).
+  void AttachDoorbell(EnvDoorbell* bell) { bell_ = bell ? bell->word() : nullptr; }
   // Waits up to timeout_ms for the response to `seq`: 1 = answered, 0 = not
   // yet (call again; lets the caller check the worker's health in between).
   int WaitResponse(uint32_t seq, int64_t timeout_ms);
@@ -76,6 +103,7 @@ class EnvChannel {
   };
   Slot* slot_ = nullptr;
   size_t bytes_ = 0;
+  std::atomic<uint32_t>* bell_ = nullptr;
 };
 
 }  // namespace sa

@@ -54,8 +54,18 @@ void register_envpool(py::module& m) {
               v, std::memory_order_acq_rel);
         });
 
+  py::class_<EnvDoorbell>(m, "EnvDoorbell")
+      .def(py::init<>())
+      .def_property_readonly("value", &EnvDoorbell::value)
+      .def("wait", [](EnvDoorbell& b, uint32_t seen, int64_t t) {
+             py::gil_scoped_release nogil;
+             return b.Wait(seen, t);
+           }, py::arg("seen"), py::arg("timeout_ms"));
+
   py::class_<EnvChannel>(m, "EnvChannel")
       .def(py::init<>())
+      // keep_alive: the channel holds a raw pointer into the bell's page
+      .def("attach_doorbell", &EnvChannel::AttachDoorbell, py::keep_alive<1, 2>())
       .def("request", &EnvChannel::Request, py::arg("method"), py::arg("kind"),
            py::arg("action"))
       .def("wait_response", [](EnvChannel& c, uint32_t seq, int64_t t) {

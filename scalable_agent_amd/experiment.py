@@ -485,7 +485,7 @@ def train(flags):
   elif not distributed_actors:
     for level, seed in zip(actors_levels, actor_seeds):
       envs.append(create_environment(flags, level, seed))
-    py_process.start_all(envs)
+    py_process.start_all(envs, per_worker=flags.envs_per_worker)
 
   device = _device(flags, parallel.world_info()[2])
   if device.type == 'cuda':

@@ -130,6 +130,11 @@ def build_parser() -> argparse.ArgumentParser:
   p.add_argument('--actor_group_splits', type=int, default=2,
                  help='Pipeline stages per actor group: split k\'s inference '
                       'runs on the GPU while the envs of another split step.')
+  p.add_argument('--envs_per_worker', type=int, default=1,
+                 help='Envs hosted by one supervised env worker process '
+                      '(py_process.start_group: the envs share one doorbell '
+                      'futex, so a step of all of them costs one wake-up). '
+                      '1 = one process per env, as the reference.')
   p.add_argument('--popart', type=_str2bool, default=False,
                  help='PopArt value normalisation (north-star config #4).')
   p.add_argument('--popart_beta', type=float, default=3e-4)

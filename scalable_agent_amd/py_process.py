@@ -19,6 +19,7 @@ a per-process shared-memory slot instead of pickling them.
 """
 
 import multiprocessing
+import multiprocessing.connection
 import multiprocessing.pool
 import threading
 import traceback
@@ -150,14 +151,20 @@ class PyProcess(object):
     return self._process is not None and self._process.is_alive()
 
 
-def start_all(processes):
-  """Starts processes in parallel (PyProcessHook.begin)."""
+def start_all(processes, per_worker=1):
+  """Starts processes in parallel (PyProcessHook.begin).  per_worker > 1:
+  consecutive EnvProcesses are hosted k at a time by one worker process
+  (start_group)."""
   processes = list(processes)
   if not processes:
     return
-  tp = multiprocessing.pool.ThreadPool(min(32, len(processes)))
+  units = [[p] for p in processes]
+  if per_worker > 1 and all(isinstance(p, EnvProcess) for p in processes):
+    units = [processes[i:i + per_worker]
+             for i in range(0, len(processes), per_worker)]
+  tp = multiprocessing.pool.ThreadPool(min(32, len(units)))
   try:
-    tp.map(lambda p: p.start(), processes)
+    tp.map(lambda u: u[0].start() if len(u) == 1 else start_group(u), units)
   finally:
     tp.close()
     tp.join()
@@ -260,10 +267,10 @@ def _decode_instr(raw):
   return raw[1:] if raw[:1] == b'b' else raw[1:].decode('utf-8', 'replace')
 
 
-def _serve_channel(env, chan, conn, frames, faults):
-  """One channel request, if any arrives within 20 ms: True = served (or
-  closed -> 'close'), False = none."""
-  seq, method, kind, vals = chan.wait_request(20)
+def _serve_channel(env, chan, conn, frames, faults, timeout_ms=20):
+  """One channel request, if any arrives within timeout_ms: True = served
+  (or closed -> 'close'), False = none."""
+  seq, method, kind, vals = chan.wait_request(timeout_ms)
   if seq < 0:
     return False
   if method == _M_CLOSE:
@@ -370,6 +377,174 @@ def _supervisor(env_ctor, args, kwargs, conn, frame_buf, frame_shape, pid_box,
       return
 
 
+def _serve_pipe(env, conn, frames, faults):
+  """One pipe message of a grouped env: False when it closed the env."""
+  msg = conn.recv()
+  if msg is None:
+    env.close()
+    conn.close()
+    return False
+  seq, name, margs = msg
+  try:
+    if name == 'initial':
+      frame, instr = env.initial()
+      frames[...] = frame
+      conn.send(('ok', seq, (instr,)))
+    elif name == 'step':
+      faults.on_step()
+      reward, done, (frame, instr) = env.step(*margs)
+      frames[...] = frame
+      conn.send(('ok', seq, (float(reward), bool(done), instr)))
+    else:
+      conn.send(('ok', seq, getattr(env, name)(*margs)))
+  except Exception as e:  # pylint: disable=broad-except
+    # the other envs of the worker keep running; this one's caller re-raises
+    try:
+      e.remote_traceback = traceback.format_exc()
+      conn.send(('error', seq, e))
+    except Exception:  # pylint: disable=broad-except
+      conn.send(('error', seq, _RemoteError(repr(e))))
+  return True
+
+
+def _group_worker(specs, conns, bufs, shapes, restarted, faults, chans, bell):
+  """k envs in ONE process: every channel request pending at a doorbell
+  wake is served in that wake (py_process.start_group)."""
+  k = len(specs)
+  envs = [None] * k
+  frames = [np.frombuffer(b, dtype=np.uint8).reshape(sh)
+            for b, sh in zip(bufs, shapes)]
+  live = [True] * k
+  try:
+    for i, (ctor, args, kwargs) in enumerate(specs):
+      envs[i] = ctor(*args, **kwargs)
+    for ch in chans:
+      if ch is not None:
+        ch.discard_pending()  # requests the dead predecessor never answered
+    for c in conns:
+      c.send(('restarted' if restarted else 'ready', -1, None))
+    while any(live):
+      seen = bell.value if bell is not None else 0
+      served = False
+      for i in range(k):
+        if not live[i]:
+          continue
+        if chans[i] is not None:
+          r = _serve_channel(envs[i], chans[i], conns[i], frames[i], faults, 0)
+          if r == 'close':
+            envs[i].close()
+            conns[i].close()
+            live[i] = False
+            continue
+          served = served or bool(r)
+        if conns[i].poll(0):
+          served = True
+          live[i] = _serve_pipe(envs[i], conns[i], frames[i], faults)
+      if not served:
+        if bell is not None:
+          bell.wait(seen, 20)
+        else:
+          multiprocessing.connection.wait(
+              [c for c, l in zip(conns, live) if l], 0.02)
+  except (EOFError, KeyboardInterrupt, BrokenPipeError):
+    pass
+  except Exception as e:  # pylint: disable=broad-except  (a constructor)
+    for i in range(k):
+      if envs[i] is not None:
+        try:
+          envs[i].close()
+        except Exception:  # pylint: disable=broad-except
+          pass
+    for i, c in enumerate(conns):
+      if live[i]:
+        try:
+          c.send(('error', -1, e))
+        except Exception:  # pylint: disable=broad-except
+          pass
+
+
+def _group_supervisor(specs, conns, bufs, shapes, pid_box, restarts_box,
+                      fault_spec, seed, max_restarts, chans, bell):
+  """_supervisor for a group: a worker that dies takes all its envs down;
+  the replacement re-creates every one and each caller sees the restart."""
+  import os
+  import signal
+  signal.signal(signal.SIGINT, signal.SIG_IGN)
+  restarts = 0
+  while True:
+    pid = os.fork()
+    if pid == 0:
+      code = 0
+      try:
+        _group_worker(specs, conns, bufs, shapes, restarts > 0,
+                      _Faults(fault_spec, seed * 7919 + restarts), chans, bell)
+      except BaseException:  # pylint: disable=broad-except
+        code = 1
+      os._exit(code)
+    pid_box.value = pid
+    _, status = os.waitpid(pid, 0)
+    if os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0:
+      return
+    restarts += 1
+    restarts_box.value = restarts
+    if restarts > max_restarts:
+      for c in conns:
+        try:
+          c.send(('error', -1, RuntimeError(
+              'env worker died %d times; giving up' % restarts)))
+        except Exception:  # pylint: disable=broad-except
+          pass
+      return
+
+
+def start_group(procs):
+  """Starts ONE supervised worker process that hosts every EnvProcess in
+  `procs` (unstarted).  Each keeps its own frame buffer, channel slot and
+  pipe, so callers use them exactly as separately started ones; the
+  channels share a doorbell, so the worker sleeps on one futex and serves
+  every pending step per wake: with an actor group stepping all its envs
+  at once, k envs cost one wake-up instead of k (the
+  reference runs one env per process, /root/reference/py_process.py:123-132).
+  A crash or a watchdog kill of the worker restarts all k envs; the
+  supervision, hang watchdog and fault injection of the first member apply
+  to the group."""
+  procs = list(procs)
+  head = procs[0]
+  bell = None
+  if all(p._chan is not None for p in procs):
+    try:
+      from .runtime import native
+      bell = native.EnvDoorbell()
+      for p in procs:
+        p._chan.attach_doorbell(bell)
+    except Exception:  # pylint: disable=broad-except  (no native module)
+      bell = None
+  pid, restarts = _CTX.RawValue('i', 0), _CTX.RawValue('i', 0)
+  pipes = [_CTX.Pipe() for _ in procs]
+  group = {'open': len(procs), 'lock': threading.Lock()}
+  process = _CTX.Process(
+      target=_group_supervisor,
+      args=([(p._ctor, p._args, p._kwargs) for p in procs],
+            [child for _, child in pipes], [p._buf for p in procs],
+            [p._shape for p in procs], pid, restarts, head._fault_spec,
+            head._fault_seed, head._max_restarts, [p._chan for p in procs],
+            bell), daemon=True)
+  process.start()
+  for p, (conn, child) in zip(procs, pipes):
+    child.close()
+    p._conn, p._pid, p._restarts, p._process = conn, pid, restarts, process
+    p._group, p._bell = group, bell
+  err = None
+  for p in procs:
+    status, _, payload = p._conn.recv()
+    if status == 'error' and err is None:
+      err = payload
+  if err is not None:
+    process.join()
+    raise err
+  return procs
+
+
 class EnvProcess(object):
   """Env in a supervised child process; frames cross via shared memory.
 
@@ -396,6 +571,8 @@ class EnvProcess(object):
     self._process = None
     self._closed = False
     self._seq = 0
+    self._group = None  # start_group: {'open': members not closed, 'lock'}
+    self._bell = None
     # initial/step over the native futex channel (created before the fork);
     # the pipe stays for other methods, errors and restart notices
     self._chan = None
@@ -564,6 +741,11 @@ class EnvProcess(object):
       self._conn.send(None)
     except (OSError, BrokenPipeError):
       pass
+    if self._group is not None:
+      with self._group['lock']:
+        self._group['open'] -= 1
+        if self._group['open'] > 0:
+          return  # the worker keeps serving the group's other envs
     self._process.join(timeout=30)
     if self._process.is_alive():
       self._kill_worker()

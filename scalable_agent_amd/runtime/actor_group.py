@@ -260,7 +260,8 @@ class ActorGroupWorker(object):
     flags = sp['flags']
     envs = [create_environment(flags, lvl, seed)
             for lvl, seed in zip(sp['levels'], sp['seeds'])]
-    py_process.start_all(envs)  # forked before this process touches the GPU
+    # forked before this process touches the GPU
+    py_process.start_all(envs, per_worker=getattr(flags, 'envs_per_worker', 1))
     board = sp.get('board')
     if board is not None:
       # CPU-only group: inference is served from the learner process

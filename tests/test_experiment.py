@@ -152,3 +152,16 @@ def test_tf_checkpoint_keeps_newest(tmp_path):
   for n, p in learner.flat.named:  # (the flat buffer's padding is not saved)
     assert torch.equal(p, saved[n]), n
   assert int(learner.frames) == 30
+
+
+@pytest.mark.parametrize('groups', [0, 1])
+def test_train_with_grouped_env_workers(tmp_path, groups):
+  """--envs_per_worker=3: the 5 envs run in two worker processes (3 + 2,
+  py_process.start_group), with actor threads (groups=0) and with an actor
+  group process stepping them split-phase (groups=1)."""
+  logdir = str(tmp_path / ('grouped%d' % groups))
+  r = _run(['--logdir=' + logdir, '--num_actors=5', '--batch_size=2',
+            '--total_environment_frames=400', '--save_summaries_secs=0',
+            '--envs_per_worker=3', '--actor_groups=%d' % groups])
+  assert r.returncode == 0, r.stderr[-3000:]
+  assert 'Episode return' in r.stderr
