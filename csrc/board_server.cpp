@@ -7,7 +7,8 @@
 // batch waited behind learner-side Python work.  This
 // thread runs the same loop with no Python in it:
 //
-//   futex-wait on the board's sequence word -> collect REQUEST slots ->
+//   futex-wait on the board's sequence word -> collect REQUEST slots (for
+//   up to a short batching window while fewer than min_ready are ready) ->
 //   row mask into pinned memory -> H2D of the whole input region + mask ->
 //   hipGraphLaunch of the captured graph (plain or with-instruction variant,
 //   picked from the instruction lengths) -> D2H of each ready slot's output
@@ -85,6 +86,13 @@ class NativeBoardServer {
     if (thread_.joinable()) thread_.join();
   }
 
+  // batching window (see serve): launch once >= min_ready slots are ready
+  // or gather_us microseconds after the first one; gather_us 0 = off
+  void set_batching(int64_t min_ready, int64_t gather_us) {
+    min_ready_ = min_ready < 1 ? 1 : (min_ready > S_ ? S_ : min_ready);
+    gather_us_ = gather_us < 0 ? 0 : (gather_us > 100000 ? 100000 : gather_us);
+  }
+  int64_t gathered() const { return gathered_.load(); }
   int64_t batches() const { return batches_.load(); }
   int64_t rows_served() const { return rows_.load(); }
   bool running() const { return thread_.joinable() && !done_.load(); }
@@ -119,15 +127,41 @@ class NativeBoardServer {
 
   bool closed() const { return __atomic_load_n(&words_[1], __ATOMIC_ACQUIRE) != 0; }
 
-  bool serve(int timeout_ms) {
-    const uint32_t seq = __atomic_load_n(&words_[0], __ATOMIC_ACQUIRE);
+  void scan() {
     ready_.clear();
     for (int64_t s = 0; s < S_; ++s)
       if (__atomic_load_n(&words_[16 + s], __ATOMIC_ACQUIRE) == kRequest) ready_.push_back(s);
+  }
+
+  static int64_t now_us() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return static_cast<int64_t>(t.tv_sec) * 1000000 + t.tv_nsec / 1000;
+  }
+
+  bool serve(int timeout_ms) {
+    uint32_t seq = __atomic_load_n(&words_[0], __ATOMIC_ACQUIRE);
+    scan();
     if (ready_.empty()) {
       timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
       futex(&words_[0], FUTEX_WAIT, seq, &ts);
       return false;
+    }
+    // Batching window: every launch runs the graph over the WHOLE board and
+    // copies its whole input region, so a launch that serves few slots
+    // wastes most of that.  With fewer than min_ready_ slots ready, wait up
+    // to gather_us_ for more posts (the board's sequence word) first.
+    if (gather_us_ > 0 && static_cast<int64_t>(ready_.size()) < min_ready_) {
+      const int64_t deadline = now_us() + gather_us_;
+      while (static_cast<int64_t>(ready_.size()) < min_ready_ && !closed()) {
+        const int64_t left = deadline - now_us();
+        if (left <= 0) break;
+        timespec ts{0, left * 1000L};
+        futex(&words_[0], FUTEX_WAIT, seq, &ts);
+        seq = __atomic_load_n(&words_[0], __ATOMIC_ACQUIRE);
+        scan();
+      }
+      gathered_.fetch_add(1);
     }
     const int64_t R = S_ * M_;
     std::memset(mask_host_, 0, sizeof(float) * R);
@@ -197,7 +231,8 @@ class NativeBoardServer {
   std::vector<int64_t> ready_;
   std::thread thread_;
   std::atomic<bool> stop_{false}, done_{false};
-  std::atomic<int64_t> batches_{0}, rows_{0};
+  std::atomic<int64_t> batches_{0}, rows_{0}, gathered_{0};
+  int64_t min_ready_ = 1, gather_us_ = 0;  // set_batching (before start)
   mutable std::mutex err_mu_;
   std::string error_;
 };
@@ -217,6 +252,9 @@ void register_board_server(pybind11::module& m) {
       .def("stop", &NativeBoardServer::stop, py::call_guard<py::gil_scoped_release>())
       .def("serve_once", &NativeBoardServer::serve_once, py::arg("timeout_ms") = 50,
            py::call_guard<py::gil_scoped_release>())
+      .def("set_batching", &NativeBoardServer::set_batching, py::arg("min_ready"),
+           py::arg("gather_us"))
+      .def("gathered", &NativeBoardServer::gathered)
       .def("batches", &NativeBoardServer::batches)
       .def("rows_served", &NativeBoardServer::rows_served)
       .def("running", &NativeBoardServer::running)

@@ -363,6 +363,11 @@ class _TrajFeeder(object):
 
 
 # --------------------------------------------------------------- train
+# --actor_groups=-1 on a GPU: from this many actors on, CPU actor groups of
+# ~50 envs with the inference board instead of one GPU group process
+AUTO_BOARD_ACTORS = 128
+
+
 def _checker(groups, server):
   """Health probe the trajectory feeder runs while it waits for a slab."""
   if groups is None and server is None:
@@ -439,10 +444,17 @@ def train(flags):
   # initialised.
   distributed_actors = flags.task >= 0 and flags.job_name == 'learner'
   n_groups = flags.actor_groups
-  if n_groups < 0:  # auto: one group process when the learner is on a GPU
+  if n_groups < 0:  # auto (profiles/r6_e2e.md)
     on_gpu = (flags.device.startswith('cuda') or
               (flags.device == 'auto' and torch.cuda.device_count() > 0))
     n_groups = 1 if on_gpu else 0
+    if on_gpu and flags.num_actors >= AUTO_BOARD_ACTORS:
+      # many actors: one GPU group process is Python-bound (~300 K frames/s
+      # at 48 or 150 actors); CPU groups of ~50 envs posting to the
+      # learner-process inference board scale further (150 actors, 3 groups:
+      # 422 K fp32 / 511 K bf16 inference)
+      n_groups = -(-flags.num_actors // 50)
+      flags.inference_server = True
   flags.actor_groups = n_groups
   use_groups = (n_groups > 0 and not distributed_actors and
                 flags.trajectory_queue and not flags.deterministic)
@@ -562,7 +574,7 @@ def train(flags):
       model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
                                            seed=flags.seed + 17 * rank)
       model.publish(learner.flat.params)
-      server = BoardServer(model, board)
+      server = BoardServer(model, board, gather_us=flags.inference_gather_us)
       server.prepare(has_instr=use_instr)
       server.start()
     else:
@@ -646,6 +658,7 @@ def train(flags):
   if flags.deterministic:
     torch.use_deterministic_algorithms(True, warn_only=True)
   timer = StepTimer(learner.frames_per_step)
+  t_loop0 = time.time()
   last_summary = time.time()
   last_log_frames = int(learner.frames.item())
   reported_skips = 0
@@ -851,6 +864,12 @@ def train(flags):
            'passed, first loss %.6f', rank, world, steps,
            int(learner.frames.item()), episode_logger.episodes, checks_ok,
            first_loss)
+  if server is not None and server.batches:
+    # the inference board's serving rate (profiles/r6_e2e.md)
+    dt = max(1e-9, time.time() - t_loop0)
+    log.info('inference board: %d launches (%.0f/s), %.1f rows per launch, '
+             '%.0f rows/s', server.batches, server.batches / dt,
+             server.rows_served / server.batches, server.rows_served / dt)
   return learner
 
 

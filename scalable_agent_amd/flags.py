@@ -120,13 +120,20 @@ def build_parser() -> argparse.ArgumentParser:
                       'processes (each: its envs stepped in parallel, one '
                       'captured inference graph per step, writes into the '
                       'trajectory queue); 0 = actor threads in the learner '
-                      'process; -1 = auto: 1 group on a GPU (more GPU '
+                      'process; -1 = auto: on a GPU 1 group (more GPU '
                       'processes share the card badly: profiles/'
-                      'r2_e2e_actors.md), threads on CPU.')
+                      'r2_e2e_actors.md), or from 128 actors on CPU groups '
+                      'of ~50 envs with --inference_server '
+                      '(profiles/r6_e2e.md); threads on CPU.')
   p.add_argument('--inference_server', type=_str2bool, default=False,
                  help='Actor groups stay CPU-only and post their rows to a '
                       'shared-memory inference board served by a thread of '
                       'the learner process (one GPU context in total).')
+  p.add_argument('--inference_gather_us', type=int, default=0,
+                 help='Inference board: with fewer than half of the board\'s '
+                      'slots requesting, the server waits up to this many '
+                      'microseconds for more before launching (every launch '
+                      'runs the whole board).  0 = launch at once.')
   p.add_argument('--actor_group_splits', type=int, default=2,
                  help='Pipeline stages per actor group: split k\'s inference '
                       'runs on the GPU while the envs of another split step.')

@@ -152,10 +152,17 @@ class BoardClient(object):
 class BoardServer(object):
   """Learner-process side: one captured inference graph over the board."""
 
-  def __init__(self, model, board, use_graph=True):
+  def __init__(self, model, board, use_graph=True, gather_us=0,
+               min_ready=None):
     import torch
     self.torch = torch
     self.model, self.board = model, board
+    # native loop's batching window (NativeBoardServer.set_batching): launch
+    # once min_ready slots (default half the board) are ready or gather_us
+    # after the first
+    self.gather_us = int(gather_us)
+    self.min_ready = (max(1, board.S // 2) if min_ready is None
+                      else int(min_ready))
     dev = model.device
     self.cuda = dev.type == 'cuda'
     self.use_graph = bool(use_graph) and self.cuda
@@ -322,6 +329,7 @@ class BoardServer(object):
         exe.get(True, 0) if m.use_instruction else 0,
         m.device.index if m.device.index is not None else
         self.torch.cuda.current_device())
+    self._native.set_batching(self.min_ready, self.gather_us)
     self._native.start()
 
   def start(self):
