@@ -29,6 +29,9 @@
 #include <type_traits>
 
 namespace sa {
+namespace cf32 {
+int conv_cus();  // conv_f32.hip: CUs left to the persistent grids
+}  // namespace cf32
 namespace conv {
 namespace {
 
@@ -1544,12 +1547,15 @@ int num_cus() {
   return cus;
 }
 
-// Persistent grid: enough workgroups for `per_cu` resident per CU.
+// Persistent grid: enough workgroups for `per_cu` resident per CU, on the
+// CUs the fp32 torso's grids use too (conv_f32.hip conv_cus: all but the
+// CUs per XCD reserved for a concurrent stream, cf32_cu_reserve).
 int grid_for(int ntiles, size_t smem, int per_cu_cap) {
   int per_cu = static_cast<int>((160 * 1024) / (smem + 1024));
   if (per_cu > per_cu_cap) per_cu = per_cu_cap;
   if (per_cu < 1) per_cu = 1;
-  const int g = num_cus() * per_cu;
+  const int reserved = num_cus() - sa::cf32::conv_cus();  // 8 R on MI355X
+  const int g = (num_cus() - reserved) * per_cu;
   return ntiles < g ? ntiles : g;
 }
 

@@ -411,7 +411,10 @@ class Agent(nn.Module):
           hs, state = ops.core_lstm(
               feats, self.linear_w, self.linear_b, self.lstm_kernel,
               self.lstm_bias, reward[n0:n1], actions[n0:n1], done[t0:t1],
-              state, self.num_actions, instr_enc=instr_enc, allow_gang=False)
+              state, self.num_actions, instr_enc=instr_enc,
+              # the gang recurrence beside the next chunk's torso: measured
+              # experiment only (profiles/experiments.md round 6)
+              allow_gang=measure_env('SA_PIPELINE_GANG') == '1')
         else:
           x.record_stream(side)
           hs, state = ops.lstm_unroll(
