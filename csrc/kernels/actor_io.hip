@@ -89,7 +89,76 @@ __global__ __launch_bounds__(256) void actor_head_sample_kernel(
   }
 }
 
+// Inference-board epilogue (runtime/inference_board.py BoardServer._body):
+// the per-row masked LSTM state update and the packing of every output field
+// into the board's slot-major output block, in ONE launch instead of two
+// compare + select + copy chains and one copy per field (12 dependent
+// launches, ~57 us of each board launch: tools/micro/board_trace.py).
+//   c[r] = mask[r] > 0 ? c2[r] : c[r], h likewise (r < R, H columns);
+//   out[(r / M) * slot_bytes + off[f] + (r % M) * per[f] + b] = src_f[r][b]
+// for every field f < nf (per-row byte counts multiples of 4).
+constexpr int kBoardFields = 6;
+struct BoardEpi {
+  const uint32_t* src[kBoardFields];
+  int per_dw[kBoardFields];  // dwords per row
+  int off_dw[kBoardFields];  // dword offset of the field in a slot block
+  int nf, R, M, slot_dw, H;
+  const float* mask;         // [R]
+  const float* c2;
+  const float* h2;
+  float* c;
+  float* h;
+  uint32_t* out;
+};
+
+__global__ __launch_bounds__(256) void board_epilogue_kernel(BoardEpi a) {
+  const int r = blockIdx.x;  // one workgroup per row
+  if (r >= a.R) return;
+  const bool keep = a.mask[r] > 0.f;
+  for (int j = threadIdx.x; j < a.H; j += blockDim.x) {
+    const int64_t o = static_cast<int64_t>(r) * a.H + j;
+    if (keep) {
+      a.c[o] = a.c2[o];
+      a.h[o] = a.h2[o];
+    }
+  }
+  const int s = r / a.M, m = r - s * a.M;
+  uint32_t* dst = a.out + static_cast<int64_t>(s) * a.slot_dw;
+  for (int f = 0; f < a.nf; ++f) {
+    const int per = a.per_dw[f];
+    const uint32_t* src = a.src[f] + static_cast<int64_t>(r) * per;
+    uint32_t* d = dst + a.off_dw[f] + m * per;
+    for (int j = threadIdx.x; j < per; j += blockDim.x) d[j] = src[j];
+  }
+}
+
 }  // namespace
+
+int board_epilogue_max_fields() { return kBoardFields; }
+
+void board_epilogue_launch(const void* const* src, const int* per_dw, const int* off_dw, int nf,
+                           int R, int M, int slot_dw, int H, const float* mask, const float* c2,
+                           const float* h2, float* c, float* h, void* out, hipStream_t stream) {
+  if (R <= 0) return;
+  BoardEpi a{};
+  for (int f = 0; f < nf && f < kBoardFields; ++f) {
+    a.src[f] = static_cast<const uint32_t*>(src[f]);
+    a.per_dw[f] = per_dw[f];
+    a.off_dw[f] = off_dw[f];
+  }
+  a.nf = nf < kBoardFields ? nf : kBoardFields;
+  a.R = R;
+  a.M = M;
+  a.slot_dw = slot_dw;
+  a.H = H;
+  a.mask = mask;
+  a.c2 = c2;
+  a.h2 = h2;
+  a.c = c;
+  a.h = h;
+  a.out = static_cast<uint32_t*>(out);
+  hipLaunchKernelGGL(board_epilogue_kernel, dim3(R), dim3(256), 0, stream, a);
+}
 
 int actor_head_max_actions() { return kMaxA; }
 

@@ -184,6 +184,12 @@ void relu_mask_bf16_launch(void* dx, const void* x, int64_t n,
 // action [B] ~ Categorical(softmax(logits)) by Gumbel-max over Philox4x32-10
 // (key = seed, counter = (row, a, offset)).  h fp32 [B,256], A <= 32.
 int actor_head_max_actions();
+// inference-board epilogue (actor_io.hip): masked state update + slot-major
+// output packing in one launch
+int board_epilogue_max_fields();
+void board_epilogue_launch(const void* const* src, const int* per_dw, const int* off_dw, int nf,
+                           int R, int M, int slot_dw, int H, const float* mask, const float* c2,
+                           const float* h2, float* c, float* h, void* out, hipStream_t stream);
 void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
                               const float* wb, const float* bb, float* logits,
                               float* baseline, int64_t* action, int B, int A,

@@ -230,6 +230,45 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
   return {logits, baseline, action};
 }
 
+// Inference-board epilogue: c / h [R, H] f32 updated in place where mask [R]
+// (or [R, 1]) > 0 from c2 / h2, and every tensor of `fields` ([R, ...], any
+// dtype, 4-byte multiple per row) packed into `out` (uint8, S slot blocks of
+// slot_bytes) at byte offset offs[f] + (r % M) * row_bytes(f) of slot r / M.
+void board_epilogue(std::vector<at::Tensor> fields, std::vector<int64_t> offs, at::Tensor out,
+                    int64_t M, int64_t slot_bytes, at::Tensor mask, at::Tensor c2,
+                    at::Tensor h2, at::Tensor c, at::Tensor h) {
+  const int nf = static_cast<int>(fields.size());
+  TORCH_CHECK(nf >= 1 && nf <= sa::board_epilogue_max_fields() &&
+              static_cast<int>(offs.size()) == nf, "board_epilogue: 1..6 fields with offsets");
+  LB_CHECK(out); LB_CHECK(mask); LB_CHECK(c2); LB_CHECK(h2); LB_CHECK(c); LB_CHECK(h);
+  LB_F32(mask); LB_F32(c2); LB_F32(h2); LB_F32(c); LB_F32(h);
+  TORCH_CHECK(out.scalar_type() == at::kByte, "out must be uint8");
+  TORCH_CHECK(c.dim() == 2 && c.sizes() == h.sizes() && c.sizes() == c2.sizes() &&
+              c.sizes() == h2.sizes(), "c / h / c2 / h2 must be [R, H]");
+  const int64_t R = c.size(0), H = c.size(1);
+  TORCH_CHECK(mask.numel() == R, "mask must have R elements");
+  TORCH_CHECK(M >= 1 && R % M == 0 && slot_bytes % 4 == 0 &&
+              out.numel() >= (R / M) * slot_bytes, "board geometry");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 4 == 0, "out 4-byte aligned");
+  const void* src[8];
+  int per[8], off[8];
+  for (int f = 0; f < nf; ++f) {
+    LB_CHECK(fields[f]);
+    TORCH_CHECK(fields[f].dim() >= 1 && fields[f].size(0) == R, "field rows != R");
+    const int64_t rb = fields[f].numel() / R * fields[f].element_size();
+    TORCH_CHECK(rb % 4 == 0 && offs[f] % 4 == 0 && offs[f] + M * rb <= slot_bytes &&
+                reinterpret_cast<uintptr_t>(fields[f].data_ptr()) % 4 == 0,
+                "field rows / offsets must be 4-byte multiples inside the slot block");
+    src[f] = fields[f].data_ptr();
+    per[f] = static_cast<int>(rb / 4);
+    off[f] = static_cast<int>(offs[f] / 4);
+  }
+  const c10::DeviceGuard guard(c.device());
+  sa::board_epilogue_launch(src, per, off, nf, static_cast<int>(R), static_cast<int>(M),
+                            static_cast<int>(slot_bytes / 4), static_cast<int>(H),
+                            mask.data_ptr<float>(), c2.data_ptr<float>(), h2.data_ptr<float>(),
+                            c.data_ptr<float>(), h.data_ptr<float>(), out.data_ptr(), stream());
+}
 
 // C[:, :N] (+)= op(A) op(B) with the fused epilogue of kernels/gemm_f32.h.
 // A / B / C / mask may be row slices of wider row-major matrices (row stride
@@ -473,6 +512,10 @@ void register_learner_ops(pybind11::module& m) {
   m.def("relu_bwd_colsum_", &relu_bwd_colsum_, pybind11::arg("dy"),
         pybind11::arg("y"), pybind11::arg("out") = pybind11::none());
   m.def("relu_mask_bf16_", &relu_mask_bf16_);
+  m.def("board_epilogue", &board_epilogue, pybind11::arg("fields"), pybind11::arg("offs"),
+        pybind11::arg("out"), pybind11::arg("M"), pybind11::arg("slot_bytes"),
+        pybind11::arg("mask"), pybind11::arg("c2"), pybind11::arg("h2"), pybind11::arg("c"),
+        pybind11::arg("h"));
   m.def("actor_head_sample", &actor_head_sample, pybind11::arg("h"),
         pybind11::arg("wp"), pybind11::arg("bp"), pybind11::arg("wb"),
         pybind11::arg("bb"), pybind11::arg("seed"), pybind11::arg("offset"),

@@ -209,12 +209,31 @@ class BoardServer(object):
     """True when the serving loop is the C++ thread."""
     return self._native is not None
 
+  def _epilogue_ext(self):
+    """The HIP extension when the fused board epilogue applies (HIP
+    backend on a GPU), else None (torch ops: CPU boards, the torch
+    backend)."""
+    if not self.cuda or getattr(self.model.agent, 'backend', '') != 'hip':
+      return None
+    from .. import ops
+    return ops.ext()
+
   def _body(self, has_instr):
     torch = self.torch
     b = self.board
     la, rw, dn, fr, ids, ln = self._dev_in
     action, logits, baseline, c2, h2 = self.model.step_device(
         la, rw, dn, fr, ids, ln, self.c, self.h, has_instr=has_instr)
+    C = self._epilogue_ext()
+    if C is not None:
+      # ONE launch for the masked state update and the slot-major output
+      # packing (the torch form below is 12 dependent launches, ~57 us of
+      # every board launch: tools/micro/board_trace.py)
+      C.board_epilogue([action, logits, baseline, c2, h2],
+                       [o for _, _, _, o, _ in b.out_fields], self.out_dev,
+                       b.M, b.slot_out_bytes, self.mask_dev, c2, h2, self.c,
+                       self.h)
+      return
     m = self.mask_dev
     self.c.copy_(torch.where(m > 0, c2, self.c))
     self.h.copy_(torch.where(m > 0, h2, self.h))

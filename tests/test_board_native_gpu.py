@@ -113,3 +113,39 @@ def test_native_thread_serves_forked_workers(cuda):
   assert float(st[16:24].abs().sum()) == 0.0  # slot 2 never asked
   assert float(st[8 + 5:16].abs().sum()) == 0.0  # slot 1's unused rows
   board.close()
+
+
+def test_board_epilogue_matches_torch_ops(cuda):
+  """The fused board epilogue (one launch: masked LSTM state update +
+  slot-major packing of every output field) against the torch ops it
+  replaces in BoardServer._body, on a 3-slot x 5-row board."""
+  from scalable_agent_amd import ops
+  C = ops.ext()
+  S, M, A, H = 3, 5, 9, 256
+  R = S * M
+  board = InferenceBoard(S, M, (8, 8, 3), A)
+  g = torch.Generator().manual_seed(3)
+  action = torch.randint(0, A, (R,), generator=g).to(cuda)
+  logits = torch.randn(R, A, generator=g).to(cuda)
+  baseline = torch.randn(R, generator=g).to(cuda)
+  c2, h2 = torch.randn(R, H, generator=g).to(cuda), torch.randn(R, H, generator=g).to(cuda)
+  c0, h0 = torch.randn(R, H, generator=g).to(cuda), torch.randn(R, H, generator=g).to(cuda)
+  mask = (torch.rand(R, 1, generator=g) > 0.5).float().to(cuda)
+  out = torch.zeros(board.out_bytes, dtype=torch.uint8, device=cuda)
+  ref = torch.zeros_like(out)
+  c, h = c0.clone(), h0.clone()
+  C.board_epilogue([action, logits, baseline, c2, h2],
+                   [o for _, _, _, o, _ in board.out_fields], out, M,
+                   board.slot_out_bytes, mask, c2, h2, c, h)
+  rc = torch.where(mask > 0, c2, c0)
+  rh = torch.where(mask > 0, h2, h0)
+  view = ref.view(S, board.slot_out_bytes)
+  for (n, s, dt, o, nb), v in zip(board.out_fields,
+                                  (action, logits, baseline, c2, h2)):
+    per = nb // M
+    view[:, o:o + M * per].copy_(
+        v.reshape(S, M, -1).contiguous().view(torch.uint8).view(S, M * per))
+  torch.cuda.synchronize()
+  assert torch.equal(c, rc) and torch.equal(h, rh)
+  assert torch.equal(out, ref)
+  board.close()
