@@ -14,7 +14,17 @@
 //   picked from the instruction lengths) -> D2H of each ready slot's output
 //   block -> wait on this batch's event -> RESPONSE + futex wake per slot.
 //
-// Everything is enqueued on the inference model's own stream, the stream the
+// Depth 2 (add_buffer, a second set of device buffers and graphs): batch k+1
+// is enqueued before batch k is answered.  Its input H2D runs on a copy
+// stream of its own while batch k's graph runs (the compute stream waits on
+// the copy's event), and the host half of the loop (event wait, responses,
+// scan, mask) overlaps the GPU instead of sitting between two launches.  A
+// slot is in at most one batch at a time: it stays REQUEST until answered,
+// so the scan skips the in-flight ones.  The LSTM state is one device array
+// updated under the row mask in stream order, so batch k+1 sees batch k's
+// update for every row batch k served.
+//
+// Everything else is enqueued on the inference model's own stream, the stream the
 // learner's weight publish (inference.py InferenceModel.publish) also copies
 // on, so stream order keeps a replay from reading a half-copied snapshot.
 // The graphs are captured by Python before start() (no capture may run on
@@ -56,22 +66,41 @@ class NativeBoardServer {
                     uintptr_t stream, uintptr_t exec_plain, uintptr_t exec_instr, int64_t device)
       : base_(reinterpret_cast<uint8_t*>(base)), hdr_(hdr), in_bytes_(in_bytes),
         so_(slot_out_bytes), S_(num_slots), M_(rows_per_slot), instr_off_(instr_len_off),
-        in_dev_(reinterpret_cast<void*>(in_dev)), out_dev_(reinterpret_cast<uint8_t*>(out_dev)),
-        mask_dev_(reinterpret_cast<void*>(mask_dev)),
-        mask_host_(reinterpret_cast<float*>(mask_host)),
-        stream_(reinterpret_cast<hipStream_t>(stream)),
-        exec_plain_(reinterpret_cast<hipGraphExec_t>(exec_plain)),
-        exec_instr_(reinterpret_cast<hipGraphExec_t>(exec_instr)), device_(static_cast<int>(device)) {
-    TORCH_CHECK(base_ && in_dev_ && out_dev_ && mask_dev_ && mask_host_, "null board pointer");
+        stream_(reinterpret_cast<hipStream_t>(stream)), device_(static_cast<int>(device)) {
+    TORCH_CHECK(base_, "null board pointer");
     TORCH_CHECK(S_ > 0 && S_ <= 250 && M_ > 0, "board geometry");
-    TORCH_CHECK(exec_plain_ || exec_instr_, "no captured inference graph");
     words_ = reinterpret_cast<uint32_t*>(base_);
     ready_.reserve(S_);
+    pend_slots_.reserve(S_);
+    inflight_.assign(S_, 0);
+    add_buffer(in_dev, out_dev, mask_dev, mask_host, exec_plain, exec_instr);
+  }
+
+  // a second buffer set (inputs, outputs, mask, graphs captured over them)
+  // turns on depth-2 serving; before start()
+  void add_buffer(uintptr_t in_dev, uintptr_t out_dev, uintptr_t mask_dev, uintptr_t mask_host,
+                  uintptr_t exec_plain, uintptr_t exec_instr) {
+    TORCH_CHECK(!thread_.joinable(), "add_buffer after start");
+    TORCH_CHECK(bufs_.size() < 2, "at most two buffer sets");
+    Buf b;
+    b.in_dev = reinterpret_cast<void*>(in_dev);
+    b.out_dev = reinterpret_cast<uint8_t*>(out_dev);
+    b.mask_dev = reinterpret_cast<void*>(mask_dev);
+    b.mask_host = reinterpret_cast<float*>(mask_host);
+    b.plain = reinterpret_cast<hipGraphExec_t>(exec_plain);
+    b.instr = reinterpret_cast<hipGraphExec_t>(exec_instr);
+    TORCH_CHECK(b.in_dev && b.out_dev && b.mask_dev && b.mask_host, "null board pointer");
+    TORCH_CHECK(b.plain || b.instr, "no captured inference graph");
+    bufs_.push_back(b);
   }
 
   ~NativeBoardServer() {
     stop();
-    if (done_ev_) (void)hipEventDestroy(done_ev_);
+    for (Buf& b : bufs_) {
+      if (b.done_ev) (void)hipEventDestroy(b.done_ev);
+      if (b.in_ev) (void)hipEventDestroy(b.in_ev);
+    }
+    if (copy_) (void)hipStreamDestroy(copy_);
   }
 
   void start() {
@@ -93,6 +122,7 @@ class NativeBoardServer {
     gather_us_ = gather_us < 0 ? 0 : (gather_us > 100000 ? 100000 : gather_us);
   }
   int64_t gathered() const { return gathered_.load(); }
+  int64_t depth() const { return static_cast<int64_t>(bufs_.size()); }
   int64_t batches() const { return batches_.load(); }
   int64_t rows_served() const { return rows_.load(); }
   bool running() const { return thread_.joinable() && !done_.load(); }
@@ -103,9 +133,13 @@ class NativeBoardServer {
   }
 
   // one pass of the loop on the caller's thread (tests); false = no request
-  bool serve_once(int64_t timeout_ms) {
+  // (drain: a depth-2 batch is answered before it returns; drain=false
+  // leaves it in flight, as the serving thread does)
+  bool serve_once(int64_t timeout_ms, bool drain) {
     if (hipSetDevice(device_) != hipSuccess) fail("hipSetDevice failed");
-    return serve(static_cast<int>(timeout_ms));
+    const bool r = serve(static_cast<int>(timeout_ms));
+    if (drain && pending_) finish();
+    return r;
   }
 
  private:
@@ -127,10 +161,12 @@ class NativeBoardServer {
 
   bool closed() const { return __atomic_load_n(&words_[1], __ATOMIC_ACQUIRE) != 0; }
 
+  // REQUEST slots not already in the batch in flight
   void scan() {
     ready_.clear();
     for (int64_t s = 0; s < S_; ++s)
-      if (__atomic_load_n(&words_[16 + s], __ATOMIC_ACQUIRE) == kRequest) ready_.push_back(s);
+      if (!inflight_[s] && __atomic_load_n(&words_[16 + s], __ATOMIC_ACQUIRE) == kRequest)
+        ready_.push_back(s);
   }
 
   static int64_t now_us() {
@@ -143,6 +179,10 @@ class NativeBoardServer {
     uint32_t seq = __atomic_load_n(&words_[0], __ATOMIC_ACQUIRE);
     scan();
     if (ready_.empty()) {
+      if (pending_) {  // nothing new: answer the batch in flight
+        finish();
+        return true;
+      }
       timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
       futex(&words_[0], FUTEX_WAIT, seq, &ts);
       return false;
@@ -163,72 +203,118 @@ class NativeBoardServer {
       }
       gathered_.fetch_add(1);
     }
+    const int k = bufs_.size() > 1 && pending_ ? 1 - pend_buf_ : 0;
+    const int64_t rows = launch(k);
+    if (pending_) finish();  // batch k-1 finishes while batch k runs
+    pending_ = true;
+    pend_buf_ = k;
+    pend_rows_ = rows;
+    pend_slots_.assign(ready_.begin(), ready_.end());
+    for (int64_t s : pend_slots_) inflight_[s] = 1;
+    if (bufs_.size() == 1) finish();
+    return true;
+  }
+
+  // enqueue one batch over the ready_ slots into buffer set k; returns rows
+  int64_t launch(int k) {
+    Buf& b = bufs_[k];
     const int64_t R = S_ * M_;
-    std::memset(mask_host_, 0, sizeof(float) * R);
+    std::memset(b.mask_host, 0, sizeof(float) * R);
     int64_t rows = 0;
     for (int64_t s : ready_) {
       int64_t n = __atomic_load_n(&words_[16 + S_ + s], __ATOMIC_ACQUIRE);
       n = n < 0 ? 0 : (n > M_ ? M_ : n);
-      for (int64_t r = 0; r < n; ++r) mask_host_[s * M_ + r] = 1.f;
+      for (int64_t r = 0; r < n; ++r) b.mask_host[s * M_ + r] = 1.f;
       rows += n;
     }
     // the with-instruction graph when any row carries an instruction (the
     // Python server's rule: over the whole board)
     bool instr = false;
-    if (exec_instr_) {
+    if (b.instr) {
       const int64_t* len = reinterpret_cast<const int64_t*>(base_ + hdr_ + instr_off_);
       for (int64_t r = 0; r < R && !instr; ++r) instr = len[r] > 0;
     }
-    hipGraphExec_t g = instr ? exec_instr_ : exec_plain_;
+    hipGraphExec_t g = instr ? b.instr : b.plain;
     if (!g) fail(instr ? "no with-instruction graph captured" : "no plain graph captured");
-    check(hipMemcpyAsync(in_dev_, base_ + hdr_, in_bytes_, hipMemcpyHostToDevice, stream_),
-          "board H2D");
-    check(hipMemcpyAsync(mask_dev_, mask_host_, sizeof(float) * R, hipMemcpyHostToDevice, stream_),
-          "mask H2D");
+    if (!b.done_ev) check(hipEventCreateWithFlags(&b.done_ev, hipEventDisableTiming), "hipEventCreate");
+    if (bufs_.size() > 1) {
+      // set k's previous batch is answered (its event waited), so its
+      // input buffers are free: copy on the copy stream, under the graph
+      // of the batch in flight
+      if (!copy_) check(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking), "hipStreamCreate");
+      if (!b.in_ev) check(hipEventCreateWithFlags(&b.in_ev, hipEventDisableTiming), "hipEventCreate");
+      check(hipMemcpyAsync(b.in_dev, base_ + hdr_, in_bytes_, hipMemcpyHostToDevice, copy_),
+            "board H2D");
+      check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice, copy_),
+            "mask H2D");
+      check(hipEventRecord(b.in_ev, copy_), "hipEventRecord");
+      check(hipStreamWaitEvent(stream_, b.in_ev, 0), "hipStreamWaitEvent");
+    } else {
+      check(hipMemcpyAsync(b.in_dev, base_ + hdr_, in_bytes_, hipMemcpyHostToDevice, stream_),
+            "board H2D");
+      check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice,
+                           stream_),
+            "mask H2D");
+    }
     check(hipGraphLaunch(g, stream_), "hipGraphLaunch");
     uint8_t* host_out = base_ + hdr_ + in_bytes_;
     for (int64_t s : ready_)
-      check(hipMemcpyAsync(host_out + s * so_, out_dev_ + s * so_, so_, hipMemcpyDeviceToHost,
+      check(hipMemcpyAsync(host_out + s * so_, b.out_dev + s * so_, so_, hipMemcpyDeviceToHost,
                            stream_),
             "slot D2H");
-    // wait on an event of this batch, not on the stream: the learner thread
+    // an event of this batch, not a stream synchronise: the learner thread
     // keeps enqueueing weight publishes onto the same stream meanwhile
     // (a stream-wide synchronise held it off: 15.6 ms of learner-loop host
     // time per step at 96 actors)
-    if (!done_ev_) check(hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming), "hipEventCreate");
-    check(hipEventRecord(done_ev_, stream_), "hipEventRecord");
-    check(hipEventSynchronize(done_ev_), "hipEventSynchronize");
-    for (int64_t s : ready_) {
+    check(hipEventRecord(b.done_ev, stream_), "hipEventRecord");
+    return rows;
+  }
+
+  // wait for the batch in flight and answer its slots
+  void finish() {
+    check(hipEventSynchronize(bufs_[pend_buf_].done_ev), "hipEventSynchronize");
+    for (int64_t s : pend_slots_) {
+      inflight_[s] = 0;
       __atomic_store_n(&words_[16 + s], kResponse, __ATOMIC_RELEASE);
       futex(&words_[16 + s], FUTEX_WAKE, INT_MAX, nullptr);
     }
+    pending_ = false;
     batches_.fetch_add(1);
-    rows_.fetch_add(rows);
-    return true;
+    rows_.fetch_add(pend_rows_);
   }
 
   void run() {
     try {
       if (hipSetDevice(device_) != hipSuccess) fail("hipSetDevice failed");
       while (!stop_.load() && !closed()) serve(50);
+      if (pending_) finish();
     } catch (const std::exception&) {
       // error_ is set and the board closed by fail()
     }
     done_.store(true);
   }
 
+  struct Buf {
+    void* in_dev = nullptr;
+    uint8_t* out_dev = nullptr;
+    void* mask_dev = nullptr;
+    float* mask_host = nullptr;
+    hipGraphExec_t plain = nullptr, instr = nullptr;
+    hipEvent_t done_ev = nullptr, in_ev = nullptr;
+  };
+
   uint8_t* base_;
   uint32_t* words_ = nullptr;
   int64_t hdr_, in_bytes_, so_, S_, M_, instr_off_;
-  void* in_dev_;
-  uint8_t* out_dev_;
-  void* mask_dev_;
-  float* mask_host_;
   hipStream_t stream_;
-  hipGraphExec_t exec_plain_, exec_instr_;
-  hipEvent_t done_ev_ = nullptr;
+  hipStream_t copy_ = nullptr;  // depth 2: the input H2D
   int device_;
-  std::vector<int64_t> ready_;
+  std::vector<Buf> bufs_;
+  std::vector<int64_t> ready_, pend_slots_;
+  std::vector<char> inflight_;
+  bool pending_ = false;
+  int pend_buf_ = 0;
+  int64_t pend_rows_ = 0;
   std::thread thread_;
   std::atomic<bool> stop_{false}, done_{false};
   std::atomic<int64_t> batches_{0}, rows_{0}, gathered_{0};
@@ -251,7 +337,12 @@ void register_board_server(pybind11::module& m) {
       .def("start", &NativeBoardServer::start)
       .def("stop", &NativeBoardServer::stop, py::call_guard<py::gil_scoped_release>())
       .def("serve_once", &NativeBoardServer::serve_once, py::arg("timeout_ms") = 50,
+           py::arg("drain") = true,
            py::call_guard<py::gil_scoped_release>())
+      .def("add_buffer", &NativeBoardServer::add_buffer, py::arg("in_dev"), py::arg("out_dev"),
+           py::arg("mask_dev"), py::arg("mask_host"), py::arg("exec_plain"),
+           py::arg("exec_instr"))
+      .def("depth", &NativeBoardServer::depth)
       .def("set_batching", &NativeBoardServer::set_batching, py::arg("min_ready"),
            py::arg("gather_us"))
       .def("gathered", &NativeBoardServer::gathered)

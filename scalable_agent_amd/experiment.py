@@ -523,6 +523,11 @@ def train(flags):
   os.makedirs(logdir, exist_ok=True)
   writer = SummaryWriter(logdir) if rank == 0 else None
 
+  if flags.learner_cu_reserve > 0 and device.type == 'cuda':
+    # before any capture: the persistent grids' sizes are baked into the
+    # learner's graphs
+    from . import ops
+    ops.ext().cf32_cu_reserve(min(16, flags.learner_cu_reserve))
   agent = _make_agent(flags, num_actions, frame_shape, device, flags.seed)
   learner = Learner(agent, flags, device, world_size=world)
   restored = ckpt_lib.restore(flags.logdir, learner)
@@ -574,7 +579,8 @@ def train(flags):
       model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
                                            seed=flags.seed + 17 * rank)
       model.publish(learner.flat.params)
-      server = BoardServer(model, board, gather_us=flags.inference_gather_us)
+      server = BoardServer(model, board, gather_us=flags.inference_gather_us,
+                           depth=flags.inference_board_depth)
       server.prepare(has_instr=use_instr)
       server.start()
     else:

@@ -134,6 +134,16 @@ def build_parser() -> argparse.ArgumentParser:
                       'slots requesting, the server waits up to this many '
                       'microseconds for more before launching (every launch '
                       'runs the whole board).  0 = launch at once.')
+  p.add_argument('--learner_cu_reserve', type=int, default=0,
+                 help='CUs per XCD (0-16) that the learner\'s persistent conv '
+                      'grids leave free, so the inference board\'s kernels '
+                      'find room beside them (profiles/r6_e2e.md).')
+  p.add_argument('--inference_board_depth', type=int, default=1,
+                 choices=(1, 2),
+                 help='Inference board: batches in flight in the native '
+                      'serving loop (2 = the next batch\'s input copy and '
+                      'host work overlap the current batch\'s graph; '
+                      'measured slower at config #4, profiles/r6_e2e.md).')
   p.add_argument('--actor_group_splits', type=int, default=2,
                  help='Pipeline stages per actor group: split k\'s inference '
                       'runs on the GPU while the envs of another split step.')

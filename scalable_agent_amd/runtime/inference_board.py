@@ -20,7 +20,9 @@ inference on the GPU (a second GPU context per group) or, with
     mask is set) -> D2H of each ready slot's outputs -> state 2 + futex wake
     On a GPU with the HIP backend the loop is a C++ thread
     (csrc/board_server.cpp, no Python and no GIL per batch); the graphs are
-    captured here first.  SA_BOARD_NATIVE=0 keeps the Python thread.
+    captured here first.  SA_BOARD_NATIVE=0 keeps the Python thread.  With
+    depth=2 the C++ loop keeps two batches in flight over two buffer sets
+    (the next batch's H2D and host work under the current batch's graph).
 
 Replaces the reference's per-request dynamic batching (experiment.py:534-546
 + batcher.cc) for process actors: the "batch" is every slot that is ready
@@ -153,7 +155,7 @@ class BoardServer(object):
   """Learner-process side: one captured inference graph over the board."""
 
   def __init__(self, model, board, use_graph=True, gather_us=0,
-               min_ready=None):
+               min_ready=None, depth=1):
     import torch
     self.torch = torch
     self.model, self.board = model, board
@@ -163,6 +165,12 @@ class BoardServer(object):
     self.gather_us = int(gather_us)
     self.min_ready = (max(1, board.S // 2) if min_ready is None
                       else int(min_ready))
+    # batches in flight in the native loop (1 or 2; the Python loop is 1).
+    # Depth 2 measured slower end to end (profiles/r6_e2e.md): every launch
+    # runs the graph over the whole board, so launching earlier only makes
+    # the batches smaller
+    self.depth = int(depth)
+    assert self.depth in (1, 2)
     dev = model.device
     self.cuda = dev.type == 'cuda'
     self.use_graph = bool(use_graph) and self.cuda
@@ -175,19 +183,13 @@ class BoardServer(object):
       from .traj_queue import _hip_host_register
       torch.cuda.init()
       self.pinned = _hip_host_register(b.base + b.HDR, b.in_bytes + b.out_bytes)
-    # zero-filled: the capture's warm-up steps read the board before any
-    # worker wrote it
-    self.in_dev = torch.zeros(b.in_bytes, dtype=torch.uint8, device=dev)
-    self.out_dev = torch.zeros(b.out_bytes, dtype=torch.uint8, device=dev)
-    tdt = lambda dt: torch.from_numpy(np.empty(0, dt)).dtype
-    self._dev_in = [self.in_dev[o:o + nb].view(tdt(dt)).view(*s)
-                    for n, s, dt, o, nb in b.in_fields]
     self.c = torch.zeros(b.R, b.core, device=dev)
     self.h = torch.zeros(b.R, b.core, device=dev)
-    self.mask_host = torch.zeros(b.R, dtype=torch.float32)
-    if self.cuda:
-      self.mask_host = self.mask_host.pin_memory()
-    self.mask_dev = torch.zeros(b.R, 1, device=dev)
+    # buffer set 0 (set 1 is allocated by the depth-2 native loop)
+    self._sets = [self._buffers()]
+    (self.in_dev, self.out_dev, self.mask_dev, self.mask_host,
+     self._dev_in) = self._sets[0]
+    # graphs: has_instr -> graph over set 0, (1, has_instr) -> over set 1
     self._graphs = {}
     self._thread = None
     self._native = None
@@ -195,6 +197,23 @@ class BoardServer(object):
     self.error = None
     self._batches = 0
     self._rows = 0
+
+  def _buffers(self):
+    """One buffer set: device inputs, outputs, row mask (device + pinned
+    host) and the typed views of the inputs."""
+    torch, b, dev = self.torch, self.board, self.model.device
+    # zero-filled: the capture's warm-up steps read the board before any
+    # worker wrote it
+    in_dev = torch.zeros(b.in_bytes, dtype=torch.uint8, device=dev)
+    out_dev = torch.zeros(b.out_bytes, dtype=torch.uint8, device=dev)
+    tdt = lambda dt: torch.from_numpy(np.empty(0, dt)).dtype
+    dev_in = [in_dev[o:o + nb].view(tdt(dt)).view(*s)
+              for n, s, dt, o, nb in b.in_fields]
+    mask_host = torch.zeros(b.R, dtype=torch.float32)
+    if self.cuda:
+      mask_host = mask_host.pin_memory()
+    mask_dev = torch.zeros(b.R, 1, device=dev)
+    return in_dev, out_dev, mask_dev, mask_host, dev_in
 
   @property
   def batches(self):
@@ -218,10 +237,11 @@ class BoardServer(object):
     from .. import ops
     return ops.ext()
 
-  def _body(self, has_instr):
+  def _body(self, has_instr, k=0):
     torch = self.torch
     b = self.board
-    la, rw, dn, fr, ids, ln = self._dev_in
+    _, out_dev, mask_dev, _, dev_in = self._sets[k]
+    la, rw, dn, fr, ids, ln = dev_in
     action, logits, baseline, c2, h2 = self.model.step_device(
         la, rw, dn, fr, ids, ln, self.c, self.h, has_instr=has_instr)
     C = self._epilogue_ext()
@@ -230,14 +250,14 @@ class BoardServer(object):
       # packing (the torch form below is 12 dependent launches, ~57 us of
       # every board launch: tools/micro/board_trace.py)
       C.board_epilogue([action, logits, baseline, c2, h2],
-                       [o for _, _, _, o, _ in b.out_fields], self.out_dev,
-                       b.M, b.slot_out_bytes, self.mask_dev, c2, h2, self.c,
+                       [o for _, _, _, o, _ in b.out_fields], out_dev,
+                       b.M, b.slot_out_bytes, mask_dev, c2, h2, self.c,
                        self.h)
       return
-    m = self.mask_dev
+    m = mask_dev
     self.c.copy_(torch.where(m > 0, c2, self.c))
     self.h.copy_(torch.where(m > 0, h2, self.h))
-    out = self.out_dev.view(b.S, b.slot_out_bytes)
+    out = out_dev.view(b.S, b.slot_out_bytes)
     for (n, s, dt, o, nb), v in zip(b.out_fields,
                                     (action, logits, baseline, c2, h2)):
       per = nb // b.M  # bytes per row
@@ -245,19 +265,19 @@ class BoardServer(object):
           b.S, b.M * per)
       out[:, o:o + b.M * per].copy_(src)
 
-  def _capture(self, has_instr):
+  def _capture(self, has_instr, k=0):
     torch = self.torch
     s = self.model.stream
     with torch.cuda.stream(s):
       c0, h0 = self.c.clone(), self.h.clone()
       for _ in range(2):
-        self._body(has_instr)
+        self._body(has_instr, k)
       self.c.copy_(c0)
       self.h.copy_(h0)
       s.synchronize()
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
-        self._body(has_instr)
+        self._body(has_instr, k)
     return g
 
   def prepare(self, has_instr=False):
@@ -338,7 +358,7 @@ class BoardServer(object):
     for v in variants:  # every graph the loop may launch, captured up front
       if v not in self._graphs:
         self.prepare(has_instr=v)
-    exe = {v: g.raw_cuda_graph_exec() for v, g in self._graphs.items()}
+    exe = {v: self._graphs[v].raw_cuda_graph_exec() for v in variants}
     instr_off = [o for n, _, _, o, _ in b.in_fields if n == 'instr_len'][0]
     self._native = ops.ext().NativeBoardServer(
         b.base, b.HDR, b.in_bytes, b.slot_out_bytes, b.S, b.M, instr_off,
@@ -348,6 +368,18 @@ class BoardServer(object):
         exe.get(True, 0) if m.use_instruction else 0,
         m.device.index if m.device.index is not None else
         self.torch.cuda.current_device())
+    if self.depth == 2:
+      self._sets.append(self._buffers())
+      in_dev, out_dev, mask_dev, mask_host, _ = self._sets[1]
+      with self.torch.no_grad():
+        for v in variants:
+          self._graphs[(1, v)] = self._capture(v, k=1)
+      self._native.add_buffer(
+          in_dev.data_ptr(), out_dev.data_ptr(), mask_dev.data_ptr(),
+          mask_host.data_ptr(),
+          self._graphs[(1, False)].raw_cuda_graph_exec(),
+          self._graphs[(1, True)].raw_cuda_graph_exec()
+          if m.use_instruction else 0)
     self._native.set_batching(self.min_ready, self.gather_us)
     self._native.start()
 

@@ -87,7 +87,62 @@ def _worker(board, slot, rows, n_steps, seed):
   os._exit(0)
 
 
-def test_native_thread_serves_forked_workers(cuda):
+def test_depth2_native_loop_matches_python_loop(cuda):
+  """Two batches in flight over two buffer sets (the depth-2 native loop):
+  slot 0's batch is still in flight when slot 2's is launched on the
+  second set, is answered while it runs, and both answers match the Python
+  loop serving the same two requests one after the other."""
+  from scalable_agent_amd import ops
+  board = InferenceBoard(3, 4, SHAPE, 9)
+  server = BoardServer(_model(cuda), board)
+  server.prepare(has_instr=False)
+  server._sets.append(server._buffers())
+  with torch.no_grad():
+    g1 = server._capture(False, k=1)
+  cl0 = _fill(board, 0, 4, seed=6)
+  cl2 = _fill(board, 2, 2, seed=7)
+  outs = []
+  for loop in ('python', 'native'):
+    server.c.zero_()
+    server.h.zero_()
+    if loop == 'python':
+      for s in (0, 2):
+        native.atomic_store_u32(board.state_addr(s), REQUEST)
+        assert server.serve_once(timeout_ms=10)
+    else:
+      b, m = board, server.model
+      off = [o for n, _, _, o, _ in b.in_fields if n == 'instr_len'][0]
+      ns = ops.ext().NativeBoardServer(
+          b.base, b.HDR, b.in_bytes, b.slot_out_bytes, b.S, b.M, off,
+          server.in_dev.data_ptr(), server.out_dev.data_ptr(),
+          server.mask_dev.data_ptr(), server.mask_host.data_ptr(),
+          m.stream.cuda_stream, server._graphs[False].raw_cuda_graph_exec(),
+          0, cuda.index or 0)
+      in1, out1, mask1, mhost1, _ = server._sets[1]
+      ns.add_buffer(in1.data_ptr(), out1.data_ptr(), mask1.data_ptr(),
+                    mhost1.data_ptr(), g1.raw_cuda_graph_exec(), 0)
+      assert ns.depth() == 2
+      native.atomic_store_u32(board.state_addr(0), REQUEST)
+      assert ns.serve_once(10, drain=False)
+      assert board.state(0) == REQUEST  # in flight, not answered yet
+      native.atomic_store_u32(board.state_addr(2), REQUEST)
+      assert ns.serve_once(10, drain=False)  # launches slot 2, answers 0
+      assert board.state(0) == RESPONSE and board.state(2) == REQUEST
+      assert ns.serve_once(10)  # nothing new: answers the batch in flight
+      assert ns.batches() == 2 and ns.rows_served() == 6
+    assert board.state(0) == RESPONSE and board.state(2) == RESPONSE
+    outs.append([x.copy() for cl in (cl0, cl2) for x in cl.wait()[1:]] +
+                [server.c.cpu().clone()])
+  for a, b in zip(outs[0], outs[1]):
+    assert np.array_equal(np.asarray(a), np.asarray(b))
+  st = outs[1][-1]
+  assert float(st[0:4].abs().sum()) > 0.0 and float(st[8:10].abs().sum()) > 0
+  assert float(st[4:8].abs().sum()) == 0.0 and float(st[10:].abs().sum()) == 0
+  board.close()
+
+
+@pytest.mark.parametrize('depth', [1, 2])
+def test_native_thread_serves_forked_workers(cuda, depth):
   board = InferenceBoard(4, 8, SHAPE, 9)
   # the forked workers only use the shared board and futexes, never HIP
   ctx = mp.get_context('fork')
@@ -95,9 +150,9 @@ def test_native_thread_serves_forked_workers(cuda):
            for s, r in ((0, 8), (1, 5), (3, 2))]
   for p in procs:
     p.start()
-  server = BoardServer(_model(cuda), board)
+  server = BoardServer(_model(cuda), board, depth=depth)
   server.start()
-  assert server.native
+  assert server.native and server._native.depth() == depth
   deadline = time.time() + 60
   while any(p.is_alive() for p in procs) and time.time() < deadline:
     server.check()
