@@ -523,11 +523,6 @@ def train(flags):
   os.makedirs(logdir, exist_ok=True)
   writer = SummaryWriter(logdir) if rank == 0 else None
 
-  if flags.learner_cu_reserve > 0 and device.type == 'cuda':
-    # before any capture: the persistent grids' sizes are baked into the
-    # learner's graphs
-    from . import ops
-    ops.ext().cf32_cu_reserve(min(16, flags.learner_cu_reserve))
   agent = _make_agent(flags, num_actions, frame_shape, device, flags.seed)
   learner = Learner(agent, flags, device, world_size=world)
   restored = ckpt_lib.restore(flags.logdir, learner)

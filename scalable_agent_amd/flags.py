@@ -134,10 +134,6 @@ def build_parser() -> argparse.ArgumentParser:
                       'slots requesting, the server waits up to this many '
                       'microseconds for more before launching (every launch '
                       'runs the whole board).  0 = launch at once.')
-  p.add_argument('--learner_cu_reserve', type=int, default=0,
-                 help='CUs per XCD (0-16) that the learner\'s persistent conv '
-                      'grids leave free, so the inference board\'s kernels '
-                      'find room beside them (profiles/r6_e2e.md).')
   p.add_argument('--inference_board_depth', type=int, default=1,
                  choices=(1, 2),
                  help='Inference board: batches in flight in the native '
