@@ -13,6 +13,11 @@
 //   hipGraphLaunch of the captured graph (plain or with-instruction variant,
 //   picked from the instruction lengths) -> D2H of each ready slot's output
 //   block -> wait on this batch's event -> RESPONSE + futex wake per slot.
+// The row mask normally lives in the board's input region (one H2D carries
+// it), and with set_direct_output the graph's epilogue writes the ready rows
+// straight into the registered host board, so a launch is ONE copy and one
+// graph: the per-slot D2H copies cost ~40-150 us each on the queue
+// (profiles/r6_e2e.md).
 //
 // Depth 2 (add_buffer, a second set of device buffers and graphs): batch k+1
 // is enqueued before batch k is answered.  Its input H2D runs on a copy
@@ -91,6 +96,18 @@ class NativeBoardServer {
     b.instr = reinterpret_cast<hipGraphExec_t>(exec_instr);
     TORCH_CHECK(b.in_dev && b.out_dev && b.mask_dev && b.mask_host, "null board pointer");
     TORCH_CHECK(b.plain || b.instr, "no captured inference graph");
+    // a host mask inside the board's input region (its row_mask field)
+    // travels with the input H2D; its device copy must then be the same
+    // offset of in_dev
+    const uint8_t* mh = reinterpret_cast<const uint8_t*>(b.mask_host);
+    const uint8_t* in0 = base_ + hdr_;
+    if (mh >= in0 && mh < in0 + in_bytes_) {
+      TORCH_CHECK(mh + sizeof(float) * S_ * M_ <= in0 + in_bytes_ &&
+                      static_cast<uint8_t*>(b.mask_dev) ==
+                          static_cast<uint8_t*>(b.in_dev) + (mh - in0),
+                  "a mask inside the board's inputs must be the same field of in_dev");
+      b.mask_in_board = true;
+    }
     bufs_.push_back(b);
   }
 
@@ -121,6 +138,9 @@ class NativeBoardServer {
     min_ready_ = min_ready < 1 ? 1 : (min_ready > S_ ? S_ : min_ready);
     gather_us_ = gather_us < 0 ? 0 : (gather_us > 100000 ? 100000 : gather_us);
   }
+  // direct output: the graph's epilogue writes the ready rows into the
+  // host board itself, so no D2H copy per slot (before start)
+  void set_direct_output(bool on) { direct_out_ = on; }
   int64_t gathered() const { return gathered_.load(); }
   int64_t depth() const { return static_cast<int64_t>(bufs_.size()); }
   int64_t batches() const { return batches_.load(); }
@@ -245,23 +265,27 @@ class NativeBoardServer {
       if (!b.in_ev) check(hipEventCreateWithFlags(&b.in_ev, hipEventDisableTiming), "hipEventCreate");
       check(hipMemcpyAsync(b.in_dev, base_ + hdr_, in_bytes_, hipMemcpyHostToDevice, copy_),
             "board H2D");
-      check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice, copy_),
-            "mask H2D");
+      if (!b.mask_in_board)
+        check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice,
+                             copy_),
+              "mask H2D");
       check(hipEventRecord(b.in_ev, copy_), "hipEventRecord");
       check(hipStreamWaitEvent(stream_, b.in_ev, 0), "hipStreamWaitEvent");
     } else {
       check(hipMemcpyAsync(b.in_dev, base_ + hdr_, in_bytes_, hipMemcpyHostToDevice, stream_),
             "board H2D");
-      check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice,
-                           stream_),
-            "mask H2D");
+      if (!b.mask_in_board)
+        check(hipMemcpyAsync(b.mask_dev, b.mask_host, sizeof(float) * R, hipMemcpyHostToDevice,
+                             stream_),
+              "mask H2D");
     }
     check(hipGraphLaunch(g, stream_), "hipGraphLaunch");
     uint8_t* host_out = base_ + hdr_ + in_bytes_;
-    for (int64_t s : ready_)
-      check(hipMemcpyAsync(host_out + s * so_, b.out_dev + s * so_, so_, hipMemcpyDeviceToHost,
-                           stream_),
-            "slot D2H");
+    if (!direct_out_)
+      for (int64_t s : ready_)
+        check(hipMemcpyAsync(host_out + s * so_, b.out_dev + s * so_, so_, hipMemcpyDeviceToHost,
+                             stream_),
+              "slot D2H");
     // an event of this batch, not a stream synchronise: the learner thread
     // keeps enqueueing weight publishes onto the same stream meanwhile
     // (a stream-wide synchronise held it off: 15.6 ms of learner-loop host
@@ -301,6 +325,7 @@ class NativeBoardServer {
     float* mask_host = nullptr;
     hipGraphExec_t plain = nullptr, instr = nullptr;
     hipEvent_t done_ev = nullptr, in_ev = nullptr;
+    bool mask_in_board = false;
   };
 
   uint8_t* base_;
@@ -313,6 +338,7 @@ class NativeBoardServer {
   std::vector<int64_t> ready_, pend_slots_;
   std::vector<char> inflight_;
   bool pending_ = false;
+  bool direct_out_ = false;
   int pend_buf_ = 0;
   int64_t pend_rows_ = 0;
   std::thread thread_;
@@ -343,6 +369,7 @@ void register_board_server(pybind11::module& m) {
            py::arg("mask_dev"), py::arg("mask_host"), py::arg("exec_plain"),
            py::arg("exec_instr"))
       .def("depth", &NativeBoardServer::depth)
+      .def("set_direct_output", &NativeBoardServer::set_direct_output, py::arg("on"))
       .def("set_batching", &NativeBoardServer::set_batching, py::arg("min_ready"),
            py::arg("gather_us"))
       .def("gathered", &NativeBoardServer::gathered)

@@ -97,12 +97,19 @@ __global__ __launch_bounds__(256) void actor_head_sample_kernel(
 //   c[r] = mask[r] > 0 ? c2[r] : c[r], h likewise (r < R, H columns);
 //   out[(r / M) * slot_bytes + off[f] + (r % M) * per[f] + b] = src_f[r][b]
 // for every field f < nf (per-row byte counts multiples of 4).
+// masked_only: rows whose mask is 0 are not packed (`out` may then be the
+// device view of the board's registered HOST output region: a slot that did
+// not ask may be being read by its worker right now), and each packing
+// thread ends with a system-scope fence so the host sees the rows once the
+// launch's completion event fires.  This replaces one D2H copy per ready
+// slot (each ~6 us, but 40-150 us apart on the queue: profiles/r6_e2e.md).
 constexpr int kBoardFields = 6;
 struct BoardEpi {
   const uint32_t* src[kBoardFields];
   int per_dw[kBoardFields];  // dwords per row
   int off_dw[kBoardFields];  // dword offset of the field in a slot block
   int nf, R, M, slot_dw, H;
+  int masked_only;
   const float* mask;         // [R]
   const float* c2;
   const float* h2;
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(256) void board_epilogue_kernel(BoardEpi a) {
       a.h[o] = a.h2[o];
     }
   }
+  if (a.masked_only && !keep) return;  // uniform per workgroup
   const int s = r / a.M, m = r - s * a.M;
   uint32_t* dst = a.out + static_cast<int64_t>(s) * a.slot_dw;
   for (int f = 0; f < a.nf; ++f) {
@@ -130,6 +138,7 @@ __global__ __launch_bounds__(256) void board_epilogue_kernel(BoardEpi a) {
     uint32_t* d = dst + a.off_dw[f] + m * per;
     for (int j = threadIdx.x; j < per; j += blockDim.x) d[j] = src[j];
   }
+  if (a.masked_only) __threadfence_system();
 }
 
 }  // namespace
@@ -138,9 +147,11 @@ int board_epilogue_max_fields() { return kBoardFields; }
 
 void board_epilogue_launch(const void* const* src, const int* per_dw, const int* off_dw, int nf,
                            int R, int M, int slot_dw, int H, const float* mask, const float* c2,
-                           const float* h2, float* c, float* h, void* out, hipStream_t stream) {
+                           const float* h2, float* c, float* h, void* out, int masked_only,
+                           hipStream_t stream) {
   if (R <= 0) return;
   BoardEpi a{};
+  a.masked_only = masked_only;
   for (int f = 0; f < nf && f < kBoardFields; ++f) {
     a.src[f] = static_cast<const uint32_t*>(src[f]);
     a.per_dw[f] = per_dw[f];

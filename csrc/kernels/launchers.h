@@ -189,7 +189,8 @@ int actor_head_max_actions();
 int board_epilogue_max_fields();
 void board_epilogue_launch(const void* const* src, const int* per_dw, const int* off_dw, int nf,
                            int R, int M, int slot_dw, int H, const float* mask, const float* c2,
-                           const float* h2, float* c, float* h, void* out, hipStream_t stream);
+                           const float* h2, float* c, float* h, void* out, int masked_only,
+                           hipStream_t stream);
 void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
                               const float* wb, const float* bb, float* logits,
                               float* baseline, int64_t* action, int B, int A,

@@ -234,9 +234,12 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
 // (or [R, 1]) > 0 from c2 / h2, and every tensor of `fields` ([R, ...], any
 // dtype, 4-byte multiple per row) packed into `out` (uint8, S slot blocks of
 // slot_bytes) at byte offset offs[f] + (r % M) * row_bytes(f) of slot r / M.
+// out_addr != 0: pack into that device-accessible address instead of `out`
+// (the board's registered host output region, out.numel() bytes long; only
+// the rows whose mask is set are written, then fenced at system scope).
 void board_epilogue(std::vector<at::Tensor> fields, std::vector<int64_t> offs, at::Tensor out,
                     int64_t M, int64_t slot_bytes, at::Tensor mask, at::Tensor c2,
-                    at::Tensor h2, at::Tensor c, at::Tensor h) {
+                    at::Tensor h2, at::Tensor c, at::Tensor h, int64_t out_addr) {
   const int nf = static_cast<int>(fields.size());
   TORCH_CHECK(nf >= 1 && nf <= sa::board_epilogue_max_fields() &&
               static_cast<int>(offs.size()) == nf, "board_epilogue: 1..6 fields with offsets");
@@ -249,7 +252,8 @@ void board_epilogue(std::vector<at::Tensor> fields, std::vector<int64_t> offs, a
   TORCH_CHECK(mask.numel() == R, "mask must have R elements");
   TORCH_CHECK(M >= 1 && R % M == 0 && slot_bytes % 4 == 0 &&
               out.numel() >= (R / M) * slot_bytes, "board geometry");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 4 == 0, "out 4-byte aligned");
+  void* dst = out_addr ? reinterpret_cast<void*>(out_addr) : out.data_ptr();
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dst) % 4 == 0, "out 4-byte aligned");
   const void* src[8];
   int per[8], off[8];
   for (int f = 0; f < nf; ++f) {
@@ -267,7 +271,8 @@ void board_epilogue(std::vector<at::Tensor> fields, std::vector<int64_t> offs, a
   sa::board_epilogue_launch(src, per, off, nf, static_cast<int>(R), static_cast<int>(M),
                             static_cast<int>(slot_bytes / 4), static_cast<int>(H),
                             mask.data_ptr<float>(), c2.data_ptr<float>(), h2.data_ptr<float>(),
-                            c.data_ptr<float>(), h.data_ptr<float>(), out.data_ptr(), stream());
+                            c.data_ptr<float>(), h.data_ptr<float>(), dst, out_addr != 0,
+                            stream());
 }
 
 // C[:, :N] (+)= op(A) op(B) with the fused epilogue of kernels/gemm_f32.h.
@@ -515,7 +520,7 @@ void register_learner_ops(pybind11::module& m) {
   m.def("board_epilogue", &board_epilogue, pybind11::arg("fields"), pybind11::arg("offs"),
         pybind11::arg("out"), pybind11::arg("M"), pybind11::arg("slot_bytes"),
         pybind11::arg("mask"), pybind11::arg("c2"), pybind11::arg("h2"), pybind11::arg("c"),
-        pybind11::arg("h"));
+        pybind11::arg("h"), pybind11::arg("out_addr") = 0);
   m.def("actor_head_sample", &actor_head_sample, pybind11::arg("h"),
         pybind11::arg("wp"), pybind11::arg("bp"), pybind11::arg("wb"),
         pybind11::arg("bb"), pybind11::arg("seed"), pybind11::arg("offset"),

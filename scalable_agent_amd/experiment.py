@@ -364,8 +364,17 @@ class _TrajFeeder(object):
 
 # --------------------------------------------------------------- train
 # --actor_groups=-1 on a GPU: from this many actors on, CPU actor groups of
-# ~50 envs with the inference board instead of one GPU group process
-AUTO_BOARD_ACTORS = 128
+# ~AUTO_GROUP_ENVS envs (at least 2 groups) with the inference board instead
+# of one GPU group process (profiles/r6_e2e.md: config #2, 48 actors,
+# 335-352 K vs 291-305 K frames/s; config #4, 150 actors, 540-551 K with
+# bf16 inference)
+AUTO_BOARD_ACTORS = 32
+AUTO_GROUP_ENVS = 40
+
+
+def auto_board_groups(num_actors):
+  """CPU actor groups the auto layout uses with the inference board."""
+  return max(2, -(-num_actors // AUTO_GROUP_ENVS))
 
 
 def _checker(groups, server):
@@ -449,11 +458,10 @@ def train(flags):
               (flags.device == 'auto' and torch.cuda.device_count() > 0))
     n_groups = 1 if on_gpu else 0
     if on_gpu and flags.num_actors >= AUTO_BOARD_ACTORS:
-      # many actors: one GPU group process is Python-bound (~300 K frames/s
-      # at 48 or 150 actors); CPU groups of ~50 envs posting to the
-      # learner-process inference board scale further (150 actors, 3 groups:
-      # 422 K fp32 / 511 K bf16 inference)
-      n_groups = -(-flags.num_actors // 50)
+      # one GPU group process is Python-bound (~300 K frames/s at 48 or 150
+      # actors); CPU groups posting to the learner-process inference board
+      # scale further
+      n_groups = min(auto_board_groups(flags.num_actors), flags.num_actors)
       flags.inference_server = True
   flags.actor_groups = n_groups
   use_groups = (n_groups > 0 and not distributed_actors and
@@ -483,9 +491,11 @@ def train(flags):
     if flags.inference_server:
       from .runtime.actor_group import board_geometry
       from .runtime.inference_board import InferenceBoard
+      lanes = max(1, min(flags.inference_lanes, n_groups))
       slots, rows = board_geometry(flags.num_actors, n_groups,
-                                   flags.actor_group_splits)
-      board = InferenceBoard(slots, rows, frame_shape, num_actions)
+                                   flags.actor_group_splits, lanes)
+      board = [InferenceBoard(slots, rows, frame_shape, num_actions)
+               for _ in range(lanes)]
       group_dev = 'cpu (board served by the learner process)'
     groups = ActorGroups(
         flags, level_names, actors_levels, actor_seeds, tq, shared_w_name,
@@ -567,15 +577,22 @@ def train(flags):
       from .runtime.inference_board import BoardServer
       inf_device = (device if flags.inference_device == 'auto' else
                     torch.device(flags.inference_device))
-      inf_agent = _make_agent(
-          flags, num_actions, frame_shape, inf_device, flags.seed,
-          dtype=(flags.dtype if flags.inference_dtype == 'auto' else
-                 flags.inference_dtype))
-      model = inference_lib.InferenceModel(inf_agent, inf_device, use_instr,
-                                           seed=flags.seed + 17 * rank)
+      from .runtime.inference_board import BoardLanes
+      servers = []
+      for lane, lane_board in enumerate(board):
+        inf_agent = _make_agent(
+            flags, num_actions, frame_shape, inf_device, flags.seed,
+            dtype=(flags.dtype if flags.inference_dtype == 'auto' else
+                   flags.inference_dtype))
+        lane_model = inference_lib.InferenceModel(
+            inf_agent, inf_device, use_instr,
+            seed=flags.seed + 17 * rank + 7919 * lane)
+        servers.append(BoardServer(lane_model, lane_board,
+                                   gather_us=flags.inference_gather_us,
+                                   depth=flags.inference_board_depth))
+      # the train loop publishes to every lane's model
+      server = model = BoardLanes(servers)
       model.publish(learner.flat.params)
-      server = BoardServer(model, board, gather_us=flags.inference_gather_us,
-                           depth=flags.inference_board_depth)
       server.prepare(has_instr=use_instr)
       server.start()
     else:
@@ -841,8 +858,8 @@ def train(flags):
     if infer is not None:
       infer.close()
     if groups is not None:
-      if board is not None:
-        board.close()
+      for b in board or ():
+        b.close()
       groups.close()
       if server is not None:
         server.stop()

@@ -120,11 +120,11 @@ def build_parser() -> argparse.ArgumentParser:
                       'processes (each: its envs stepped in parallel, one '
                       'captured inference graph per step, writes into the '
                       'trajectory queue); 0 = actor threads in the learner '
-                      'process; -1 = auto: on a GPU 1 group (more GPU '
-                      'processes share the card badly: profiles/'
-                      'r2_e2e_actors.md), or from 128 actors on CPU groups '
-                      'of ~50 envs with --inference_server '
-                      '(profiles/r6_e2e.md); threads on CPU.')
+                      'process; -1 = auto: on a GPU from 32 actors on CPU '
+                      'groups of ~40 envs (at least 2) with '
+                      '--inference_server (profiles/r6_e2e.md), below that '
+                      '1 GPU group (more GPU processes share the card badly: '
+                      'profiles/r2_e2e_actors.md); threads on CPU.')
   p.add_argument('--inference_server', type=_str2bool, default=False,
                  help='Actor groups stay CPU-only and post their rows to a '
                       'shared-memory inference board served by a thread of '
@@ -134,6 +134,12 @@ def build_parser() -> argparse.ArgumentParser:
                       'slots requesting, the server waits up to this many '
                       'microseconds for more before launching (every launch '
                       'runs the whole board).  0 = launch at once.')
+  p.add_argument('--inference_lanes', type=int, default=2,
+                 help='Inference board: boards served side by side, each by '
+                      'its own thread, model snapshot and stream (actor '
+                      'group g posts to lane g %% lanes; at most one lane per '
+                      'group).  2 measured 1-3 %% above 1 at configs #2 and #4 '
+                      '(profiles/r6_e2e.md).')
   p.add_argument('--inference_board_depth', type=int, default=1,
                  choices=(1, 2),
                  help='Inference board: batches in flight in the native '

@@ -215,13 +215,15 @@ class _Done(object):
     pass
 
 
-def board_geometry(num_actors, groups, splits):
-  """(slots, rows per slot) of the inference board for this actor layout."""
+def board_geometry(num_actors, groups, splits, lanes=1):
+  """(slots, rows per slot) of each inference board for this actor layout:
+  group g posts to board g % lanes, slots from (g // lanes) * splits."""
   parts = split_actors(num_actors, groups)
   splits = max(1, int(splits))
   rows = max(max(len(p) for p in split_actors(len(g), min(splits, len(g))))
              for g in parts)
-  return len(parts) * splits, rows
+  lanes = max(1, min(int(lanes), len(parts)))
+  return -(-len(parts) // lanes) * splits, rows
 
 
 def split_actors(num_actors, groups):
@@ -550,7 +552,11 @@ class ActorGroups(object):
   def __init__(self, flags, level_names, actor_levels, actor_seeds, tq,
                weights, frame_shape, action_set, use_instr, device_str,
                dtype, board=None):
+    """board: None (GPU groups), one InferenceBoard, or a list of them (one
+    per lane: group g posts to board g % len(list), board_geometry)."""
     import multiprocessing
+    boards = (None if board is None else
+              list(board) if isinstance(board, (list, tuple)) else [board])
     ctx = multiprocessing.get_context('fork')
     self.tq = tq
     self.counters = ctx.RawArray('q', max(1, flags.actor_groups))
@@ -564,8 +570,10 @@ class ActorGroups(object):
                   num_actions=len(action_set), action_set=action_set,
                   frame_shape=tuple(frame_shape), use_instr=use_instr,
                   unroll_length=flags.unroll_length, dtype=dtype,
-                  splits=flags.actor_group_splits, board=board,
-                  slot0=gid * max(1, flags.actor_group_splits))
+                  splits=flags.actor_group_splits,
+                  board=boards[gid % len(boards)] if boards else None,
+                  slot0=(gid // len(boards) if boards else gid) *
+                  max(1, flags.actor_group_splits))
       p = ctx.Process(target=_group_main,
                       args=(gid, spec, tq, weights, self.counters, device_str),
                       daemon=False, name='actor-group-%d' % gid)

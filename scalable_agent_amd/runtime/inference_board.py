@@ -9,7 +9,9 @@ inference on the GPU (a second GPU context per group) or, with
               flag, per-slot state words (0 idle, 1 request, 2 response) and
               per-slot row counts
     inputs  : every input field for ALL rows (slot s owns rows [s*M, s*M+M)),
-              field-major - ONE H2D copy moves the whole board to the device
+              field-major - ONE H2D copy moves the whole board to the device,
+              the server's row mask (row_mask, written by the server only)
+              included
     outputs : slot-major [action | logits | baseline | c | h] per slot, so a
               slot's response is ONE D2H copy and responding to one slot
               never overwrites the rows another worker is still reading
@@ -17,7 +19,9 @@ inference on the GPU (a second GPU context per group) or, with
     wait for request slots -> mask of their rows -> H2D inputs + mask ->
     ONE captured graph over all rows (torso, core, heads + Gumbel sampler; the
     LSTM state of every row resident on the device, updated only where the
-    mask is set) -> D2H of each ready slot's outputs -> state 2 + futex wake
+    mask is set) -> the masked rows' outputs -> state 2 + futex wake.  On a
+    GPU the graph's epilogue writes those rows straight into the registered
+    host board (no D2H copy per slot); elsewhere they are copied back.
     On a GPU with the HIP backend the loop is a C++ thread
     (csrc/board_server.cpp, no Python and no GIL per batch); the graphs are
     captured here first.  SA_BOARD_NATIVE=0 keeps the Python thread.  With
@@ -63,7 +67,8 @@ class InferenceBoard(object):
     fields = [('last_action', (), np.int64), ('reward', (), np.float32),
               ('done', (), np.bool_), ('frame', tuple(frame_shape), np.uint8),
               ('instr_ids', (int(instr_len),), np.int64),
-              ('instr_len', (), np.int64)]
+              ('instr_len', (), np.int64),
+              ('row_mask', (), np.float32)]  # written by the server only
     self.in_fields, off = [], 0
     for name, shape, dt in fields:
       nb = R * int(np.prod(shape, dtype=np.int64)) * np.dtype(dt).itemsize
@@ -185,8 +190,15 @@ class BoardServer(object):
       self.pinned = _hip_host_register(b.base + b.HDR, b.in_bytes + b.out_bytes)
     self.c = torch.zeros(b.R, b.core, device=dev)
     self.h = torch.zeros(b.R, b.core, device=dev)
+    # direct output: the graph's epilogue packs the ready rows into the
+    # registered host board itself (HIP backend on a GPU)
+    self._out_addr = 0
+    if self.pinned and getattr(model.agent, 'backend', '') == 'hip':
+      from .traj_queue import _hip_host_device_ptr
+      d = _hip_host_device_ptr(b.base + b.HDR)  # the registration's start
+      self._out_addr = d + b.in_bytes if d else 0
     # buffer set 0 (set 1 is allocated by the depth-2 native loop)
-    self._sets = [self._buffers()]
+    self._sets = [self._buffers(0)]
     (self.in_dev, self.out_dev, self.mask_dev, self.mask_host,
      self._dev_in) = self._sets[0]
     # graphs: has_instr -> graph over set 0, (1, has_instr) -> over set 1
@@ -198,22 +210,32 @@ class BoardServer(object):
     self._batches = 0
     self._rows = 0
 
-  def _buffers(self):
-    """One buffer set: device inputs, outputs, row mask (device + pinned
-    host) and the typed views of the inputs."""
+  @property
+  def direct_out(self):
+    """True when the graph writes the responses into the host board."""
+    return self._out_addr != 0
+
+  def _buffers(self, k):
+    """Buffer set k: device inputs, outputs, row mask (device view inside
+    the inputs + host) and the typed views of the inputs.  Set 0's host mask
+    is the board's own row_mask field, so the input H2D carries it; set 1
+    (depth 2) has a pinned mask of its own, copied after its inputs."""
     torch, b, dev = self.torch, self.board, self.model.device
     # zero-filled: the capture's warm-up steps read the board before any
-    # worker wrote it
+    # worker wrote it (and a zero mask packs no rows)
     in_dev = torch.zeros(b.in_bytes, dtype=torch.uint8, device=dev)
     out_dev = torch.zeros(b.out_bytes, dtype=torch.uint8, device=dev)
     tdt = lambda dt: torch.from_numpy(np.empty(0, dt)).dtype
     dev_in = [in_dev[o:o + nb].view(tdt(dt)).view(*s)
               for n, s, dt, o, nb in b.in_fields]
-    mask_host = torch.zeros(b.R, dtype=torch.float32)
-    if self.cuda:
-      mask_host = mask_host.pin_memory()
-    mask_dev = torch.zeros(b.R, 1, device=dev)
-    return in_dev, out_dev, mask_dev, mask_host, dev_in
+    mask_dev = dev_in[-1].view(b.R, 1)
+    if k == 0:
+      mask_host = torch.from_numpy(b.inputs['row_mask'])
+    else:
+      mask_host = torch.zeros(b.R, dtype=torch.float32)
+      if self.cuda:
+        mask_host = mask_host.pin_memory()
+    return in_dev, out_dev, mask_dev, mask_host, dev_in[:-1]
 
   @property
   def batches(self):
@@ -252,7 +274,7 @@ class BoardServer(object):
       C.board_epilogue([action, logits, baseline, c2, h2],
                        [o for _, _, _, o, _ in b.out_fields], out_dev,
                        b.M, b.slot_out_bytes, mask_dev, c2, h2, self.c,
-                       self.h)
+                       self.h, out_addr=self._out_addr)
       return
     m = mask_dev
     self.c.copy_(torch.where(m > 0, c2, self.c))
@@ -306,14 +328,12 @@ class BoardServer(object):
                      int(b.inputs['instr_len'].max(initial=0)) > 0)
     with torch.no_grad(), m._lock:
       if not self.cuda:
-        self.in_dev.copy_(self._host_in)
-        self.mask_dev.copy_(mask.view(-1, 1))
+        self.in_dev.copy_(self._host_in)  # the row mask included
         self._body(has_instr)
         self._host_out.copy_(self.out_dev)
       else:
         with torch.cuda.stream(m.stream):
           self.in_dev.copy_(self._host_in, non_blocking=self.pinned)
-          self.mask_dev.copy_(mask.view(-1, 1), non_blocking=True)
           if self.use_graph:
             g = self._graphs.get(has_instr)
             if g is None:
@@ -322,7 +342,7 @@ class BoardServer(object):
           else:
             self._body(has_instr)
           so = b.slot_out_bytes
-          for s in ready:
+          for s in ready if not self.direct_out else ():
             self._host_out[s * so:(s + 1) * so].copy_(
                 self.out_dev[s * so:(s + 1) * so], non_blocking=self.pinned)
           m.stream.synchronize()
@@ -369,7 +389,7 @@ class BoardServer(object):
         m.device.index if m.device.index is not None else
         self.torch.cuda.current_device())
     if self.depth == 2:
-      self._sets.append(self._buffers())
+      self._sets.append(self._buffers(1))
       in_dev, out_dev, mask_dev, mask_host, _ = self._sets[1]
       with self.torch.no_grad():
         for v in variants:
@@ -380,6 +400,7 @@ class BoardServer(object):
           self._graphs[(1, False)].raw_cuda_graph_exec(),
           self._graphs[(1, True)].raw_cuda_graph_exec()
           if m.use_instruction else 0)
+    self._native.set_direct_output(self.direct_out)
     self._native.set_batching(self.min_ready, self.gather_us)
     self._native.start()
 
@@ -406,3 +427,45 @@ class BoardServer(object):
       self._native.stop()
     if self._thread is not None:
       self._thread.join(timeout=10)
+
+
+class BoardLanes(object):
+  """Several boards served side by side (`--inference_lanes`): lane l is its
+  own board, BoardServer (native thread), InferenceModel (weight snapshot
+  and stream), so the lanes' graphs run concurrently on the GPU.  A board
+  launch at a few dozen rows is ~25 small kernels that leave most CUs idle
+  (profiles/r6_e2e.md), so a second lane adds launches instead of waiting
+  behind the first.  Same interface as one BoardServer for the train loop,
+  plus publish() to every lane's model."""
+
+  def __init__(self, servers):
+    self.servers = list(servers)
+
+  def publish(self, flat_params):
+    for s in self.servers:
+      s.model.publish(flat_params)
+
+  def prepare(self, has_instr=False):
+    for s in self.servers:
+      s.prepare(has_instr=has_instr)
+
+  def start(self):
+    for s in self.servers:
+      s.start()
+
+  def check(self):
+    for s in self.servers:
+      s.check()
+
+  def stop(self):
+    for s in self.servers:
+      s.stop()
+
+  @property
+  def batches(self):
+    return sum(s.batches for s in self.servers)
+
+  @property
+  def rows_served(self):
+    return sum(s.rows_served for s in self.servers)
+

@@ -101,6 +101,21 @@ def _hip_host_register(address, nbytes):
   return fn(ctypes.c_void_p(address), ctypes.c_size_t(nbytes), 0) == 0
 
 
+def _hip_host_device_ptr(address):
+  """Device-side address of registered host memory (None if unavailable)."""
+  try:
+    lib = ctypes.CDLL('libamdhip64.so')
+  except OSError:
+    return None
+  fn = lib.hipHostGetDevicePointer
+  fn.restype = ctypes.c_int
+  fn.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+  out = ctypes.c_void_p()
+  if fn(ctypes.byref(out), ctypes.c_void_p(address), 0) != 0 or not out.value:
+    return None
+  return int(out.value)
+
+
 def _hip_host_unregister(address):
   try:
     lib = ctypes.CDLL('libamdhip64.so')

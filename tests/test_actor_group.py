@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 import torch
 
-from scalable_agent_amd.runtime.actor_group import SharedWeights, split_actors
+from scalable_agent_amd.runtime.actor_group import (SharedWeights, board_geometry,
+                                                   split_actors)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COMMON = ['--level_name=synthetic', '--unroll_length=5', '--device=cpu',
@@ -198,12 +199,24 @@ def test_inference_board_serves_forked_workers():
   board.close()
 
 
-def test_train_with_inference_server(tmp_path):
+@pytest.mark.parametrize('lanes', [1, 2])
+def test_train_with_inference_server(tmp_path, lanes):
   logdir = str(tmp_path / 'board')
   r = _run(['--logdir=' + logdir, '--num_actors=6', '--batch_size=2',
-            '--actor_groups=2', '--inference_server=true',
+            '--actor_groups=3', '--inference_server=true',
+            '--inference_lanes=%d' % lanes,
             '--total_environment_frames=480', '--save_summaries_secs=0'])
   assert r.returncode == 0, r.stderr[-3000:]
   assert 'board served by the learner process' in r.stderr
   assert 'Episode return' in r.stderr
+  assert 'inference board:' in r.stderr
   assert os.path.exists(os.path.join(logdir, 'checkpoint'))
+
+
+def test_board_geometry_lanes():
+  # 3 groups x 2 splits: one board of 6 slots, or lane 0 (groups 0, 2) and
+  # lane 1 (group 1) on boards of 4 slots; rows = the largest split
+  assert board_geometry(150, 3, 2) == (6, 25)
+  assert board_geometry(150, 3, 2, lanes=2) == (4, 25)
+  assert board_geometry(48, 2, 2, lanes=2) == (2, 12)
+  assert board_geometry(6, 3, 2, lanes=8) == (2, 1)  # lanes <= groups

@@ -37,16 +37,26 @@ def _fill(board, slot, rows, seed):
   return cl
 
 
+def _out_block(board, slot):
+  o0 = board.HDR + board.in_bytes + slot * board.slot_out_bytes
+  return board.buf[o0:o0 + board.slot_out_bytes]
+
+
 def test_native_loop_matches_python_loop(cuda):
+  """Also: the graph's epilogue writes the answer straight into the host
+  board (direct output, no D2H copy) and only the requesting slot's valid
+  rows: the other slots' output blocks and slot 1's unused row keep their
+  bytes."""
   board = InferenceBoard(3, 4, SHAPE, 9)
   server = BoardServer(_model(cuda), board)
-  assert server._native_ok()
+  assert server._native_ok() and server.direct_out
   server.prepare(has_instr=False)
   cl = _fill(board, 1, 3, seed=5)
   outs = []
   for loop in ('python', 'native'):
     server.c.zero_()
     server.h.zero_()
+    board.buf[board.HDR + board.in_bytes:] = 0x5A
     native.atomic_store_u32(board.state_addr(1), REQUEST)
     if loop == 'python':
       assert server.serve_once(timeout_ms=10)
@@ -60,8 +70,14 @@ def test_native_loop_matches_python_loop(cuda):
           server.mask_dev.data_ptr(), server.mask_host.data_ptr(),
           m.stream.cuda_stream, server._graphs[False].raw_cuda_graph_exec(),
           0, cuda.index or 0)
+      ns.set_direct_output(server.direct_out)
       assert ns.serve_once(10) and ns.rows_served() == 3
     assert board.state(1) == RESPONSE
+    for s in (0, 2):
+      assert np.all(_out_block(board, s) == 0x5A)
+    for name, _, _, o, nb in board.out_fields:  # slot 1's row 3 (unused)
+      per = nb // board.M
+      assert np.all(_out_block(board, 1)[o + 3 * per:o + 4 * per] == 0x5A)
     _, logits, baseline, c, h = [x.copy() for x in cl.wait()]
     outs.append((logits, baseline, c, h, server.c.cpu().clone()))
   for a, b in zip(outs[0], outs[1]):
@@ -96,7 +112,7 @@ def test_depth2_native_loop_matches_python_loop(cuda):
   board = InferenceBoard(3, 4, SHAPE, 9)
   server = BoardServer(_model(cuda), board)
   server.prepare(has_instr=False)
-  server._sets.append(server._buffers())
+  server._sets.append(server._buffers(1))
   with torch.no_grad():
     g1 = server._capture(False, k=1)
   cl0 = _fill(board, 0, 4, seed=6)
@@ -118,6 +134,7 @@ def test_depth2_native_loop_matches_python_loop(cuda):
           server.mask_dev.data_ptr(), server.mask_host.data_ptr(),
           m.stream.cuda_stream, server._graphs[False].raw_cuda_graph_exec(),
           0, cuda.index or 0)
+      ns.set_direct_output(server.direct_out)
       in1, out1, mask1, mhost1, _ = server._sets[1]
       ns.add_buffer(in1.data_ptr(), out1.data_ptr(), mask1.data_ptr(),
                     mhost1.data_ptr(), g1.raw_cuda_graph_exec(), 0)
@@ -203,4 +220,22 @@ def test_board_epilogue_matches_torch_ops(cuda):
   torch.cuda.synchronize()
   assert torch.equal(c, rc) and torch.equal(h, rh)
   assert torch.equal(out, ref)
+  # out_addr (the direct-output form): only the masked rows are packed, the
+  # bytes of every other row stay as they were
+  out2 = torch.full_like(out, 0x5A)
+  c, h = c0.clone(), h0.clone()
+  C.board_epilogue([action, logits, baseline, c2, h2],
+                   [o for _, _, _, o, _ in board.out_fields], out, M,
+                   board.slot_out_bytes, mask, c2, h2, c, h,
+                   out_addr=out2.data_ptr())
+  ref2 = torch.full_like(out, 0x5A)
+  v2, vr = ref2.view(S, board.slot_out_bytes), ref.view(S, board.slot_out_bytes)
+  for r in torch.nonzero(mask.view(-1) > 0).view(-1).tolist():
+    s_, m_ = divmod(r, M)
+    for _, _, _, o, nb in board.out_fields:
+      per = nb // M
+      v2[s_, o + m_ * per:o + (m_ + 1) * per] = vr[s_, o + m_ * per:o + (m_ + 1) * per]
+  torch.cuda.synchronize()
+  assert torch.equal(c, rc) and torch.equal(h, rh)
+  assert torch.equal(out2, ref2)
   board.close()

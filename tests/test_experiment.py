@@ -165,3 +165,12 @@ def test_train_with_grouped_env_workers(tmp_path, groups):
             '--envs_per_worker=3', '--actor_groups=%d' % groups])
   assert r.returncode == 0, r.stderr[-3000:]
   assert 'Episode return' in r.stderr
+
+
+def test_auto_board_layout_group_counts():
+  """--actor_groups=-1 on a GPU: CPU groups of ~40 envs (>= 2) with the
+  inference board from AUTO_BOARD_ACTORS actors on (profiles/r6_e2e.md)."""
+  from scalable_agent_amd import experiment as ex
+  assert ex.AUTO_BOARD_ACTORS == 32
+  assert [ex.auto_board_groups(n) for n in (32, 48, 80, 81, 150, 200)] == \
+      [2, 2, 2, 3, 4, 5]
