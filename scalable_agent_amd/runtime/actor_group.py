@@ -365,6 +365,14 @@ class ActorGroupWorker(object):
                      encode_instruction, py_process) for k in range(K)]
     wstate = {'version': -1}
     parent = os.getppid()
+    # measurement only (SA_MEASURE_KNOBS=1 SA_GROUP_PROFILE=1): where a
+    # group's time goes, logged every 2 s (profiles/r6_e2e.md)
+    from ..utils.knobs import measure_env
+    prof = ({'wait': 0.0, 'env': 0.0, 'record': 0.0, 'launch': 0.0,
+             'idle': 0.0, 'steps': 0, 't0': time.perf_counter()}
+            if measure_env('SA_GROUP_PROFILE') == '1' else None)
+    for sp in splits:
+      sp.prof = prof
     # the first snapshot (e.g. a restored checkpoint) before any inference
     while wstate['version'] <= 0:
       if os.getppid() != parent or self.tq.closed:
@@ -399,7 +407,24 @@ class ActorGroupWorker(object):
         self._sync_weights(model, wstate)
         sp.launch()
       if not progressed:
+        if prof is not None:
+          t_idle = time.perf_counter()
         time.sleep(0.0002)  # every split waits for queue room
+        if prof is not None:
+          prof['idle'] += time.perf_counter() - t_idle
+      if prof is not None and time.perf_counter() - prof['t0'] > 2.0:
+        dt = time.perf_counter() - prof['t0']
+        n = max(1, prof['steps'])
+        log.info('group %d profile: %d split steps/s; per split step: '
+                 'inference wait %.0f us, env step %.0f us, record %.0f us, '
+                 'launch %.0f us; idle %.0f %%', self.gid, n / dt,
+                 1e6 * prof['wait'] / n, 1e6 * prof['env'] / n,
+                 1e6 * prof['record'] / n, 1e6 * prof['launch'] / n,
+                 100 * prof['idle'] / dt)
+        for k in ('wait', 'env', 'record', 'launch', 'idle'):
+          prof[k] = 0.0
+        prof['steps'] = 0
+        prof['t0'] = time.perf_counter()
       if time.time() - last_check > 1.0:
         last_check = time.time()
         if os.getppid() != parent or self.tq.closed:
@@ -437,6 +462,7 @@ class _Split(object):
     self.instr = [env.initial_nocopy() for env in envs]
     self.cols = []
     self.t = 0
+    self.prof = None  # _loop's measurement dict (SA_GROUP_PROFILE)
 
   def try_begin_unroll(self):
     """Claims one column per env at once (or none): True when claimed
@@ -478,6 +504,12 @@ class _Split(object):
             self.instr[i])
 
   def launch(self):
+    t0 = time.perf_counter() if self.prof is not None else 0.0
+    self._launch()
+    if self.prof is not None:
+      self.prof['launch'] += time.perf_counter() - t0
+
+  def _launch(self):
     inp = self.vi.inputs
     inp['last_action'][:] = self.action
     inp['reward'][:] = self.reward
@@ -489,8 +521,13 @@ class _Split(object):
     self.vi.launch()
 
   def finish_step(self):
+    prof = self.prof
+    t0 = time.perf_counter() if prof is not None else 0.0
     pp = self.pp
     a, lg, b, c2, h2 = self.vi.wait()
+    if prof is not None:
+      t1 = time.perf_counter()
+      prof['wait'] += t1 - t0
     self.action[:] = a
     self.logits[:] = lg
     self.baseline[:] = b
@@ -525,8 +562,14 @@ class _Split(object):
       if d:
         self.run_ret[i] = 0.0
         self.run_step[i] = 0
+    if prof is not None:
+      t2 = time.perf_counter()
+      prof['env'] += t2 - t1
     self.t += 1
     self._record(self.t)
+    if prof is not None:
+      prof['record'] += time.perf_counter() - t2
+      prof['steps'] += 1
 
 
 def _group_main(gid, spec, tq, weights, counters, device_str):
