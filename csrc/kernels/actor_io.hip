@@ -31,17 +31,13 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
-__global__ __launch_bounds__(256) void actor_head_sample_kernel(
+// heads + Gumbel-max sample of one row (one wave)
+__device__ __forceinline__ void sample_row(
     const float* __restrict__ h, const float* __restrict__ wp,
     const float* __restrict__ bp, const float* __restrict__ wb,
     const float* __restrict__ bb, float* __restrict__ logits,
-    float* __restrict__ baseline, int64_t* __restrict__ action, int B, int A,
-    unsigned long long seed, unsigned long long offset,
-    const unsigned long long* __restrict__ offset_ptr) {
-  const int lane = threadIdx.x & 63;
-  if (offset_ptr != nullptr) offset = *offset_ptr;  // graph-replayed stream
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;  // whole wave exits together
+    float* __restrict__ baseline, int64_t* __restrict__ action, int A,
+    unsigned long long seed, unsigned long long offset, int row, int lane) {
   const float4 x = reinterpret_cast<const float4*>(h + (int64_t)row * 256)[lane];
   const float* w0 = wp + (4 * lane) * A;
   float acc[kMaxA + 1];
@@ -89,6 +85,32 @@ __global__ __launch_bounds__(256) void actor_head_sample_kernel(
   }
 }
 
+__global__ __launch_bounds__(256) void actor_head_sample_kernel(
+    const float* __restrict__ h, const float* __restrict__ wp,
+    const float* __restrict__ bp, const float* __restrict__ wb,
+    const float* __restrict__ bb, float* __restrict__ logits,
+    float* __restrict__ baseline, int64_t* __restrict__ action, int B, int A,
+    unsigned long long seed, unsigned long long offset,
+    unsigned long long* __restrict__ offset_ptr, int advance) {
+  const int lane = threadIdx.x & 63;
+  if (offset_ptr != nullptr) offset = *offset_ptr;  // graph-replayed stream
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row < B) sample_row(h, wp, bp, wb, bb, logits, baseline, action, A, seed, offset, row, lane);
+  // advance: the stream's counter pair {offset, waves done} moves to the next
+  // offset in this launch (no separate add kernel in the board's graph).
+  // Every wave counts itself once after its sampling (which consumed the
+  // offset it read); the last one stores offset + 1 and re-arms the count.
+  // Lane 0 only: divergent, so vector-memory atomics and stores.
+  if (advance && lane == 0) {
+    const unsigned long long waves = static_cast<unsigned long long>(gridDim.x) * 4;
+    const unsigned long long done = __hip_atomic_fetch_add(
+        offset_ptr + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == waves - 1) {
+      __hip_atomic_store(offset_ptr, offset + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(offset_ptr + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
 // Inference-board epilogue (runtime/inference_board.py BoardServer._body):
 // the per-row masked LSTM state update and the packing of every output field
 // into the board's slot-major output block, in ONE launch instead of two
@@ -177,12 +199,12 @@ void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
                               const float* wb, const float* bb, float* logits,
                               float* baseline, int64_t* action, int B, int A,
                               unsigned long long seed, unsigned long long offset,
-                              const unsigned long long* offset_ptr,
+                              unsigned long long* offset_ptr, int advance,
                               hipStream_t stream) {
   if (B <= 0) return;
   hipLaunchKernelGGL(actor_head_sample_kernel, dim3((B + 3) / 4), dim3(256), 0,
                      stream, h, wp, bp, wb, bb, logits, baseline, action, B, A,
-                     seed, offset, offset_ptr);
+                     seed, offset, offset_ptr, advance);
 }
 
 }  // namespace sa

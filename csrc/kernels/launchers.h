@@ -195,7 +195,7 @@ void actor_head_sample_launch(const float* h, const float* wp, const float* bp,
                               const float* wb, const float* bb, float* logits,
                               float* baseline, int64_t* action, int B, int A,
                               unsigned long long seed, unsigned long long offset,
-                              const unsigned long long* offset_ptr,
+                              unsigned long long* offset_ptr, int advance,
                               hipStream_t stream);
 
 // ---- calibration ----------------------------------------------------------

@@ -209,12 +209,19 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
   TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0 &&
               reinterpret_cast<uintptr_t>(wb.data_ptr()) % 16 == 0,
               "h / baseline w must be 16-byte aligned");
-  const unsigned long long* op = nullptr;
+  // offset_dev: one int64 (the caller advances it), or the pair {offset,
+  // waves done} the kernel advances itself (zero-initialised, then owned by
+  // the kernel)
+  unsigned long long* op = nullptr;
+  int advance = 0;
   if (offset_dev.has_value()) {
     LB_CHECK(*offset_dev);
-    TORCH_CHECK(offset_dev->scalar_type() == at::kLong && offset_dev->numel() == 1,
-                "offset_dev must be one int64");
-    op = reinterpret_cast<const unsigned long long*>(offset_dev->data_ptr());
+    TORCH_CHECK(offset_dev->scalar_type() == at::kLong &&
+                    (offset_dev->numel() == 1 || offset_dev->numel() == 2) &&
+                    offset_dev->is_contiguous(),
+                "offset_dev must be one int64 or a contiguous pair");
+    op = reinterpret_cast<unsigned long long*>(offset_dev->data_ptr());
+    advance = offset_dev->numel() == 2;
   }
   const c10::DeviceGuard guard(h.device());
   auto logits = at::empty({B, A}, h.options());
@@ -226,7 +233,8 @@ std::vector<at::Tensor> actor_head_sample(at::Tensor h, at::Tensor wp, at::Tenso
                                baseline.data_ptr<float>(),
                                action.data_ptr<int64_t>(), B, A,
                                static_cast<unsigned long long>(seed),
-                               static_cast<unsigned long long>(offset), op, stream());
+                               static_cast<unsigned long long>(offset), op, advance,
+                               stream());
   return {logits, baseline, action};
 }
 

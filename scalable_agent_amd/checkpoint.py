@@ -153,6 +153,8 @@ def restore_agent(agent, state):
   with torch.no_grad():
     for n, p in agent.named_parameters():
       p.copy_(params[names[n]].to(p.device))
+  if hasattr(agent, 'refresh_inference_cache'):
+    agent.refresh_inference_cache()  # an inference agent's bf16 copies
 
 
 def restore(logdir, learner):

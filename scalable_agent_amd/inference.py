@@ -47,6 +47,9 @@ class InferenceModel(object):
       self._gen = PhiloxStream(seed, device=self.device)
     else:
       self._gen = torch.Generator(device=self.device).manual_seed(seed)
+    # bf16 core weights cast once per publish, not per step (HIP bf16 agent)
+    if hasattr(self.agent, 'inference_cache'):
+      self.agent.inference_cache()
 
   @property
   def stream(self):
@@ -72,13 +75,19 @@ class InferenceModel(object):
           self._stream.wait_event(ev)
         with torch.cuda.stream(self._stream):
           self.flat.params.copy_(flat_params, non_blocking=True)
+          self._refresh_cache()
           done = torch.cuda.Event()
           done.record(self._stream)
         if cur is not None:
           cur.wait_event(done)
       else:
         self.flat.params.copy_(flat_params)
+        self._refresh_cache()
       self.version = self.version + 1 if version is None else version
+
+  def _refresh_cache(self):
+    if hasattr(self.agent, 'refresh_inference_cache'):
+      self.agent.refresh_inference_cache()
 
   @torch.no_grad()
   def step_device(self, last_action, reward, done, frame, instr_ids,

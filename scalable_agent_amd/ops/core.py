@@ -53,7 +53,7 @@ class _CoreLSTM(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc, allow_gang=True):
+              done_u8, num_actions, instr_enc, allow_gang=True, w16=None):
     # the final cell state is rarely used: its gradient arrives as None
     # instead of a zero-filled tensor (the backward handles both)
     ctx.set_materialize_grads(False)
@@ -64,7 +64,9 @@ class _CoreLSTM(torch.autograd.Function):
     c_instr = CORE + 1 + num_actions
     assert kernel.shape[0] == f_in + CORE
     bf = torch.bfloat16
-    w16_fc = w_fc.to(bf)
+    # w16: an inference agent's bf16 weight copies, refreshed once per
+    # weight publish instead of cast on every step (Agent.inference_cache)
+    w16_fc = w_fc.to(bf) if w16 is None else w16[0]
     if instr_enc is None:
       # the instruction columns are all zero: their W_x rows drop out
       K = ld = aug_width(num_actions)
@@ -81,7 +83,7 @@ class _CoreLSTM(torch.autograd.Function):
                 aug_reward=rewards, aug_action=actions)
     if instr_enc is not None:
       h_aug[:, c_instr:f_in].copy_(instr_enc)
-    wx16 = kernel[:K].to(bf)
+    wx16 = kernel[:K].to(bf) if w16 is None else w16[1][:K]
     xw = torch.empty(N, 4 * CORE, dtype=torch.float32, device=feats.device)
     C.gemm_bf16(h_aug, wx16, False, False, xw, bias=bias)
     # bf16 path: the gang may run - unless the caller runs the conv torso
@@ -155,7 +157,7 @@ class _CoreLSTM(torch.autograd.Function):
       C.gemm_bf16(dg16_2, wx16[ctx.c_instr:f_in], False, True, d_instr)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
     return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
-            d_instr, None)
+            d_instr, None, None)
 
 
 class _CoreLSTMF32(torch.autograd.Function):
@@ -179,7 +181,8 @@ class _CoreLSTMF32(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc, allow_gang=True):
+              done_u8, num_actions, instr_enc, allow_gang=True, w16=None):
+    del w16  # fp32 operands: nothing to cast
     # the final cell state is rarely used: its gradient arrives as None
     # instead of a zero-filled tensor (the backward handles both)
     ctx.set_materialize_grads(False)
@@ -260,7 +263,7 @@ class _CoreLSTMF32(torch.autograd.Function):
       C.gemm_f32(dg2, kernel[ctx.c_instr:f_in], False, True, d_instr)
     g_wfc, g_bfc, g_k, g_b = grad_sink.returned((gwfc, gbfc, gk, gb), direct)
     return (dfeats, g_wfc, g_bfc, g_k, g_b, None, None, dc0, dh0, None, None,
-            d_instr, None)
+            d_instr, None, None)
 
 
 def _as_u8(done):
@@ -273,11 +276,12 @@ def _as_u8(done):
 
 
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
-              num_actions, instr_enc=None, allow_gang=True):
+              num_actions, instr_enc=None, allow_gang=True, w16=None):
   """feats [T*B, F] (ReLU'd torso output: bf16 -> the bf16-operand path,
   fp32 -> the exact-fp32 path), rewards [T*B] f32, actions [T*B] (last
   actions), done [T,B] bool, state (c, h) [B,256], instr_enc None or the
-  language-LSTM output [T*B, 64] (gradients flow back into it)
+  language-LSTM output [T*B, 64] (gradients flow back into it), w16 None
+  or (w_fc, kernel[:K_max]) as bf16 copies (inference, no gradients)
   -> (hs [T,B,256] f32, (c_T, h_T))."""
   c0, h0 = state
   fn = _CoreLSTMF32 if feats.dtype == torch.float32 else _CoreLSTM
@@ -288,5 +292,5 @@ def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
       c0.float().contiguous(), h0.float().contiguous(),
       _as_u8(done), int(num_actions),
       None if instr_enc is None else instr_enc.float().contiguous(),
-      bool(allow_gang))
+      bool(allow_gang), w16)
   return hs, (c_last, hs[-1])

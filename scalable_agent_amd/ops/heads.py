@@ -96,13 +96,20 @@ class PhiloxStream(object):
   reproducible from its seed (the device-side analogue of a torch
   Generator).  With `device`, the offset lives in device memory and the
   sampler advances it on the device, so a captured inference graph draws new
-  samples on every replay."""
+  samples on every replay.  The device counter is the pair {offset, waves
+  done} that the sampler kernel itself moves to the next offset (no separate
+  increment kernel per step)."""
 
   def __init__(self, seed, device=None):
     self.seed = int(seed) & ((1 << 63) - 1)
     self.offset = 0
     self.counter = (None if device is None else
-                    torch.zeros(1, dtype=torch.int64, device=device))
+                    torch.zeros(2, dtype=torch.int64, device=device))
+
+  @property
+  def device_offset(self):
+    """The device counter's offset (host read; tests and checkpoints)."""
+    return int(self.counter[0].item())
 
   def manual_seed(self, seed):
     self.seed = int(seed) & ((1 << 63) - 1)
@@ -128,7 +135,6 @@ def actor_heads_sample(core_out, policy_w, policy_b, baseline_w, baseline_b,
   if stream.counter is not None and stream.counter.device == core_out.device:
     logits, baseline, action = ext().actor_head_sample(*args, 0,
                                                        stream.counter)
-    stream.counter.add_(1)
   else:
     logits, baseline, action = ext().actor_head_sample(*args,
                                                        stream.next_offset())

@@ -319,6 +319,7 @@ class ActorGroupWorker(object):
         host = np.empty(w.numel, np.float32)
         state['version'] = w.read_into(host)
         model.flat.params.copy_(torch.from_numpy(host))
+        model._refresh_cache()
       return
     if state.get('inflight') is not None:
       v, b, s, ev = state['inflight']
@@ -328,6 +329,7 @@ class ActorGroupWorker(object):
       if w.seq(b) == s:  # not overwritten while the copy ran
         with torch.cuda.stream(model.stream):
           model.flat.params.copy_(state['staging'], non_blocking=True)
+          model._refresh_cache()
         state['version'] = v
       return
     if v == 0 or v == state['version']:

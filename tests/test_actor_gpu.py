@@ -127,14 +127,16 @@ def test_agent_step_fused_sampler(cuda):
 
 def test_device_counter_stream(cuda):
   ops = _ops()
-  h = torch.randn(64, 256, device=cuda)
+  h = torch.randn(63, 256, device=cuda)  # a partial last workgroup
   wp = torch.randn(256, 9, device=cuda)
   bp, wb, bb = (torch.zeros(9, device=cuda), torch.zeros(256, 1, device=cuda),
                 torch.zeros(1, device=cuda))
   s = ops.PhiloxStream(5, device=cuda)
   a1, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, s)
   a2, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, s)
-  assert int(s.counter.item()) == 2 and s.offset == 0
+  # the kernel advanced its own counter: offset 2, wave count re-armed
+  assert s.device_offset == 2 and int(s.counter[1].item()) == 0
+  assert s.offset == 0
   host = ops.PhiloxStream(5)
   b1, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, host)
   b2, _, _ = ops.actor_heads_sample(h, wp, bp, wb, bb, host)
@@ -185,3 +187,42 @@ def test_staged_server_gpu(cuda, graphs):
   srv.join(30)
   assert not errors, errors[0]
   assert st['requests'] == 48
+
+
+def test_inference_weight_cache_tracks_publish(cuda):
+  """A bf16 inference agent casts the core's FC / W_x weights once per
+  publish (Agent.inference_cache) instead of on every step: its step is
+  bitwise that of an uncached agent with the same weights, before and after
+  a publish of new weights."""
+  _ops()
+  from scalable_agent_amd.optim import FlatParams
+  from scalable_agent_amd.structs import StepOutput
+  mk = lambda seed: Agent(9, torso='deep', backend='hip', seed=seed,
+                          compute_dtype=torch.bfloat16)
+  model = inference.InferenceModel(mk(1), cuda, False, seed=3)
+  assert model.agent._inference_w16 is not None
+  ref, other = mk(1).to(cuda), mk(2).to(cuda)
+  assert ref._inference_w16 is None
+  B = 10
+  g = torch.Generator().manual_seed(4)
+  frame = torch.randint(0, 255, (B, 72, 96, 3), generator=g,
+                        dtype=torch.uint8).to(cuda)
+  eo = StepOutput(torch.randn(B, generator=g).to(cuda), None,
+                  torch.zeros(B, dtype=torch.bool, device=cuda), (frame, None))
+  last = torch.randint(0, 9, (B,), generator=g).to(cuda)
+  state = (torch.randn(B, 256, generator=g).to(cuda),
+           torch.randn(B, 256, generator=g).to(cuda))
+
+  def run(agent):
+    with torch.no_grad():
+      out, (c2, h2) = agent.step(last, eo, state,
+                                 generator=torch.Generator(cuda).manual_seed(0))
+    torch.cuda.synchronize()
+    return out.policy_logits, out.baseline, c2, h2
+
+  for a, b in zip(run(model.agent), run(ref)):
+    assert torch.equal(a, b)
+  model.publish(FlatParams(other).params)
+  torch.cuda.synchronize()
+  for a, b in zip(run(model.agent), run(other)):
+    assert torch.equal(a, b)
