@@ -170,9 +170,13 @@ at::Tensor lstm_xbuf(bool bwd, const at::TensorOptions& o) {
 }
 
 // Returns {hs, cs, acts, hpm, wt}: hpm[t] = keep_t * h_{t-1} (A operand of
-// the dW_h GEMM), wt = W_h^T packed for lstm_bwd.
+// the dW_h GEMM), wt = W_h^T packed for lstm_bwd.  w4 (optional, per-step /
+// persistent modes): W_h already packed by lstm_pack_fwd - an inference
+// agent packs once per weight publish instead of on every step; wt is then
+// empty (no backward).
 std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
-                                 at::Tensor h0, at::Tensor w_h, int64_t mode) {
+                                 at::Tensor h0, at::Tensor w_h, int64_t mode,
+                                 c10::optional<at::Tensor> w4_in) {
   SA_CHECK(xw); SA_CHECK(done); SA_CHECK(c0); SA_CHECK(h0); SA_CHECK(w_h);
   SA_CHECK_F32(xw); SA_CHECK_F32(c0); SA_CHECK_F32(h0); SA_CHECK_F32(w_h);
   const int T = xw.size(0), B = xw.size(1), H4 = xw.size(2), H = H4 / 4;
@@ -185,8 +189,14 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
   auto cs = at::empty({T, B, H}, xw.options());
   auto acts = at::empty({T, B, H4}, xw.options());
   auto hpm = at::empty({T, B, H}, xw.options());
-  auto w4 = at::empty({H * H4}, xw.options());
-  auto wt = at::empty({H * H4}, xw.options());
+  const bool packed = w4_in.has_value();
+  if (packed) {
+    SA_CHECK(*w4_in); SA_CHECK_F32(*w4_in);
+    TORCH_CHECK(w4_in->numel() == static_cast<int64_t>(H) * H4 && mode != kGang,
+                "w4: the per-step packing of W_h (not for the gang)");
+  }
+  auto w4 = packed ? *w4_in : at::empty({H * H4}, xw.options());
+  auto wt = at::empty({packed ? 0 : H * H4}, xw.options());
   const int64_t RT = (B + 31) / 32;
   auto hpk = at::empty({2, RT * 32 * H}, xw.options());
   auto s = cur_stream();
@@ -206,8 +216,9 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
         reinterpret_cast<unsigned*>(lstm_err_word(xw.device()).data_ptr<int>()), T, B, s);
     return {hs, cs, acts, hpm, wt};
   }
-  sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
-                               wt.data_ptr<float>(), H, s);
+  if (!packed)
+    sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
+                                 wt.data_ptr<float>(), H, s);
   if (mode == kPersistent) {
     auto xbuf = lstm_xbuf(false, xw.options());
     sa::lstm_fwd_persistent_launch(
@@ -228,6 +239,19 @@ std::vector<at::Tensor> lstm_fwd(at::Tensor xw, at::Tensor done, at::Tensor c0,
                              hpm[t].data_ptr<float>(), B, H, s);
   }
   return {hs, cs, acts, hpm, wt};
+}
+
+// W_h [H, 4H] -> w4 (the per-step / persistent kernels' packing, H*4H
+// floats) in place; the backward packing goes to a scratch buffer.
+void lstm_pack_fwd(at::Tensor w_h, at::Tensor w4) {
+  SA_CHECK(w_h); SA_CHECK(w4); SA_CHECK_F32(w_h); SA_CHECK_F32(w4);
+  const int H = w_h.size(0);
+  TORCH_CHECK((H == 256 || H == 64) && w_h.size(1) == 4 * H && w4.numel() == H * 4 * H,
+              "W_h [H,4H] and w4 of H*4H floats");
+  const c10::DeviceGuard guard(w_h.device());
+  auto scratch = at::empty({H * 4 * H}, w_h.options());
+  sa::lstm_pack_weights_launch(w_h.data_ptr<float>(), w4.data_ptr<float>(),
+                               scratch.data_ptr<float>(), H, cur_stream());
 }
 
 // Returns {dG [T,B,4H] f32, dc0 [B,H], dG bf16 (or an empty tensor)}.
@@ -344,7 +368,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("vtrace_loss", &vtrace_loss);
   m.def("lstm_fwd", &lstm_fwd, pybind11::arg("xw"), pybind11::arg("done"),
         pybind11::arg("c0"), pybind11::arg("h0"), pybind11::arg("w_h"),
-        pybind11::arg("mode"));
+        pybind11::arg("mode"), pybind11::arg("w4") = pybind11::none());
+  m.def("lstm_pack_fwd", &lstm_pack_fwd, pybind11::arg("w_h"), pybind11::arg("w4"));
   m.def("lstm_bwd", &lstm_bwd, pybind11::arg("dh_out"), pybind11::arg("done"),
         pybind11::arg("wt"), pybind11::arg("acts"), pybind11::arg("cs"),
         pybind11::arg("c0"), pybind11::arg("dc_last") = pybind11::none(),

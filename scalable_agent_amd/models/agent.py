@@ -442,33 +442,41 @@ class Agent(nn.Module):
     return logits, values.gather(-1, idx).squeeze(-1)
 
   # ------------------------------------------------------------------ API
-  _inference_w16 = None
+  _inference_cache = None
 
   def inference_cache(self):
-    """For an inference-only agent (InferenceModel): keep bf16 copies of
-    the core's FC and W_x weights, refreshed by refresh_inference_cache()
-    after every weight publish, so a bf16 inference step (and the board's
-    captured graph) reads them instead of casting both matrices on every
-    step.  No-op unless the fused bf16 core applies."""
-    if not (self.fused_core_ready() and self.compute_dtype == torch.bfloat16
-            and self.linear_w.is_cuda):
+    """For an inference-only agent (InferenceModel): keep the fused core's
+    per-step weight forms - W_h packed for the per-step LSTM kernel and, on
+    the bf16 path, bf16 copies of the FC and W_x weights - refreshed by
+    refresh_inference_cache() after every weight publish, so an inference
+    step (and the board's captured graph) reads them instead of packing /
+    casting them on every step.  No-op unless the fused core applies."""
+    if not (self.fused_core_ready() and self.linear_w.is_cuda):
       return
-    bf = torch.bfloat16
-    k_max = (self.core_input_size + 15) // 16 * 16
-    self._inference_w16 = (
-        torch.empty(self.linear_w.shape, dtype=bf, device=self.linear_w.device),
-        torch.empty(k_max, self.lstm_kernel.shape[1], dtype=bf,
-                    device=self.lstm_kernel.device))
+    dev = self.lstm_kernel.device
+    cache = {'w4': torch.empty(CORE_SIZE * 4 * CORE_SIZE, device=dev),
+             'w16': None}
+    if self.compute_dtype == torch.bfloat16:
+      bf = torch.bfloat16
+      k_max = (self.core_input_size + 15) // 16 * 16
+      cache['w16'] = (
+          torch.empty(self.linear_w.shape, dtype=bf, device=dev),
+          torch.empty(k_max, self.lstm_kernel.shape[1], dtype=bf, device=dev))
+    self._inference_cache = cache
     self.refresh_inference_cache()
 
   @torch.no_grad()
   def refresh_inference_cache(self):
-    """Re-casts the cached bf16 weights (on the current stream)."""
-    if self._inference_w16 is None:
+    """Re-packs / re-casts the cached weights (on the current stream)."""
+    cache = self._inference_cache
+    if cache is None:
       return
-    w16_fc, wx16 = self._inference_w16
-    w16_fc.copy_(self.linear_w)
-    wx16.copy_(self.lstm_kernel[:wx16.shape[0]])
+    from .. import ops
+    ops.ext().lstm_pack_fwd(self.lstm_kernel[self.core_input_size:], cache['w4'])
+    if cache['w16'] is not None:
+      w16_fc, wx16 = cache['w16']
+      w16_fc.copy_(self.linear_w)
+      wx16.copy_(self.lstm_kernel[:wx16.shape[0]])
 
   def fused_core_ready(self, instr=None):
     """True when the HIP learner path (fused torso-FC/core-input/LSTM op,
@@ -498,12 +506,12 @@ class Agent(nn.Module):
       feats = self.conv_features(frames)
       instr_enc = (None if instr is None else
                    self.instruction_encoding(instr, T * B, frames.device))
-      w16 = (self._inference_w16 if not torch.is_grad_enabled() else None)
+      cache = (self._inference_cache if not torch.is_grad_enabled() else None)
       return ops.core_lstm(feats, self.linear_w, self.linear_b,
                            self.lstm_kernel, self.lstm_bias,
                            reward.reshape(T * B), actions.reshape(T * B), done,
                            core_state, self.num_actions, instr_enc=instr_enc,
-                           w16=w16)
+                           cache=cache)
     x = self.core_inputs(frames, reward.reshape(T * B),
                          actions.reshape(T * B), instr)
     x = x.view(T, B, -1)

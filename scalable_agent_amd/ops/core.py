@@ -53,7 +53,7 @@ class _CoreLSTM(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc, allow_gang=True, w16=None):
+              done_u8, num_actions, instr_enc, allow_gang=True, cache=None):
     # the final cell state is rarely used: its gradient arrives as None
     # instead of a zero-filled tensor (the backward handles both)
     ctx.set_materialize_grads(False)
@@ -64,8 +64,10 @@ class _CoreLSTM(torch.autograd.Function):
     c_instr = CORE + 1 + num_actions
     assert kernel.shape[0] == f_in + CORE
     bf = torch.bfloat16
-    # w16: an inference agent's bf16 weight copies, refreshed once per
-    # weight publish instead of cast on every step (Agent.inference_cache)
+    # cache: an inference agent's bf16 weight copies and packed W_h,
+    # refreshed once per weight publish instead of on every step
+    # (Agent.inference_cache)
+    w16 = None if cache is None else cache.get('w16')
     w16_fc = w_fc.to(bf) if w16 is None else w16[0]
     if instr_enc is None:
       # the instruction columns are all zero: their W_x rows drop out
@@ -91,7 +93,8 @@ class _CoreLSTM(torch.autograd.Function):
     # co-reside, which persistent conv grids next to it cannot guarantee
     mode = C.lstm_mode(CORE, B, T, not allow_gang)
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
-                                       kernel[f_in:], mode)
+                                       kernel[f_in:], mode,
+                                       _packed_w4(cache, mode))
     ctx.mode = mode
     ctx.save_for_backward(feats, w_fc, b_fc, kernel, bias, w16_fc, wx16, h_aug,
                           wt, acts, cs, c0, hpm, done_u8)
@@ -181,8 +184,7 @@ class _CoreLSTMF32(torch.autograd.Function):
 
   @staticmethod
   def forward(ctx, feats, w_fc, b_fc, kernel, bias, rewards, actions, c0, h0,
-              done_u8, num_actions, instr_enc, allow_gang=True, w16=None):
-    del w16  # fp32 operands: nothing to cast
+              done_u8, num_actions, instr_enc, allow_gang=True, cache=None):
     # the final cell state is rarely used: its gradient arrives as None
     # instead of a zero-filled tensor (the backward handles both)
     ctx.set_materialize_grads(False)
@@ -207,7 +209,8 @@ class _CoreLSTMF32(torch.autograd.Function):
     C.gemm_f32(h_aug, kernel[:K], False, False, xw, bias=bias)
     mode = C.lstm_mode(CORE, B, T, True)  # exact: never the bf16 gang
     hs, cs, acts, hpm, wt = C.lstm_fwd(xw.view(T, B, 4 * CORE), done_u8, c0, h0,
-                                       kernel[f_in:], mode)
+                                       kernel[f_in:], mode,
+                                       _packed_w4(cache, mode))
     ctx.mode = mode
     ctx.save_for_backward(feats, w_fc, b_fc, kernel, bias, h_aug, wt, acts, cs,
                           c0, hpm, done_u8)
@@ -266,6 +269,13 @@ class _CoreLSTMF32(torch.autograd.Function):
             d_instr, None, None)
 
 
+def _packed_w4(cache, mode):
+  """The cached per-step packing of W_h (inference agents), or None."""
+  if cache is None or cache.get('w4') is None or mode == 2:  # 2: the gang
+    return None
+  return cache['w4']
+
+
 def _as_u8(done):
   """done as a contiguous uint8 tensor: a bool tensor is reinterpreted in
   place (same 1-byte elements), anything else converted."""
@@ -276,12 +286,13 @@ def _as_u8(done):
 
 
 def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
-              num_actions, instr_enc=None, allow_gang=True, w16=None):
+              num_actions, instr_enc=None, allow_gang=True, cache=None):
   """feats [T*B, F] (ReLU'd torso output: bf16 -> the bf16-operand path,
   fp32 -> the exact-fp32 path), rewards [T*B] f32, actions [T*B] (last
   actions), done [T,B] bool, state (c, h) [B,256], instr_enc None or the
-  language-LSTM output [T*B, 64] (gradients flow back into it), w16 None
-  or (w_fc, kernel[:K_max]) as bf16 copies (inference, no gradients)
+  language-LSTM output [T*B, 64] (gradients flow back into it), cache None
+  or an inference agent's {'w16': bf16 (w_fc, kernel[:K_max]) or None,
+  'w4': W_h packed by lstm_pack_fwd} (no gradients)
   -> (hs [T,B,256] f32, (c_T, h_T))."""
   c0, h0 = state
   fn = _CoreLSTMF32 if feats.dtype == torch.float32 else _CoreLSTM
@@ -292,5 +303,5 @@ def core_lstm(feats, w_fc, b_fc, kernel, bias, rewards, actions, done, state,
       c0.float().contiguous(), h0.float().contiguous(),
       _as_u8(done), int(num_actions),
       None if instr_enc is None else instr_enc.float().contiguous(),
-      bool(allow_gang), w16)
+      bool(allow_gang), cache)
   return hs, (c_last, hs[-1])

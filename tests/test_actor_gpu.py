@@ -189,20 +189,23 @@ def test_staged_server_gpu(cuda, graphs):
   assert st['requests'] == 48
 
 
-def test_inference_weight_cache_tracks_publish(cuda):
-  """A bf16 inference agent casts the core's FC / W_x weights once per
-  publish (Agent.inference_cache) instead of on every step: its step is
-  bitwise that of an uncached agent with the same weights, before and after
-  a publish of new weights."""
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_inference_weight_cache_tracks_publish(cuda, dtype):
+  """An inference agent packs W_h (and on the bf16 path casts the core's FC
+  / W_x weights) once per publish (Agent.inference_cache) instead of on
+  every step: its step is bitwise that of an uncached agent with the same
+  weights, before and after a publish of new weights."""
   _ops()
   from scalable_agent_amd.optim import FlatParams
   from scalable_agent_amd.structs import StepOutput
   mk = lambda seed: Agent(9, torso='deep', backend='hip', seed=seed,
-                          compute_dtype=torch.bfloat16)
+                          compute_dtype=dtype)
   model = inference.InferenceModel(mk(1), cuda, False, seed=3)
-  assert model.agent._inference_w16 is not None
+  cache = model.agent._inference_cache
+  assert cache['w4'] is not None
+  assert (cache['w16'] is not None) == (dtype == torch.bfloat16)
   ref, other = mk(1).to(cuda), mk(2).to(cuda)
-  assert ref._inference_w16 is None
+  assert ref._inference_cache is None
   B = 10
   g = torch.Generator().manual_seed(4)
   frame = torch.randint(0, 255, (B, 72, 96, 3), generator=g,
