@@ -138,7 +138,7 @@ struct WinoArgs {
   int relu_in, relu_out;
   int maxrows;  // LDS row capacity (>= rows of every range)
   int ablate;  // measurement knob (SA_WINO_ABLATE): 1 no tasks, 2 no global
-               // loads, 4 no LDS commit, 8 no stores
+               // loads, 4 no LDS commit, 8 no stores, 16 no weight transform
   int runs;    // 1: each workgroup walks a contiguous run of ranges (halo rows
                // shared with the previous range hit this CU's L2), 0: strided
   int prio;    // SA_WINO_PRIO=1: waves NW/2.. run at s_setprio 1 (static
@@ -354,8 +354,9 @@ __global__ __launch_bounds__(64 * NW, WPS) void wino_conv_kernel(WinoArgs a) {
   float* U_s = smem;                   // [16 xi][NB][4 g][COUT][4]
   float* x_s = smem + 16 * CIN * COUT;  // [rows][Wl][PP]
 
-  // ---- weight transform U = G g G^T into LDS (once per workgroup)
-  for (int e = threadIdx.x; e < CIN * COUT; e += NTH) {
+  // ---- weight transform U = G g G^T into LDS (once per workgroup; the
+  // measurement bit 16 skips it to time the rest)
+  for (int e = threadIdx.x; e < (knob(a.ablate, 16) ? 0 : CIN * COUT); e += NTH) {
     const int co = e % COUT, ci = e / COUT;
     float gk[3][3];
 #pragma unroll
