@@ -307,3 +307,23 @@ def test_res_block_fwd_matches_two_convs(cuda, C, H, W, last):
   t, y = _C().res_block_fwd(x, w1, b1, w2, b2, last)
   assert torch.equal(t, t_ref)
   assert torch.equal(y, y_ref)
+
+
+@pytest.mark.parametrize('shape', [(72, 96, 3), (84, 84, 4)])
+def test_inference_torso_fused_blocks_match_learner_path(cuda, shape):
+  """Small no-grad batches (actor inference) run the bf16 torso with the
+  fused residual-block kernel (ops/conv.py _DeepTorsoInfer); the learner's
+  autograd path runs two convs per block: bitwise the same features."""
+  from scalable_agent_amd.models import Agent
+  from scalable_agent_amd.ops import conv
+  agent = Agent(9, torso='deep', frame_shape=shape, seed=4, backend='hip',
+                compute_dtype=torch.bfloat16).to(cuda)
+  g = torch.Generator().manual_seed(6)
+  frames = torch.randint(0, 256, (37,) + shape, generator=g,
+                         dtype=torch.uint8).to(cuda)
+  with torch.no_grad():
+    f_inf = conv.torso_forward(agent, frames)
+  with torch.enable_grad():
+    f_lrn = conv.torso_forward(agent, frames)
+  assert f_lrn.requires_grad and not f_inf.requires_grad
+  assert torch.equal(f_inf, f_lrn.detach())
