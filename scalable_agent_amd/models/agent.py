@@ -455,7 +455,14 @@ class Agent(nn.Module):
       return
     dev = self.lstm_kernel.device
     cache = {'w4': torch.empty(CORE_SIZE * 4 * CORE_SIZE, device=dev),
-             'w16': None}
+             'w16': None, 'w0pad': None}
+    if (self.compute_dtype == torch.float32 and self.torso_kind == 'deep' and
+        self.frame_shape[2] < 4):
+      # the fp32 torso's stage-0 weights padded to the 4-channel image
+      from ..ops.conv import deep_param_list
+      w0 = deep_param_list(self)[0]
+      cache['w0pad'] = torch.zeros(w0.shape[:2] + (4,) + w0.shape[3:],
+                                   dtype=w0.dtype, device=dev)
     if self.compute_dtype == torch.bfloat16:
       bf = torch.bfloat16
       k_max = (self.core_input_size + 15) // 16 * 16
@@ -473,6 +480,9 @@ class Agent(nn.Module):
       return
     from .. import ops
     ops.ext().lstm_pack_fwd(self.lstm_kernel[self.core_input_size:], cache['w4'])
+    if cache['w0pad'] is not None:
+      w0 = ops.conv.deep_param_list(self)[0]
+      cache['w0pad'][:, :, :w0.shape[2]].copy_(w0)  # pad channels stay 0
     if cache['w16'] is not None:
       w16_fc, wx16 = cache['w16']
       w16_fc.copy_(self.linear_w)

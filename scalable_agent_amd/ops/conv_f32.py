@@ -327,7 +327,14 @@ def torso_forward_f32(agent, frames):
   if agent.torso_kind == 'shallow':
     return _chunked(_ShallowTorsoF32, frames, shallow_param_list(agent))
   from .conv import deep_param_list
-  return _chunked(_DeepTorsoF32, frames, deep_param_list(agent))
+  params = deep_param_list(agent)
+  cache = getattr(agent, '_inference_cache', None)
+  if (cache is not None and cache.get('w0pad') is not None and
+      not torch.is_grad_enabled() and not U8_DIRECT['deep']):
+    # an inference agent's stage-0 weights, zero-padded to the image's 4
+    # channels once per weight publish (no concatenation kernel per step)
+    params = [cache['w0pad']] + params[1:]
+  return _chunked(_DeepTorsoF32, frames, params)
 
 
 def linear_relu_f32(x, w, b):

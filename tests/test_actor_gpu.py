@@ -204,6 +204,7 @@ def test_inference_weight_cache_tracks_publish(cuda, dtype):
   cache = model.agent._inference_cache
   assert cache['w4'] is not None
   assert (cache['w16'] is not None) == (dtype == torch.bfloat16)
+  assert (cache['w0pad'] is not None) == (dtype == torch.float32)
   ref, other = mk(1).to(cuda), mk(2).to(cuda)
   assert ref._inference_cache is None
   B = 10
