@@ -153,8 +153,12 @@ def restore_agent(agent, state):
   with torch.no_grad():
     for n, p in agent.named_parameters():
       p.copy_(params[names[n]].to(p.device))
-  if hasattr(agent, 'refresh_inference_cache'):
-    agent.refresh_inference_cache()  # an inference agent's bf16 copies
+  if getattr(agent, '_inference_cache', None) is not None:
+    # an inference agent's per-step weight forms; its inference runs on its
+    # model's own stream, so the refresh is finished here
+    agent.refresh_inference_cache()
+    if agent.lstm_kernel.is_cuda:
+      torch.cuda.current_stream(agent.lstm_kernel.device).synchronize()
 
 
 def restore(logdir, learner):

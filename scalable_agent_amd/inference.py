@@ -47,9 +47,13 @@ class InferenceModel(object):
       self._gen = PhiloxStream(seed, device=self.device)
     else:
       self._gen = torch.Generator(device=self.device).manual_seed(seed)
-    # bf16 core weights cast once per publish, not per step (HIP bf16 agent)
+    # the core's per-step weight forms packed / cast once per publish, not
+    # per step (HIP agent); this first fill runs on the current stream, which
+    # the model's own stream does not wait for: finish it here
     if hasattr(self.agent, 'inference_cache'):
       self.agent.inference_cache()
+      if self._stream is not None:
+        torch.cuda.current_stream(self.device).synchronize()
 
   @property
   def stream(self):
